@@ -1,0 +1,100 @@
+/*
+ * ttship — MI355X-native Tacotron2-DDC + MultiBand-MelGAN inference path, C ABI.
+ *
+ * Drop-in boundary. The reference has no FFI/plugin registry: its boundary is
+ * nn.Module duck typing. Each entry point below replaces one reference call, cited as
+ * path:line relative to the reference checkout:
+ *
+ *   tts_taco_set_tensor/finalize  <- Tacotron2.load_state_dict(cp['model'])
+ *                                    (TTS/server/synthesizer.py:68-79, TTS/tts/utils/io.py:9-24)
+ *   tts_taco_infer                <- Tacotron2.inference(text)  (TTS/tts/models/tacotron2.py:142-163)
+ *                                    with decoder.set_r / max_decoder_steps (layers/tacotron2.py:209,156)
+ *   tts_taco_encoder              <- embedding + Encoder.inference (models/tacotron2.py:144-145,
+ *                                    layers/tacotron2.py:112-119)
+ *   tts_taco_postnet              <- Postnet + residual (models/tacotron2.py:159-160)
+ *   tts_melgan_set_tensor/finalize<- MultibandMelganGenerator.load_state_dict + remove_weight_norm
+ *                                    (TTS/server/synthesizer.py:81-91, melgan_generator.py:91-97)
+ *   tts_melgan_infer              <- MultibandMelganGenerator.inference (multiband_melgan_generator.py:32-39)
+ *   tts_melgan_generator          <- MelganGenerator.layers(c) (melgan_generator.py:28-81)
+ *   tts_pqmf_synthesis            <- PQMF.synthesis (TTS/vocoder/layers/pqmf.py:51-56)
+ *
+ * Conventions: every function returns 0 on success and nonzero on failure; the message is
+ * available from tts_last_error() (thread-local). Pointers prefixed d_ are device (HIP) memory
+ * owned by the caller; h_ are host memory. `stream` is a hipStream_t (NULL = default stream);
+ * work is ordered after prior work on `stream` and later work on `stream` is ordered after it.
+ * Tensors are fp32, C-contiguous, in the layouts documented per function.
+ */
+#ifndef TTSHIP_H
+#define TTSHIP_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct tts_ctx tts_ctx;
+
+int tts_version(void);
+const char* tts_last_error(void);
+
+/* One context per (process, device). Owns packed weights, workspace and captured graphs. */
+int tts_ctx_create(int device, tts_ctx** out);
+int tts_ctx_destroy(tts_ctx* ctx);
+
+/* ---- Tacotron2 (DDC LJSpeech architecture; coarse_decoder.* accepted and ignored) ---- */
+/* Register one state_dict tensor by its reference key, fp32 host data. */
+int tts_taco_set_tensor(tts_ctx* ctx, const char* name, const float* h_data, const int64_t* shape, int ndim);
+/* Fold BatchNorm, permute/swizzle and upload. attn_norm: 0 = sigmoid, 1 = softmax.
+   r_init = reduction factor the model was constructed with (projection width 80*r_init). */
+int tts_taco_finalize(tts_ctx* ctx, int num_chars, int r_init, int attn_norm);
+
+/* Batched Tacotron2.inference. Output i equals the reference B=1 call on utterance i.
+   d_ids      (B, T_max) int64 token ids; row b valid for t < h_lens[b] (1 <= h_lens[b] <= T_max)
+   r          reduction factor in use (1 <= r <= r_init)
+   h_max_steps per-utterance max_decoder_steps (>= 1); S_cap >= max(h_max_steps)
+   d_dec, d_post (B, S_cap*r, 80): frames [0, steps_b*r) valid, rest zero
+   d_align    (B, S_cap, T_max);  d_stop (B, S_cap) sigmoid(stop logit)
+   h_steps    out: decoder steps taken per utterance; h_status out: 1 stopnet, 2 max steps */
+int tts_taco_infer(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                   const int32_t* h_max_steps, int S_cap, float stop_threshold, float* d_dec, float* d_post,
+                   float* d_align, float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream);
+
+/* encoder outputs (B, T_max, 512), zero for t >= h_lens[b] */
+int tts_taco_encoder(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max,
+                     float* d_out, void* stream);
+
+/* postnet(dec) + dec on time-major (B, M_max, 80) frames, valid for t < h_lens[b] */
+int tts_taco_postnet(tts_ctx* ctx, const float* d_dec, const int32_t* h_lens, int B, int M_max, float* d_out,
+                     void* stream);
+
+/* ---- MultiBand-MelGAN generator ---- */
+int tts_melgan_set_tensor(tts_ctx* ctx, const char* name, const float* h_data, const int64_t* shape, int ndim);
+/* upsample_factors: n_up entries (even), base_channels, num_res_blocks, out_channels (4 with PQMF) */
+int tts_melgan_finalize(tts_ctx* ctx, int in_channels, int out_channels, int base_channels,
+                        const int32_t* upsample_factors, int n_up, int num_res_blocks, int use_pqmf);
+
+/* d_mel (B, in_channels, M_max) channel-major, utterance b valid for m < h_lens[b];
+   pad = inference_padding (replicate). Requires h_lens[b] + 2*pad >= 4 (ReflectionPad1d(3)).
+   d_wav (B, 1, hop*(M_max + 2*pad)), hop = prod(upsample_factors) * (out_channels if PQMF else 1);
+   samples past hop*(h_lens[b] + 2*pad) are zero. */
+int tts_melgan_infer(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
+                     float* d_wav, void* stream);
+
+/* generator layers only: d_out (B, out_channels, up*(M_max + 2*pad)), up = prod(upsample_factors) */
+int tts_melgan_generator(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
+                         float* d_out, void* stream);
+
+/* PQMF synthesis on (B, N, L) subbands with filter d_G (N, taps+1) -> d_y (B, 1, N*L) */
+int tts_pqmf_synthesis(tts_ctx* ctx, const float* d_x, int B, int N, int L, const float* d_G, int taps,
+                       float* d_y, void* stream);
+
+/* Measurement hook for bench.py: average device time (ms) of `iters` launches of one kernel of the
+   last tts_taco_infer configuration, timed with hipEvents on the context's stream.
+   which: 0 = decoder LSTM GEMM step kernel (K4), 1 = full decoder step (all 7 kernels). */
+int tts_time_decoder_kernel(tts_ctx* ctx, int which, int iters, float* ms_out);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

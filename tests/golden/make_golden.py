@@ -1,0 +1,226 @@
+"""Generate the golden parity fixtures by running the REFERENCE PyTorch CPU path.
+
+Run in the build container only (the reference is not on the GPU box):
+
+    PYTHONPATH=/root/reference:/root/repo python tests/golden/make_golden.py
+
+It imports the reference modules (``TTS.tts.models.tacotron2.Tacotron2``,
+``TTS.vocoder.models.multiband_melgan_generator.MultibandMelganGenerator``,
+``TTS.vocoder.layers.pqmf.PQMF``), loads deterministic synthetic weights from
+``tts_amd.weights`` (the fixtures store only seeds), and records inputs and outputs into
+small ``.npz`` files next to this script. Nothing from the reference source is copied;
+only its outputs on our inputs are stored.
+"""
+
+import json
+import math
+import os
+import sys
+
+import numpy as np
+import torch
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path.insert(0, REPO)
+
+from tts_amd.spec import TacotronConfig, MelganConfig, tacotron2_spec, melgan_spec  # noqa: E402
+from tts_amd.weights import synth_state_dict  # noqa: E402
+
+REF = os.environ.get("TTS_REFERENCE", "/root/reference")
+if REF not in sys.path:
+    sys.path.insert(0, REF)
+
+from TTS.tts.models.tacotron2 import Tacotron2  # noqa: E402
+from TTS.vocoder.models.multiband_melgan_generator import MultibandMelganGenerator  # noqa: E402
+from TTS.vocoder.layers.pqmf import PQMF  # noqa: E402
+
+torch.set_num_threads(8)
+
+
+STOP_GAIN = {"linear_sigmoid": 100.0, "attn_v": 4.0, "linear_tanh": 3.0}
+# larger stop logits -> wider stop margins; sharper attention -> wider argmax margins
+
+
+def build_taco(cfg: TacotronConfig, seed: int, stop_bias: float, dtype=torch.float32):
+    torch.set_default_dtype(dtype)
+    m = Tacotron2(num_chars=cfg.num_chars, num_speakers=0, r=cfg.r, attn_norm=cfg.attn_norm,
+                  prenet_dropout=False, location_attn=cfg.location_attn,
+                  double_decoder_consistency=cfg.double_decoder_consistency, ddc_r=cfg.ddc_r,
+                  separate_stopnet=True)
+    sd = synth_state_dict(tacotron2_spec(cfg), seed, STOP_GAIN)
+    sd["decoder.stopnet.1.linear_layer.bias"] = np.array([stop_bias], np.float32)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.eval()
+    if dtype == torch.float64:
+        m.double()
+    torch.set_default_dtype(torch.float32)
+    return m
+
+
+def run_taco(m, ids, r, max_steps, dtype=torch.float32):
+    m.decoder.set_r(r)
+    m.decoder.max_decoder_steps = max_steps
+    logits = []
+    h = m.decoder.stopnet.register_forward_hook(lambda mod, i, o: logits.append(o.detach().clone()))
+    torch.set_default_dtype(dtype)
+    with torch.no_grad():
+        x = torch.from_numpy(ids[None].astype(np.int64))
+        emb = m.embedding(x).transpose(1, 2)
+        enc_out = m.encoder.inference(emb)
+        dec, post, align, stop = m.inference(x)
+    h.remove()
+    torch.set_default_dtype(torch.float32)
+    lg = torch.cat(logits, 0).reshape(-1).double().numpy()
+    return (dec[0].double().numpy(), post[0].double().numpy(), align[0].double().numpy(),
+            stop[0, :, 0].double().numpy(), lg, enc_out[0].double().numpy())
+
+
+def choose_stop_bias(raw_logits_list, max_steps, min_stopping, min_stop_step=4):
+    """Bias b maximising the min margin |l_t + b| over steps 1..stop (or 1..max)."""
+    best = None
+    cands = np.concatenate([-l[1:] for l in raw_logits_list])
+    srt = np.sort(cands)
+    mids = (srt[:-1] + srt[1:]) / 2
+    for b in mids:
+        margins, nstop = [], 0
+        for l in raw_logits_list:
+            z = l[1:] + b
+            idx = np.nonzero(z > 0)[0]
+            if len(idx) and idx[0] + 1 < min_stop_step:
+                nstop = -100
+            if len(idx):
+                nstop += 1
+                margins.append(np.min(np.abs(z[: idx[0] + 1])))
+            else:
+                margins.append(np.min(np.abs(z)))
+        if nstop < min_stopping:
+            continue
+        mm = min(margins)
+        if best is None or mm > best[1]:
+            best = (float(b), float(mm))
+    return best
+
+
+def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_seed):
+    rs = np.random.RandomState(id_seed)
+    utts = [rs.randint(1, cfg.num_chars, size=T).astype(np.int64) for T in utt_lens]
+    # pass 1: never stop; record bias-free logits at the largest r (same decoder state
+    # trajectory for any stop bias, since the stopnet output is never fed back)
+    out = {"seed": seed, "cfg": json.dumps(cfg.__dict__), "r_list": np.array(r_list),
+           "overrides": json.dumps(STOP_GAIN)}
+    for r in r_list:
+        m = build_taco(cfg, seed, -1e4)
+        raw = []
+        for ids in utts:
+            lg = run_taco(m, ids, r, max_steps[r])[4]
+            raw.append(lg + 1e4)
+        b, margin = choose_stop_bias(raw, max_steps[r], min_stopping)
+        print(f"[{name}] r={r} stop bias {b:.6f} min margin {margin:.3e}")
+        m32 = build_taco(cfg, seed, b)
+        m64 = build_taco(cfg, seed, b, torch.float64)
+        for i, ids in enumerate(utts):
+            dec, post, align, stop, lg, enc = run_taco(m32, ids, r, max_steps[r])
+            dec64, post64, _, _, _, _ = run_taco(m64, ids, r, max_steps[r], torch.float64)
+            n = min(len(dec), len(dec64))
+            drift = float(np.max(np.abs(post[:n] - post64[:n]))) if len(dec) == len(dec64) else float("nan")
+            am = np.sort(align, axis=1)
+            top2 = am[:, -1] - am[:, -2] if align.shape[1] > 1 else np.full(len(align), np.inf)
+            k = f"r{r}_u{i}"
+            out[f"{k}_ids"] = ids
+            out[f"{k}_dec"] = dec.astype(np.float32)
+            out[f"{k}_post"] = post.astype(np.float32)
+            out[f"{k}_align"] = align.astype(np.float32)
+            out[f"{k}_stop"] = stop.astype(np.float32)
+            out[f"{k}_logit"] = lg.astype(np.float32)
+            out[f"{k}_top2"] = top2.astype(np.float32)
+            out[f"{k}_drift64"] = np.float64(drift)
+            if i == 1:
+                out[f"{k}_enc"] = enc.astype(np.float32)
+            print(f"  utt{i} T={len(ids)} steps={len(stop)} frames={len(dec)} drift64={drift:.2e} "
+                  f"min top2={top2.min():.2e}")
+        out[f"r{r}_stop_bias"] = np.float32(b)
+        out[f"r{r}_max_steps"] = np.int32(max_steps[r])
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def vocoder_case(name, seed):
+    c = MelganConfig()
+    v = MultibandMelganGenerator(in_channels=c.in_channels, out_channels=c.out_channels,
+                                 proj_kernel=c.proj_kernel, base_channels=c.base_channels,
+                                 upsample_factors=list(c.upsample_factors), res_kernel=c.res_kernel,
+                                 num_res_blocks=c.num_res_blocks)
+    sd = synth_state_dict(melgan_spec(c, weight_norm=True), seed)
+    full = v.state_dict()
+    for k, t in sd.items():
+        full[k] = torch.from_numpy(t)
+    v.load_state_dict(full)
+    v.remove_weight_norm()
+    v.eval()
+    out = {"seed": seed}
+    rs = np.random.RandomState(11)
+    for M, pad in ((7, 0), (64, 0), (5, 2), (33, 2)):
+        mel = (rs.uniform(-1, 1, size=(1, 80, M)) * 2.0).astype(np.float32)
+        v.inference_padding = pad
+        with torch.no_grad():
+            wav = v.inference(torch.from_numpy(mel))
+            bands = v.layers(torch.nn.functional.pad(torch.from_numpy(mel), (pad, pad), "replicate"))
+        k = f"M{M}_p{pad}"
+        out[f"{k}_mel"] = mel
+        out[f"{k}_wav"] = wav.numpy().astype(np.float32)
+        out[f"{k}_bands"] = bands.numpy().astype(np.float32)
+        print(f"[{name}] M={M} pad={pad} wav {tuple(wav.shape)} |w|max {wav.abs().max():.3f}")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
+def pqmf_case(name):
+    import scipy.io.wavfile as wavfile
+    p = PQMF(N=4, taps=62, cutoff=0.15, beta=9.0)
+    rs = np.random.RandomState(5)
+    x = rs.uniform(-1, 1, size=(2, 4, 300)).astype(np.float32)
+    with torch.no_grad():
+        y = p.synthesis(torch.from_numpy(x)).numpy()
+    sr, w = wavfile.read(os.path.join(REF, "tests/inputs/example_1.wav"))
+    sr2, ka = wavfile.read(os.path.join(REF, "TTS/vocoder/pqmf_output.wav"))
+    wf = (w.astype(np.float32) / 32768.0)[None, None, :]
+    with torch.no_grad():
+        bands = p.analysis(torch.from_numpy(wf))
+        rec = p.synthesis(bands).numpy()
+    out = dict(x=x, y=y, H=p.H.numpy(), G=p.G.numpy(), updown=p.updown_filter.numpy(),
+               example_wav_int16=w, example_bands=bands.numpy(),
+               known_answer_int16=ka, example_rec=rec)
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+    print(f"[{name}] synth {y.shape}; known answer {ka.shape}")
+
+
+def lj_profile():
+    import scipy.io.wavfile as wavfile
+    d = os.path.join(REF, "tests/data/ljspeech")
+    rows = []
+    with open(os.path.join(d, "metadata.csv"), encoding="utf-8") as f:
+        for line in f:
+            parts = line.rstrip("\n").split("|")
+            sr, w = wavfile.read(os.path.join(d, "wavs", parts[0] + ".wav"))
+            rows.append({"id": parts[0], "T": len(parts[2]), "M": int(math.ceil(len(w) / 256)),
+                         "samples": int(len(w)), "sr": int(sr)})
+    json.dump({"source": "reference tests/data/ljspeech (metadata col 3 length, ceil(wav/256))",
+               "utterances": rows}, open(os.path.join(HERE, "lj_profile.json"), "w"), indent=1)
+    print("LJ profile: sum T", sum(r["T"] for r in rows), "sum M", sum(r["M"] for r in rows),
+          "max T", max(r["T"] for r in rows), "max M", max(r["M"] for r in rows))
+
+
+if __name__ == "__main__":
+    which = sys.argv[1:] or ["lj", "pqmf", "vocoder", "taco_sigmoid", "taco_softmax"]
+    if "lj" in which:
+        lj_profile()
+    if "pqmf" in which:
+        pqmf_case("pqmf")
+    if "vocoder" in which:
+        vocoder_case("mbmelgan", seed=3)
+    if "taco_sigmoid" in which:
+        taco_case("taco_sigmoid", TacotronConfig(attn_norm="sigmoid"), seed=1,
+                  utt_lens=[12, 37, 80], r_list=[2, 1], max_steps={2: 70, 1: 110},
+                  min_stopping=2, id_seed=7)
+    if "taco_softmax" in which:
+        taco_case("taco_softmax", TacotronConfig(attn_norm="softmax"), seed=2,
+                  utt_lens=[25, 9], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=8)

@@ -1,0 +1,284 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the reference fixtures and the
+oracle. Tolerances (fp32): mel / frames <= 1e-4 L-inf (north_star), waveforms <= 1e-4 L-inf,
+stop steps and alignment argmax bit-exact (argmax only where the reference's top-2 margin
+exceeds 1e-5; ties below that are implementation-defined in fp32).
+"""
+import numpy as np
+import pytest
+import torch
+
+from helpers import (build_melgan, build_taco, load_fixture, melgan_oracle, melgan_state_dict,
+                     taco_state_dict)
+
+pytestmark = pytest.mark.gpu
+
+MEL_TOL = 1e-4
+WAV_TOL = 1e-4
+ALIGN_MARGIN = 1e-5
+
+
+def _dev():
+    if not torch.cuda.is_available():
+        pytest.fail("GPU test requires a ROCm device")
+    return torch.device("cuda:0")
+
+
+# ------------------------------------------------------------------------------- PQMF
+def test_pqmf_synthesis_matches_reference():
+    from tts_amd import PQMF
+    dev = _dev()
+    fx = load_fixture("pqmf")
+    p = PQMF().to(dev)
+    assert np.array_equal(p.G.cpu().numpy(), fx["G"])
+    y = p.synthesis(torch.from_numpy(fx["x"]).to(dev)).cpu().numpy()
+    assert y.shape == fx["y"].shape
+    assert np.abs(y - fx["y"]).max() <= 1e-5
+
+
+def test_pqmf_known_answer_wav():
+    """TTS/vocoder/pqmf_output.wav (reference's committed output) within int16 rounding."""
+    from tts_amd import PQMF
+    dev = _dev()
+    fx = load_fixture("pqmf")
+    y = PQMF().to(dev).synthesis(torch.from_numpy(fx["example_bands"]).to(dev)).cpu().numpy()[0, 0]
+    assert np.abs(y - fx["example_rec"][0, 0]).max() <= 1e-5
+    ka = fx["known_answer_int16"].astype(np.float64)
+    n = len(ka) - 64
+    pcm = y[:n].astype(np.float64) * 32768.0
+    assert np.abs(pcm - ka[:n]).max() <= 2.0
+
+
+# ------------------------------------------------------------------------------ MelGAN
+@pytest.fixture(scope="module")
+def melgan():
+    dev = _dev()
+    fx = load_fixture("mbmelgan")
+    cfg, sd = melgan_state_dict(int(fx["seed"]))
+    return fx, cfg, sd, build_melgan(cfg, sd, dev)
+
+
+@pytest.mark.parametrize("key", ["M7_p0", "M64_p0", "M5_p2", "M33_p2"])
+def test_mbmelgan_inference_matches_reference(melgan, key):
+    fx, cfg, sd, v = melgan
+    v.inference_padding = int(key.split("_p")[1])
+    mel = torch.from_numpy(fx[key + "_mel"]).cuda()
+    wav = v.inference(mel).cpu().numpy()
+    ref = fx[key + "_wav"]
+    assert wav.shape == ref.shape
+    assert np.abs(wav - ref).max() <= WAV_TOL
+    bands = v.generator(mel).cpu().numpy()
+    assert np.abs(bands - fx[key + "_bands"]).max() <= WAV_TOL
+
+
+def test_mbmelgan_batched_equals_single(melgan):
+    fx, cfg, sd, v = melgan
+    v.inference_padding = 0
+    mels = [fx["M64_p0_mel"][0], fx["M7_p0_mel"][0]]
+    M = max(m.shape[1] for m in mels)
+    batch = np.zeros((2, 80, M), np.float32)
+    for i, m in enumerate(mels):
+        batch[i, :, :m.shape[1]] = m
+    wav = v.inference(torch.from_numpy(batch).cuda(), lengths=[64, 7]).cpu().numpy()
+    for i, key in enumerate(["M64_p0", "M7_p0"]):
+        ref = fx[key + "_wav"][0, 0]
+        assert np.abs(wav[i, 0, :len(ref)] - ref).max() <= WAV_TOL
+        assert not wav[i, 0, len(ref):].any()
+
+
+def test_mbmelgan_random_vs_oracle(melgan):
+    fx, cfg, sd, v = melgan
+    orc = melgan_oracle(cfg, sd)
+    rs = np.random.RandomState(3)
+    lens = [9, 23, 4]
+    M = max(lens)
+    batch = np.zeros((3, 80, M), np.float32)
+    for i, L in enumerate(lens):
+        batch[i, :, :L] = rs.normal(0, 1.5, (80, L))
+    v.inference_padding = 1
+    wav = v.inference(torch.from_numpy(batch).cuda(), lengths=lens).cpu().numpy()
+    for i, L in enumerate(lens):
+        ref = orc.inference(batch[i, :, :L], pad=1)[0]
+        assert np.abs(wav[i, 0, :len(ref)] - ref).max() <= WAV_TOL
+
+
+def test_mbmelgan_too_short_raises(melgan):
+    fx, cfg, sd, v = melgan
+    v.inference_padding = 0
+    with pytest.raises(RuntimeError):
+        v.inference(torch.zeros(1, 80, 3, device="cuda"))
+
+
+# --------------------------------------------------------------------------- Tacotron2
+@pytest.fixture(scope="module")
+def taco_sig():
+    _dev()
+    return load_fixture("taco_sigmoid")
+
+
+def test_encoder_matches_reference(taco_sig):
+    from tts_amd._lib import get_engine
+    fx = taco_sig
+    cfg, sd = taco_state_dict(fx, r=2)
+    m = build_taco(cfg, sd)
+    eng = get_engine("cuda:0")
+    m._sync(eng)
+    ids = [fx["r2_u0_ids"], fx["r2_u1_ids"], fx["r2_u2_ids"]]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((3, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    out = torch.empty(3, T, 512, device="cuda")
+    eng.taco_encoder(torch.from_numpy(batch).cuda(), [len(x) for x in ids], out)
+    enc = out[1, :len(ids[1])].cpu().numpy()
+    assert np.abs(enc - fx["r2_u1_enc"]).max() <= 1e-5
+    assert not out[1, len(ids[1]):].any()
+
+
+def _check_taco(fx, r, dec, post, align, stop, steps, utts):
+    for i in utts:
+        k = f"r{r}_u{i}"
+        S = len(fx[k + "_stop"])
+        assert steps[i] == S, f"{k}: steps {steps[i]} != reference {S}"
+        M = S * r
+        assert np.abs(dec[i, :M] - fx[k + "_dec"]).max() <= MEL_TOL
+        assert np.abs(post[i, :M] - fx[k + "_post"]).max() <= MEL_TOL
+        assert not post[i, M:].any() and not dec[i, M:].any()
+        a = align[i, :S, :fx[k + "_align"].shape[1]]
+        assert np.abs(a - fx[k + "_align"]).max() <= 1e-5
+        sel = fx[k + "_top2"] > ALIGN_MARGIN
+        assert np.array_equal(a.argmax(1)[sel], fx[k + "_align"].argmax(1)[sel])
+        assert np.abs(stop[i, :S, 0] - fx[k + "_stop"]).max() <= 1e-4
+
+
+@pytest.mark.parametrize("r", [2, 1])
+def test_tacotron2_batched_matches_reference(taco_sig, r):
+    fx = taco_sig
+    cfg, sd = taco_state_dict(fx, r=r)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(r)
+    m.decoder.max_decoder_steps = int(fx[f"r{r}_max_steps"])
+    ids = [fx[f"r{r}_u{i}_ids"] for i in range(3)]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((3, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=[len(x) for x in ids])
+    _check_taco(fx, r, dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy(), stop.cpu().numpy(),
+                m.last_steps, range(3))
+
+
+@pytest.mark.parametrize("u", [0, 1, 2])
+def test_tacotron2_single_utterance_matches_reference(taco_sig, u):
+    fx = taco_sig
+    r = 2
+    cfg, sd = taco_state_dict(fx, r=r)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(r)
+    m.decoder.max_decoder_steps = int(fx[f"r{r}_max_steps"])
+    ids = fx[f"r{r}_u{u}_ids"]
+    dec, post, align, stop = m.inference(torch.from_numpy(ids[None]).cuda())
+    S = len(fx[f"r{r}_u{u}_stop"])
+    assert dec.shape == (1, S * r, 80) and align.shape == (1, S, len(ids)) and stop.shape == (1, S, 1)
+    k = f"r{r}_u{u}"
+    assert np.abs(dec[0].cpu().numpy() - fx[k + "_dec"]).max() <= MEL_TOL
+    assert np.abs(post[0].cpu().numpy() - fx[k + "_post"]).max() <= MEL_TOL
+
+
+def test_tacotron2_softmax_matches_reference():
+    _dev()
+    fx = load_fixture("taco_softmax")
+    r = 2
+    cfg, sd = taco_state_dict(fx, r=r)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(r)
+    m.decoder.max_decoder_steps = int(fx[f"r{r}_max_steps"])
+    ids = [fx[f"r{r}_u{i}_ids"] for i in range(2)]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((2, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=[len(x) for x in ids])
+    _check_taco(fx, r, dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy(), stop.cpu().numpy(),
+                m.last_steps, range(2))
+
+
+def test_tacotron2_random_batch_vs_oracle():
+    """Seeded xavier-scale model, 6 ragged utterances, forced length (stop bias -1e4)."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=11, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    r = 2
+    m.decoder.set_r(r)
+    rs = np.random.RandomState(4)
+    lens = [17, 5, 40, 1, 29, 12]
+    steps = [9, 14, 6, 3, 11, 7]
+    T = max(lens)
+    batch = np.zeros((len(lens), T), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, L)
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=lens, max_decoder_steps=steps)
+    assert list(m.last_steps) == steps
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    dec, post, align = dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy()
+    for i, L in enumerate(lens):
+        d, p, a, s = orc.inference(batch[i, :L], r, steps[i])
+        M = steps[i] * r
+        assert np.abs(dec[i, :M] - d).max() <= MEL_TOL
+        assert np.abs(post[i, :M] - p).max() <= MEL_TOL
+        assert np.abs(align[i, :steps[i], :L] - a).max() <= 1e-5
+        assert not align[i, :, L:].any()
+
+
+def test_tacotron2_deterministic():
+    _dev()
+    fx = load_fixture("taco_sigmoid")
+    cfg, sd = taco_state_dict(fx, r=2)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(2)
+    m.decoder.max_decoder_steps = 30
+    ids = torch.from_numpy(fx["r2_u2_ids"][None]).cuda()
+    a = [t.cpu().numpy() for t in m.inference(ids)]
+    b = [t.cpu().numpy() for t in m.inference(ids)]
+    for x, y in zip(a, b):
+        assert np.array_equal(x, y)
+
+
+def test_tacotron2_edge_single_token_single_step():
+    _dev()
+    fx = load_fixture("taco_sigmoid")
+    cfg, sd = taco_state_dict(fx, r=2)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(2)
+    m.decoder.max_decoder_steps = 1
+    dec, post, align, stop = m.inference(torch.tensor([[7]], device="cuda"))
+    assert dec.shape == (1, 2, 80) and align.shape == (1, 1, 1)
+    assert abs(float(align[0, 0, 0]) - 1.0) < 1e-6
+    assert list(m.last_status) == [2]
+
+
+def test_postnet_vs_oracle():
+    from oracle.taco_np import TacoOracle
+    from tts_amd._lib import get_engine
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=5, overrides={}, stop_bias=0.0, cfg=cfg)
+    m = build_taco(cfg, sd)
+    eng = get_engine("cuda:0")
+    m._sync(eng)
+    rs = np.random.RandomState(9)
+    lens = [33, 8, 61]
+    M = max(lens)
+    dec = np.zeros((3, M, 80), np.float32)
+    for i, L in enumerate(lens):
+        dec[i, :L] = rs.normal(0, 1, (L, 80))
+    out = torch.empty(3, M, 80, device="cuda")
+    eng.taco_postnet(torch.from_numpy(dec).cuda(), lens, out)
+    out = out.cpu().numpy()
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for i, L in enumerate(lens):
+        assert np.abs(out[i, :L] - orc.postnet(dec[i, :L])).max() <= 1e-4
+        assert not out[i, L:].any()

@@ -1,0 +1,185 @@
+"""ctypes binding of ``libttship.so`` (the C ABI in ``include/ttship.h``).
+
+The library is built in-tree (``tts_amd/libttship.so``, see ``tts_amd/csrc/Makefile`` and
+``__graft_entry__.build``). There is no CPU fallback: if the library or a ROCm device is
+missing, every entry point raises ``RuntimeError``.
+"""
+
+import ctypes
+import os
+import threading
+from typing import Dict
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.environ.get("TTSHIP_LIB", os.path.join(_HERE, "libttship.so"))
+
+_lib = None
+_lock = threading.Lock()
+
+_c_int_p = ctypes.POINTER(ctypes.c_int32)
+_c_i64_p = ctypes.POINTER(ctypes.c_int64)
+_c_f_p = ctypes.POINTER(ctypes.c_float)
+_vp = ctypes.c_void_p
+
+# (name, restype, argtypes) for every symbol declared in include/ttship.h
+SIGNATURES = [
+    ("tts_version", ctypes.c_int, []),
+    ("tts_last_error", ctypes.c_char_p, []),
+    ("tts_ctx_create", ctypes.c_int, [ctypes.c_int, ctypes.POINTER(_vp)]),
+    ("tts_ctx_destroy", ctypes.c_int, [_vp]),
+    ("tts_taco_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
+    ("tts_taco_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("tts_taco_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p,
+                                      ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _c_int_p, _c_int_p, _vp]),
+    ("tts_taco_encoder", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    ("tts_taco_postnet", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    ("tts_melgan_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
+    ("tts_melgan_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_int,
+                                           ctypes.c_int, ctypes.c_int]),
+    ("tts_melgan_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    ("tts_melgan_generator", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
+                                            _vp]),
+    ("tts_pqmf_synthesis", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int,
+                                          _vp, _vp]),
+    ("tts_time_decoder_kernel", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_f_p]),
+]
+
+
+def load_library():
+    """Load and type the shared library (no GPU calls are made here)."""
+    global _lib
+    with _lock:
+        if _lib is None:
+            if not os.path.exists(LIB_PATH):
+                raise RuntimeError(f"libttship.so not found at {LIB_PATH}; run __graft_entry__.build() "
+                                   f"(make -C tts_amd/csrc)")
+            lib = ctypes.CDLL(LIB_PATH)
+            for name, res, args in SIGNATURES:
+                fn = getattr(lib, name)
+                fn.restype = res
+                fn.argtypes = args
+            _lib = lib
+    return _lib
+
+
+def _check(rc: int):
+    if rc != 0:
+        msg = load_library().tts_last_error()
+        raise RuntimeError("ttship: " + (msg.decode() if msg else "unknown error"))
+
+
+def _i32(a):
+    arr = np.ascontiguousarray(np.asarray(a, dtype=np.int32))
+    return arr, arr.ctypes.data_as(_c_int_p)
+
+
+def _ptr(t):
+    return ctypes.c_void_p(t.data_ptr())
+
+
+def _stream(device):
+    import torch
+    return ctypes.c_void_p(torch.cuda.current_stream(device).cuda_stream)
+
+
+class Engine:
+    """One library context per device (owns packed weights, workspace, captured graphs)."""
+
+    def __init__(self, device_index: int):
+        self.lib = load_library()
+        self.device = device_index
+        h = ctypes.c_void_p()
+        _check(self.lib.tts_ctx_create(device_index, ctypes.byref(h)))
+        self.h = h
+        self.taco_key = None
+        self.melgan_key = None
+
+    def close(self):
+        if self.h:
+            self.lib.tts_ctx_destroy(self.h)
+            self.h = None
+
+    # -- weights ---------------------------------------------------------------------
+    def _set(self, fn, name, arr):
+        a = np.ascontiguousarray(arr, dtype=np.float32)
+        shape = (ctypes.c_int64 * max(1, a.ndim))(*a.shape)
+        _check(fn(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), shape, a.ndim))
+
+    def load_tacotron(self, tensors: Dict[str, np.ndarray], num_chars: int, r_init: int, attn_norm: str):
+        for k, v in tensors.items():
+            self._set(self.lib.tts_taco_set_tensor, k, v)
+        _check(self.lib.tts_taco_finalize(self.h, num_chars, r_init, 1 if attn_norm == "softmax" else 0))
+
+    def load_melgan(self, tensors: Dict[str, np.ndarray], in_channels, out_channels, base_channels,
+                    upsample_factors, num_res_blocks, use_pqmf):
+        for k, v in tensors.items():
+            self._set(self.lib.tts_melgan_set_tensor, k, v)
+        ups, ups_p = _i32(list(upsample_factors))
+        _check(self.lib.tts_melgan_finalize(self.h, in_channels, out_channels, base_channels, ups_p, len(ups),
+                                            num_res_blocks, 1 if use_pqmf else 0))
+
+    # -- compute (device tensors) ----------------------------------------------------
+    def taco_infer(self, ids, lens, r, max_steps, S_cap, stop_threshold, dec, post, align, stop):
+        B, T = ids.shape
+        lens_a, lens_p = _i32(lens)
+        ms_a, ms_p = _i32(max_steps)
+        steps = np.zeros(B, np.int32)
+        status = np.zeros(B, np.int32)
+        _check(self.lib.tts_taco_infer(self.h, _ptr(ids), lens_p, B, T, r, ms_p, S_cap, float(stop_threshold),
+                                       _ptr(dec), _ptr(post), _ptr(align), _ptr(stop),
+                                       steps.ctypes.data_as(_c_int_p), status.ctypes.data_as(_c_int_p),
+                                       _stream(ids.device)))
+        return steps, status
+
+    def taco_encoder(self, ids, lens, out):
+        B, T = ids.shape
+        lens_a, lens_p = _i32(lens)
+        _check(self.lib.tts_taco_encoder(self.h, _ptr(ids), lens_p, B, T, _ptr(out), _stream(ids.device)))
+
+    def taco_postnet(self, dec, lens, out):
+        B, M, _ = dec.shape
+        lens_a, lens_p = _i32(lens)
+        _check(self.lib.tts_taco_postnet(self.h, _ptr(dec), lens_p, B, M, _ptr(out), _stream(dec.device)))
+
+    def melgan_infer(self, mel, lens, pad, wav):
+        B, _, M = mel.shape
+        lens_a, lens_p = _i32(lens)
+        _check(self.lib.tts_melgan_infer(self.h, _ptr(mel), lens_p, B, M, pad, _ptr(wav), _stream(mel.device)))
+
+    def melgan_generator(self, mel, lens, pad, out):
+        B, _, M = mel.shape
+        lens_a, lens_p = _i32(lens)
+        _check(self.lib.tts_melgan_generator(self.h, _ptr(mel), lens_p, B, M, pad, _ptr(out),
+                                             _stream(mel.device)))
+
+    def pqmf_synthesis(self, x, G, y):
+        B, N, L = x.shape
+        taps = G.shape[-1] - 1
+        _check(self.lib.tts_pqmf_synthesis(self.h, _ptr(x), B, N, L, _ptr(G), taps, _ptr(y), _stream(x.device)))
+
+    def time_decoder_kernel(self, which: int, iters: int) -> float:
+        ms = ctypes.c_float(0.0)
+        _check(self.lib.tts_time_decoder_kernel(self.h, which, iters, ctypes.byref(ms)))
+        return float(ms.value)
+
+
+_engines: Dict[int, Engine] = {}
+
+
+def get_engine(device) -> Engine:
+    """Engine for a torch device (must be a ROCm 'cuda' device)."""
+    import torch
+    dev = torch.device(device)
+    if dev.type != "cuda":
+        raise RuntimeError("tts_amd runs on MI355X (ROCm 'cuda' devices) only; got device "
+                           f"'{dev}'. There is no CPU fallback: move the model with .cuda().")
+    idx = dev.index if dev.index is not None else torch.cuda.current_device()
+    with _lock:
+        eng = _engines.get(idx)
+    if eng is None:
+        eng = Engine(idx)
+        with _lock:
+            _engines[idx] = eng
+    return eng

@@ -1,0 +1,1282 @@
+// C-ABI of the ttship library: context, weight folding / packing, workspace, the
+// graph-captured autoregressive decode loop, and the vocoder pipeline.
+#include "common.h"
+#include "decoder.h"
+#include "../../include/ttship.h"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <map>
+#include <memory>
+#include <stdexcept>
+#include <string>
+#include <vector>
+
+void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int num_rows, int D,
+                         const int* lens, int B, float* out, hipStream_t s);
+void launch_bilstm_rec(const float* Gin, const float* WhhT, const int* lens, int T_max, int B, float* out,
+                       hipStream_t s);
+
+static thread_local std::string g_err;
+void tts_set_error(const std::string& m) { g_err = m; }
+
+namespace {
+
+constexpr int CHUNK = 8;  // decoder steps per captured graph (even: parity of t == parity of j)
+constexpr int BMAX = 64;  // utterances per call (Bp <= 64)
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  DevBuf(DevBuf&& o) noexcept : p(o.p), bytes(o.bytes) { o.p = nullptr; o.bytes = 0; }
+  ~DevBuf() {
+    if (p) (void)hipFree(p);
+  }
+  // grow-only; returns true when the address changed
+  bool ensure(size_t n) {
+    if (n <= bytes && p) return false;
+    if (p) HIP_OK(hipFree(p));
+    p = nullptr;
+    HIP_OK(hipMalloc(&p, std::max<size_t>(n, 256)));
+    bytes = std::max<size_t>(n, 256);
+    return true;
+  }
+  template <class T>
+  void upload(const std::vector<T>& v) {
+    ensure(v.size() * sizeof(T));
+    HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
+  }
+  float* f() const { return static_cast<float*>(p); }
+  int* i() const { return static_cast<int*>(p); }
+};
+
+struct HostT {
+  std::vector<float> d;
+  std::vector<int64_t> shape;
+};
+using HostMap = std::map<std::string, HostT>;
+
+const HostT& need(const HostMap& m, const std::string& k, std::vector<int64_t> shape) {
+  auto it = m.find(k);
+  TTS_CHECK(it != m.end(), "missing tensor: " + k);
+  if (!shape.empty()) {
+    bool ok = it->second.shape == shape;
+    if (!ok) {
+      std::string s = "shape mismatch for " + k + ": got (";
+      for (auto x : it->second.shape) s += std::to_string(x) + ",";
+      s += ") expected (";
+      for (auto x : shape) s += std::to_string(x) + ",";
+      throw std::runtime_error(s + ")");
+    }
+  }
+  return it->second;
+}
+
+struct ConvLayer {
+  DevBuf W, bias;
+  int Cin = 0, Cout = 0, Cout_pad = 0, K = 1, dil = 1, tile = 0, nphase = 1;
+  int pad_left[8] = {0};
+  long phase_stride = 0;
+};
+
+// Wm: nphase blocks of [Cout][Cin*K] row-major
+void pack_conv(ConvLayer& L, const std::vector<float>& Wm, const std::vector<float>& bias, int Cin, int Cout,
+               int K, int dil, int nphase, const int* pad_left) {
+  TTS_CHECK(Cin % 16 == 0, "conv Cin must be a multiple of 16");
+  L.Cin = Cin;
+  L.Cout = Cout;
+  L.K = K;
+  L.dil = dil;
+  L.nphase = nphase;
+  L.tile = conv_tile_for_cout(Cout);
+  const int TC = conv_tile_tc(L.tile);
+  L.Cout_pad = (Cout + TC - 1) / TC * TC;
+  const int Kdim = Cin * K;
+  const size_t per = (size_t)L.Cout_pad * Kdim;
+  std::vector<float> sw(per * nphase);
+  for (int ph = 0; ph < nphase; ++ph)
+    swizzle_rows16(Wm.data() + (size_t)ph * Cout * Kdim, Cout, L.Cout_pad, Kdim, sw.data() + ph * per);
+  L.phase_stride = (long)per;
+  L.W.upload(sw);
+  L.bias.upload(bias);
+  for (int ph = 0; ph < nphase; ++ph) L.pad_left[ph] = pad_left[ph];
+}
+
+struct ConvCall {
+  ConvSrc s[2];
+  int nsrc = 1;
+  int pad_mode = 0;
+  const int* lens = nullptr;
+  int len_add = 0, in_mul = 1, q_mul = 1, rep_pad = 0, out_mul = 1;
+  float* out = nullptr;
+  long ob = 0;
+  int oc = 0, ot = 0;
+  int epi = 0;
+  const float* resid = nullptr;
+  long rb = 0;
+  int rc = 0, rt = 0;
+  int max_q = 0, B = 0;
+};
+
+void run_conv(const ConvLayer& L, const ConvCall& c, hipStream_t st) {
+  ConvArgs a{};
+  a.src[0] = c.s[0];
+  a.src[1] = c.nsrc > 1 ? c.s[1] : c.s[0];
+  if (c.nsrc == 1) a.src[0].C = L.Cin;
+  a.nsrc = c.nsrc;
+  a.Cin = L.Cin;
+  a.K = L.K;
+  a.dil = L.dil;
+  a.pad_mode = c.pad_mode;
+  a.lens = c.lens;
+  a.len_add = c.len_add;
+  a.in_mul = c.in_mul;
+  a.q_mul = c.q_mul;
+  a.rep_pad = c.rep_pad;
+  a.nphase = L.nphase;
+  for (int i = 0; i < 8; ++i) a.pad_left[i] = L.pad_left[i];
+  a.w_phase_stride = L.phase_stride;
+  a.W = L.W.f();
+  a.bias = L.bias.f();
+  a.Cout = L.Cout;
+  a.Cout_pad = L.Cout_pad;
+  a.out = c.out;
+  a.ob = c.ob;
+  a.oc = c.oc;
+  a.ot = c.ot;
+  a.out_mul = c.out_mul;
+  a.epi_act = c.epi;
+  a.resid = c.resid;
+  a.rb = c.rb;
+  a.rc = c.rc;
+  a.rt = c.rt;
+  a.max_q = c.max_q;
+  a.B = c.B;
+  launch_conv(a, L.tile, st);
+}
+
+ConvSrc src_of(const float* p, long sb, int sc, int st, int C, int act) {
+  ConvSrc s;
+  s.ptr = p;
+  s.sb = sb;
+  s.sc = sc;
+  s.st = st;
+  s.C = C;
+  s.act = act;
+  return s;
+}
+
+// ---------------------------------------------------------------- Tacotron2 -----------
+struct TacoModel {
+  bool ready = false;
+  int num_chars = 0, r_init = 7, softmax = 0;
+  DevBuf emb;
+  ConvLayer enc[3], lstm_in, penc, post[5];
+  DevBuf whhT;
+  DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b, stop_w;
+  float bv = 0.f, stop_b = 0.f;
+};
+
+struct TacoWS {
+  int B = 0, T_max = 0, S_cap = 0, r = 0, MT = 0;
+  long gen = 0;
+  DevBuf lens, mlens, x0, ca, cb, gin, enc, penc;
+  DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, alpha, acum, energy, ctl;
+  DevBuf dec, align, stop, pa, pbb;
+  hipGraphExec_t graph = nullptr;
+  long graph_gen = -1;
+  int gB = -1, gT = -1, gS = -1, gr = -1;
+  float thr = 0.5f, gthr = -1.f;
+};
+
+struct MelganModel {
+  bool ready = false;
+  int in_ch = 80, out_ch = 4, base = 384, nres = 4, pqmf = 1, taps = 62;
+  std::vector<int> ups;
+  ConvLayer conv_in, conv_out;
+  std::vector<ConvLayer> convT;
+  std::vector<ConvLayer> dconv, fused;  // [stage*nres + block]
+  DevBuf G;
+};
+
+struct MelganWS {
+  DevBuf lens, xa, xb, h, bands;
+};
+
+}  // namespace
+
+struct tts_ctx {
+  int device = 0;
+  hipStream_t s = nullptr;
+  hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_chunk[2] = {nullptr, nullptr};
+  int* pinned = nullptr;  // [4]
+  HostMap taco_host, mg_host;
+  TacoModel taco;
+  TacoWS tws;
+  MelganModel mg;
+  MelganWS mws;
+  // last decode configuration (for tts_time_decoder_kernel)
+  int last_B = 0, last_T = 0, last_S = 0, last_r = 0;
+};
+
+namespace {
+
+struct DeviceGuard {
+  int prev = -1;
+  explicit DeviceGuard(int d) {
+    HIP_OK(hipGetDevice(&prev));
+    if (prev != d) HIP_OK(hipSetDevice(d));
+  }
+  ~DeviceGuard() {
+    if (prev >= 0) (void)hipSetDevice(prev);
+  }
+};
+
+// stream ordering with the caller's stream
+void enter(tts_ctx* c, void* stream) {
+  HIP_OK(hipEventRecord(c->ev_in, (hipStream_t)stream));
+  HIP_OK(hipStreamWaitEvent(c->s, c->ev_in, 0));
+}
+void leave(tts_ctx* c, void* stream) {
+  HIP_OK(hipEventRecord(c->ev_out, c->s));
+  HIP_OK(hipStreamWaitEvent((hipStream_t)stream, c->ev_out, 0));
+}
+
+std::vector<float> lstm_tile_rows(const std::vector<float>& W, int H, int K) {
+  std::vector<float> out((size_t)4 * H * K);
+  for (int t = 0; t < H / 4; ++t)
+    for (int g = 0; g < 4; ++g)
+      for (int u = 0; u < 4; ++u) {
+        const size_t src = (size_t)(g * H + 4 * t + u) * K, dst = (size_t)(t * 16 + g * 4 + u) * K;
+        std::memcpy(&out[dst], &W[src], K * sizeof(float));
+      }
+  return out;
+}
+
+// concatenate column blocks of matrices with equal row counts
+std::vector<float> hcat(const std::vector<std::pair<const float*, int>>& parts, int rows, int ld_src_first = 0) {
+  (void)ld_src_first;
+  int K = 0;
+  for (auto& p : parts) K += p.second;
+  std::vector<float> out((size_t)rows * K);
+  for (int r = 0; r < rows; ++r) {
+    int off = 0;
+    for (auto& p : parts) {
+      std::memcpy(&out[(size_t)r * K + off], p.first + (size_t)r * p.second, p.second * sizeof(float));
+      off += p.second;
+    }
+  }
+  return out;
+}
+
+std::vector<float> slice_cols(const std::vector<float>& W, int rows, int K, int c0, int c1) {
+  std::vector<float> out((size_t)rows * (c1 - c0));
+  for (int r = 0; r < rows; ++r)
+    std::memcpy(&out[(size_t)r * (c1 - c0)], &W[(size_t)r * K + c0], (c1 - c0) * sizeof(float));
+  return out;
+}
+
+std::vector<float> swz(const std::vector<float>& Wm, int rows, int K) {
+  const int rp = (rows + 15) / 16 * 16;
+  std::vector<float> out((size_t)rp * K);
+  swizzle_rows16(Wm.data(), rows, rp, K, out.data());
+  return out;
+}
+
+void fold_convbn(const HostMap& m, const std::string& pfx, int Cin, int Cout, int K, std::vector<float>& Wm,
+                 std::vector<float>& bias) {
+  const auto& W = need(m, pfx + ".convolution1d.weight", {Cout, Cin, K}).d;
+  const auto& b = need(m, pfx + ".convolution1d.bias", {Cout}).d;
+  const auto& g = need(m, pfx + ".batch_normalization.weight", {Cout}).d;
+  const auto& be = need(m, pfx + ".batch_normalization.bias", {Cout}).d;
+  const auto& mu = need(m, pfx + ".batch_normalization.running_mean", {Cout}).d;
+  const auto& var = need(m, pfx + ".batch_normalization.running_var", {Cout}).d;
+  Wm.resize((size_t)Cout * Cin * K);
+  bias.resize(Cout);
+  for (int co = 0; co < Cout; ++co) {
+    const double sc = (double)g[co] / std::sqrt((double)var[co] + 1e-5);
+    for (int i = 0; i < Cin * K; ++i) Wm[(size_t)co * Cin * K + i] = (float)(W[(size_t)co * Cin * K + i] * sc);
+    bias[co] = (float)(((double)b[co] - mu[co]) * sc + be[co]);
+  }
+}
+
+void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
+  auto& M = c->taco;
+  const auto& h = c->taco_host;
+  M.ready = false;
+  M.num_chars = num_chars;
+  M.r_init = r_init;
+  M.softmax = attn_norm;
+  const int E = 512, H = 256, Q = 1024, D = 1024, P = 256, A = 128, F = 80;
+  M.emb.upload(need(h, "embedding.weight", {num_chars, E}).d);
+  int pl2[8] = {2}, pl0[8] = {0};
+  for (int i = 0; i < 3; ++i) {
+    std::vector<float> Wm, b;
+    fold_convbn(h, "encoder.convolutions." + std::to_string(i), E, E, 5, Wm, b);
+    pack_conv(M.enc[i], Wm, b, E, E, 5, 1, 1, pl2);
+  }
+  {  // BiLSTM input projection for both directions as one K=1 conv (Cout 2048), b_ih + b_hh folded
+    std::vector<float> Wm((size_t)2048 * E), b(2048);
+    std::vector<float> whhT((size_t)2 * 4 * 64 * 256 * 4);
+    for (int dir = 0; dir < 2; ++dir) {
+      const std::string sfx = dir ? "_reverse" : "";
+      const auto& wih = need(h, "encoder.lstm.weight_ih_l0" + sfx, {4 * H, E}).d;
+      const auto& whh = need(h, "encoder.lstm.weight_hh_l0" + sfx, {4 * H, H}).d;
+      const auto& bih = need(h, "encoder.lstm.bias_ih_l0" + sfx, {4 * H}).d;
+      const auto& bhh = need(h, "encoder.lstm.bias_hh_l0" + sfx, {4 * H}).d;
+      std::memcpy(&Wm[(size_t)dir * 1024 * E], wih.data(), (size_t)1024 * E * 4);
+      for (int i = 0; i < 1024; ++i) b[dir * 1024 + i] = bih[i] + bhh[i];
+      for (int g = 0; g < 4; ++g)
+        for (int k4 = 0; k4 < 64; ++k4)
+          for (int j = 0; j < 256; ++j)
+            for (int e = 0; e < 4; ++e)
+              whhT[((((size_t)dir * 4 + g) * 64 + k4) * 256 + j) * 4 + e] = whh[(size_t)(g * 256 + j) * H + 4 * k4 + e];
+    }
+    pack_conv(M.lstm_in, Wm, b, E, 2048, 1, 1, 1, pl0);
+    M.whhT.upload(whhT);
+  }
+  {  // processed_inputs = inputs_layer(enc)  (common_layers.py:262-263), K=1 conv, no bias
+    const auto& win = need(h, "decoder.attention.inputs_layer.linear_layer.weight", {A, E}).d;
+    pack_conv(M.penc, win, std::vector<float>(A, 0.f), E, A, 1, 1, 1, pl0);
+  }
+  M.pre1.upload(swz(need(h, "decoder.prenet.linear_layers.0.linear_layer.weight", {P, F}).d, P, F));
+  M.pre2.upload(swz(need(h, "decoder.prenet.linear_layers.1.linear_layer.weight", {P, P}).d, P, P));
+  {
+    const auto& wih = need(h, "decoder.attention_rnn.weight_ih", {4 * Q, P + E}).d;
+    const auto& whh = need(h, "decoder.attention_rnn.weight_hh", {4 * Q, Q}).d;
+    const auto& bih = need(h, "decoder.attention_rnn.bias_ih", {4 * Q}).d;
+    const auto& bhh = need(h, "decoder.attention_rnn.bias_hh", {4 * Q}).d;
+    auto wp = slice_cols(wih, 4 * Q, P + E, 0, P);
+    auto wc = slice_cols(wih, 4 * Q, P + E, P, P + E);
+    M.att_p.upload(swz(lstm_tile_rows(wp, Q, P), 4 * Q, P));
+    auto pre = hcat({{wc.data(), E}, {whh.data(), Q}}, 4 * Q);
+    M.att_pre.upload(swz(lstm_tile_rows(pre, Q, E + Q), 4 * Q, E + Q));
+    std::vector<float> bsum(4 * Q);
+    for (int i = 0; i < 4 * Q; ++i) bsum[i] = bih[i] + bhh[i];
+    M.att_bias.upload(lstm_tile_rows(bsum, Q, 1));
+  }
+  {
+    const auto& wq = need(h, "decoder.attention.query_layer.linear_layer.weight", {A, Q}).d;
+    std::vector<float> t((size_t)Q * A);
+    for (int a = 0; a < A; ++a)
+      for (int k = 0; k < Q; ++k) t[(size_t)k * A + a] = wq[(size_t)a * Q + k];
+    M.WqT.upload(t);
+    M.Wloc.upload(need(h, "decoder.attention.location_layer.location_conv1d.weight", {32, 2, 31}).d);
+    M.Wdense.upload(need(h, "decoder.attention.location_layer.location_dense.linear_layer.weight", {A, 32}).d);
+    M.v.upload(need(h, "decoder.attention.v.linear_layer.weight", {1, A}).d);
+    M.bv = need(h, "decoder.attention.v.linear_layer.bias", {1}).d[0];
+  }
+  {
+    const auto& wih = need(h, "decoder.decoder_rnn.weight_ih", {4 * D, Q + E}).d;
+    const auto& whh = need(h, "decoder.decoder_rnn.weight_hh", {4 * D, D}).d;
+    const auto& bih = need(h, "decoder.decoder_rnn.bias_ih", {4 * D}).d;
+    const auto& bhh = need(h, "decoder.decoder_rnn.bias_hh", {4 * D}).d;
+    auto w = hcat({{wih.data(), Q + E}, {whh.data(), D}}, 4 * D);
+    M.dec_w.upload(swz(lstm_tile_rows(w, D, Q + E + D), 4 * D, Q + E + D));
+    std::vector<float> bsum(4 * D);
+    for (int i = 0; i < 4 * D; ++i) bsum[i] = bih[i] + bhh[i];
+    M.dec_bias.upload(lstm_tile_rows(bsum, D, 1));
+  }
+  {
+    const int NP = F * r_init;
+    M.proj_w.upload(swz(need(h, "decoder.linear_projection.linear_layer.weight", {NP, D + E}).d, NP, D + E));
+    M.proj_b.upload(need(h, "decoder.linear_projection.linear_layer.bias", {NP}).d);
+    M.stop_w.upload(need(h, "decoder.stopnet.1.linear_layer.weight", {1, D + NP}).d);
+    M.stop_b = need(h, "decoder.stopnet.1.linear_layer.bias", {1}).d[0];
+  }
+  const int pc[6] = {F, 512, 512, 512, 512, F};
+  for (int i = 0; i < 5; ++i) {
+    std::vector<float> Wm, b;
+    fold_convbn(h, "postnet.convolutions." + std::to_string(i), pc[i], pc[i + 1], 5, Wm, b);
+    pack_conv(M.post[i], Wm, b, pc[i], pc[i + 1], 5, 1, 1, pl2);
+  }
+  HIP_OK(hipDeviceSynchronize());
+  M.ready = true;
+  c->tws.gen++;  // weights moved: captured graphs are stale
+}
+
+template <class T>
+bool grow(DevBuf& b, size_t n, long& gen) {
+  if (b.ensure(n * sizeof(T))) {
+    gen++;
+    return true;
+  }
+  return false;
+}
+
+void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
+  auto& W = c->tws;
+  const int Bp = 16 * ((B + 15) / 16);
+  long& g = W.gen;
+  grow<int>(W.lens, BMAX, g);
+  grow<int>(W.mlens, BMAX, g);
+  grow<float>(W.x0, (size_t)B * T_max * 512, g);
+  grow<float>(W.ca, (size_t)B * T_max * 512, g);
+  grow<float>(W.cb, (size_t)B * T_max * 512, g);
+  grow<float>(W.gin, (size_t)B * T_max * 2048, g);
+  grow<float>(W.enc, (size_t)B * T_max * 512, g);
+  grow<float>(W.penc, (size_t)B * T_max * 128, g);
+  grow<float>(W.p1, (size_t)Bp * 256, g);
+  grow<float>(W.pb, (size_t)Bp * 256, g);
+  grow<float>(W.gatt, (size_t)Bp * 4096, g);
+  grow<float>(W.hatt, (size_t)Bp * 1024, g);
+  grow<float>(W.catt, (size_t)Bp * 1024, g);
+  grow<float>(W.hdec0, (size_t)Bp * 1024, g);
+  grow<float>(W.hdec1, (size_t)Bp * 1024, g);
+  grow<float>(W.cdec, (size_t)Bp * 1024, g);
+  grow<float>(W.ctx, (size_t)Bp * 512, g);
+  grow<float>(W.y, (size_t)Bp * 80 * c->taco.r_init, g);
+  grow<float>(W.pq, (size_t)64 * Bp * 128, g);
+  grow<float>(W.alpha, (size_t)B * T_max, g);
+  grow<float>(W.acum, (size_t)B * T_max, g);
+  grow<float>(W.energy, (size_t)B * T_max, g);
+  grow<int>(W.ctl, 4 + 4 * BMAX, g);
+  grow<float>(W.dec, (size_t)B * S_cap * r * 80, g);
+  grow<float>(W.align, (size_t)B * S_cap * T_max, g);
+  grow<float>(W.stop, (size_t)B * S_cap, g);
+  grow<float>(W.pa, (size_t)B * 512 * S_cap * r, g);
+  grow<float>(W.pbb, (size_t)B * 512 * S_cap * r, g);
+  W.B = B;
+  W.T_max = T_max;
+  W.S_cap = S_cap;
+  W.r = r;
+  W.MT = Bp / 16;
+}
+
+DecDev make_dev(tts_ctx* c) {
+  auto& W = c->tws;
+  DecDev d{};
+  int* ci = W.ctl.i();
+  d.ctl = reinterpret_cast<DecCtl*>(ci);
+  d.done = ci + 4;
+  d.steps = ci + 4 + BMAX;
+  d.status = ci + 4 + 2 * BMAX;
+  d.max_steps = ci + 4 + 3 * BMAX;
+  d.lens = W.lens.i();
+  d.dec_out = W.dec.f();
+  d.align_out = W.align.f();
+  d.stop_out = W.stop.f();
+  d.S_cap = W.S_cap;
+  d.T_max = W.T_max;
+  d.B = W.B;
+  return d;
+}
+
+SkSeg seg(const float* p, int ld, int K) {
+  SkSeg s;
+  s.ptr = p;
+  s.ld = ld;
+  s.K = K;
+  return s;
+}
+
+SkJob job0() {
+  SkJob j;
+  std::memset(&j, 0, sizeof(j));
+  return j;
+}
+
+// the 7 launches of decoder step j of a chunk (parity j & 1 selects the h_dec buffer)
+void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
+  auto& M = c->taco;
+  auto& W = c->tws;
+  const DecDev d = make_dev(c);
+  const int r = W.r, MT = W.MT, YLD = 80 * M.r_init;
+  float* hd_cur = (j & 1) ? W.hdec1.f() : W.hdec0.f();
+  float* hd_nxt = (j & 1) ? W.hdec0.f() : W.hdec1.f();
+  if (which_only < 0 || which_only == 1) {
+    SkArgs a{};
+    a.njobs = 1;
+    a.MT = MT;
+    SkJob& J = a.job[0] = job0();
+    J.seg[0] = seg(W.y.f() + 80 * (r - 1), YLD, 80);
+    J.nseg = 1;
+    J.K = 80;
+    J.W = M.pre1.f();
+    J.ntiles = 16;
+    J.epi = EPI_STORE;
+    J.act = 1;
+    J.out = W.p1.f();
+    J.out_ld = 256;
+    StopArgs st{};
+    st.ws = M.stop_w.f();
+    st.bs = M.stop_b;
+    st.hdec = hd_cur;
+    st.y = W.y.f();
+    st.y_ld = YLD;
+    st.ny = YLD;
+    st.threshold = W.thr;
+    launch_prenet1_stop(a, d, st, j, s);
+  }
+  if (which_only < 0 || which_only == 2) {
+    SkArgs a{};
+    a.njobs = 1;
+    a.MT = MT;
+    SkJob& J = a.job[0] = job0();
+    J.seg[0] = seg(W.p1.f(), 256, 256);
+    J.nseg = 1;
+    J.K = 256;
+    J.W = M.pre2.f();
+    J.ntiles = 16;
+    J.epi = EPI_STORE;
+    J.act = 1;
+    J.out = W.pb.f();
+    J.out_ld = 256;
+    launch_skinny(a, d, j, 1, 4, s);
+  }
+  if (which_only < 0 || which_only == 3) {
+    SkArgs a{};
+    a.njobs = 1;
+    a.MT = MT;
+    SkJob& J = a.job[0] = job0();
+    J.seg[0] = seg(W.pb.f(), 256, 256);
+    J.nseg = 1;
+    J.K = 256;
+    J.W = M.att_p.f();
+    J.ntiles = 256;
+    J.epi = EPI_LSTM;
+    J.addin = W.gatt.f();
+    J.addin_ld = 4096;
+    J.h_out = W.hatt.f();
+    J.c_state = W.catt.f();
+    J.hc_ld = 1024;
+    J.WqT = M.WqT.f();
+    J.pq_part = W.pq.f();
+    launch_skinny(a, d, j, 4, 4, s);
+  }
+  if (which_only < 0 || which_only == 4) {
+    AttnArgs p{};
+    p.pq_part = W.pq.f();
+    p.npq = 64;
+    p.Bp = MT * 16;
+    p.alpha = W.alpha.f();
+    p.alpha_cum = W.acum.f();
+    p.Wloc = M.Wloc.f();
+    p.Wdense = M.Wdense.f();
+    p.v = M.v.f();
+    p.bv = M.bv;
+    p.penc = W.penc.f();
+    p.energy = W.energy.f();
+    p.enc = W.enc.f();
+    p.ctx = W.ctx.f();
+    p.softmax = M.softmax;
+    launch_attention(p, d, j, s);
+  }
+  if (which_only < 0 || which_only == 0) {
+    SkArgs a{};
+    a.njobs = 2;
+    a.MT = MT;
+    SkJob& J = a.job[0] = job0();  // decoder_rnn LSTMCell
+    J.seg[0] = seg(W.hatt.f(), 1024, 1024);
+    J.seg[1] = seg(W.ctx.f(), 512, 512);
+    J.seg[2] = seg(hd_cur, 1024, 1024);
+    J.nseg = 3;
+    J.K = 2560;
+    J.W = M.dec_w.f();
+    J.ntiles = 256;
+    J.epi = EPI_LSTM;
+    J.bias = M.dec_bias.f();
+    J.h_out = hd_nxt;
+    J.c_state = W.cdec.f();
+    J.hc_ld = 1024;
+    SkJob& J2 = a.job[1] = job0();  // next step's attention_rnn ctx/h part (+ biases)
+    J2.seg[0] = seg(W.ctx.f(), 512, 512);
+    J2.seg[1] = seg(W.hatt.f(), 1024, 1024);
+    J2.nseg = 2;
+    J2.K = 1536;
+    J2.W = M.att_pre.f();
+    J2.ntiles = 256;
+    J2.epi = EPI_STORE;
+    J2.bias = M.att_bias.f();
+    J2.out = W.gatt.f();
+    J2.out_ld = 4096;
+    launch_skinny(a, d, j, 1, 4, s);
+  }
+  if (which_only < 0 || which_only == 5) {
+    SkArgs a{};
+    a.njobs = 1;
+    a.MT = MT;
+    SkJob& J = a.job[0] = job0();
+    J.seg[0] = seg(hd_nxt, 1024, 1024);
+    J.seg[1] = seg(W.ctx.f(), 512, 512);
+    J.nseg = 2;
+    J.K = 1536;
+    J.W = M.proj_w.f();
+    J.ntiles = 5 * M.r_init;
+    J.epi = EPI_STORE;
+    J.bias = M.proj_b.f();
+    J.out = W.y.f();
+    J.out_ld = YLD;
+    J.frames_r = r;
+    launch_skinny(a, d, j, 1, 16, s);
+  }
+}
+
+__global__ void bcast_rows_kernel(const float* src, int n, float* dst, int rows) {
+  for (int i = blockIdx.x * blockDim.x + threadIdx.x; i < n * rows; i += gridDim.x * blockDim.x)
+    dst[i] = src[i % n];
+}
+
+void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_out, hipStream_t s) {
+  auto& M = c->taco;
+  auto& W = c->tws;
+  const int* lens = W.lens.i();
+  launch_embed_gather(ids, T_max, M.emb.f(), M.num_chars, 512, lens, B, W.x0.f(), s);
+  ConvCall cc;
+  cc.lens = lens;
+  cc.B = B;
+  cc.max_q = T_max;
+  cc.pad_mode = 0;
+  cc.epi = 1;
+  cc.s[0] = src_of(W.x0.f(), (long)T_max * 512, 1, 512, 512, 0);
+  cc.out = W.ca.f();
+  cc.ob = (long)512 * T_max;
+  cc.oc = T_max;
+  cc.ot = 1;
+  run_conv(M.enc[0], cc, s);
+  cc.s[0] = src_of(W.ca.f(), (long)512 * T_max, T_max, 1, 512, 0);
+  cc.out = W.cb.f();
+  run_conv(M.enc[1], cc, s);
+  cc.s[0] = src_of(W.cb.f(), (long)512 * T_max, T_max, 1, 512, 0);
+  cc.out = W.ca.f();
+  run_conv(M.enc[2], cc, s);
+  cc.s[0] = src_of(W.ca.f(), (long)512 * T_max, T_max, 1, 512, 0);
+  cc.out = W.gin.f();
+  cc.ob = (long)2048 * T_max;
+  cc.oc = T_max;
+  cc.ot = 1;
+  cc.epi = 0;
+  run_conv(M.lstm_in, cc, s);
+  HIP_OK(hipMemsetAsync(enc_out, 0, (size_t)B * T_max * 512 * 4, s));
+  launch_bilstm_rec(W.gin.f(), M.whhT.f(), lens, T_max, B, enc_out, s);
+}
+
+void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int B, int Mmax_alloc, int max_q,
+                 float* out, long out_b, hipStream_t s) {
+  auto& M = c->taco;
+  auto& W = c->tws;
+  ConvCall cc;
+  cc.lens = mlens;
+  cc.B = B;
+  cc.max_q = max_q;
+  cc.pad_mode = 0;
+  cc.epi = 2;
+  cc.s[0] = src_of(dec, dec_b, 1, 80, 80, 0);
+  cc.out = W.pa.f();
+  cc.ob = (long)512 * Mmax_alloc;
+  cc.oc = Mmax_alloc;
+  cc.ot = 1;
+  run_conv(M.post[0], cc, s);
+  float* bufs[2] = {W.pa.f(), W.pbb.f()};
+  for (int i = 1; i < 4; ++i) {
+    cc.s[0] = src_of(bufs[(i - 1) & 1], (long)512 * Mmax_alloc, Mmax_alloc, 1, 512, 0);
+    cc.out = bufs[i & 1];
+    run_conv(M.post[i], cc, s);
+  }
+  cc.s[0] = src_of(bufs[1], (long)512 * Mmax_alloc, Mmax_alloc, 1, 512, 0);
+  cc.out = out;
+  cc.ob = out_b;
+  cc.oc = 1;
+  cc.ot = 80;
+  cc.epi = 0;
+  cc.resid = dec;
+  cc.rb = dec_b;
+  cc.rc = 1;
+  cc.rt = 80;
+  run_conv(M.post[4], cc, s);
+}
+
+void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, int T_max, int r,
+                const int32_t* h_max_steps, int S_cap, float thr, float* d_dec, float* d_post, float* d_align,
+                float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream) {
+  auto& M = c->taco;
+  TTS_CHECK(M.ready, "tacotron2 weights not finalized");
+  TTS_CHECK(B >= 1 && B <= BMAX, "B must be in [1, 64]");
+  TTS_CHECK(T_max >= 1 && T_max <= 4096, "T_max must be in [1, 4096]");
+  TTS_CHECK(r >= 1 && r <= M.r_init, "r must be in [1, r_init]");
+  int max_ms = 0;
+  for (int b = 0; b < B; ++b) {
+    TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= T_max, "lens out of range");
+    TTS_CHECK(h_max_steps[b] >= 1, "max_decoder_steps must be >= 1");
+    max_ms = std::max(max_ms, (int)h_max_steps[b]);
+  }
+  TTS_CHECK(S_cap >= max_ms, "S_cap < max(max_steps)");
+  taco_workspace(c, B, T_max, S_cap, r);
+  auto& W = c->tws;
+  hipStream_t s = c->s;
+  enter(c, stream);
+  // control block: base = 0, all_done = 0, done/steps/status = 0, max_steps
+  std::vector<int> ctl(4 + 4 * BMAX, 0);
+  for (int b = 0; b < B; ++b) ctl[4 + 3 * BMAX + b] = h_max_steps[b];
+  HIP_OK(hipMemcpyAsync(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice, s));
+  std::vector<int> lens(h_lens, h_lens + B);
+  HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  W.thr = thr;
+  // encoder + processed inputs
+  run_encoder(c, ids, B, T_max, W.enc.f(), s);
+  {
+    ConvCall cc;
+    cc.lens = W.lens.i();
+    cc.B = B;
+    cc.max_q = T_max;
+    cc.s[0] = src_of(W.enc.f(), (long)T_max * 512, 1, 512, 512, 0);
+    cc.out = W.penc.f();
+    cc.ob = (long)T_max * 128;
+    cc.oc = 1;
+    cc.ot = 128;
+    run_conv(M.penc, cc, s);
+  }
+  // decoder state
+  const int Bp = W.MT * 16;
+  HIP_OK(hipMemsetAsync(W.catt.p, 0, (size_t)Bp * 1024 * 4, s));
+  HIP_OK(hipMemsetAsync(W.hatt.p, 0, (size_t)Bp * 1024 * 4, s));
+  HIP_OK(hipMemsetAsync(W.hdec0.p, 0, (size_t)Bp * 1024 * 4, s));
+  HIP_OK(hipMemsetAsync(W.hdec1.p, 0, (size_t)Bp * 1024 * 4, s));
+  HIP_OK(hipMemsetAsync(W.cdec.p, 0, (size_t)Bp * 1024 * 4, s));
+  HIP_OK(hipMemsetAsync(W.ctx.p, 0, (size_t)Bp * 512 * 4, s));
+  HIP_OK(hipMemsetAsync(W.y.p, 0, (size_t)Bp * 80 * M.r_init * 4, s));
+  HIP_OK(hipMemsetAsync(W.alpha.p, 0, (size_t)B * T_max * 4, s));
+  HIP_OK(hipMemsetAsync(W.acum.p, 0, (size_t)B * T_max * 4, s));
+  HIP_OK(hipMemsetAsync(W.dec.p, 0, (size_t)B * S_cap * r * 80 * 4, s));
+  HIP_OK(hipMemsetAsync(W.align.p, 0, (size_t)B * S_cap * T_max * 4, s));
+  HIP_OK(hipMemsetAsync(W.stop.p, 0, (size_t)B * S_cap * 4, s));
+  bcast_rows_kernel<<<256, 256, 0, s>>>(M.att_bias.f(), 4096, W.gatt.f(), Bp);
+  HIP_OK(hipGetLastError());
+  // graph for CHUNK steps (+ base advance), cached per configuration / buffer generation
+  if (!W.graph || W.graph_gen != W.gen || W.gB != B || W.gT != T_max || W.gS != S_cap || W.gr != r || W.gthr != thr) {
+    if (W.graph) {
+      HIP_OK(hipGraphExecDestroy(W.graph));
+      W.graph = nullptr;
+    }
+    hipGraph_t g;
+    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+    try {
+      for (int j = 0; j < CHUNK; ++j) enqueue_step(c, j, -1, s);
+      launch_dec_advance(reinterpret_cast<DecCtl*>(W.ctl.p), CHUNK, s);
+    } catch (...) {
+      hipGraph_t tmp;
+      (void)hipStreamEndCapture(s, &tmp);
+      throw;
+    }
+    HIP_OK(hipStreamEndCapture(s, &g));
+    HIP_OK(hipGraphInstantiate(&W.graph, g, nullptr, nullptr, 0));
+    HIP_OK(hipGraphDestroy(g));
+    W.graph_gen = W.gen;
+    W.gB = B;
+    W.gT = T_max;
+    W.gS = S_cap;
+    W.gr = r;
+    W.gthr = thr;
+  }
+  // run chunks until every utterance is done (checked one chunk behind) or t > max steps
+  int nchunks = 0;
+  const int chunks_max = max_ms / CHUNK + 1;  // covers t = max_ms (stop of the last step)
+  bool done = false;
+  for (int ch = 0; ch < chunks_max && !done; ++ch) {
+    HIP_OK(hipGraphLaunch(W.graph, s));
+    HIP_OK(hipMemcpyAsync(&c->pinned[ch & 1], &reinterpret_cast<DecCtl*>(W.ctl.p)->all_done, 4,
+                          hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(c->ev_chunk[ch & 1], s));
+    ++nchunks;
+    if (ch >= 1) {
+      HIP_OK(hipEventSynchronize(c->ev_chunk[(ch - 1) & 1]));
+      if (c->pinned[(ch - 1) & 1]) done = true;
+    }
+  }
+  HIP_OK(hipStreamSynchronize(s));
+  std::vector<int> res(3 * BMAX);
+  HIP_OK(hipMemcpy(res.data(), W.ctl.i() + 4, 3 * BMAX * 4, hipMemcpyDeviceToHost));
+  int maxM = 0;
+  std::vector<int> mlens(B);
+  for (int b = 0; b < B; ++b) {
+    TTS_CHECK(res[b] == 1, "decoder did not finish an utterance (internal error)");
+    h_steps[b] = res[BMAX + b];
+    h_status[b] = res[2 * BMAX + b];
+    mlens[b] = h_steps[b] * r;
+    maxM = std::max(maxM, mlens[b]);
+  }
+  HIP_OK(hipMemcpyAsync(W.mlens.p, mlens.data(), B * 4, hipMemcpyHostToDevice, s));
+  const long fb = (long)S_cap * r * 80;
+  HIP_OK(hipMemsetAsync(d_post, 0, (size_t)B * fb * 4, s));
+  run_postnet(c, W.dec.f(), fb, W.mlens.i(), B, S_cap * r, maxM, d_post, fb, s);
+  HIP_OK(hipMemcpyAsync(d_dec, W.dec.p, (size_t)B * fb * 4, hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemcpyAsync(d_align, W.align.p, (size_t)B * S_cap * T_max * 4, hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemcpyAsync(d_stop, W.stop.p, (size_t)B * S_cap * 4, hipMemcpyDeviceToDevice, s));
+  leave(c, stream);
+  c->last_B = B;
+  c->last_T = T_max;
+  c->last_S = S_cap;
+  c->last_r = r;
+}
+
+// ---------------------------------------------------------------- MelGAN -------------
+std::vector<float> wn_weight(const HostMap& m, const std::string& name, std::vector<int64_t> shape) {
+  auto itw = m.find(name + ".weight");
+  if (itw != m.end()) return need(m, name + ".weight", shape).d;
+  const auto& v = need(m, name + ".weight_v", shape).d;
+  const auto& g = need(m, name + ".weight_g", {shape[0], 1, 1}).d;
+  const size_t per = v.size() / shape[0];
+  std::vector<float> w(v.size());
+  for (int64_t o = 0; o < shape[0]; ++o) {
+    double n = 0;
+    for (size_t i = 0; i < per; ++i) n += (double)v[o * per + i] * v[o * per + i];
+    n = std::sqrt(n);
+    const double sc = g[o] / n;
+    for (size_t i = 0; i < per; ++i) w[o * per + i] = (float)(v[o * per + i] * sc);
+  }
+  return w;
+}
+
+void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t* ups, int n_up, int nres,
+                     int use_pqmf) {
+  auto& G = c->mg;
+  const auto& m = c->mg_host;
+  G.ready = false;
+  G.in_ch = in_ch;
+  G.out_ch = out_ch;
+  G.base = base;
+  G.nres = nres;
+  G.pqmf = use_pqmf;
+  G.ups.assign(ups, ups + n_up);
+  G.convT.clear();
+  G.dconv.clear();
+  G.fused.clear();
+  G.convT.resize(n_up);
+  G.dconv.resize((size_t)n_up * nres);
+  G.fused.resize((size_t)n_up * nres);
+  int pl3[8] = {3}, pl0[8] = {0};
+  {
+    auto w = wn_weight(m, "layers.1", {base, in_ch, 7});
+    pack_conv(G.conv_in, w, need(m, "layers.1.bias", {base}).d, in_ch, base, 7, 1, 1, pl3);
+  }
+  int idx = 2, C = base;
+  for (int i = 0; i < n_up; ++i) {
+    const int u = ups[i];
+    TTS_CHECK(u % 2 == 0 && u <= 8, "upsample factors must be even and <= 8");
+    const int cin = base >> i, cout = base >> (i + 1);
+    const int p = u / 2;
+    const std::string nm = "layers." + std::to_string(idx + 1);
+    auto wt = wn_weight(m, nm, {cin, cout, 2 * u});  // ConvTranspose1d weight (Cin, Cout, K)
+    std::vector<float> Wm((size_t)u * cout * cin * 2);
+    int pls[8] = {0};
+    for (int ph = 0; ph < u; ++ph) {
+      const int dmax = (ph + p) / u, dmin = dmax - 1;
+      pls[ph] = -dmin;
+      for (int co = 0; co < cout; ++co)
+        for (int ci = 0; ci < cin; ++ci)
+          for (int jj = 0; jj < 2; ++jj) {
+            const int delta = dmin + jj;
+            const int k = ph + p - delta * u;
+            Wm[(((size_t)ph * cout + co) * cin + ci) * 2 + jj] = wt[((size_t)ci * cout + co) * (2 * u) + k];
+          }
+    }
+    pack_conv(G.convT[i], Wm, need(m, nm + ".bias", {cout}).d, cin, cout, 2, 1, u, pls);
+    C = cout;
+    for (int bk = 0; bk < nres; ++bk) {
+      const int d = 1;
+      int dil = 1;
+      for (int q = 0; q < bk; ++q) dil *= 3;
+      (void)d;
+      const std::string bn = "layers." + std::to_string(idx + 2) + ".blocks." + std::to_string(bk);
+      auto wd = wn_weight(m, bn + ".2", {C, C, 3});
+      int pld[8] = {dil};
+      pack_conv(G.dconv[(size_t)i * nres + bk], wd, need(m, bn + ".2.bias", {C}).d, C, C, 3, dil, 1, pld);
+      auto w1 = wn_weight(m, bn + ".4", {C, C, 1});
+      const std::string sn = "layers." + std::to_string(idx + 2) + ".shortcuts." + std::to_string(bk);
+      auto ws = wn_weight(m, sn, {C, C, 1});
+      std::vector<float> Wf((size_t)C * 2 * C), bf(C);
+      const auto& b1 = need(m, bn + ".4.bias", {C}).d;
+      const auto& bs = need(m, sn + ".bias", {C}).d;
+      for (int co = 0; co < C; ++co) {
+        std::memcpy(&Wf[(size_t)co * 2 * C], &w1[(size_t)co * C], C * 4);
+        std::memcpy(&Wf[(size_t)co * 2 * C + C], &ws[(size_t)co * C], C * 4);
+        bf[co] = b1[co] + bs[co];
+      }
+      pack_conv(G.fused[(size_t)i * nres + bk], Wf, bf, 2 * C, C, 1, 1, 1, pl0);
+    }
+    idx += 3;
+  }
+  {
+    const std::string nm = "layers." + std::to_string(idx + 2);
+    auto w = wn_weight(m, nm, {out_ch, C, 7});
+    pack_conv(G.conv_out, w, need(m, nm + ".bias", {out_ch}).d, C, out_ch, 7, 1, 1, pl3);
+  }
+  if (use_pqmf) {
+    const auto& g = need(m, "pqmf_layer.G", {}).d;
+    auto it = m.find("pqmf_layer.G");
+    TTS_CHECK(it->second.shape.size() == 3 && it->second.shape[1] == out_ch, "pqmf_layer.G shape");
+    G.taps = (int)it->second.shape[2] - 1;
+    G.G.upload(g);
+  }
+  HIP_OK(hipDeviceSynchronize());
+  G.ready = true;
+}
+
+// returns total upsampling factor; writes bands (B, out_ch, up*(M_max+2pad)) into `out`
+int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int M_max, int pad, float* out,
+                  hipStream_t s) {
+  auto& G = c->mg;
+  auto& W = c->mws;
+  TTS_CHECK(G.ready, "melgan weights not finalized");
+  TTS_CHECK(B >= 1, "B >= 1");
+  for (int b = 0; b < B; ++b) {
+    TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= M_max, "mel lens out of range");
+    TTS_CHECK(h_lens[b] + 2 * pad >= 4, "ReflectionPad1d(3): mel frames + 2*padding must be >= 4");
+  }
+  const int Lb = M_max + 2 * pad;
+  int up = 1;
+  for (int u : G.ups) up *= u;
+  size_t maxelems = (size_t)G.base * Lb;
+  {
+    int mul = 1, Cc = G.base;
+    for (int u : G.ups) {
+      mul *= u;
+      Cc /= 2;
+      maxelems = std::max(maxelems, (size_t)Cc * Lb * mul);
+    }
+  }
+  W.lens.ensure(B * 4);
+  W.xa.ensure((size_t)B * maxelems * 4);
+  W.xb.ensure((size_t)B * maxelems * 4);
+  W.h.ensure((size_t)B * maxelems * 4);
+  std::vector<int> lens(h_lens, h_lens + B);
+  HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  ConvCall cc;
+  cc.lens = W.lens.i();
+  cc.B = B;
+  cc.len_add = 2 * pad;
+  // layers[0..1]: replicate pad (inference_padding) + ReflectionPad1d(3) + Conv1d(k7)
+  cc.s[0] = src_of(mel, (long)G.in_ch * M_max, M_max, 1, G.in_ch, 0);
+  cc.pad_mode = 1;
+  cc.rep_pad = pad;
+  cc.in_mul = cc.q_mul = 1;
+  cc.max_q = Lb;
+  float* x = W.xa.f();
+  float* xo = W.xb.f();
+  int C = G.base, mul = 1;
+  long Ls = Lb;
+  cc.out = x;
+  cc.ob = (long)C * Ls;
+  cc.oc = Ls;
+  cc.ot = 1;
+  run_conv(G.conv_in, cc, s);
+  cc.rep_pad = 0;
+  for (size_t i = 0; i < G.ups.size(); ++i) {
+    const int u = G.ups[i];
+    // LeakyReLU + ConvTranspose1d as u polyphase 2-tap convs
+    ConvCall t = cc;
+    t.s[0] = src_of(x, (long)C * Ls, Ls, 1, C, 1);
+    t.pad_mode = 0;
+    t.in_mul = t.q_mul = mul;
+    t.max_q = Lb * mul;
+    t.out_mul = u;
+    const int Cn = C / 2;
+    const long Ln = Ls * u;
+    t.out = xo;
+    t.ob = (long)Cn * Ln;
+    t.oc = Ln;
+    t.ot = 1;
+    run_conv(G.convT[i], t, s);
+    std::swap(x, xo);
+    C = Cn;
+    Ls = Ln;
+    mul *= u;
+    for (int bk = 0; bk < G.nres; ++bk) {
+      const ConvLayer& dl = G.dconv[i * G.nres + bk];
+      ConvCall d = cc;
+      d.s[0] = src_of(x, (long)C * Ls, Ls, 1, C, 1);
+      d.pad_mode = 1;
+      d.in_mul = d.q_mul = mul;
+      d.max_q = Lb * mul;
+      d.out_mul = 1;
+      d.out = W.h.f();
+      d.ob = (long)C * Ls;
+      d.oc = Ls;
+      d.ot = 1;
+      run_conv(dl, d, s);
+      ConvCall f = d;
+      f.nsrc = 2;
+      f.s[0] = src_of(W.h.f(), (long)C * Ls, Ls, 1, C, 1);
+      f.s[1] = src_of(x, (long)C * Ls, Ls, 1, C, 0);
+      f.pad_mode = 0;
+      f.out = xo;
+      run_conv(G.fused[i * G.nres + bk], f, s);
+      std::swap(x, xo);
+    }
+  }
+  ConvCall o = cc;
+  o.s[0] = src_of(x, (long)C * Ls, Ls, 1, C, 1);
+  o.pad_mode = 1;
+  o.in_mul = o.q_mul = mul;
+  o.max_q = Lb * mul;
+  o.epi = 2;
+  o.out = out;
+  o.ob = (long)G.out_ch * Ls;
+  o.oc = Ls;
+  o.ot = 1;
+  HIP_OK(hipMemsetAsync(out, 0, (size_t)B * G.out_ch * Ls * 4, s));
+  run_conv(G.conv_out, o, s);
+  return up;
+}
+
+template <class F>
+int guarded(F&& f) {
+  try {
+    f();
+    return 0;
+  } catch (const std::exception& e) {
+    tts_set_error(e.what());
+    return 1;
+  } catch (...) {
+    tts_set_error("unknown error");
+    return 1;
+  }
+}
+
+void set_tensor(HostMap& m, const char* name, const float* h, const int64_t* shape, int ndim) {
+  TTS_CHECK(name && (h || ndim == 0), "set_tensor: null argument");
+  HostT t;
+  size_t n = 1;
+  for (int i = 0; i < ndim; ++i) {
+    TTS_CHECK(shape[i] >= 0, "negative dim");
+    t.shape.push_back(shape[i]);
+    n *= (size_t)shape[i];
+  }
+  t.d.assign(h, h + n);
+  m[name] = std::move(t);
+}
+
+}  // namespace
+
+extern "C" {
+
+int tts_version(void) { return 1; }
+const char* tts_last_error(void) { return g_err.c_str(); }
+
+int tts_ctx_create(int device, tts_ctx** out) {
+  return guarded([&] {
+    TTS_CHECK(out, "null out");
+    int n = 0;
+    HIP_OK(hipGetDeviceCount(&n));
+    TTS_CHECK(device >= 0 && device < n, "invalid device");
+    auto c = std::make_unique<tts_ctx>();
+    c->device = device;
+    DeviceGuard g(device);
+    HIP_OK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[0], hipEventDisableTiming));
+    HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[1], hipEventDisableTiming));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), 16, hipHostMallocDefault));
+    std::memset(c->pinned, 0, 16);
+    *out = c.release();
+  });
+}
+
+int tts_ctx_destroy(tts_ctx* c) {
+  return guarded([&] {
+    if (!c) return;
+    {
+      DeviceGuard g(c->device);
+      (void)hipStreamSynchronize(c->s);
+      if (c->tws.graph) (void)hipGraphExecDestroy(c->tws.graph);
+      c->tws.graph = nullptr;
+    }
+    int dev = c->device;
+    {
+      DeviceGuard g(dev);
+      hipStream_t s = c->s;
+      hipEvent_t e[4] = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1]};
+      int* pin = c->pinned;
+      delete c;
+      for (auto ev : e) (void)hipEventDestroy(ev);
+      (void)hipStreamDestroy(s);
+      (void)hipHostFree(pin);
+    }
+  });
+}
+
+int tts_taco_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    set_tensor(c->taco_host, name, h, shape, ndim);
+  });
+}
+
+int tts_taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    TTS_CHECK(attn_norm == 0 || attn_norm == 1, "attn_norm must be 0 (sigmoid) or 1 (softmax)");
+    TTS_CHECK(r_init >= 1 && r_init <= 16, "r_init out of range");
+    DeviceGuard g(c->device);
+    taco_finalize(c, num_chars, r_init, attn_norm);
+  });
+}
+
+int tts_taco_infer(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                   const int32_t* h_max_steps, int S_cap, float thr, float* d_dec, float* d_post, float* d_align,
+                   float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && h_steps && h_status,
+              "null argument");
+    DeviceGuard g(c->device);
+    taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+               h_status, stream);
+  });
+}
+
+int tts_taco_encoder(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, float* d_out,
+                     void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_ids && h_lens && d_out, "null argument");
+    TTS_CHECK(c->taco.ready, "tacotron2 weights not finalized");
+    TTS_CHECK(B >= 1 && B <= BMAX && T_max >= 1, "bad sizes");
+    for (int b = 0; b < B; ++b) TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= T_max, "lens out of range");
+    DeviceGuard g(c->device);
+    taco_workspace(c, B, T_max, std::max(1, c->tws.S_cap), std::max(1, c->tws.r));
+    enter(c, stream);
+    std::vector<int> lens(h_lens, h_lens + B);
+    HIP_OK(hipMemcpyAsync(c->tws.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, c->s));
+    run_encoder(c, d_ids, B, T_max, d_out, c->s);
+    HIP_OK(hipStreamSynchronize(c->s));
+    leave(c, stream);
+  });
+}
+
+int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int B, int M_max, float* d_out,
+                     void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_dec && h_lens && d_out, "null argument");
+    TTS_CHECK(c->taco.ready, "tacotron2 weights not finalized");
+    TTS_CHECK(B >= 1 && B <= BMAX && M_max >= 1, "bad sizes");
+    DeviceGuard g(c->device);
+    auto& W = c->tws;
+    long gen = W.gen;
+    grow<int>(W.mlens, BMAX, gen);
+    grow<float>(W.pa, (size_t)B * 512 * M_max, gen);
+    grow<float>(W.pbb, (size_t)B * 512 * M_max, gen);
+    W.gen = gen;
+    int maxM = 0;
+    for (int b = 0; b < B; ++b) {
+      TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= M_max, "lens out of range");
+      maxM = std::max(maxM, (int)h_lens[b]);
+    }
+    enter(c, stream);
+    std::vector<int> lens(h_lens, h_lens + B);
+    HIP_OK(hipMemcpyAsync(W.mlens.p, lens.data(), B * 4, hipMemcpyHostToDevice, c->s));
+    HIP_OK(hipMemsetAsync(d_out, 0, (size_t)B * M_max * 80 * 4, c->s));
+    run_postnet(c, d_dec, (long)M_max * 80, W.mlens.i(), B, M_max, maxM, d_out, (long)M_max * 80, c->s);
+    HIP_OK(hipStreamSynchronize(c->s));
+    leave(c, stream);
+  });
+}
+
+int tts_melgan_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    set_tensor(c->mg_host, name, h, shape, ndim);
+  });
+}
+
+int tts_melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t* ups, int n_up, int nres,
+                        int use_pqmf) {
+  return guarded([&] {
+    TTS_CHECK(c && ups && n_up >= 1 && n_up <= 6, "bad arguments");
+    DeviceGuard g(c->device);
+    melgan_finalize(c, in_ch, out_ch, base, ups, n_up, nres, use_pqmf);
+  });
+}
+
+int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
+                         float* d_out, void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_mel && h_lens && d_out, "null argument");
+    TTS_CHECK(pad >= 0, "pad >= 0");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    run_generator(c, d_mel, h_lens, B, M_max, pad, d_out, c->s);
+    leave(c, stream);
+  });
+}
+
+int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
+                     float* d_wav, void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_mel && h_lens && d_wav, "null argument");
+    TTS_CHECK(pad >= 0, "pad >= 0");
+    auto& G = c->mg;
+    TTS_CHECK(G.ready && G.pqmf, "melgan (with PQMF) not finalized");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    int up = 1;
+    for (int u : G.ups) up *= u;
+    const long Ls = (long)(M_max + 2 * pad) * up;
+    c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
+    run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s);
+    HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
+    launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
+                          2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
+    leave(c, stream);
+  });
+}
+
+int tts_pqmf_synthesis(tts_ctx* c, const float* d_x, int B, int N, int L, const float* d_G, int taps, float* d_y,
+                       void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_x && d_G && d_y, "null argument");
+    TTS_CHECK(B >= 1 && N >= 1 && N <= 8 && L >= 1 && taps >= 0, "bad sizes");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    std::vector<int> lens(B, L);
+    c->mws.lens.ensure(B * 4);
+    HIP_OK(hipMemcpyAsync(c->mws.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, c->s));
+    launch_pqmf_synthesis(d_x, (long)N * L, L, d_G, N, taps, c->mws.lens.i(), 0, 1, L, B, d_y, (long)N * L, c->s);
+    HIP_OK(hipStreamSynchronize(c->s));
+    leave(c, stream);
+  });
+}
+
+int tts_time_decoder_kernel(tts_ctx* c, int which, int iters, float* ms_out) {
+  return guarded([&] {
+    TTS_CHECK(c && ms_out && iters >= 1, "bad arguments");
+    TTS_CHECK(c->last_B > 0 && c->tws.graph, "run tts_taco_infer first");
+    TTS_CHECK(c->tws.S_cap >= CHUNK + 2, "S_cap too small for timing");
+    DeviceGuard g(c->device);
+    auto& W = c->tws;
+    hipStream_t s = c->s;
+    // live state of the last decode, re-armed: base = 1, nothing done, unbounded max steps
+    std::vector<int> ctl(4 + 4 * BMAX, 0);
+    ctl[0] = 1;
+    for (int b = 0; b < BMAX; ++b) ctl[4 + 3 * BMAX + b] = 1 << 30;
+    hipEvent_t e0, e1;
+    HIP_OK(hipEventCreate(&e0));
+    HIP_OK(hipEventCreate(&e1));
+    HIP_OK(hipMemcpyAsync(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice, s));
+    if (which == 0) enqueue_step(c, 0, 0, s);  // warm-up
+    else HIP_OK(hipGraphLaunch(W.graph, s));
+    HIP_OK(hipMemcpyAsync(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice, s));
+    HIP_OK(hipEventRecord(e0, s));
+    for (int i = 0; i < iters; ++i) {
+      if (which == 0) enqueue_step(c, 0, 0, s);
+      else {
+        HIP_OK(hipGraphLaunch(W.graph, s));
+      }
+    }
+    HIP_OK(hipEventRecord(e1, s));
+    HIP_OK(hipEventSynchronize(e1));
+    float ms = 0.f;
+    HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+    *ms_out = which == 0 ? ms / iters : ms / (iters * CHUNK);
+    // leave the control block in a finished state
+    ctl[1] = 1;
+    HIP_OK(hipMemcpy(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice));
+    HIP_OK(hipEventDestroy(e0));
+    HIP_OK(hipEventDestroy(e1));
+  });
+}
+
+}  // extern "C"

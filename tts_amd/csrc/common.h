@@ -1,0 +1,90 @@
+// Shared definitions for the ttship HIP library (gfx950 / CDNA4 only).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+#include <string>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+
+// 16x16x4 f32-in / f32-accumulate MFMA (exact f32, k-ordered fma chain).
+// Operand lane maps (cdna_hip_programming.md §3): A[i=l&15][k=l>>4], B[k=l>>4][j=l&15];
+// D: col j = l&15, row i = 4*(l>>4) + reg.
+#define MFMA16(a, b, c) __builtin_amdgcn_mfma_f32_16x16x4f32((a), (b), (c), 0, 0, 0)
+
+// Error plumbing: every C-ABI entry returns 0 on success, nonzero on failure, and stores a
+// message retrievable with tts_last_error().
+void tts_set_error(const std::string& msg);
+
+#define HIP_OK(expr)                                                                   \
+  do {                                                                                 \
+    hipError_t _e = (expr);                                                            \
+    if (_e != hipSuccess) {                                                            \
+      throw std::runtime_error(std::string(#expr) + ": " + hipGetErrorString(_e));     \
+    }                                                                                  \
+  } while (0)
+
+#define TTS_CHECK(cond, msg)                                                           \
+  do {                                                                                 \
+    if (!(cond)) throw std::runtime_error(std::string(msg));                           \
+  } while (0)
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
+__device__ __forceinline__ float lrelu02(float x) { return x >= 0.f ? x : 0.2f * x; }
+
+// ---------------------------------------------------------------------------------------
+// Generic fp32 MFMA Conv1d (implicit GEMM): out[b][co][q*out_mul+ph] =
+//   epi( sum_{ci,tap} W[co][ci][tap] * in_act(src[b][ci][pad_map(q + tap*dil - pad_left[ph])]) )
+// Used for: encoder convs (BN folded), LSTM input projection, processed_inputs, postnet,
+// every MelGAN conv, and ConvTranspose1d as `nphase` polyphase 2-tap convs.
+// ---------------------------------------------------------------------------------------
+struct ConvSrc {
+  const float* ptr;
+  long sb;     // batch stride (elements)
+  int sc, st;  // channel / time strides (elements)
+  int C;       // channels contributed by this source
+  int act;     // 0 none, 1 leaky-relu(0.2) applied on load
+};
+
+struct ConvArgs {
+  ConvSrc src[2];
+  int nsrc;
+  int Cin;            // total input channels (multiple of 16)
+  int K, dil;
+  int pad_mode;       // 0 zero, 1 reflect, 2 clamp (replicate)
+  const int* lens;    // per-utterance base length (device)
+  int len_add;        // base' = lens[b] + len_add (vocoder: 2*inference_padding)
+  int in_mul;         // input length  = base' * in_mul
+  int q_mul;          // output positions per phase = base' * q_mul
+  int rep_pad;        // virtual replicate padding of the raw source (first vocoder conv)
+  int nphase;         // 1, or stride of a ConvTranspose1d
+  int pad_left[8];    // per phase
+  long w_phase_stride;
+  const float* W;     // swizzled [co16][kc][64][4] per phase
+  const float* bias;  // [Cout]
+  int Cout, Cout_pad;
+  float* out;
+  long ob;
+  int oc, ot;
+  int out_mul;        // t_out = q*out_mul + phase
+  int epi_act;        // 0 none, 1 relu, 2 tanh
+  const float* resid; // optional residual added after activation
+  long rb;
+  int rc, rt;
+  int max_q;          // max over batch of output positions per phase (grid x extent)
+  int B;
+};
+
+// tile configs: TC = output channels per workgroup, TQ = output positions per workgroup
+enum ConvTile { TILE_64x64 = 0, TILE_32x128 = 1, TILE_16x256 = 2 };
+int conv_tile_tc(int tile);
+int conv_tile_for_cout(int cout);
+void launch_conv(const ConvArgs& a, int tile, hipStream_t s);
+
+// host-side swizzle of a row-major weight matrix Wm[Cout][Kdim] (Kdim % 16 == 0) into the
+// MFMA fragment order: dst[((m*nkc + kc)*64 + l)*4 + s] = Wm[m*16 + (l&15)][kc*16 + 4*(l>>4) + s]
+void swizzle_rows16(const float* Wm, int rows, int rows_pad, int Kdim, float* dst);
+
+// PQMF synthesis (pqmf.py:51-56): x (B, N, L) -> y (B, 1, N*L)
+void launch_pqmf_synthesis(const float* x, long xb, long xc, const float* G, int N, int taps,
+                           const int* lens, int len_add, int L_mul, int maxL, int B, float* y, long yb,
+                           hipStream_t s);

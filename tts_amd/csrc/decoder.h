@@ -1,0 +1,91 @@
+// Decoder-step data structures shared by decoder.hip and api.hip.
+#pragma once
+#include "common.h"
+
+enum { EPI_STORE = 0, EPI_LSTM = 1 };
+
+struct SkSeg {
+  const float* ptr;  // row-major activations, row m at ptr + m*ld
+  int ld;
+  int K;             // multiple of 16
+};
+
+struct SkJob {
+  SkSeg seg[3];
+  int nseg;
+  int K;
+  const float* W;      // swizzled [tile][K/16][64][4]
+  int ntiles;
+  int epi;             // EPI_STORE | EPI_LSTM
+  int act;             // store: 0 none, 1 relu
+  const float* bias;   // per swizzled row (tile order)
+  const float* addin;  // optional pre-activation addend [m][row]
+  int addin_ld;
+  float* out;          // store target [m][row]
+  int out_ld;
+  float* h_out;        // LSTM: h[m][unit]
+  float* c_state;      // LSTM: c[m][unit], updated in place
+  int hc_ld;
+  const float* WqT;    // optional: W_query^T [units][128] for partial query projection
+  float* pq_part;      // [workgroup][Bp][128]
+  int frames_r;        // projection: write the first 80*r columns as frames of active utts
+};
+
+struct SkArgs {
+  SkJob job[2];
+  int njobs;
+  int MT;  // batch tiles of 16 (Bp = 16*MT <= 64)
+};
+
+struct DecCtl {
+  int base;      // step index of j = 0 in the current chunk
+  int all_done;  // every utterance finished: all later kernels exit at entry
+  int pad0, pad1;
+};
+
+struct DecDev {
+  DecCtl* ctl;
+  int* done;
+  int* steps;
+  int* status;          // 1 = stopnet, 2 = max_decoder_steps
+  const int* max_steps;
+  const int* lens;      // encoder lengths T_b
+  float* dec_out;       // (B, S_cap*r, 80)
+  float* align_out;     // (B, S_cap, T_max)
+  float* stop_out;      // (B, S_cap)
+  int S_cap;
+  int T_max;
+  int B;
+};
+
+struct StopArgs {
+  const float* ws;    // stopnet weight [1024 + 80*r_init]
+  float bs;
+  const float* hdec;  // [Bp][1024]
+  const float* y;     // [Bp][y_ld] full projection (80*r_init)
+  int y_ld;
+  int ny;
+  float threshold;
+};
+
+struct AttnArgs {
+  const float* pq_part;
+  int npq;
+  int Bp;
+  float* alpha;       // (B, T_max) previous step weights, updated by K3b
+  float* alpha_cum;   // (B, T_max)
+  const float* Wloc;  // (32, 2, 31)
+  const float* Wdense;// (128, 32)
+  const float* v;     // (128)
+  float bv;
+  const float* penc;  // (B, T_max, 128)
+  float* energy;      // (B, T_max)
+  const float* enc;   // (B, T_max, 512)
+  float* ctx;         // (Bp, 512)
+  int softmax;
+};
+
+void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s);
+void launch_prenet1_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s);
+void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t s);
+void launch_dec_advance(DecCtl* ctl, int n, hipStream_t s);

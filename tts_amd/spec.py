@@ -1,0 +1,196 @@
+"""Parameter specs (state_dict names and shapes) of the two models on the hot path.
+
+The names are the reference checkpoint keys, so a reference ``.pth.tar`` ``['model']``
+state_dict loads unchanged:
+
+* Tacotron2: ``TTS/tts/models/tacotron2.py:61-87`` (embedding, encoder, decoder, postnet,
+  DDC ``coarse_decoder``), layers from ``TTS/tts/layers/tacotron2.py:9-233`` and
+  ``TTS/tts/layers/common_layers.py:6-110,196-263``.
+* MultiBand-MelGAN: ``TTS/vocoder/models/melgan_generator.py:28-78`` (``layers.N``),
+  ``TTS/vocoder/layers/melgan.py:5-39`` (ResidualStack), ``TTS/vocoder/layers/pqmf.py:34-43``
+  (buffers ``H``, ``G``, ``updown_filter``).
+
+Each entry is ``(name, shape, kind)``; ``kind`` is a tag used by the synthetic weight
+generator (``tts_amd.weights``) to pick a scale, and by the packers to know what a tensor is.
+"""
+
+from dataclasses import dataclass, field
+from typing import List, Tuple
+
+Spec = List[Tuple[str, Tuple[int, ...], str]]
+
+
+@dataclass
+class TacotronConfig:
+    """Architecture knobs of ``Tacotron2(...)`` that change tensor shapes or math.
+
+    Defaults follow the DDC LJSpeech config (``TTS/tts/configs/config.json:66-140``):
+    r=7 at construction, sigmoid attention norm, location attention, DDC coarse decoder.
+    """
+    num_chars: int = 129
+    r: int = 7                      # r_init: width of linear_projection = 80 * r
+    frame_channels: int = 80
+    postnet_channels: int = 80
+    attn_norm: str = "sigmoid"      # 'sigmoid' | 'softmax'  (common_layers.py:347-354)
+    location_attn: bool = True
+    double_decoder_consistency: bool = True
+    ddc_r: int = 7
+    encoder_dim: int = 512
+    query_dim: int = 1024
+    decoder_rnn_dim: int = 1024
+    prenet_dim: int = 256
+    attn_dim: int = 128
+    loc_filters: int = 32
+    loc_kernel: int = 31
+
+
+@dataclass
+class MelganConfig:
+    """``MultibandMelganGenerator`` constructor args as ``setup_generator`` passes them
+    (``TTS/vocoder/utils/generic_utils.py:61-69``; MB config ``multiband_melgan_config.json:83-87``)."""
+    in_channels: int = 80
+    out_channels: int = 4
+    proj_kernel: int = 7
+    base_channels: int = 384
+    upsample_factors: Tuple[int, ...] = (8, 4, 2)
+    res_kernel: int = 3
+    num_res_blocks: int = 4
+    pqmf: bool = True
+    pqmf_taps: int = 62
+    pqmf_cutoff: float = 0.15
+    pqmf_beta: float = 9.0
+
+
+def _conv_bn(prefix: str, cin: int, cout: int, k: int) -> Spec:
+    return [
+        (f"{prefix}.convolution1d.weight", (cout, cin, k), "conv"),
+        (f"{prefix}.convolution1d.bias", (cout,), "bias"),
+        (f"{prefix}.batch_normalization.weight", (cout,), "bn_w"),
+        (f"{prefix}.batch_normalization.bias", (cout,), "bn_b"),
+        (f"{prefix}.batch_normalization.running_mean", (cout,), "bn_mean"),
+        (f"{prefix}.batch_normalization.running_var", (cout,), "bn_var"),
+        (f"{prefix}.batch_normalization.num_batches_tracked", (), "count"),
+    ]
+
+
+def _decoder(prefix: str, c: TacotronConfig, r: int) -> Spec:
+    E, Q, D, P, A = c.encoder_dim, c.query_dim, c.decoder_rnn_dim, c.prenet_dim, c.attn_dim
+    F = c.frame_channels
+    s: Spec = [
+        (f"{prefix}.prenet.linear_layers.0.linear_layer.weight", (P, F), "linear_relu"),
+        (f"{prefix}.prenet.linear_layers.1.linear_layer.weight", (P, P), "linear_relu"),
+        (f"{prefix}.attention_rnn.weight_ih", (4 * Q, P + E), "lstm"),
+        (f"{prefix}.attention_rnn.weight_hh", (4 * Q, Q), "lstm"),
+        (f"{prefix}.attention_rnn.bias_ih", (4 * Q,), "lstm"),
+        (f"{prefix}.attention_rnn.bias_hh", (4 * Q,), "lstm"),
+        (f"{prefix}.attention.query_layer.linear_layer.weight", (A, Q), "linear_tanh"),
+        (f"{prefix}.attention.inputs_layer.linear_layer.weight", (A, E), "linear_tanh"),
+        (f"{prefix}.attention.v.linear_layer.weight", (1, A), "attn_v"),
+        (f"{prefix}.attention.v.linear_layer.bias", (1,), "bias"),
+    ]
+    if c.location_attn:
+        s += [
+            (f"{prefix}.attention.location_layer.location_conv1d.weight",
+             (c.loc_filters, 2, c.loc_kernel), "conv"),
+            (f"{prefix}.attention.location_layer.location_dense.linear_layer.weight",
+             (A, c.loc_filters), "linear_tanh"),
+        ]
+    s += [
+        (f"{prefix}.decoder_rnn.weight_ih", (4 * D, Q + E), "lstm"),
+        (f"{prefix}.decoder_rnn.weight_hh", (4 * D, D), "lstm"),
+        (f"{prefix}.decoder_rnn.bias_ih", (4 * D,), "lstm"),
+        (f"{prefix}.decoder_rnn.bias_hh", (4 * D,), "lstm"),
+        (f"{prefix}.linear_projection.linear_layer.weight", (F * r, D + E), "linear"),
+        (f"{prefix}.linear_projection.linear_layer.bias", (F * r,), "bias"),
+        (f"{prefix}.stopnet.1.linear_layer.weight", (1, D + F * r), "linear_sigmoid"),
+        (f"{prefix}.stopnet.1.linear_layer.bias", (1,), "stop_bias"),
+    ]
+    return s
+
+
+def tacotron2_spec(c: TacotronConfig) -> Spec:
+    """Ordered state_dict spec of ``Tacotron2`` (single speaker, no GST)."""
+    E = c.encoder_dim
+    s: Spec = [("embedding.weight", (c.num_chars, E), "embedding")]
+    for i in range(3):
+        s += _conv_bn(f"encoder.convolutions.{i}", E, E, 5)
+    H = E // 2
+    for sfx in ("", "_reverse"):
+        s += [
+            (f"encoder.lstm.weight_ih_l0{sfx}", (4 * H, E), "lstm_enc"),
+            (f"encoder.lstm.weight_hh_l0{sfx}", (4 * H, H), "lstm_enc"),
+            (f"encoder.lstm.bias_ih_l0{sfx}", (4 * H,), "lstm_enc"),
+            (f"encoder.lstm.bias_hh_l0{sfx}", (4 * H,), "lstm_enc"),
+        ]
+    s += _decoder("decoder", c, c.r)
+    F = c.postnet_channels
+    chans = [F, 512, 512, 512, 512, F]
+    for i in range(5):
+        s += _conv_bn(f"postnet.convolutions.{i}", chans[i], chans[i + 1], 5)
+    if c.double_decoder_consistency:
+        s += _decoder("coarse_decoder", c, c.ddc_r)
+    return s
+
+
+@dataclass
+class MelganLayer:
+    """One weight-bearing op of the generator, in execution order."""
+    kind: str            # 'conv_in' | 'convT' | 'res_dconv' | 'res_1x1' | 'res_sc' | 'conv_out'
+    name: str            # state_dict prefix, e.g. 'layers.4.blocks.0.2'
+    cin: int
+    cout: int
+    k: int
+    stride: int = 1
+    dilation: int = 1
+    padding: int = 0
+    transposed: bool = False
+    extra: dict = field(default_factory=dict)
+
+
+def melgan_layers(c: MelganConfig) -> List[MelganLayer]:
+    """Generator topology (melgan_generator.py:28-78, melgan.py:9-33)."""
+    L: List[MelganLayer] = []
+    pad = (c.proj_kernel - 1) // 2
+    L.append(MelganLayer("conv_in", "layers.1", c.in_channels, c.base_channels, c.proj_kernel,
+                         padding=pad))
+    idx = 2
+    cout = c.base_channels
+    for i, u in enumerate(c.upsample_factors):
+        cin = c.base_channels // (2 ** i)
+        cout = c.base_channels // (2 ** (i + 1))
+        op = u % 2
+        p = u // 2 + op
+        # layers[idx] = LeakyReLU, layers[idx+1] = ConvTranspose1d, layers[idx+2] = ResidualStack
+        L.append(MelganLayer("convT", f"layers.{idx + 1}", cin, cout, 2 * u, stride=u, padding=p,
+                             transposed=True, extra={"output_padding": op}))
+        base_pad = (c.res_kernel - 1) // 2
+        for b in range(c.num_res_blocks):
+            d = c.res_kernel ** b
+            L.append(MelganLayer("res_dconv", f"layers.{idx + 2}.blocks.{b}.2", cout, cout,
+                                 c.res_kernel, dilation=d, padding=base_pad * d))
+            L.append(MelganLayer("res_1x1", f"layers.{idx + 2}.blocks.{b}.4", cout, cout, 1))
+            L.append(MelganLayer("res_sc", f"layers.{idx + 2}.shortcuts.{b}", cout, cout, 1))
+        idx += 3
+    # layers[idx] = LeakyReLU, [idx+1] = ReflectionPad, [idx+2] = Conv, [idx+3] = Tanh
+    L.append(MelganLayer("conv_out", f"layers.{idx + 2}", cout, c.out_channels, c.proj_kernel,
+                         padding=pad))
+    return L
+
+
+def melgan_spec(c: MelganConfig, weight_norm: bool = True) -> Spec:
+    """Ordered state_dict spec; ``weight_norm=True`` is the checkpoint (pre-removal) naming."""
+    s: Spec = []
+    for l in melgan_layers(c):
+        wshape = (l.cin, l.cout, l.k) if l.transposed else (l.cout, l.cin, l.k)
+        s.append((f"{l.name}.bias", (l.cout,), "bias"))
+        if weight_norm:
+            s.append((f"{l.name}.weight_g", (wshape[0], 1, 1), "wn_g"))
+            s.append((f"{l.name}.weight_v", wshape, "conv"))
+        else:
+            s.append((f"{l.name}.weight", wshape, "conv"))
+    if c.pqmf:
+        N, taps = c.out_channels, c.pqmf_taps
+        s += [("pqmf_layer.H", (N, 1, taps + 1), "buffer"),
+              ("pqmf_layer.G", (1, N, taps + 1), "buffer"),
+              ("pqmf_layer.updown_filter", (N, N, N), "buffer")]
+    return s

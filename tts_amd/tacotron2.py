@@ -1,0 +1,182 @@
+"""Drop-in ``Tacotron2`` whose ``inference`` runs on MI355X through ``libttship.so``.
+
+Mirrors the reference surface used by ``TTS/server/synthesizer.py:43-79`` and
+``TTS/tts/utils/synthesis.py:48-67``: the constructor signature of
+``TTS/tts/models/tacotron2.py:10-37``, checkpoint keys (``load_state_dict(cp['model'])``),
+``.cuda()`` / ``.eval()``, ``decoder.set_r(r)`` (``layers/tacotron2.py:208-209``),
+``decoder.max_decoder_steps`` (``:156``) and ``inference(text, speaker_ids, style_mel,
+speaker_embeddings)`` returning ``(decoder_outputs (B,M,80), postnet_outputs (B,M,80),
+alignments (B,S,T), stop_tokens (B,S,1))`` (``models/tacotron2.py:142-163``).
+
+Batching (new, optional): ``text`` may hold B > 1 padded rows with ``text_lengths``; row i
+of the outputs equals the reference B=1 call on utterance i (the reference itself cannot
+run B > 1: ``layers/tacotron2.py:362``). Per-utterance lengths are in ``last_steps`` /
+``last_mel_lengths`` after the call; padded positions are zero.
+"""
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+from ._lib import get_engine
+from .params import Container, host_tensors, new_token, populate
+from .spec import TacotronConfig, tacotron2_spec
+
+BATCH_LIMIT = 64
+
+
+class Decoder(Container):
+    """Holds decoder parameters plus the runtime knobs the reference exposes."""
+
+    def __init__(self, r: int, frame_channels: int = 80):
+        super().__init__()
+        self.r_init = r
+        self.r = r
+        self.frame_channels = frame_channels
+        self.max_decoder_steps = 1000
+        self.stop_threshold = 0.5
+
+    def set_r(self, new_r):
+        self.r = int(new_r)
+
+
+class Tacotron2(nn.Module):
+    def __init__(self, num_chars, num_speakers=0, r=7, postnet_output_dim=80, decoder_output_dim=80,
+                 attn_type="original", attn_win=False, attn_norm="softmax", prenet_type="original",
+                 prenet_dropout=True, forward_attn=False, trans_agent=False, forward_attn_mask=False,
+                 location_attn=True, attn_K=5, separate_stopnet=True, bidirectional_decoder=False,
+                 double_decoder_consistency=False, ddc_r=None, encoder_in_features=512,
+                 decoder_in_features=512, speaker_embedding_dim=None, gst=False, gst_embedding_dim=512,
+                 gst_num_heads=4, gst_style_tokens=10, gst_use_speaker_embedding=False):
+        super().__init__()
+        unsupported = []
+        if num_speakers > 1:
+            unsupported.append("multi-speaker embeddings")
+        if gst:
+            unsupported.append("GST")
+        if attn_type != "original":
+            unsupported.append(f"attn_type={attn_type}")
+        if attn_win:
+            unsupported.append("attention windowing")
+        if forward_attn or trans_agent or forward_attn_mask:
+            unsupported.append("forward attention")
+        if not location_attn:
+            unsupported.append("location_attn=False")
+        if prenet_type != "original":
+            unsupported.append(f"prenet_type={prenet_type}")
+        if bidirectional_decoder:
+            unsupported.append("bidirectional_decoder")
+        if encoder_in_features != 512 or decoder_in_features != 512:
+            unsupported.append("non-default encoder/decoder feature sizes")
+        if decoder_output_dim != 80 or postnet_output_dim != 80:
+            unsupported.append("frame channels != 80")
+        if attn_norm not in ("sigmoid", "softmax"):
+            raise ValueError("Unknown value for attention norm type")
+        if unsupported:
+            raise NotImplementedError("tts_amd Tacotron2 does not implement: " + ", ".join(unsupported) +
+                                      " (SURVEY.md §8f lists these as next steps)")
+        self.num_chars = num_chars
+        self.num_speakers = num_speakers
+        self.r = r
+        self.attn_norm = attn_norm
+        self.double_decoder_consistency = double_decoder_consistency
+        self.cfg = TacotronConfig(num_chars=num_chars, r=r, attn_norm=attn_norm,
+                                  double_decoder_consistency=double_decoder_consistency,
+                                  ddc_r=ddc_r if ddc_r is not None else r)
+        self.decoder = Decoder(r, decoder_output_dim)
+        populate(self, tacotron2_spec(self.cfg))
+        self._version = 0
+        self._token = new_token()
+        self.last_steps = None
+        self.last_mel_lengths = None
+        self.last_status = None
+
+    # any change of parameters or placement invalidates the packed device copy
+    def load_state_dict(self, state_dict, strict=True, **kw):
+        res = super().load_state_dict(state_dict, strict=strict, **kw)
+        self._version += 1
+        return res
+
+    def _apply(self, fn, *args, **kwargs):
+        res = super()._apply(fn, *args, **kwargs)
+        self._version += 1
+        return res
+
+    def invalidate(self):
+        """Call after editing parameters in place."""
+        self._version += 1
+
+    def forward(self, *args, **kwargs):
+        raise NotImplementedError("training forward is out of scope; use inference()")
+
+    def _sync(self, eng):
+        key = (self._token, self._version)
+        if eng.taco_key != key:
+            eng.load_tacotron(host_tensors(self, skip_prefixes=("coarse_decoder.",)), self.num_chars,
+                              self.decoder.r_init, self.attn_norm)
+            eng.taco_key = key
+
+    @torch.no_grad()
+    def inference(self, text, speaker_ids=None, style_mel=None, speaker_embeddings=None,
+                  text_lengths: Optional[Sequence[int]] = None, max_decoder_steps=None):
+        if speaker_ids is not None or speaker_embeddings is not None or style_mel is not None:
+            raise NotImplementedError("speaker / style conditioning is not implemented (SURVEY.md §8f)")
+        dev = self.embedding.weight.device
+        eng = get_engine(dev)
+        self._sync(eng)
+        text = torch.as_tensor(text).to(dev, torch.int64)
+        if text.dim() == 1:
+            text = text[None]
+        text = text.contiguous()
+        B, T = text.shape
+        lens = np.full(B, T, np.int64) if text_lengths is None else np.asarray(
+            torch.as_tensor(text_lengths).cpu(), dtype=np.int64)
+        if len(lens) != B or lens.min() < 1 or lens.max() > T:
+            raise ValueError("text_lengths must have B entries in [1, T]")
+        ms = self.decoder.max_decoder_steps if max_decoder_steps is None else max_decoder_steps
+        ms = np.broadcast_to(np.asarray(ms, dtype=np.int64), (B,)).copy()
+        r = int(self.decoder.r)
+        if not 1 <= r <= self.decoder.r_init:
+            raise ValueError(f"r={r} must be in [1, r_init={self.decoder.r_init}]")
+        outs = []
+        for b0 in range(0, B, BATCH_LIMIT):
+            b1 = min(B, b0 + BATCH_LIMIT)
+            sub = text[b0:b1]
+            Tn = int(lens[b0:b1].max())
+            sub = sub[:, :Tn].contiguous()
+            S_cap = int(ms[b0:b1].max())
+            nb = b1 - b0
+            dec = torch.empty(nb, S_cap * r, 80, device=dev, dtype=torch.float32)
+            post = torch.empty_like(dec)
+            align = torch.empty(nb, S_cap, Tn, device=dev, dtype=torch.float32)
+            stop = torch.empty(nb, S_cap, device=dev, dtype=torch.float32)
+            steps, status = eng.taco_infer(sub, lens[b0:b1], r, ms[b0:b1], S_cap, self.decoder.stop_threshold,
+                                           dec, post, align, stop)
+            outs.append((dec, post, align, stop, steps, status, Tn))
+        steps = np.concatenate([o[4] for o in outs])
+        status = np.concatenate([o[5] for o in outs])
+        for s in status:
+            if s == 2:
+                print("   | > Decoder stopped with 'max_decoder_steps")
+        S = int(steps.max())
+        M = S * r
+        dec = torch.cat([o[0][:, :M] for o in outs]) if len(outs) > 1 else outs[0][0][:, :M]
+        post = torch.cat([o[1][:, :M] for o in outs]) if len(outs) > 1 else outs[0][1][:, :M]
+        if len(outs) > 1:
+            align = torch.zeros(B, S, T, device=dev)
+            b0 = 0
+            for o in outs:
+                n = o[2].shape[0]
+                align[b0:b0 + n, :, :o[6]] = o[2][:, :S]
+                b0 += n
+        else:
+            align = outs[0][2][:, :S]
+            if align.shape[2] != T:
+                align = torch.nn.functional.pad(align, (0, T - align.shape[2]))
+        stop = torch.cat([o[3][:, :S] for o in outs]) if len(outs) > 1 else outs[0][3][:, :S]
+        self.last_steps = steps
+        self.last_mel_lengths = steps * r
+        self.last_status = status
+        return dec, post, align, stop[:, :, None]

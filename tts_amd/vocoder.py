@@ -1,0 +1,180 @@
+"""Drop-in MelGAN-family generators whose ``inference`` runs on MI355X via ``libttship.so``.
+
+Mirrors ``TTS/vocoder/models/melgan_generator.py:8-97`` (constructor, ``layers.N`` checkpoint
+keys with ``weight_g`` / ``weight_v`` before ``remove_weight_norm()``, ``inference_padding``),
+``multiband_melgan_generator.py:7-39`` (``pqmf_layer`` buffers, PQMF synthesis) and
+``fullband_melgan_generator.py``. Batching (new, optional): ``inference(c, lengths=...)`` on
+(B, 80, M) padded mels; row b equals the reference call on ``c[b:b+1, :, :lengths[b]]``,
+zero past ``hop * (lengths[b] + 2 * inference_padding)`` samples.
+"""
+
+from typing import Optional, Sequence
+
+import numpy as np
+import torch
+from torch import nn
+
+from ._lib import get_engine
+from .params import Container, host_tensors, new_token, populate
+from .pqmf import pqmf_filters
+from .spec import MelganConfig, melgan_layers, melgan_spec
+
+
+class PQMF(Container):
+    """Buffers of ``TTS/vocoder/layers/pqmf.py:10-43``; synthesis runs in the HIP library."""
+
+    def __init__(self, N=4, taps=62, cutoff=0.15, beta=9.0):
+        super().__init__()
+        self.N, self.taps, self.cutoff, self.beta = N, taps, cutoff, beta
+        H, G, updown = pqmf_filters(N, taps, cutoff, beta)
+        self.register_buffer("H", torch.from_numpy(H))
+        self.register_buffer("G", torch.from_numpy(G))
+        self.register_buffer("updown_filter", torch.from_numpy(updown))
+
+    @torch.no_grad()
+    def synthesis(self, x):
+        eng = get_engine(x.device)
+        x = x.to(torch.float32).contiguous()
+        B, N, L = x.shape
+        if N != self.N:
+            raise ValueError(f"expected {self.N} subbands, got {N}")
+        y = torch.empty(B, 1, N * L, device=x.device, dtype=torch.float32)
+        G = self.G.to(x.device, torch.float32).reshape(N, -1).contiguous()
+        eng.pqmf_synthesis(x, G, y)
+        return y
+
+    def analysis(self, x):  # training-only path in the reference (pqmf.py:48-49)
+        raise NotImplementedError("PQMF analysis is training-only and out of scope")
+
+
+class MelganGenerator(nn.Module):
+    _use_pqmf = False
+
+    def __init__(self, in_channels=80, out_channels=1, proj_kernel=7, base_channels=512,
+                 upsample_factors=(8, 8, 2, 2), res_kernel=3, num_res_blocks=3):
+        super().__init__()
+        if proj_kernel != 7 or res_kernel != 3:
+            raise NotImplementedError("only proj_kernel=7, res_kernel=3 (the reference configs) are built")
+        if any(u % 2 or u > 8 for u in upsample_factors):
+            raise NotImplementedError("upsample factors must be even and <= 8")
+        if in_channels % 16 or base_channels % (16 << len(upsample_factors)):
+            raise NotImplementedError("channel counts must keep multiples of 16 at every stage")
+        self.cfg = MelganConfig(in_channels=in_channels, out_channels=out_channels, proj_kernel=proj_kernel,
+                                base_channels=base_channels, upsample_factors=tuple(upsample_factors),
+                                res_kernel=res_kernel, num_res_blocks=num_res_blocks, pqmf=False)
+        self.inference_padding = 2
+        self._wn = True
+        populate(self, melgan_spec(self.cfg, weight_norm=True))
+        self._version = 0
+        self._token = new_token()
+
+    @property
+    def hop(self):
+        return int(np.prod(self.cfg.upsample_factors)) * (self.cfg.out_channels if self._use_pqmf else 1)
+
+    def load_state_dict(self, state_dict, strict=True, **kw):
+        res = super().load_state_dict(state_dict, strict=strict, **kw)
+        self._version += 1
+        return res
+
+    def _apply(self, fn, *args, **kwargs):
+        res = super()._apply(fn, *args, **kwargs)
+        self._version += 1
+        return res
+
+    def invalidate(self):
+        self._version += 1
+
+    def remove_weight_norm(self):
+        """Fold w = g * v / ||v|| (melgan_generator.py:91-97, melgan.py:41-45)."""
+        if not self._wn:
+            return
+        for l in melgan_layers(self.cfg):
+            *path, = l.name.split(".")
+            m = self
+            for p in path:
+                m = m._modules[p]
+            g, v = m.weight_g.data, m.weight_v.data
+            w = torch._weight_norm(v, g, 0)
+            del m._parameters["weight_g"]
+            del m._parameters["weight_v"]
+            m.weight = nn.Parameter(w.contiguous(), requires_grad=False)
+        self._wn = False
+        self._version += 1
+
+    def forward(self, c):
+        return self.inference(c)
+
+    def _sync(self, eng):
+        key = (self._token, self._version)
+        if eng.melgan_key != key:
+            eng.load_melgan(host_tensors(self, skip_prefixes=("pqmf_layer.H", "pqmf_layer.updown")),
+                            self.cfg.in_channels, self.cfg.out_channels, self.cfg.base_channels,
+                            self.cfg.upsample_factors, self.cfg.num_res_blocks, self._use_pqmf)
+            eng.melgan_key = key
+
+    def _prep(self, c, lengths):
+        dev = self.layers._modules["1"].bias.device
+        eng = get_engine(dev)
+        self._sync(eng)
+        c = torch.as_tensor(c).to(dev, torch.float32)
+        if c.dim() == 2:
+            c = c[None]
+        c = c.contiguous()
+        B, C, M = c.shape
+        if C != self.cfg.in_channels:
+            raise ValueError(f"expected {self.cfg.in_channels} mel channels, got {C}")
+        lens = np.full(B, M, np.int64) if lengths is None else np.asarray(torch.as_tensor(lengths).cpu(), np.int64)
+        pad = int(self.inference_padding)
+        if (lens + 2 * pad < 4).any():
+            raise RuntimeError("ReflectionPad1d: padding (3) must be < input length; need frames + 2*padding >= 4")
+        return eng, c, lens, pad
+
+    @torch.no_grad()
+    def generator(self, c, lengths: Optional[Sequence[int]] = None):
+        """``self.layers(pad(c))``: (B, out_channels, up * (M + 2p))."""
+        eng, c, lens, pad = self._prep(c, lengths)
+        B, _, M = c.shape
+        up = int(np.prod(self.cfg.upsample_factors))
+        out = torch.empty(B, self.cfg.out_channels, up * (M + 2 * pad), device=c.device)
+        eng.melgan_generator(c, lens, pad, out)
+        return out
+
+    @torch.no_grad()
+    def inference(self, c, lengths: Optional[Sequence[int]] = None):
+        return self.generator(c, lengths)
+
+
+class MultibandMelganGenerator(MelganGenerator):
+    _use_pqmf = True
+
+    def __init__(self, in_channels=80, out_channels=4, proj_kernel=7, base_channels=384,
+                 upsample_factors=(2, 8, 2, 2), res_kernel=3, num_res_blocks=3):
+        super().__init__(in_channels=in_channels, out_channels=out_channels, proj_kernel=proj_kernel,
+                         base_channels=base_channels, upsample_factors=upsample_factors, res_kernel=res_kernel,
+                         num_res_blocks=num_res_blocks)
+        self.pqmf_layer = PQMF(N=4, taps=62, cutoff=0.15, beta=9.0)
+        self.cfg.pqmf = True
+        self._version += 1
+
+    def pqmf_synthesis(self, x):
+        return self.pqmf_layer.synthesis(x)
+
+    def pqmf_analysis(self, x):
+        return self.pqmf_layer.analysis(x)
+
+    @torch.no_grad()
+    def inference(self, cond_features, lengths: Optional[Sequence[int]] = None):
+        eng, c, lens, pad = self._prep(cond_features, lengths)
+        B, _, M = c.shape
+        wav = torch.empty(B, 1, self.hop * (M + 2 * pad), device=c.device)
+        eng.melgan_infer(c, lens, pad, wav)
+        return wav
+
+
+class FullbandMelganGenerator(MelganGenerator):
+    def __init__(self, in_channels=80, out_channels=1, proj_kernel=7, base_channels=512,
+                 upsample_factors=(2, 8, 2, 2), res_kernel=3, num_res_blocks=4):
+        super().__init__(in_channels=in_channels, out_channels=out_channels, proj_kernel=proj_kernel,
+                         base_channels=base_channels, upsample_factors=upsample_factors, res_kernel=res_kernel,
+                         num_res_blocks=num_res_blocks)
