@@ -185,7 +185,7 @@ struct TacoWS {
   int B = 0, T_max = 0, S_cap = 0, r = 0, MT = 0;
   long gen = 0;
   DevBuf lens, mlens, x0, ca, cb, gin, enc, penc;
-  DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, alpha, acum, energy, ctl;
+  DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, spart, alpha, acum, energy, ctl;
   DevBuf dec, align, stop, pa, pbb;
   hipGraphExec_t graph = nullptr;
   long graph_gen = -1;
@@ -366,7 +366,13 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
       for (int k = 0; k < Q; ++k) t[(size_t)k * A + a] = wq[(size_t)a * Q + k];
     M.WqT.upload(t);
     M.Wloc.upload(need(h, "decoder.attention.location_layer.location_conv1d.weight", {32, 2, 31}).d);
-    M.Wdense.upload(need(h, "decoder.attention.location_layer.location_dense.linear_layer.weight", {A, 32}).d);
+    {
+      const auto& wd = need(h, "decoder.attention.location_layer.location_dense.linear_layer.weight", {A, 32}).d;
+      std::vector<float> wdT((size_t)32 * A);
+      for (int a = 0; a < A; ++a)
+        for (int c = 0; c < 32; ++c) wdT[(size_t)c * A + a] = wd[(size_t)a * 32 + c];
+      M.Wdense.upload(wdT);
+    }
     M.v.upload(need(h, "decoder.attention.v.linear_layer.weight", {1, A}).d);
     M.bv = need(h, "decoder.attention.v.linear_layer.bias", {1}).d[0];
   }
@@ -431,6 +437,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.ctx, (size_t)Bp * 512, g);
   grow<float>(W.y, (size_t)Bp * 80 * c->taco.r_init, g);
   grow<float>(W.pq, (size_t)64 * Bp * 128, g);
+  grow<float>(W.spart, (size_t)(5 * c->taco.r_init + 1) * Bp, g);
   grow<float>(W.alpha, (size_t)B * T_max, g);
   grow<float>(W.acum, (size_t)B * T_max, g);
   grow<float>(W.energy, (size_t)B * T_max, g);
@@ -503,12 +510,10 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.out = W.p1.f();
     J.out_ld = 256;
     StopArgs st{};
-    st.ws = M.stop_w.f();
+    st.part = W.spart.f();
+    st.nparts = 5 * M.r_init + 1;
+    st.Bp = MT * 16;
     st.bs = M.stop_b;
-    st.hdec = hd_cur;
-    st.y = W.y.f();
-    st.y_ld = YLD;
-    st.ny = YLD;
     st.threshold = W.thr;
     launch_prenet1_stop(a, d, st, j, s);
   }
@@ -556,7 +561,7 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     p.alpha = W.alpha.f();
     p.alpha_cum = W.acum.f();
     p.Wloc = M.Wloc.f();
-    p.Wdense = M.Wdense.f();
+    p.WdT = M.Wdense.f();
     p.v = M.v.f();
     p.bv = M.bv;
     p.penc = W.penc.f();
@@ -612,6 +617,10 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.out = W.y.f();
     J.out_ld = YLD;
     J.frames_r = r;
+    J.stop_wy = M.stop_w.f() + 1024;
+    J.stop_wh = M.stop_w.f();
+    J.stop_h = hd_nxt;
+    J.stop_part = W.spart.f();
     launch_skinny(a, d, j, 1, 16, s);
   }
 }
@@ -773,7 +782,6 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     W.gthr = thr;
   }
   // run chunks until every utterance is done (checked one chunk behind) or t > max steps
-  int nchunks = 0;
   const int chunks_max = max_ms / CHUNK + 1;  // covers t = max_ms (stop of the last step)
   bool done = false;
   for (int ch = 0; ch < chunks_max && !done; ++ch) {
@@ -781,7 +789,6 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     HIP_OK(hipMemcpyAsync(&c->pinned[ch & 1], &reinterpret_cast<DecCtl*>(W.ctl.p)->all_done, 4,
                           hipMemcpyDeviceToHost, s));
     HIP_OK(hipEventRecord(c->ev_chunk[ch & 1], s));
-    ++nchunks;
     if (ch >= 1) {
       HIP_OK(hipEventSynchronize(c->ev_chunk[(ch - 1) & 1]));
       if (c->pinned[(ch - 1) & 1]) done = true;

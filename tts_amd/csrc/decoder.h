@@ -29,6 +29,12 @@ struct SkJob {
   const float* WqT;    // optional: W_query^T [units][128] for partial query projection
   float* pq_part;      // [workgroup][Bp][128]
   int frames_r;        // projection: write the first 80*r columns as frames of active utts
+  // projection only: stopnet partial dot products, stop_part[tile][Bp]; tile == ntiles holds
+  // w_h . h_dec (computed by one extra workgroup), tiles < ntiles hold w_y[cols] . y[cols]
+  const float* stop_wy;  // [ntiles*16]
+  const float* stop_wh;  // [1024]
+  const float* stop_h;   // h_dec [Bp][1024]
+  float* stop_part;
 };
 
 struct SkArgs {
@@ -59,12 +65,10 @@ struct DecDev {
 };
 
 struct StopArgs {
-  const float* ws;    // stopnet weight [1024 + 80*r_init]
+  const float* part;  // stop_part [nparts][Bp] written by the projection kernel
+  int nparts;
+  int Bp;
   float bs;
-  const float* hdec;  // [Bp][1024]
-  const float* y;     // [Bp][y_ld] full projection (80*r_init)
-  int y_ld;
-  int ny;
   float threshold;
 };
 
@@ -75,7 +79,7 @@ struct AttnArgs {
   float* alpha;       // (B, T_max) previous step weights, updated by K3b
   float* alpha_cum;   // (B, T_max)
   const float* Wloc;  // (32, 2, 31)
-  const float* Wdense;// (128, 32)
+  const float* WdT;   // location_dense transposed (32, 128)
   const float* v;     // (128)
   float bv;
   const float* penc;  // (B, T_max, 128)

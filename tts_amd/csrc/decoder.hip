@@ -7,88 +7,166 @@
 // device-side done flag per utterance plus an all_done word that turns every later kernel
 // into an early exit.
 //
-//   K1a  stop(t-1) + per-utterance done flags  ||  prenet layer 1 (common_layers.py:76-82)
+//   K1a  stop(t-1) from the projection kernel's partial dots + done flags
+//        || prenet layer 1 (common_layers.py:76-82)
 //   K1b  prenet layer 2
 //   K2   attention_rnn LSTMCell (only the K=256 prenet part; the ctx/h part was precomputed
 //        by K4 of the previous step) + partial query projection (common_layers.py:272)
 //   K3a  location-sensitive energies over T chunks (common_layers.py:268-278, 90-110)
 //   K3b  sigmoid/softmax norm, alpha_cum, alignment, context (common_layers.py:347-366)
 //   K4   decoder_rnn LSTMCell (tacotron2.py:279-282) || next step's attention_rnn ctx/h part
-//   K5   linear_projection (tacotron2.py:286-289) + frame store
+//   K5   linear_projection (tacotron2.py:286-289) + frame store + stopnet partial dots (:291-295)
 //
 // All GEMMs are "skinny" (M = batch <= 64): v_mfma_f32_16x16x4_f32 with M = 16 utterances,
 // N = 16 gate rows, weights pre-swizzled into fragment order (one contiguous 1 KiB read per
 // wave instruction), K split across the waves of a workgroup and reduced through LDS in a
 // fixed order (deterministic).
+//
+// Every kernel here is latency-bound (microseconds of work, ~1 us per dependent trip to
+// MALL/HBM), so each one issues all of its independent global loads first -- including before
+// the all_done early-exit test -- never guards a load with a per-element condition (indices are
+// clamped instead, cdna_hip_programming.md §5 trap (c)), and the GEMM k-loop is a two-stage
+// register pipeline: fragments for k-group g+1 are in flight while group g's MFMAs issue.
 #include "common.h"
 #include "decoder.h"
 
-// --------------------------------------------------------------------------------------
-// skinny GEMM core: partial[wave][m][n] for one 16-row tile over this wave's K range
-// --------------------------------------------------------------------------------------
-__device__ __forceinline__ void skinny_accumulate(const SkJob& J, int tile, int w, int KS, int MT,
-                                                  int lane, f32x4 (&acc)[4]) {
-  const int nkc = J.K / 16;
-  const int kc_lo = (w * nkc) / KS, kc_hi = ((w + 1) * nkc) / KS;
-  const f32x4* Wv = reinterpret_cast<const f32x4*>(J.W) + (long)tile * nkc * 64 + lane;
-  const int row = lane & 15;
-  const int kl = 4 * (lane >> 4);
-  int seg_start = 0;
-  for (int sgi = 0; sgi < J.nseg; ++sgi) {
-    const SkSeg S = J.seg[sgi];
-    const int s_lo = seg_start / 16, s_hi = (seg_start + S.K) / 16;
-    const int lo = kc_lo > s_lo ? kc_lo : s_lo;
-    const int hi = kc_hi < s_hi ? kc_hi : s_hi;
-    const float* xb = S.ptr + (long)row * S.ld + kl - seg_start;
-    for (int kc = lo; kc < hi; ++kc) {
-      const f32x4 wv = Wv[(long)kc * 64];
-      f32x4 xv[4];
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt)
-        if (mt < MT) xv[mt] = *reinterpret_cast<const f32x4*>(xb + (long)mt * 16 * S.ld + kc * 16);
-#pragma unroll
-      for (int mt = 0; mt < 4; ++mt) {
-        if (mt < MT) {
-          acc[mt] = MFMA16(xv[mt][0], wv[0], acc[mt]);
-          acc[mt] = MFMA16(xv[mt][1], wv[1], acc[mt]);
-          acc[mt] = MFMA16(xv[mt][2], wv[2], acc[mt]);
-          acc[mt] = MFMA16(xv[mt][3], wv[3], acc[mt]);
-        }
-      }
+struct SegPick {
+  const float* ptr;
+  int ld;
+};
+
+__device__ __forceinline__ SegPick seg_at(const SkJob& J, int kc) {
+  int k = kc * 16;
+  if (J.nseg > 1 && k >= J.seg[0].K) {
+    k -= J.seg[0].K;
+    if (J.nseg > 2 && k >= J.seg[1].K) {
+      k -= J.seg[1].K;
+      return {J.seg[2].ptr + k, J.seg[2].ld};
     }
-    seg_start += S.K;
+    return {J.seg[1].ptr + k, J.seg[1].ld};
+  }
+  return {J.seg[0].ptr + k, J.seg[0].ld};
+}
+
+template <int MT, int U>
+struct SkFrag {
+  f32x4 w[U];
+  f32x4 x[U][MT];
+};
+
+// load k-group [kc0, kc0+U) (indices clamped to kc_last: always valid addresses)
+template <int MT, int U>
+__device__ __forceinline__ void sk_load(SkFrag<MT, U>& F, const SkJob& J, const f32x4* Wv, int kc0, int kc_last,
+                                        int row, int kl) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    const int kc = min(kc0 + u, kc_last);
+    F.w[u] = Wv[(long)kc * 64];
+    const SegPick sp = seg_at(J, kc);
+    const float* xp = sp.ptr + (long)row * sp.ld + kl;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) F.x[u][mt] = *reinterpret_cast<const f32x4*>(xp + (long)mt * 16 * sp.ld);
   }
 }
 
-// part layout in LDS: [grp][w][m][17]
-__device__ __forceinline__ void skinny_to_lds(float* part, int KS, int Bp, int w, int lane, int MT,
-                                              const f32x4 (&acc)[4]) {
+template <int MT, int U>
+__device__ __forceinline__ void sk_mma(const SkFrag<MT, U>& F, int nvalid, f32x4 (&acc)[MT]) {
+#pragma unroll
+  for (int u = 0; u < U; ++u) {
+    if (u < nvalid) {  // wave-uniform
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[mt] = MFMA16(F.x[u][mt][s], F.w[u][s], acc[mt]);
+    }
+  }
+}
+
+template <int MT, int NTHR = 256>
+struct SkPipe {
+  // 1024-thread workgroups are capped at 128 VGPRs: shallower groups, the 4 waves per SIMD hide latency
+  static constexpr int U = (NTHR >= 1024 || MT > 2) ? 2 : 4;
+  SkFrag<MT, U> A, B;
+  const f32x4* Wv;
+  int kc_lo, kc_hi, row, kl;
+  __device__ __forceinline__ void init(const SkJob& J, int tile, int w, int KS, int lane) {
+    const int nkc = J.K / 16;
+    kc_lo = (w * nkc) / KS;
+    kc_hi = ((w + 1) * nkc) / KS;
+    Wv = reinterpret_cast<const f32x4*>(J.W) + (long)tile * nkc * 64 + lane;
+    row = lane & 15;
+    kl = 4 * (lane >> 4);
+  }
+  // first group's loads: issue before anything that waits on memory
+  __device__ __forceinline__ void prefetch(const SkJob& J) {
+    if (kc_hi > kc_lo) sk_load<MT, U>(A, J, Wv, kc_lo, kc_hi - 1, row, kl);
+  }
+  __device__ __forceinline__ void run(const SkJob& J, f32x4 (&acc)[MT]) {
+    for (int kc0 = kc_lo; kc0 < kc_hi; kc0 += 2 * U) {
+      if (kc0 + U < kc_hi) sk_load<MT, U>(B, J, Wv, kc0 + U, kc_hi - 1, row, kl);
+      sk_mma<MT, U>(A, kc_hi - kc0, acc);
+      if (kc0 + U >= kc_hi) break;
+      if (kc0 + 2 * U < kc_hi) sk_load<MT, U>(A, J, Wv, kc0 + 2 * U, kc_hi - 1, row, kl);
+      sk_mma<MT, U>(B, kc_hi - kc0 - U, acc);
+    }
+  }
+};
+
+// partial sums in LDS: [wave][m][17]
+template <int MT>
+__device__ __forceinline__ void skinny_to_lds(float* part, int w, int lane, const f32x4 (&acc)[MT]) {
+  constexpr int Bp = MT * 16;
   float* p = part + (long)w * Bp * 17;
 #pragma unroll
-  for (int mt = 0; mt < 4; ++mt) {
-    if (mt < MT) {
+  for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
-    }
-  }
+    for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
 }
 
-__device__ __forceinline__ float skinny_sum(const float* part, int KS, int Bp, int m, int n) {
+template <int KS, int Bp>
+__device__ __forceinline__ float skinny_sum(const float* part, int m, int n) {
   float s = part[m * 17 + n];
-  for (int w = 1; w < KS; ++w) s += part[((long)w * Bp + m) * 17 + n];
+#pragma unroll
+  for (int w = 1; w < KS; ++w) s += part[(w * Bp + m) * 17 + n];
   return s;
 }
 
-// frame / stop bookkeeping shared by the epilogues
-__device__ __forceinline__ int dec_step(const DecDev& D, int j) { return D.ctl->base + j; }
+__device__ __forceinline__ float wave_sum(float v) {
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off, 64);
+  return v;
+}
+
+// stopnet h-part: stop_part[ntiles][m] = w_h . h_dec[m]   (one extra workgroup of the projection)
+template <int MT>
+__device__ void stop_h_role(const SkJob& J, int nthr) {
+  constexpr int Bp = MT * 16;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = nthr / 64;
+  float w[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i) w[i] = J.stop_wh[lane + 64 * i];
+  for (int m = wave; m < Bp; m += nw) {
+    const float* h = J.stop_h + (long)m * 1024;
+    float x[16];
+#pragma unroll
+    for (int i = 0; i < 16; ++i) x[i] = h[lane + 64 * i];
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < 16; ++i) s = fmaf(w[i], x[i], s);
+    s = wave_sum(s);
+    if (lane == 0) J.stop_part[(long)J.ntiles * Bp + m] = s;
+  }
+}
 
 // --------------------------------------------------------------------------------------
-// generic skinny kernel: NT tiles per workgroup, KS waves per tile
+// generic skinny kernel: NT tiles per workgroup, KS waves per tile, MT batch tiles of 16
 // --------------------------------------------------------------------------------------
-template <int NT, int KS>
+template <int NT, int KS, int MT>
 __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D, int jstep) {
-  if (D.ctl->all_done) return;
   extern __shared__ __attribute__((aligned(16))) float smem[];
+  constexpr int Bp = MT * 16;
+  constexpr int nthr = NT * KS * 64;
+  constexpr int SITEMS = (NT * Bp * 16 + nthr - 1) / nthr;  // store items per thread (<= 4)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = wave / KS, w = wave % KS;
@@ -98,55 +176,98 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
     ji = 1;
   }
   const SkJob& J = A.job[ji];
-  const int Bp = A.MT * 16;
+  const int all_done = D.ctl->all_done;
+  if (J.stop_h && wg == J.ntiles / NT) {
+    if (!all_done) stop_h_role<MT>(J, nthr);
+    return;
+  }
   const int tile = wg * NT + grp;
-  float* part = smem + (long)grp * KS * Bp * 17;
-
-  f32x4 acc[4];
+  SkPipe<MT, nthr> pipe;
+  pipe.init(J, tile, w, KS, lane);
+  pipe.prefetch(J);
+  // epilogue operands, fetched under the GEMM
+  float eb[SITEMS];
+  float lb[4] = {0.f, 0.f, 0.f, 0.f}, la[4] = {0.f, 0.f, 0.f, 0.f}, lc = 0.f;
+  float wq[4 * NT];
+  if (J.epi == EPI_STORE) {
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  skinny_accumulate(J, tile, w, KS, A.MT, lane, acc);
-  skinny_to_lds(part, KS, Bp, w, lane, A.MT, acc);
+    for (int i = 0; i < SITEMS; ++i) {
+      const int idx = min(tid + i * nthr, NT * Bp * 16 - 1);
+      const int g = idx / (Bp * 16), n = idx % 16;
+      eb[i] = J.bias ? J.bias[(wg * NT + g) * 16 + n] : 0.f;
+    }
+  } else {
+    const int idx = min(tid, NT * Bp * 4 - 1);
+    const int g = idx / (Bp * 4), rem = idx % (Bp * 4);
+    const int m = rem / 4, u = rem % 4;
+    const int tl = wg * NT + g;
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int col = tl * 16 + q * 4 + u;
+      if (J.bias) lb[q] = J.bias[col];
+      if (J.addin) la[q] = J.addin[(long)m * J.addin_ld + col];
+    }
+    lc = J.c_state[(long)m * J.hc_ld + tl * 4 + u];
+    if (J.pq_part) {
+      const int a = tid % 128;
+#pragma unroll
+      for (int u2 = 0; u2 < 4 * NT; ++u2) wq[u2] = J.WqT[(long)(wg * NT * 4 + u2) * 128 + a];
+    }
+  }
+  if (all_done) return;
+  const int t = D.ctl->base + jstep;
+
+  f32x4 acc[MT];
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  pipe.run(J, acc);
+  float* part = smem + (long)grp * KS * Bp * 17;
+  float* extra = smem + (long)NT * KS * Bp * 17;  // [NT][Bp][16]
+  skinny_to_lds<MT>(part, w, lane, acc);
   __syncthreads();
 
-  const int nthr = NT * KS * 64;
   if (J.epi == EPI_STORE) {
-    const int t = dec_step(D, jstep);
-    for (int idx = tid; idx < NT * Bp * 16; idx += nthr) {
+#pragma unroll
+    for (int i = 0; i < SITEMS; ++i) {
+      const int idx = tid + i * nthr;
+      if (idx >= NT * Bp * 16) break;
       const int g = idx / (Bp * 16), rem = idx % (Bp * 16);
       const int m = rem / 16, n = rem % 16;
       const int col = (wg * NT + g) * 16 + n;
-      float v = skinny_sum(smem + (long)g * KS * Bp * 17, KS, Bp, m, n);
-      if (J.bias) v += J.bias[col];
-      if (J.addin) v += J.addin[(long)m * J.addin_ld + col];
+      float v = skinny_sum<KS, Bp>(smem + (long)g * KS * Bp * 17, m, n) + eb[i];
       if (J.act == 1) v = fmaxf(v, 0.f);
       J.out[(long)m * J.out_ld + col] = v;
       if (J.frames_r > 0 && m < D.B && col < 80 * J.frames_r && t < D.S_cap && !D.done[m])
         D.dec_out[((long)m * D.S_cap + t) * J.frames_r * 80 + col] = v;
+      if (J.stop_part) extra[idx] = v * J.stop_wy[col];
+    }
+    if (J.stop_part) {
+      __syncthreads();
+      for (int idx = tid; idx < NT * Bp; idx += nthr) {
+        const int g = idx / Bp, m = idx % Bp;
+        const float* e = extra + ((long)g * Bp + m) * 16;
+        float s = e[0];
+#pragma unroll
+        for (int n = 1; n < 16; ++n) s += e[n];
+        J.stop_part[(long)(wg * NT + g) * Bp + m] = s;
+      }
     }
   } else {  // EPI_LSTM: tile rows are gate-major [i0..i3 f0..f3 g0..g3 o0..o3] of 4 units
-    float* hs = smem + (long)NT * KS * Bp * 17;  // [Bp][4*NT]
-    for (int idx = tid; idx < NT * Bp * 4; idx += nthr) {
-      const int g = idx / (Bp * 4), rem = idx % (Bp * 4);
+    float* hs = extra;  // [Bp][4*NT]
+    if (tid < NT * Bp * 4) {
+      const int g = tid / (Bp * 4), rem = tid % (Bp * 4);
       const int m = rem / 4, u = rem % 4;
       const int tl = wg * NT + g;
       const float* pg = smem + (long)g * KS * Bp * 17;
       float pre[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int col = tl * 16 + q * 4 + u;
-        float v = skinny_sum(pg, KS, Bp, m, q * 4 + u);
-        if (J.bias) v += J.bias[col];
-        if (J.addin) v += J.addin[(long)m * J.addin_ld + col];
-        pre[q] = v;
-      }
-      const int unit = tl * 4 + u;
-      const long ci = (long)m * J.hc_ld + unit;
+      for (int q = 0; q < 4; ++q) pre[q] = skinny_sum<KS, Bp>(pg, m, q * 4 + u) + lb[q] + la[q];
+      const long ci = (long)m * J.hc_ld + tl * 4 + u;
       const float ig = 1.f / (1.f + expf(-pre[0]));
       const float fg = 1.f / (1.f + expf(-pre[1]));
       const float gg = tanhf(pre[2]);
       const float og = 1.f / (1.f + expf(-pre[3]));
-      const float c = fg * J.c_state[ci] + ig * gg;
+      const float c = fg * lc + ig * gg;
       const float h = og * tanhf(c);
       J.c_state[ci] = c;
       J.h_out[ci] = h;
@@ -154,11 +275,11 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
     }
     if (J.pq_part) {  // partial query projection over this workgroup's 4*NT hidden units
       __syncthreads();
-      const int unit0 = wg * NT * 4;
       for (int idx = tid; idx < Bp * 128; idx += nthr) {
         const int m = idx / 128, a = idx % 128;
         float s = 0.f;
-        for (int u = 0; u < 4 * NT; ++u) s = fmaf(J.WqT[(long)(unit0 + u) * 128 + a], hs[m * 4 * NT + u], s);
+#pragma unroll
+        for (int u = 0; u < 4 * NT; ++u) s = fmaf(wq[u], hs[m * 4 * NT + u], s);
         J.pq_part[((long)wg * Bp + m) * 128 + a] = s;
       }
     }
@@ -168,36 +289,51 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
 // --------------------------------------------------------------------------------------
 // K1a: stop decision for step t-1 (one workgroup) || prenet layer 1 (16 workgroups)
 // --------------------------------------------------------------------------------------
+constexpr int NPARTS_MAX = 64;
+
+template <int MT>
 __global__ __launch_bounds__(256) void prenet1_stop_kernel(SkArgs A, DecDev D, StopArgs S, int jstep) {
-  if (D.ctl->all_done) return;
-  const int t = dec_step(D, jstep);
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int Bp = A.MT * 16;
+  constexpr int Bp = MT * 16;
   if (blockIdx.x == A.job[0].ntiles) {
-    // ---- stop role: logit = w_s . [h_dec, y_full] + b_s; sigma; reference stop rule ----
-    for (int m = wave; m < D.B; m += 4) {
-      float s = 0.f;
-      for (int k = lane; k < 1024; k += 64) s = fmaf(S.ws[k], S.hdec[(long)m * 1024 + k], s);
-      for (int k = lane; k < S.ny; k += 64) s = fmaf(S.ws[1024 + k], S.y[(long)m * S.y_ld + k], s);
+    // ---- stop role: logit = sum of the projection kernel's partial dots + b_s; sigma;
+    //      reference stop rule (tacotron2.py:357-366): stop iff sigma > thr and t > 0,
+    //      else stop when max_decoder_steps outputs exist. One thread per utterance.
+    __shared__ int dflag[64];
+    const int m = min(tid, Bp - 1);
+    float pv[NPARTS_MAX];
 #pragma unroll
-      for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-      if (lane == 0 && t >= 1 && t <= D.S_cap && !D.done[m]) {
+    for (int p = 0; p < NPARTS_MAX; ++p) pv[p] = S.part[(long)min(p, S.nparts - 1) * S.Bp + m];
+    const int dn0 = D.done[m];
+    const int mx = D.max_steps[m];
+    const int all_done = D.ctl->all_done;
+    const int t = D.ctl->base + jstep;
+    if (all_done) return;
+    if (tid < D.B) {
+      int dn = dn0;
+      if (t >= 1 && !dn) {
+        float s = 0.f;
+#pragma unroll
+        for (int p = 0; p < NPARTS_MAX; ++p)
+          if (p < S.nparts) s += pv[p];
         const float logit = s + S.bs;
         const float sg = 1.f / (1.f + expf(-logit));
-        D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
+        if (t - 1 < D.S_cap) D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
         const bool st = (sg > S.threshold) && (t - 1) > 0;
-        if (st || t >= D.max_steps[m]) {
+        if (st || t >= mx) {
           D.done[m] = 1;
           D.steps[m] = t;
           D.status[m] = st ? 1 : 2;
+          dn = 1;
         }
       }
+      dflag[m] = dn;
     }
     __syncthreads();
     if (tid == 0) {
       int all = 1;
-      for (int m = 0; m < D.B; ++m) all &= D.done[m];
+      for (int k = 0; k < D.B; ++k) all &= dflag[k];
       D.ctl->all_done = all;
     }
     return;
@@ -205,15 +341,19 @@ __global__ __launch_bounds__(256) void prenet1_stop_kernel(SkArgs A, DecDev D, S
   // ---- prenet layer 1: relu(W1 . memory) with memory = y[:, 80(r-1):80r] (go frame = 0) ----
   const SkJob& J = A.job[0];
   const int tile = blockIdx.x;
-  f32x4 acc[4];
+  SkPipe<MT> pipe;
+  pipe.init(J, tile, wave, 4, lane);
+  pipe.prefetch(J);
+  if (D.ctl->all_done) return;
+  f32x4 acc[MT];
 #pragma unroll
-  for (int i = 0; i < 4; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  skinny_accumulate(J, tile, wave, 4, A.MT, lane, acc);
-  skinny_to_lds(smem, 4, Bp, wave, lane, A.MT, acc);
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  pipe.run(J, acc);
+  skinny_to_lds<MT>(smem, wave, lane, acc);
   __syncthreads();
   for (int idx = tid; idx < Bp * 16; idx += 256) {
     const int m = idx / 16, n = idx % 16;
-    const float v = skinny_sum(smem, 4, Bp, m, n);
+    const float v = skinny_sum<4, Bp>(smem, m, n);
     J.out[(long)m * J.out_ld + tile * 16 + n] = fmaxf(v, 0.f);
   }
 }
@@ -222,66 +362,82 @@ __global__ __launch_bounds__(256) void prenet1_stop_kernel(SkArgs A, DecDev D, S
 // K3a: energies e[b][t] for a chunk of TCH encoder positions
 // --------------------------------------------------------------------------------------
 constexpr int TCH = 16;
-constexpr int LOCK = 31, LOCF = 32, ADIM = 128;
+constexpr int LOCK = 31, LOCF = 32, ADIM = 128, NPQ = 64;
 
 __global__ __launch_bounds__(256) void attn_energy_kernel(AttnArgs P, DecDev D) {
-  if (D.ctl->all_done) return;
   const int b = blockIdx.y;
-  if (D.done[b]) return;
-  const int T = D.lens[b];
   const int t0 = blockIdx.x * TCH;
-  if (t0 >= T) return;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  __shared__ float pq[ADIM];
+  const int a = tid & 127, grp = tid >> 7;
   __shared__ float red[2][ADIM];
   __shared__ float A0[TCH + LOCK], A1[TCH + LOCK];
   __shared__ float Wl[LOCF * 2 * LOCK];
   __shared__ float f[LOCF][TCH];
   __shared__ float er[2][TCH];
   const int Bp = P.Bp;
-  {  // 1. query projection = sum of K2 partials (fixed order)
-    const int a = tid & 127, h = tid >> 7;
-    float s = 0.f;
-    for (int p = h; p < P.npq; p += 2) s += P.pq_part[((long)p * Bp + b) * ADIM + a];
-    red[h][a] = s;
+  const int T = D.lens[b];
+  const int Tm1 = max(T - 1, 0);
+  // -- every independent global load up front (clamped indices, no guarded loads) --
+  float pen[TCH / 2];
+#pragma unroll
+  for (int i = 0; i < TCH / 2; ++i) {
+    const int t = min(t0 + grp * (TCH / 2) + i, Tm1);
+    pen[i] = P.penc[((long)b * D.T_max + t) * ADIM + a];
   }
-  for (int i = tid; i < TCH + LOCK - 1; i += 256) {
-    const int pos = t0 - (LOCK - 1) / 2 + i;
-    const bool ok = pos >= 0 && pos < T;
-    A0[i] = ok ? P.alpha[(long)b * D.T_max + pos] : 0.f;
-    A1[i] = ok ? P.alpha_cum[(long)b * D.T_max + pos] : 0.f;
-  }
-  for (int i = tid; i < LOCF * 2 * LOCK; i += 256) Wl[i] = P.Wloc[i];
-  __syncthreads();
-  if (tid < ADIM) pq[tid] = red[0][tid] + red[1][tid];
-  // 2. location conv: f[c][tt] = sum_i sum_k Wl[c][i][k] * A_i[tt + k]
-  for (int idx = tid; idx < LOCF * TCH; idx += 256) {
-    const int c = idx / TCH, tt = idx % TCH;
-    float s = 0.f;
-    const float* w0 = Wl + c * 2 * LOCK;
-    for (int k = 0; k < LOCK; ++k) s = fmaf(w0[k], A0[tt + k], s);
-    for (int k = 0; k < LOCK; ++k) s = fmaf(w0[LOCK + k], A1[tt + k], s);
-    f[c][tt] = s;
-  }
-  __syncthreads();
-  // 3. loc = W_dense . f ; e = v . tanh(pq + loc + penc) + b_v
-  const int a = tid & 127, grp = tid >> 7;
   float wd[LOCF];
 #pragma unroll
-  for (int c = 0; c < LOCF; ++c) wd[c] = P.Wdense[a * LOCF + c];
-  const float va = P.v[a], pqa = pq[a];
+  for (int c = 0; c < LOCF; ++c) wd[c] = P.WdT[c * ADIM + a];
+  const float va = P.v[a];
+  float pp[NPQ / 2];
+#pragma unroll
+  for (int i = 0; i < NPQ / 2; ++i) pp[i] = P.pq_part[((long)(grp * (NPQ / 2) + i) * Bp + b) * ADIM + a];
+  float a0 = 0.f, a1 = 0.f;
+  {
+    const int pos = t0 - (LOCK - 1) / 2 + min(tid, TCH + LOCK - 2);
+    const int pc = min(max(pos, 0), Tm1);
+    a0 = P.alpha[(long)b * D.T_max + pc];
+    a1 = P.alpha_cum[(long)b * D.T_max + pc];
+    if (pos < 0 || pos >= T) a0 = a1 = 0.f;
+  }
+  float wl[(LOCF * 2 * LOCK + 255) / 256];
+#pragma unroll
+  for (int i = 0; i < (LOCF * 2 * LOCK + 255) / 256; ++i) wl[i] = P.Wloc[min(tid + 256 * i, LOCF * 2 * LOCK - 1)];
+  if (D.ctl->all_done || D.done[b] || t0 >= T) return;
+  if (tid < TCH + LOCK - 1) {
+    A0[tid] = a0;
+    A1[tid] = a1;
+  }
+#pragma unroll
+  for (int i = 0; i < (LOCF * 2 * LOCK + 255) / 256; ++i)
+    if (tid + 256 * i < LOCF * 2 * LOCK) Wl[tid + 256 * i] = wl[i];
+  // query projection = sum of the attention-LSTM kernel's 64 partials (fixed order)
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPQ / 2; ++i) s += pp[i];
+  red[grp][a] = s;
+  __syncthreads();
+  const float pqa = red[0][a] + red[1][a];
+  // location conv: f[c][tt] = sum_i sum_k Wl[c][i][k] * A_i[tt + k]
+  for (int idx = tid; idx < LOCF * TCH; idx += 256) {
+    const int c = idx / TCH, tt = idx % TCH;
+    float sc = 0.f;
+    const float* w0 = Wl + c * 2 * LOCK;
+#pragma unroll
+    for (int k = 0; k < LOCK; ++k) sc = fmaf(w0[k], A0[tt + k], sc);
+#pragma unroll
+    for (int k = 0; k < LOCK; ++k) sc = fmaf(w0[LOCK + k], A1[tt + k], sc);
+    f[c][tt] = sc;
+  }
+  __syncthreads();
+  // loc = W_dense . f ; e = v . tanh(pq + loc + penc) + b_v
+#pragma unroll
   for (int i = 0; i < TCH / 2; ++i) {
     const int tt = grp * (TCH / 2) + i;
-    const int t = t0 + tt;
-    float z = 0.f;
-    if (t < T) {
-      float l = 0.f;
+    float l = 0.f;
 #pragma unroll
-      for (int c = 0; c < LOCF; ++c) l = fmaf(wd[c], f[c][tt], l);
-      z = tanhf(pqa + l + P.penc[((long)b * D.T_max + t) * ADIM + a]) * va;
-    }
-#pragma unroll
-    for (int off = 32; off > 0; off >>= 1) z += __shfl_xor(z, off, 64);
+    for (int c = 0; c < LOCF; ++c) l = fmaf(wd[c], f[c][tt], l);
+    float z = (t0 + tt < T) ? tanhf(pqa + l + pen[i]) * va : 0.f;
+    z = wave_sum(z);
     if (lane == 0) er[wave & 1][tt] = z;
   }
   __syncthreads();
@@ -291,42 +447,57 @@ __global__ __launch_bounds__(256) void attn_energy_kernel(AttnArgs P, DecDev D) 
 // --------------------------------------------------------------------------------------
 // K3b: normalisation, alignment, alpha_cum and the context vector (slice of 128 dims)
 // --------------------------------------------------------------------------------------
+__device__ __forceinline__ float block_reduce(float v, float* wred, bool is_max) {
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1) {
+    const float o = __shfl_xor(v, off, 64);
+    v = is_max ? fmaxf(v, o) : v + o;
+  }
+  __syncthreads();
+  if (lane == 0) wred[wave] = v;
+  __syncthreads();
+  return is_max ? fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]))
+                : (wred[0] + wred[1]) + (wred[2] + wred[3]);
+}
+
+constexpr int CTX_PRE = 4;  // encoder rows per thread prefetched before the normalisation
+
 __global__ __launch_bounds__(256) void attn_context_kernel(AttnArgs P, DecDev D, int jstep) {
-  if (D.ctl->all_done) return;
   const int b = blockIdx.y, slice = blockIdx.x;
-  if (D.done[b]) return;
-  const int T = D.lens[b];
-  const int t_step = dec_step(D, jstep);
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int tid = threadIdx.x;
   extern __shared__ __attribute__((aligned(16))) float al[];  // [T_max]
   __shared__ float wred[4];
-  __shared__ float bc[2];
+  __shared__ f32x4 cr[8][32];
+  const int T = D.lens[b];
+  const int Tm1 = max(T - 1, 0);
+  const int d4 = tid & 31, g = tid >> 5;
+  const f32x4* enc = reinterpret_cast<const f32x4*>(P.enc + (long)b * D.T_max * 512 + slice * 128) + d4;
+  // prefetch: first energies and the first encoder rows of this thread's context slice
   const float* e = P.energy + (long)b * D.T_max;
-  float mx = -INFINITY;
-  if (P.softmax) {
-    for (int t = tid; t < T; t += 256) mx = fmaxf(mx, e[t]);
+  float e0 = e[min(tid, Tm1)];
+  f32x4 ep[CTX_PRE];
 #pragma unroll
-    for (int off = 32; off > 0; off >>= 1) mx = fmaxf(mx, __shfl_xor(mx, off, 64));
-    if (lane == 0) wred[wave] = mx;
-    __syncthreads();
-    if (tid == 0) bc[0] = fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]));
-    __syncthreads();
-    mx = bc[0];
+  for (int i = 0; i < CTX_PRE; ++i) ep[i] = enc[(long)min(g + 8 * i, Tm1) * 128];
+  if (D.ctl->all_done || D.done[b]) return;
+  const int t_step = D.ctl->base + jstep;
+  if (tid < T) al[tid] = e0;
+  for (int t = tid + 256; t < T; t += 256) al[t] = e[t];
+  __syncthreads();
+  float mx = 0.f;
+  if (P.softmax) {
+    float m = -INFINITY;
+    for (int t = tid; t < T; t += 256) m = fmaxf(m, al[t]);
+    mx = block_reduce(m, wred, true);
   }
   float s = 0.f;
   for (int t = tid; t < T; t += 256) {
-    const float v = P.softmax ? expf(e[t] - mx) : 1.f / (1.f + expf(-e[t]));
+    const float x = al[t];
+    const float v = P.softmax ? expf(x - mx) : 1.f / (1.f + expf(-x));
     al[t] = v;
     s += v;
   }
-#pragma unroll
-  for (int off = 32; off > 0; off >>= 1) s += __shfl_xor(s, off, 64);
-  __syncthreads();
-  if (lane == 0) wred[wave] = s;
-  __syncthreads();
-  if (tid == 0) bc[1] = (wred[0] + wred[1]) + (wred[2] + wred[3]);
-  __syncthreads();
-  const float S = bc[1];
+  const float S = block_reduce(s, wred, false);
   for (int t = tid; t < T; t += 256) {
     const float a = al[t] / S;
     al[t] = a;
@@ -338,14 +509,28 @@ __global__ __launch_bounds__(256) void attn_context_kernel(AttnArgs P, DecDev D,
   }
   __syncthreads();
   // context slice: ctx[b][slice*128 + d] = sum_t a_t * enc[b][t][slice*128 + d]
-  const int d = tid & 127, h = tid >> 7;
-  const float* enc = P.enc + (long)b * D.T_max * 512 + slice * 128 + d;
-  float c = 0.f;
-  for (int t = h; t < T; t += 2) c = fmaf(al[t], enc[(long)t * 512], c);
-  __shared__ float cr[2][128];
-  cr[h][d] = c;
+  f32x4 c = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int i = 0; i < CTX_PRE; ++i)
+    if (g + 8 * i < T) c += al[g + 8 * i] * ep[i];
+  int t = g + 8 * CTX_PRE;
+  for (; t + 24 < T; t += 32) {
+    const f32x4 x0 = enc[(long)t * 128], x1 = enc[(long)(t + 8) * 128];
+    const f32x4 x2 = enc[(long)(t + 16) * 128], x3 = enc[(long)(t + 24) * 128];
+    c += al[t] * x0;
+    c += al[t + 8] * x1;
+    c += al[t + 16] * x2;
+    c += al[t + 24] * x3;
+  }
+  for (; t < T; t += 8) c += al[t] * enc[(long)t * 128];
+  cr[g][d4] = c;
   __syncthreads();
-  if (tid < 128) P.ctx[(long)b * 512 + slice * 128 + tid] = cr[0][tid] + cr[1][tid];
+  if (tid < 32) {
+    f32x4 r = cr[0][tid];
+#pragma unroll
+    for (int k = 1; k < 8; ++k) r += cr[k][tid];
+    *reinterpret_cast<f32x4*>(P.ctx + (long)b * 512 + slice * 128 + 4 * tid) = r;
+  }
 }
 
 __global__ void dec_advance_kernel(DecCtl* ctl, int n) {
@@ -355,28 +540,52 @@ __global__ void dec_advance_kernel(DecCtl* ctl, int n) {
 // --------------------------------------------------------------------------------------
 // host launchers
 // --------------------------------------------------------------------------------------
-static size_t skinny_lds(int NT, int KS, int Bp, bool lstm) {
-  return (size_t)NT * KS * Bp * 17 * 4 + (lstm ? (size_t)Bp * 4 * NT * 4 : 0);
+static size_t skinny_lds(int NT, int KS, int Bp) {
+  return ((size_t)NT * KS * Bp * 17 + (size_t)NT * Bp * 16) * 4;
+}
+
+template <int NT, int KS>
+static void launch_skinny_nt(const SkArgs& a, const DecDev& d, int jstep, int nwg, hipStream_t s) {
+  const size_t lds = skinny_lds(NT, KS, a.MT * 16);
+  switch (a.MT) {
+    case 1: skinny_kernel<NT, KS, 1><<<nwg, NT * KS * 64, lds, s>>>(a, d, jstep); break;
+    case 2: skinny_kernel<NT, KS, 2><<<nwg, NT * KS * 64, lds, s>>>(a, d, jstep); break;
+    case 3: skinny_kernel<NT, KS, 3><<<nwg, NT * KS * 64, lds, s>>>(a, d, jstep); break;
+    default: skinny_kernel<NT, KS, 4><<<nwg, NT * KS * 64, lds, s>>>(a, d, jstep); break;
+  }
 }
 
 void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s) {
+  TTS_CHECK(a.MT >= 1 && a.MT <= 4, "skinny: MT in [1,4]");
+  for (int j = 0; j < a.njobs; ++j) {
+    TTS_CHECK(a.job[j].ntiles % NT == 0, "skinny: ntiles % NT");
+    if (a.job[j].epi == EPI_LSTM) TTS_CHECK(NT * a.MT * 16 * 4 <= NT * KS * 64, "skinny: LSTM items per thread");
+  }
   int nwg = a.job[0].ntiles / NT + (a.njobs > 1 ? a.job[1].ntiles / NT : 0);
-  bool lstm = a.job[0].epi == EPI_LSTM || (a.njobs > 1 && a.job[1].epi == EPI_LSTM);
-  const size_t lds = skinny_lds(NT, KS, a.MT * 16, lstm);
-  if (NT == 1 && KS == 4) skinny_kernel<1, 4><<<nwg, 256, lds, s>>>(a, d, jstep);
-  else if (NT == 1 && KS == 16) skinny_kernel<1, 16><<<nwg, 1024, lds, s>>>(a, d, jstep);
-  else if (NT == 4 && KS == 4) skinny_kernel<4, 4><<<nwg, 1024, lds, s>>>(a, d, jstep);
+  if (a.njobs == 1 && a.job[0].stop_h) nwg += 1;
+  if (NT == 1 && KS == 4) launch_skinny_nt<1, 4>(a, d, jstep, nwg, s);
+  else if (NT == 1 && KS == 16) launch_skinny_nt<1, 16>(a, d, jstep, nwg, s);
+  else if (NT == 4 && KS == 4) launch_skinny_nt<4, 4>(a, d, jstep, nwg, s);
   else TTS_CHECK(false, "skinny: unsupported tile config");
   HIP_OK(hipGetLastError());
 }
 
 void launch_prenet1_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s) {
-  const size_t lds = skinny_lds(1, 4, a.MT * 16, false);
-  prenet1_stop_kernel<<<a.job[0].ntiles + 1, 256, lds, s>>>(a, d, st, jstep);
+  TTS_CHECK(a.MT >= 1 && a.MT <= 4, "prenet: MT in [1,4]");
+  TTS_CHECK(st.nparts >= 1 && st.nparts <= NPARTS_MAX, "stop: too many partials (r_init <= 12)");
+  const size_t lds = skinny_lds(1, 4, a.MT * 16);
+  const int g = a.job[0].ntiles + 1;
+  switch (a.MT) {
+    case 1: prenet1_stop_kernel<1><<<g, 256, lds, s>>>(a, d, st, jstep); break;
+    case 2: prenet1_stop_kernel<2><<<g, 256, lds, s>>>(a, d, st, jstep); break;
+    case 3: prenet1_stop_kernel<3><<<g, 256, lds, s>>>(a, d, st, jstep); break;
+    default: prenet1_stop_kernel<4><<<g, 256, lds, s>>>(a, d, st, jstep); break;
+  }
   HIP_OK(hipGetLastError());
 }
 
 void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t s) {
+  TTS_CHECK(p.npq == NPQ, "attention: expects 64 query partials");
   dim3 g1((d.T_max + TCH - 1) / TCH, d.B);
   attn_energy_kernel<<<g1, 256, 0, s>>>(p, d);
   HIP_OK(hipGetLastError());
