@@ -27,7 +27,8 @@ F32 = np.float32
 
 def sigmoid(x):
     x = np.asarray(x, F32)
-    return (F32(1.0) / (F32(1.0) + np.exp(-x))).astype(F32)
+    with np.errstate(over="ignore"):
+        return (F32(1.0) / (F32(1.0) + np.exp(-x))).astype(F32)
 
 
 def conv1d(x, w, b=None, padding=0, dilation=1):

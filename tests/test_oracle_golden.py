@@ -1,0 +1,87 @@
+"""CPU: pin the oracle (numpy restatement) against the reference's golden outputs.
+
+Fixtures were produced by running the reference in the build container
+(tests/golden/make_golden.py); the PQMF known answer is the reference's own committed
+TTS/vocoder/pqmf_output.wav.
+"""
+import numpy as np
+import pytest
+
+from helpers import load_fixture, melgan_oracle, melgan_state_dict, taco_state_dict
+from oracle.melgan_np import pqmf_synthesis
+from oracle.taco_np import TacoOracle
+from tts_amd.pqmf import pqmf_filters
+
+
+def test_pqmf_filters_match_reference_buffers():
+    fx = load_fixture("pqmf")
+    H, G, U = pqmf_filters()
+    assert np.array_equal(H, fx["H"]) and np.array_equal(G, fx["G"]) and np.array_equal(U, fx["updown"])
+
+
+def test_pqmf_oracle_matches_reference():
+    fx = load_fixture("pqmf")
+    y = np.stack([pqmf_synthesis(fx["x"][b], fx["G"]) for b in range(fx["x"].shape[0])])
+    assert y.shape == fx["y"].shape
+    assert np.abs(y - fx["y"]).max() <= 2e-6
+
+
+def test_pqmf_oracle_known_answer_wav():
+    fx = load_fixture("pqmf")
+    y = pqmf_synthesis(fx["example_bands"][0], fx["G"])[0]
+    assert np.abs(y - fx["example_rec"][0, 0]).max() <= 2e-6
+    ka = fx["known_answer_int16"].astype(np.float64)
+    n = len(ka) - 64
+    assert np.abs(y[:n] * 32768.0 - ka[:n]).max() <= 2.0
+
+
+@pytest.mark.parametrize("key", ["M7_p0", "M64_p0", "M5_p2", "M33_p2"])
+def test_melgan_oracle_matches_reference(key):
+    fx = load_fixture("mbmelgan")
+    cfg, sd = melgan_state_dict(int(fx["seed"]))
+    orc = melgan_oracle(cfg, sd)
+    pad = int(key.split("_p")[1])
+    mel = fx[key + "_mel"][0]
+    c = np.concatenate([np.repeat(mel[:, :1], pad, 1), mel, np.repeat(mel[:, -1:], pad, 1)], 1) if pad else mel
+    bands = orc.generator(c)
+    assert np.abs(bands - fx[key + "_bands"][0]).max() <= 1e-5
+    wav = orc.inference(mel, pad)
+    assert wav.shape == fx[key + "_wav"][0].shape
+    assert np.abs(wav - fx[key + "_wav"][0]).max() <= 1e-5
+
+
+@pytest.mark.parametrize("r", [2, 1])
+def test_tacotron2_oracle_matches_reference(r):
+    fx = load_fixture("taco_sigmoid")
+    cfg, sd = taco_state_dict(fx, r=r)
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for u in range(3):
+        k = f"r{r}_u{u}"
+        dec, post, align, stop = orc.inference(fx[k + "_ids"], r, int(fx[f"r{r}_max_steps"]))
+        assert len(stop) == len(fx[k + "_stop"])
+        assert np.abs(dec - fx[k + "_dec"]).max() <= 1e-5
+        assert np.abs(post - fx[k + "_post"]).max() <= 1e-5
+        assert np.abs(align - fx[k + "_align"]).max() <= 1e-6
+        assert np.abs(stop - fx[k + "_stop"]).max() <= 1e-5
+        if k + "_enc" in fx:
+            assert np.abs(orc.encoder(fx[k + "_ids"]) - fx[k + "_enc"]).max() <= 1e-6
+
+
+def test_tacotron2_oracle_softmax_matches_reference():
+    fx = load_fixture("taco_softmax")
+    cfg, sd = taco_state_dict(fx, r=2)
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for u in range(2):
+        k = f"r2_u{u}"
+        dec, post, align, stop = orc.inference(fx[k + "_ids"], 2, int(fx["r2_max_steps"]))
+        assert len(stop) == len(fx[k + "_stop"])
+        assert np.abs(post - fx[k + "_post"]).max() <= 1e-5
+        assert np.abs(align - fx[k + "_align"]).max() <= 1e-6
+
+
+def test_fixture_fp64_drift_is_small():
+    """Every Tacotron2 fixture records its fp32-vs-fp64 drift; the 1e-4 tolerance needs it tiny."""
+    for name in ("taco_sigmoid", "taco_softmax"):
+        fx = load_fixture(name)
+        drifts = [float(fx[k]) for k in fx.files if k.endswith("_drift64")]
+        assert drifts and max(drifts) < 1e-6
