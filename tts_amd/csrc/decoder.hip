@@ -30,84 +30,88 @@
 #include "common.h"
 #include "decoder.h"
 
-struct SegPick {
-  const float* ptr;
-  int ld;
-};
-
-__device__ __forceinline__ SegPick seg_at(const SkJob& J, int kc) {
-  int k = kc * 16;
-  if (J.nseg > 1 && k >= J.seg[0].K) {
-    k -= J.seg[0].K;
-    if (J.nseg > 2 && k >= J.seg[1].K) {
-      k -= J.seg[1].K;
-      return {J.seg[2].ptr + k, J.seg[2].ld};
-    }
-    return {J.seg[1].ptr + k, J.seg[1].ld};
-  }
-  return {J.seg[0].ptr + k, J.seg[0].ld};
-}
-
 template <int MT, int U>
 struct SkFrag {
   f32x4 w[U];
   f32x4 x[U][MT];
 };
 
-// load k-group [kc0, kc0+U) (indices clamped to kc_last: always valid addresses)
-template <int MT, int U>
-__device__ __forceinline__ void sk_load(SkFrag<MT, U>& F, const SkJob& J, const f32x4* Wv, int kc0, int kc_last,
-                                        int row, int kl) {
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    const int kc = min(kc0 + u, kc_last);
-    F.w[u] = Wv[(long)kc * 64];
-    const SegPick sp = seg_at(J, kc);
-    const float* xp = sp.ptr + (long)row * sp.ld + kl;
-#pragma unroll
-    for (int mt = 0; mt < MT; ++mt) F.x[u][mt] = *reinterpret_cast<const f32x4*>(xp + (long)mt * 16 * sp.ld);
-  }
-}
-
-template <int MT, int U>
-__device__ __forceinline__ void sk_mma(const SkFrag<MT, U>& F, int nvalid, f32x4 (&acc)[MT]) {
-#pragma unroll
-  for (int u = 0; u < U; ++u) {
-    if (u < nvalid) {  // wave-uniform
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-        for (int s = 0; s < 4; ++s) acc[mt] = MFMA16(F.x[u][mt][s], F.w[u][s], acc[mt]);
-    }
-  }
-}
-
+// Per-wave k-loop state. Segment bases, boundaries and strides are resolved once into
+// registers: reading SkJob fields inside the loop made hipcc emit a dependent load plus
+// `s_waitcnt vmcnt(0)` before every weight load, draining the pipeline.
 template <int MT, int NTHR = 256>
 struct SkPipe {
   // 1024-thread workgroups are capped at 128 VGPRs: shallower groups, the 4 waves per SIMD hide latency
   static constexpr int U = (NTHR >= 1024 || MT > 2) ? 2 : 4;
-  SkFrag<MT, U> A, B;
+  using Frag = SkFrag<MT, U>;
   const f32x4* Wv;
-  int kc_lo, kc_hi, row, kl;
+  const float* xb0;
+  long d01, d12;  // element offsets xb1 - xb0, xb2 - xb1
+  int ld0, dl01, dl12, e0, e1;
+  int kc_lo, kc_hi;
   __device__ __forceinline__ void init(const SkJob& J, int tile, int w, int KS, int lane) {
     const int nkc = J.K / 16;
     kc_lo = (w * nkc) / KS;
     kc_hi = ((w + 1) * nkc) / KS;
     Wv = reinterpret_cast<const f32x4*>(J.W) + (long)tile * nkc * 64 + lane;
-    row = lane & 15;
-    kl = 4 * (lane >> 4);
+    const int row = lane & 15, kl = 4 * (lane >> 4);
+    // read every field by value first: selecting between member addresses forces the
+    // kernarg struct into scratch
+    const int ns = J.nseg;
+    const float* p0 = J.seg[0].ptr;
+    const float* p1 = J.seg[1].ptr;
+    const float* p2 = J.seg[2].ptr;
+    const int l0 = J.seg[0].ld, l1 = J.seg[1].ld, l2 = J.seg[2].ld;
+    const int k0 = J.seg[0].K, k1 = J.seg[1].K;
+    const int ld1 = ns > 1 ? l1 : l0;
+    const int ld2 = ns > 2 ? l2 : ld1;
+    ld0 = l0;
+    dl01 = ld1 - ld0;
+    dl12 = ld2 - ld1;
+    e0 = k0 / 16;
+    e1 = ns > 1 ? e0 + k1 / 16 : (1 << 30);
+    if (ns < 2) e0 = 1 << 30;
+    xb0 = p0 + (long)row * ld0 + kl;
+    const float* xb1 = (ns > 1 ? p1 : p0) + (long)row * ld1 + kl - (long)e0 * 16;
+    const float* xb2 = (ns > 2 ? p2 : p0) + (long)row * ld2 + kl - (long)e1 * 16;
+    d01 = xb1 - xb0;
+    d12 = xb2 - xb1;
+  }
+  // load k-group [kc0, kc0+U) (indices clamped to the last chunk: always valid addresses)
+  __device__ __forceinline__ void load(SkFrag<MT, U>& F, int kc0) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const int kc = min(kc0 + u, kc_hi - 1);
+      F.w[u] = Wv[(long)kc * 64];
+      // segment select as conditional adds of deltas (a 3-way pointer select became a
+      // scratch lookup table)
+      const long d = (kc >= e0 ? d01 : 0l) + (kc >= e1 ? d12 : 0l);
+      const float* xp = xb0 + d + kc * 16;
+      const int ld = ld0 + (kc >= e0 ? dl01 : 0) + (kc >= e1 ? dl12 : 0);
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) F.x[u][mt] = *reinterpret_cast<const f32x4*>(xp + (long)mt * 16 * ld);
+    }
+  }
+  __device__ __forceinline__ void mma(const SkFrag<MT, U>& F, int nvalid, f32x4 (&acc)[MT]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < nvalid) {  // wave-uniform
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(F.x[u][mt][s], F.w[u][s], acc[mt]);
+      }
+    }
   }
   // first group's loads: issue before anything that waits on memory
-  __device__ __forceinline__ void prefetch(const SkJob& J) {
-    if (kc_hi > kc_lo) sk_load<MT, U>(A, J, Wv, kc_lo, kc_hi - 1, row, kl);
-  }
-  __device__ __forceinline__ void run(const SkJob& J, f32x4 (&acc)[MT]) {
+  __device__ __forceinline__ void prefetch(Frag& A) { load(A, kc_lo); }
+  __device__ __forceinline__ void run(Frag& A, Frag& B, f32x4 (&acc)[MT]) {
     for (int kc0 = kc_lo; kc0 < kc_hi; kc0 += 2 * U) {
-      if (kc0 + U < kc_hi) sk_load<MT, U>(B, J, Wv, kc0 + U, kc_hi - 1, row, kl);
-      sk_mma<MT, U>(A, kc_hi - kc0, acc);
+      if (kc0 + U < kc_hi) load(B, kc0 + U);
+      mma(A, kc_hi - kc0, acc);
       if (kc0 + U >= kc_hi) break;
-      if (kc0 + 2 * U < kc_hi) sk_load<MT, U>(A, J, Wv, kc0 + 2 * U, kc_hi - 1, row, kl);
-      sk_mma<MT, U>(B, kc_hi - kc0 - U, acc);
+      if (kc0 + 2 * U < kc_hi) load(A, kc0 + 2 * U);
+      mma(B, kc_hi - kc0 - U, acc);
     }
   }
 };
@@ -161,21 +165,17 @@ __device__ void stop_h_role(const SkJob& J, int nthr) {
 // --------------------------------------------------------------------------------------
 // generic skinny kernel: NT tiles per workgroup, KS waves per tile, MT batch tiles of 16
 // --------------------------------------------------------------------------------------
+// body of one workgroup for job J (always called with a constant job index so J's fields stay
+// scalar loads from the kernarg segment; a runtime-selected reference made hipcc copy the whole
+// argument struct to scratch)
 template <int NT, int KS, int MT>
-__global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D, int jstep) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
+__device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int jstep, int wg, float* smem) {
   constexpr int Bp = MT * 16;
   constexpr int nthr = NT * KS * 64;
   constexpr int SITEMS = (NT * Bp * 16 + nthr - 1) / nthr;  // store items per thread (<= 4)
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = wave / KS, w = wave % KS;
-  int wg = blockIdx.x, ji = 0;
-  if (A.njobs > 1 && wg >= A.job[0].ntiles / NT) {
-    wg -= A.job[0].ntiles / NT;
-    ji = 1;
-  }
-  const SkJob& J = A.job[ji];
   const int all_done = D.ctl->all_done;
   if (J.stop_h && wg == J.ntiles / NT) {
     if (!all_done) stop_h_role<MT>(J, nthr);
@@ -183,8 +183,9 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
   }
   const int tile = wg * NT + grp;
   SkPipe<MT, nthr> pipe;
+  typename SkPipe<MT, nthr>::Frag fa, fb;
   pipe.init(J, tile, w, KS, lane);
-  pipe.prefetch(J);
+  pipe.prefetch(fa);
   // epilogue operands, fetched under the GEMM
   float eb[SITEMS];
   float lb[4] = {0.f, 0.f, 0.f, 0.f}, la[4] = {0.f, 0.f, 0.f, 0.f}, lc = 0.f;
@@ -220,7 +221,7 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
   f32x4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  pipe.run(J, acc);
+  pipe.run(fa, fb, acc);
   float* part = smem + (long)grp * KS * Bp * 17;
   float* extra = smem + (long)NT * KS * Bp * 17;  // [NT][Bp][16]
   skinny_to_lds<MT>(part, w, lane, acc);
@@ -286,6 +287,16 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
   }
 }
 
+template <int NT, int KS, int MT>
+__global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D, int jstep) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int n0 = A.job[0].ntiles / NT;
+  if (A.njobs > 1 && (int)blockIdx.x >= n0)
+    skinny_body<NT, KS, MT>(A.job[1], D, jstep, (int)blockIdx.x - n0, smem);
+  else
+    skinny_body<NT, KS, MT>(A.job[0], D, jstep, (int)blockIdx.x, smem);
+}
+
 // --------------------------------------------------------------------------------------
 // K1a: stop decision for step t-1 (one workgroup) || prenet layer 1 (16 workgroups)
 // --------------------------------------------------------------------------------------
@@ -342,13 +353,14 @@ __global__ __launch_bounds__(256) void prenet1_stop_kernel(SkArgs A, DecDev D, S
   const SkJob& J = A.job[0];
   const int tile = blockIdx.x;
   SkPipe<MT> pipe;
+  typename SkPipe<MT>::Frag fa, fb;
   pipe.init(J, tile, wave, 4, lane);
-  pipe.prefetch(J);
+  pipe.prefetch(fa);
   if (D.ctl->all_done) return;
   f32x4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  pipe.run(J, acc);
+  pipe.run(fa, fb, acc);
   skinny_to_lds<MT>(smem, wave, lane, acc);
   __syncthreads();
   for (int idx = tid; idx < Bp * 16; idx += 256) {
