@@ -204,7 +204,7 @@ struct MelganModel {
 };
 
 struct MelganWS {
-  DevBuf lens, xa, xb, h, bands;
+  DevBuf lens, xa, xb, bands;
 };
 
 }  // namespace
@@ -843,6 +843,7 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
   auto& G = c->mg;
   const auto& m = c->mg_host;
   G.ready = false;
+  TTS_CHECK(nres >= 1 && nres <= 4, "num_res_blocks must be in [1, 4] (dilation <= 27)");
   G.in_ch = in_ch;
   G.out_ch = out_ch;
   G.base = base;
@@ -949,7 +950,6 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   W.lens.ensure(B * 4);
   W.xa.ensure((size_t)B * maxelems * 4);
   W.xb.ensure((size_t)B * maxelems * 4);
-  W.h.ensure((size_t)B * maxelems * 4);
   std::vector<int> lens(h_lens, h_lens + B);
   HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
   ConvCall cc;
@@ -992,26 +992,25 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     C = Cn;
     Ls = Ln;
     mul *= u;
-    for (int bk = 0; bk < G.nres; ++bk) {
+    for (int bk = 0; bk < G.nres; ++bk) {  // fused ResidualStack blocks (resblock.hip)
       const ConvLayer& dl = G.dconv[i * G.nres + bk];
-      ConvCall d = cc;
-      d.s[0] = src_of(x, (long)C * Ls, Ls, 1, C, 1);
-      d.pad_mode = 1;
-      d.in_mul = d.q_mul = mul;
-      d.max_q = Lb * mul;
-      d.out_mul = 1;
-      d.out = W.h.f();
-      d.ob = (long)C * Ls;
-      d.oc = Ls;
-      d.ot = 1;
-      run_conv(dl, d, s);
-      ConvCall f = d;
-      f.nsrc = 2;
-      f.s[0] = src_of(W.h.f(), (long)C * Ls, Ls, 1, C, 1);
-      f.s[1] = src_of(x, (long)C * Ls, Ls, 1, C, 0);
-      f.pad_mode = 0;
-      f.out = xo;
-      run_conv(G.fused[i * G.nres + bk], f, s);
+      const ConvLayer& fl = G.fused[i * G.nres + bk];
+      ResArgs ra{};
+      ra.x = x;
+      ra.y = xo;
+      ra.sb = (long)C * Ls;
+      ra.Ls = (int)Ls;
+      ra.lens = W.lens.i();
+      ra.len_add = 2 * pad;
+      ra.mul = mul;
+      ra.dil = dl.dil;
+      ra.Wd = dl.W.f();
+      ra.bd = dl.bias.f();
+      ra.Wf = fl.W.f();
+      ra.bf = fl.bias.f();
+      ra.max_q = Lb * mul;
+      ra.B = B;
+      launch_resblock(ra, C, s);
       std::swap(x, xo);
     }
   }

@@ -75,7 +75,7 @@ struct ConvArgs {
 };
 
 // tile configs: TC = output channels per workgroup, TQ = output positions per workgroup
-enum ConvTile { TILE_64x64 = 0, TILE_32x128 = 1, TILE_16x256 = 2 };
+enum ConvTile { TILE_128x64 = 0, TILE_64x64, TILE_192x64, TILE_96x64, TILE_48x128, TILE_80x64, TILE_16x256 };
 int conv_tile_tc(int tile);
 int conv_tile_for_cout(int cout);
 void launch_conv(const ConvArgs& a, int tile, hipStream_t s);
@@ -88,3 +88,21 @@ void swizzle_rows16(const float* Wm, int rows, int rows_pad, int Kdim, float* ds
 void launch_pqmf_synthesis(const float* x, long xb, long xc, const float* G, int N, int taps,
                            const int* lens, int len_add, int L_mul, int maxL, int B, float* y, long yb,
                            hipStream_t s);
+
+// Fused MelGAN ResidualStack block (TTS/vocoder/layers/melgan.py:35-39):
+//   y = [W_1x1 | W_sc] . [lrelu(conv_k3_dil(reflectpad(lrelu(x))) + b_d); x] + (b_1x1 + b_sc)
+struct ResArgs {
+  const float* x;   // (B, C, Ls)
+  float* y;         // (B, C, Ls)
+  long sb;          // batch stride (C * Ls)
+  int Ls;           // channel stride
+  const int* lens;  // base length per utterance
+  int len_add, mul; // L = (lens[b] + len_add) * mul
+  int dil;
+  const float* Wd;  // dilated conv, swizzled rows C, K = 3C
+  const float* bd;
+  const float* Wf;  // [W_1x1 | W_sc], swizzled rows C, K = 2C
+  const float* bf;
+  int max_q, B;
+};
+void launch_resblock(const ResArgs& a, int C, hipStream_t s);

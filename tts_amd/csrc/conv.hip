@@ -1,16 +1,18 @@
 // Generic fp32 MFMA Conv1d / polyphase ConvTranspose1d, and PQMF synthesis (gfx950).
 //
 // Replaces the ATen conv sequences of: ConvBNBlock (TTS/tts/layers/tacotron2.py:9-44),
-// MelGAN generator convs (TTS/vocoder/models/melgan_generator.py:28-78),
-// ResidualStack (TTS/vocoder/layers/melgan.py:5-39) and PQMF.synthesis
-// (TTS/vocoder/layers/pqmf.py:51-56).
+// MelGAN generator convs (TTS/vocoder/models/melgan_generator.py:28-78) and PQMF.synthesis
+// (TTS/vocoder/layers/pqmf.py:51-56). (ResidualStack blocks have their own fused kernel,
+// resblock.hip.)
 //
-// Implicit GEMM: M = output channels, N = output time positions, K = Cin*taps.
-// A (weights) is pre-swizzled into MFMA fragment order so every wave-load is one contiguous
-// 1 KiB float4 read (L2-resident: the largest layer is 5 MB); B (activations) is staged per
-// 16-channel chunk into LDS with padding / reflection / activation resolved at staging time,
-// and read through a per-K offset table so dilation and taps cost no index math in the
-// MFMA loop. v_mfma_f32_16x16x4_f32 keeps exact fp32 numerics.
+// Implicit GEMM: M = output channels, N = output time positions, K = Cin*taps, on
+// v_mfma_f32_16x16x4_f32 (exact fp32). A (weights) is pre-swizzled into MFMA fragment order:
+// one contiguous 1 KiB float4 read per wave instruction, L2-resident, prefetched one k-chunk
+// ahead. B (activations) is staged per 16-input-channel chunk into LDS with padding / reflection
+// / activation resolved at staging time (read through a per-K offset table so taps and dilation
+// cost nothing in the MFMA loop); staging is register double-buffered -- the global loads of chunk
+// c+1 are in flight while chunk c's MFMAs issue -- into two LDS buffers (one barrier per chunk).
+// A wave owns MI x NI 16x16 tiles so each LDS read feeds MI MFMAs and each weight fragment NI.
 #include "common.h"
 #include <stdexcept>
 
@@ -27,10 +29,20 @@ __device__ __forceinline__ int map_pad_index(int i, int L, int mode, bool& valid
   return i < 0 ? 0 : (i >= L ? L - 1 : i);
 }
 
+constexpr int CONV_MAX_SPAN = 7;  // (K-1)*dil of the generic kernel (k <= 7, dilation 1)
+
+template <int MI, int NI, int WM, int WN>
+struct ConvTileCfg {
+  static constexpr int TC = 16 * MI * WM;
+  static constexpr int TQ = 16 * NI * WN;
+  static constexpr int ROWMAX = TQ + CONV_MAX_SPAN + 1;
+  static constexpr int SPT = (16 * ROWMAX + 255) / 256;  // staged elements per thread
+};
+
 template <int MI, int NI, int WM, int WN>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
-  constexpr int TC = 16 * MI * WM;
-  constexpr int TQ = 16 * NI * WN;
+  using Cfg = ConvTileCfg<MI, NI, WM, WN>;
+  constexpr int TC = Cfg::TC, TQ = Cfg::TQ, SPT = Cfg::SPT;
   static_assert(WM * WN == 4, "4 waves per workgroup");
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
@@ -45,13 +57,14 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   const int K = a.K, dil = a.dil;
   const int span = (K - 1) * dil;
   const int ROW = TQ + span + 1;
-  float* X = smem;
-  int* offs = reinterpret_cast<int*>(smem + ((16 * ROW + 3) & ~3));
+  const int XS = (16 * ROW + 3) & ~3;  // one LDS X buffer (floats)
+  float* X0 = smem;
+  float* X1 = smem + XS;
+  int* offs = reinterpret_cast<int*>(smem + 2 * XS);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-
   for (int i = tid; i < 16 * K; i += 256) offs[i] = (i / K) * ROW + (i % K) * dil;
 
   const int i0 = q0 - a.pad_left[ph];
@@ -62,6 +75,55 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   const int qb = wn * 16 * NI + (lane & 15);
   const int g4 = 4 * (lane >> 4);
   const int rawL = a.lens[b];
+  // interior tile: every staged position is inside [0, Lin) and needs no index remapping
+  const bool interior = (a.rep_pad == 0) && i0 >= 0 && i0 + TQ + span <= Lin;
+
+  // this thread's staged (channel, position) pairs, fixed for the whole kernel
+  int sc_[SPT], sp_[SPT];
+#pragma unroll
+  for (int j = 0; j < SPT; ++j) {
+    const int e = tid + 256 * j;
+    sc_[j] = e / ROW;
+    sp_[j] = e - sc_[j] * ROW;
+  }
+  float st[SPT];
+  auto stage_load = [&](int chunk) {
+    const int cbase = chunk * 16;
+    const bool first = cbase < a.src[0].C;
+    const float* sp = first ? a.src[0].ptr : a.src[1].ptr;
+    const long sb = first ? a.src[0].sb : a.src[1].sb;
+    const int ssc = first ? a.src[0].sc : a.src[1].sc;
+    const int sst = first ? a.src[0].st : a.src[1].st;
+    const int cs = first ? cbase : cbase - a.src[0].C;
+    const float* bp = sp + (long)b * sb + (long)cs * ssc;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int c = sc_[j], p = sp_[j];
+      float v = 0.f;
+      if (c < 16 && p < TQ + span) {
+        int i = i0 + p;
+        bool valid = true;
+        if (!interior) {
+          i = map_pad_index(i, Lin, a.pad_mode, valid);
+          if (a.rep_pad) {
+            i -= a.rep_pad;
+            i = i < 0 ? 0 : (i >= rawL ? rawL - 1 : i);
+          }
+        }
+        if (valid) v = bp[(long)c * ssc + (long)i * sst];
+      }
+      st[j] = v;
+    }
+  };
+  auto stage_store = [&](float* X, int chunk) {
+    const int cbase = chunk * 16;
+    const int act = cbase < a.src[0].C ? a.src[0].act : a.src[1].act;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      const int e = tid + 256 * j;
+      if (e < 16 * ROW) X[e] = act ? lrelu02(st[j]) : st[j];
+    }
+  };
 
   f32x4 acc[MI][NI];
 #pragma unroll
@@ -69,39 +131,23 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
+  stage_load(0);
+  f32x4 Anext[MI];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi) Anext[mi] = Wv[((long)(mt0 + mi) * nkc_total + 0) * 64 + lane];
+  stage_store(X0, 0);
+  __syncthreads();
   for (int chunk = 0; chunk < nchunks; ++chunk) {
-    __syncthreads();
-    {  // stage 16 channels x ROW positions
-      const int cbase = chunk * 16;
-      const ConvSrc& S = (cbase < a.src[0].C) ? a.src[0] : a.src[1];
-      const int cs = (cbase < a.src[0].C) ? cbase : cbase - a.src[0].C;
-      const float* sp = S.ptr + (long)b * S.sb;
-      for (int c = wave * 4; c < wave * 4 + 4; ++c) {
-        const float* rowp = sp + (long)(cs + c) * S.sc;
-        for (int p = lane; p < ROW; p += 64) {
-          float v = 0.f;
-          if (p < TQ + span) {
-            bool valid = true;
-            int i = map_pad_index(i0 + p, Lin, a.pad_mode, valid);
-            if (valid) {
-              if (a.rep_pad) {
-                i -= a.rep_pad;
-                i = i < 0 ? 0 : (i >= rawL ? rawL - 1 : i);
-              }
-              v = rowp[(long)i * S.st];
-              if (S.act) v = lrelu02(v);
-            }
-          }
-          X[c * ROW + p] = v;
-        }
-      }
-    }
-    __syncthreads();
+    float* X = (chunk & 1) ? X1 : X0;
+    if (chunk + 1 < nchunks) stage_load(chunk + 1);  // in flight during this chunk's MFMAs
     for (int kq = 0; kq < K; ++kq) {
       const int kc = chunk * K + kq;
       f32x4 A[MI];
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) A[mi] = Wv[((long)(mt0 + mi) * nkc_total + kc) * 64 + lane];
+      for (int mi = 0; mi < MI; ++mi) A[mi] = Anext[mi];
+      const int kn = min(kc + 1, nkc_total - 1);
+#pragma unroll
+      for (int mi = 0; mi < MI; ++mi) Anext[mi] = Wv[((long)(mt0 + mi) * nkc_total + kn) * 64 + lane];
       const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
       const int ov[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -115,11 +161,19 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
           for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
       }
     }
+    if (chunk + 1 < nchunks) stage_store((chunk & 1) ? X0 : X1, chunk + 1);
+    __syncthreads();
   }
 
   // epilogue: bias, activation, optional residual, strided store
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi) {
+    float bias4[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = min(co0 + wm * 16 * MI + mi * 16 + g4 + j, a.Cout - 1);
+      bias4[j] = a.bias[co];
+    }
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) {
       const int q = q0 + qb + ni * 16;
@@ -129,7 +183,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
       for (int j = 0; j < 4; ++j) {
         const int co = co0 + wm * 16 * MI + mi * 16 + g4 + j;
         if (co >= a.Cout) continue;
-        float v = acc[mi][ni][j] + a.bias[co];
+        float v = acc[mi][ni][j] + bias4[j];
         if (a.epi_act == 1) v = fmaxf(v, 0.f);
         else if (a.epi_act == 2) v = tanhf(v);
         if (a.resid) v += a.resid[(long)b * a.rb + (long)co * a.rc + (long)t * a.rt];
@@ -139,12 +193,40 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   }
 }
 
-int conv_tile_tc(int tile) { return tile == TILE_64x64 ? 64 : (tile == TILE_32x128 ? 32 : 16); }
-static int conv_tile_tq(int tile) { return tile == TILE_64x64 ? 64 : (tile == TILE_32x128 ? 128 : 256); }
+// tile catalogue: {MI, NI, WM, WN} -> TC x TQ
+//   TILE_128x64 : 4,2,2,2   (Cout % 128 == 0: 512, 384, 2048, 128)
+//   TILE_64x64  : 2,2,2,2   (Cout % 64 == 0)
+//   TILE_192x64 : 3,4,4,1   (Cout == 192)
+//   TILE_96x64  : 3,2,2,2   (Cout == 96)
+//   TILE_48x128 : 3,2,1,4   (Cout == 48)
+//   TILE_80x64  : 5,1,1,4   (Cout == 80)
+//   TILE_16x256 : 1,4,1,4   (anything else, Cout padded to 16)
+int conv_tile_tc(int tile) {
+  switch (tile) {
+    case TILE_128x64: return 128;
+    case TILE_64x64: return 64;
+    case TILE_192x64: return 192;
+    case TILE_96x64: return 96;
+    case TILE_48x128: return 48;
+    case TILE_80x64: return 80;
+    default: return 16;
+  }
+}
+static int conv_tile_tq(int tile) {
+  switch (tile) {
+    case TILE_48x128: return 128;
+    case TILE_16x256: return 256;
+    default: return 64;
+  }
+}
 
 int conv_tile_for_cout(int cout) {
+  if (cout % 128 == 0) return TILE_128x64;
+  if (cout == 192) return TILE_192x64;
+  if (cout == 96) return TILE_96x64;
+  if (cout == 80) return TILE_80x64;
+  if (cout == 48) return TILE_48x128;
   if (cout % 64 == 0) return TILE_64x64;
-  if (cout % 32 == 0) return TILE_32x128;
   return TILE_16x256;
 }
 
@@ -152,16 +234,20 @@ void launch_conv(const ConvArgs& a, int tile, hipStream_t s) {
   TTS_CHECK(a.Cin % 16 == 0, "conv: Cin must be a multiple of 16");
   TTS_CHECK(a.Cout_pad % conv_tile_tc(tile) == 0, "conv: Cout_pad / tile mismatch");
   TTS_CHECK(a.nphase >= 1 && a.nphase <= 8, "conv: nphase");
+  TTS_CHECK((a.K - 1) * a.dil <= CONV_MAX_SPAN, "conv: receptive span too large for the generic kernel");
   if (a.max_q <= 0 || a.B <= 0) return;
   const int TQ = conv_tile_tq(tile);
   const int span = (a.K - 1) * a.dil;
   const int ROW = TQ + span + 1;
-  const size_t lds = (size_t)(((16 * ROW + 3) & ~3) + 16 * a.K) * 4;
-  TTS_CHECK(lds <= 64 * 1024, "conv: LDS tile too large");
+  const size_t lds = (size_t)(2 * ((16 * ROW + 3) & ~3) + 16 * a.K) * 4;
   dim3 grid((a.max_q + TQ - 1) / TQ, a.Cout_pad / conv_tile_tc(tile), a.B * a.nphase);
   switch (tile) {
+    case TILE_128x64: conv_mfma_kernel<4, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
     case TILE_64x64: conv_mfma_kernel<2, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
-    case TILE_32x128: conv_mfma_kernel<1, 4, 2, 2><<<grid, 256, lds, s>>>(a); break;
+    case TILE_192x64: conv_mfma_kernel<3, 4, 4, 1><<<grid, 256, lds, s>>>(a); break;
+    case TILE_96x64: conv_mfma_kernel<3, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
+    case TILE_48x128: conv_mfma_kernel<3, 2, 1, 4><<<grid, 256, lds, s>>>(a); break;
+    case TILE_80x64: conv_mfma_kernel<5, 1, 1, 4><<<grid, 256, lds, s>>>(a); break;
     default: conv_mfma_kernel<1, 4, 1, 4><<<grid, 256, lds, s>>>(a); break;
   }
   HIP_OK(hipGetLastError());
