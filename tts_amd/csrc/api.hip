@@ -187,6 +187,7 @@ struct TacoWS {
   DevBuf lens, mlens, x0, ca, cb, gin, enc, penc;
   DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, spart, alpha, acum, energy, ctl;
   DevBuf dec, align, stop, pa, pbb;
+  DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
   hipGraphExec_t graph = nullptr;
   long graph_gen = -1;
   int gB = -1, gT = -1, gS = -1, gr = -1;
@@ -441,6 +442,11 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.alpha, (size_t)B * T_max, g);
   grow<float>(W.acum, (size_t)B * T_max, g);
   grow<float>(W.energy, (size_t)B * T_max, g);
+  const int nch = (T_max + 15) / 16;
+  grow<float>(W.aps, (size_t)B * nch, g);
+  grow<float>(W.apm, (size_t)B * nch, g);
+  grow<float>(W.apu, (size_t)B * nch * 512, g);
+  grow<unsigned>(W.acnt, BMAX, g);
   grow<int>(W.ctl, 4 + 4 * BMAX, g);
   grow<float>(W.dec, (size_t)B * S_cap * r * 80, g);
   grow<float>(W.align, (size_t)B * S_cap * T_max, g);
@@ -473,10 +479,11 @@ DecDev make_dev(tts_ctx* c) {
   return d;
 }
 
-SkSeg seg(const float* p, int ld, int K) {
+// columns [k0, k0 + K) of a fragment-order activation with Ktot columns
+SkSeg seg(const float* base, int Ktot, int k0, int K) {
   SkSeg s;
-  s.ptr = p;
-  s.ld = ld;
+  s.ptr = base + (long)(k0 / 16) * 256;
+  s.ms = 16 * Ktot;
   s.K = K;
   return s;
 }
@@ -495,50 +502,37 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
   const int r = W.r, MT = W.MT, YLD = 80 * M.r_init;
   float* hd_cur = (j & 1) ? W.hdec1.f() : W.hdec0.f();
   float* hd_nxt = (j & 1) ? W.hdec0.f() : W.hdec1.f();
-  if (which_only < 0 || which_only == 1) {
+  if (which_only < 0 || which_only == 1) {  // K1: prenet layers 1+2 || stop(t-1)
     SkArgs a{};
-    a.njobs = 1;
+    a.njobs = 2;
     a.MT = MT;
-    SkJob& J = a.job[0] = job0();
-    J.seg[0] = seg(W.y.f() + 80 * (r - 1), YLD, 80);
+    SkJob& J = a.job[0] = job0();  // layer 1 (result kept in LDS)
+    J.seg[0] = seg(W.y.f(), YLD, 80 * (r - 1), 80);
     J.nseg = 1;
     J.K = 80;
     J.W = M.pre1.f();
     J.ntiles = 16;
-    J.epi = EPI_STORE;
-    J.act = 1;
-    J.out = W.p1.f();
-    J.out_ld = 256;
+    SkJob& J2 = a.job[1] = job0();  // layer 2
+    J2.K = 256;
+    J2.W = M.pre2.f();
+    J2.ntiles = 16;
+    J2.out = W.pb.f();
+    J2.out_ld = 256;
+    J2.out_frag = 1;
     StopArgs st{};
     st.part = W.spart.f();
     st.nparts = 5 * M.r_init + 1;
     st.Bp = MT * 16;
     st.bs = M.stop_b;
     st.threshold = W.thr;
-    launch_prenet1_stop(a, d, st, j, s);
+    launch_prenet_stop(a, d, st, j, s);
   }
-  if (which_only < 0 || which_only == 2) {
+  if (which_only < 0 || which_only == 3) {  // K2: attention_rnn + partial query projection
     SkArgs a{};
     a.njobs = 1;
     a.MT = MT;
     SkJob& J = a.job[0] = job0();
-    J.seg[0] = seg(W.p1.f(), 256, 256);
-    J.nseg = 1;
-    J.K = 256;
-    J.W = M.pre2.f();
-    J.ntiles = 16;
-    J.epi = EPI_STORE;
-    J.act = 1;
-    J.out = W.pb.f();
-    J.out_ld = 256;
-    launch_skinny(a, d, j, 1, 4, s);
-  }
-  if (which_only < 0 || which_only == 3) {
-    SkArgs a{};
-    a.njobs = 1;
-    a.MT = MT;
-    SkJob& J = a.job[0] = job0();
-    J.seg[0] = seg(W.pb.f(), 256, 256);
+    J.seg[0] = seg(W.pb.f(), 256, 0, 256);
     J.nseg = 1;
     J.K = 256;
     J.W = M.att_p.f();
@@ -553,7 +547,7 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.pq_part = W.pq.f();
     launch_skinny(a, d, j, 4, 4, s);
   }
-  if (which_only < 0 || which_only == 4) {
+  if (which_only < 0 || which_only == 4) {  // K3: attention
     AttnArgs p{};
     p.pq_part = W.pq.f();
     p.npq = 64;
@@ -568,17 +562,22 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     p.energy = W.energy.f();
     p.enc = W.enc.f();
     p.ctx = W.ctx.f();
+    p.part_s = W.aps.f();
+    p.part_m = W.apm.f();
+    p.part_u = W.apu.f();
+    p.counter = reinterpret_cast<unsigned*>(W.acnt.p);
+    p.nchmax = (W.T_max + 15) / 16;
     p.softmax = M.softmax;
     launch_attention(p, d, j, s);
   }
-  if (which_only < 0 || which_only == 0) {
+  if (which_only < 0 || which_only == 0) {  // K4: decoder_rnn LSTMCell
     SkArgs a{};
-    a.njobs = 2;
+    a.njobs = 1;
     a.MT = MT;
-    SkJob& J = a.job[0] = job0();  // decoder_rnn LSTMCell
-    J.seg[0] = seg(W.hatt.f(), 1024, 1024);
-    J.seg[1] = seg(W.ctx.f(), 512, 512);
-    J.seg[2] = seg(hd_cur, 1024, 1024);
+    SkJob& J = a.job[0] = job0();
+    J.seg[0] = seg(W.hatt.f(), 1024, 0, 1024);
+    J.seg[1] = seg(W.ctx.f(), 512, 0, 512);
+    J.seg[2] = seg(hd_cur, 1024, 0, 1024);
     J.nseg = 3;
     J.K = 2560;
     J.W = M.dec_w.f();
@@ -588,26 +587,15 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.h_out = hd_nxt;
     J.c_state = W.cdec.f();
     J.hc_ld = 1024;
-    SkJob& J2 = a.job[1] = job0();  // next step's attention_rnn ctx/h part (+ biases)
-    J2.seg[0] = seg(W.ctx.f(), 512, 512);
-    J2.seg[1] = seg(W.hatt.f(), 1024, 1024);
-    J2.nseg = 2;
-    J2.K = 1536;
-    J2.W = M.att_pre.f();
-    J2.ntiles = 256;
-    J2.epi = EPI_STORE;
-    J2.bias = M.att_bias.f();
-    J2.out = W.gatt.f();
-    J2.out_ld = 4096;
     launch_skinny(a, d, j, 1, 4, s);
   }
-  if (which_only < 0 || which_only == 5) {
+  if (which_only < 0 || which_only == 5) {  // K5: projection + stop partials || next attention_rnn ctx/h part
     SkArgs a{};
-    a.njobs = 1;
+    a.njobs = 2;
     a.MT = MT;
     SkJob& J = a.job[0] = job0();
-    J.seg[0] = seg(hd_nxt, 1024, 1024);
-    J.seg[1] = seg(W.ctx.f(), 512, 512);
+    J.seg[0] = seg(hd_nxt, 1024, 0, 1024);
+    J.seg[1] = seg(W.ctx.f(), 512, 0, 512);
     J.nseg = 2;
     J.K = 1536;
     J.W = M.proj_w.f();
@@ -616,12 +604,24 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.bias = M.proj_b.f();
     J.out = W.y.f();
     J.out_ld = YLD;
+    J.out_frag = 1;
     J.frames_r = r;
     J.stop_wy = M.stop_w.f() + 1024;
     J.stop_wh = M.stop_w.f();
     J.stop_h = hd_nxt;
     J.stop_part = W.spart.f();
-    launch_skinny(a, d, j, 1, 16, s);
+    SkJob& J2 = a.job[1] = job0();  // (+ biases)
+    J2.seg[0] = seg(W.ctx.f(), 512, 0, 512);
+    J2.seg[1] = seg(W.hatt.f(), 1024, 0, 1024);
+    J2.nseg = 2;
+    J2.K = 1536;
+    J2.W = M.att_pre.f();
+    J2.ntiles = 256;
+    J2.epi = EPI_STORE;
+    J2.bias = M.att_bias.f();
+    J2.out = W.gatt.f();
+    J2.out_ld = 4096;
+    launch_skinny(a, d, j, 1, 8, s);  // 292 workgroups: 512 threads lets two share a CU
   }
 }
 
@@ -753,6 +753,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   HIP_OK(hipMemsetAsync(W.dec.p, 0, (size_t)B * S_cap * r * 80 * 4, s));
   HIP_OK(hipMemsetAsync(W.align.p, 0, (size_t)B * S_cap * T_max * 4, s));
   HIP_OK(hipMemsetAsync(W.stop.p, 0, (size_t)B * S_cap * 4, s));
+  HIP_OK(hipMemsetAsync(W.acnt.p, 0, BMAX * sizeof(unsigned), s));
   bcast_rows_kernel<<<256, 256, 0, s>>>(M.att_bias.f(), 4096, W.gatt.f(), Bp);
   HIP_OK(hipGetLastError());
   // graph for CHUNK steps (+ base advance), cached per configuration / buffer generation

@@ -4,9 +4,18 @@
 
 enum { EPI_STORE = 0, EPI_LSTM = 1 };
 
+// GEMM activations live in HBM in MFMA fragment order so that one wave's A-operand load of a
+// 16 x 16 block is one contiguous 1 KiB (row-major rows made it 16 half-used cache lines per
+// load, the dominant cost of the skinny GEMMs: tools/skinny_bench.hip):
+//   element (m, k) of a (Bp x K) activation is at frag_idx(m, k, K)
+//   = ((m/16 * K/16 + k/16) * 64 + (k%16)/4 * 16 + m%16) * 4 + k%4
+__host__ __device__ inline long frag_idx(int m, int k, int K) {
+  return ((long)((m >> 4) * (K >> 4) + (k >> 4)) * 64 + ((k & 15) >> 2) * 16 + (m & 15)) * 4 + (k & 3);
+}
+
 struct SkSeg {
-  const float* ptr;  // row-major activations, row m at ptr + m*ld
-  int ld;
+  const float* ptr;  // fragment-order activation, at the segment's first 16-column chunk
+  int ms;            // floats between 16-row blocks (= 16 * total columns of the activation)
   int K;             // multiple of 16
 };
 
@@ -21,9 +30,10 @@ struct SkJob {
   const float* bias;   // per swizzled row (tile order)
   const float* addin;  // optional pre-activation addend [m][row]
   int addin_ld;
-  float* out;          // store target [m][row]
+  float* out;          // store target [m][row] (out_frag: fragment order with out_ld columns)
   int out_ld;
-  float* h_out;        // LSTM: h[m][unit]
+  int out_frag;
+  float* h_out;        // LSTM: h, fragment order with hc_ld columns
   float* c_state;      // LSTM: c[m][unit], updated in place
   int hc_ld;
   const float* WqT;    // optional: W_query^T [units][128] for partial query projection
@@ -33,7 +43,7 @@ struct SkJob {
   // w_h . h_dec (computed by one extra workgroup), tiles < ntiles hold w_y[cols] . y[cols]
   const float* stop_wy;  // [ntiles*16]
   const float* stop_wh;  // [1024]
-  const float* stop_h;   // h_dec [Bp][1024]
+  const float* stop_h;   // h_dec, fragment order (1024 columns)
   float* stop_part;
 };
 
@@ -73,23 +83,29 @@ struct StopArgs {
 };
 
 struct AttnArgs {
-  const float* pq_part;
+  const float* pq_part;  // [npq][Bp][128] partial query projections from the attention-LSTM kernel
   int npq;
   int Bp;
-  float* alpha;       // (B, T_max) previous step weights, updated by K3b
+  float* alpha;       // (B, T_max) previous step weights, updated by the combining workgroup
   float* alpha_cum;   // (B, T_max)
   const float* Wloc;  // (32, 2, 31)
   const float* WdT;   // location_dense transposed (32, 128)
   const float* v;     // (128)
   float bv;
   const float* penc;  // (B, T_max, 128)
-  float* energy;      // (B, T_max)
+  float* energy;      // (B, T_max) raw energies
   const float* enc;   // (B, T_max, 512)
   float* ctx;         // (Bp, 512)
+  float* part_s;      // (B, nchmax) chunk sums of sigmoid(e) / exp(e - m_chunk)
+  float* part_m;      // (B, nchmax) chunk max (softmax)
+  float* part_u;      // (B, nchmax, 512) chunk partial contexts
+  unsigned* counter;  // (B) arrivals of the current step (zeroed per call; reset by the last arriver)
+  int nchmax;
   int softmax;
 };
 
 void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s);
-void launch_prenet1_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s);
+// prenet layer 1 + layer 2 in one launch (16 workgroups) plus the stop workgroup
+void launch_prenet_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s);
 void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t s);
 void launch_dec_advance(DecCtl* ctl, int n, hipStream_t s);

@@ -1,21 +1,22 @@
 // Tacotron2 autoregressive decoder step kernels (gfx950).
 //
 // One reference decoder step (TTS/tts/layers/tacotron2.py:354-369 -> decode :259-298) becomes a
-// chain of 7 stream-ordered launches, captured once into a hipGraph of CHUNK steps and
+// chain of 5 stream-ordered launches, captured once into a hipGraph of CHUNK steps and
 // replayed; the step index lives in device memory (DecCtl::base + j) so the same graph serves
 // every chunk, and the reference's per-step host sync (`if stop_token > ...`, :362) becomes a
 // device-side done flag per utterance plus an all_done word that turns every later kernel
 // into an early exit.
 //
-//   K1a  stop(t-1) from the projection kernel's partial dots + done flags
-//        || prenet layer 1 (common_layers.py:76-82)
-//   K1b  prenet layer 2
+//   K1   stop(t-1) from the projection kernel's partial dots + done flags
+//        || prenet layers 1 and 2 (common_layers.py:76-82)
 //   K2   attention_rnn LSTMCell (only the K=256 prenet part; the ctx/h part was precomputed
-//        by K4 of the previous step) + partial query projection (common_layers.py:272)
-//   K3a  location-sensitive energies over T chunks (common_layers.py:268-278, 90-110)
-//   K3b  sigmoid/softmax norm, alpha_cum, alignment, context (common_layers.py:347-366)
-//   K4   decoder_rnn LSTMCell (tacotron2.py:279-282) || next step's attention_rnn ctx/h part
+//        by K5 of the previous step) + partial query projection (common_layers.py:272)
+//   K3   location-sensitive energies over T chunks (common_layers.py:268-278, 90-110), chunk
+//        partial contexts, last-arriving chunk normalises (sigmoid/softmax), updates alpha_cum,
+//        writes the alignment row and the context (common_layers.py:347-366)
+//   K4   decoder_rnn LSTMCell (tacotron2.py:279-282)
 //   K5   linear_projection (tacotron2.py:286-289) + frame store + stopnet partial dots (:291-295)
+//        || next step's attention_rnn ctx/h part (+ biases)
 //
 // All GEMMs are "skinny" (M = batch <= 64): v_mfma_f32_16x16x4_f32 with M = 16 utterances,
 // N = 16 gate rows, weights pre-swizzled into fragment order (one contiguous 1 KiB read per
@@ -30,88 +31,90 @@
 #include "common.h"
 #include "decoder.h"
 
-template <int MT, int U>
+template <int MT, int D>
 struct SkFrag {
-  f32x4 w[U];
-  f32x4 x[U][MT];
+  f32x4 w[D];
+  f32x4 x[D][MT];
 };
 
 // Per-wave k-loop state. Segment bases, boundaries and strides are resolved once into
 // registers: reading SkJob fields inside the loop made hipcc emit a dependent load plus
 // `s_waitcnt vmcnt(0)` before every weight load, draining the pipeline.
-template <int MT, int NTHR = 256>
+//
+// The k-loop is a rolling ring of D chunks: chunk i's MFMAs are followed by the load of chunk
+// i + D into the same registers, so D chunks stay in flight at all times. At M = 32 the MFMAs of
+// one chunk take ~256 cycles per wave and a loaded HBM round trip several microseconds; a
+// two-group pipeline stalled once per group, the ring overlaps the weight stream with the MFMA
+// stream (tools/skinny_bench.hip).
+template <int MT, int NTHR = 256, int DD = 0>
 struct SkPipe {
-  // 1024-thread workgroups are capped at 128 VGPRs: shallower groups, the 4 waves per SIMD hide latency
-  static constexpr int U = (NTHR >= 1024 || MT > 2) ? 2 : 4;
-  using Frag = SkFrag<MT, U>;
+  // measured best at B = 32 (tools/skinny_bench.hip): deeper rings thrash the memory pipeline
+  static constexpr int D = DD > 0 ? DD : NTHR >= 1024 ? 2 : 4;
+  using Frag = SkFrag<MT, D>;
   const f32x4* Wv;
   const float* xb0;
   long d01, d12;  // element offsets xb1 - xb0, xb2 - xb1
-  int ld0, dl01, dl12, e0, e1;
+  int ms0, dm01, dm12, e0, e1;
   int kc_lo, kc_hi;
   __device__ __forceinline__ void init(const SkJob& J, int tile, int w, int KS, int lane) {
     const int nkc = J.K / 16;
     kc_lo = (w * nkc) / KS;
     kc_hi = ((w + 1) * nkc) / KS;
     Wv = reinterpret_cast<const f32x4*>(J.W) + (long)tile * nkc * 64 + lane;
-    const int row = lane & 15, kl = 4 * (lane >> 4);
     // read every field by value first: selecting between member addresses forces the
     // kernarg struct into scratch
     const int ns = J.nseg;
     const float* p0 = J.seg[0].ptr;
     const float* p1 = J.seg[1].ptr;
     const float* p2 = J.seg[2].ptr;
-    const int l0 = J.seg[0].ld, l1 = J.seg[1].ld, l2 = J.seg[2].ld;
+    const int l0 = J.seg[0].ms, l1 = J.seg[1].ms, l2 = J.seg[2].ms;
     const int k0 = J.seg[0].K, k1 = J.seg[1].K;
-    const int ld1 = ns > 1 ? l1 : l0;
-    const int ld2 = ns > 2 ? l2 : ld1;
-    ld0 = l0;
-    dl01 = ld1 - ld0;
-    dl12 = ld2 - ld1;
+    const int ms1 = ns > 1 ? l1 : l0;
+    const int ms2 = ns > 2 ? l2 : ms1;
+    ms0 = l0;
+    dm01 = ms1 - ms0;
+    dm12 = ms2 - ms1;
     e0 = k0 / 16;
     e1 = ns > 1 ? e0 + k1 / 16 : (1 << 30);
     if (ns < 2) e0 = 1 << 30;
-    xb0 = p0 + (long)row * ld0 + kl;
-    const float* xb1 = (ns > 1 ? p1 : p0) + (long)row * ld1 + kl - (long)e0 * 16;
-    const float* xb2 = (ns > 2 ? p2 : p0) + (long)row * ld2 + kl - (long)e1 * 16;
+    // fragment order: chunk kc of 16-row block mt at ptr + mt*ms + kc*256, lane's float4 at +4*lane
+    xb0 = p0 + 4 * lane;
+    const float* xb1 = (ns > 1 ? p1 : p0) + 4 * lane - (long)e0 * 256;
+    const float* xb2 = (ns > 2 ? p2 : p0) + 4 * lane - (long)e1 * 256;
     d01 = xb1 - xb0;
     d12 = xb2 - xb1;
   }
-  // load k-group [kc0, kc0+U) (indices clamped to the last chunk: always valid addresses)
-  __device__ __forceinline__ void load(SkFrag<MT, U>& F, int kc0) {
+  // load chunk kc into ring slot u (index clamped to the last chunk: always a valid address;
+  // the ring's tail re-reads that chunk from cache instead of branching around the loads)
+  __device__ __forceinline__ void load1(Frag& F, int u, int kc_in) {
+    const int kc = min(kc_in, kc_hi - 1);
+    F.w[u] = Wv[(long)kc * 64];
+    // segment select as conditional adds of deltas (a 3-way pointer select became a
+    // scratch lookup table)
+    const long d = (kc >= e0 ? d01 : 0l) + (kc >= e1 ? d12 : 0l);
+    const float* xp = xb0 + d + (long)kc * 256;
+    const int ms = ms0 + (kc >= e0 ? dm01 : 0) + (kc >= e1 ? dm12 : 0);
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const int kc = min(kc0 + u, kc_hi - 1);
-      F.w[u] = Wv[(long)kc * 64];
-      // segment select as conditional adds of deltas (a 3-way pointer select became a
-      // scratch lookup table)
-      const long d = (kc >= e0 ? d01 : 0l) + (kc >= e1 ? d12 : 0l);
-      const float* xp = xb0 + d + kc * 16;
-      const int ld = ld0 + (kc >= e0 ? dl01 : 0) + (kc >= e1 ? dl12 : 0);
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) F.x[u][mt] = *reinterpret_cast<const f32x4*>(xp + (long)mt * 16 * ld);
-    }
+    for (int mt = 0; mt < MT; ++mt) F.x[u][mt] = *reinterpret_cast<const f32x4*>(xp + (long)mt * ms);
   }
-  __device__ __forceinline__ void mma(const SkFrag<MT, U>& F, int nvalid, f32x4 (&acc)[MT]) {
+  __device__ __forceinline__ void mma1(const Frag& F, int u, f32x4 (&acc)[MT]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < nvalid) {  // wave-uniform
+    for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int s = 0; s < 4; ++s)
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(F.x[u][mt][s], F.w[u][s], acc[mt]);
+  }
+  // the ring's first D loads: issue before anything that waits on memory
+  __device__ __forceinline__ void prefetch(Frag& F) {
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(F.x[u][mt][s], F.w[u][s], acc[mt]);
+    for (int u = 0; u < D; ++u) load1(F, u, kc_lo + u);
+  }
+  __device__ __forceinline__ void run(Frag& F, f32x4 (&acc)[MT]) {
+    for (int kc0 = kc_lo; kc0 < kc_hi; kc0 += D) {
+#pragma unroll
+      for (int u = 0; u < D; ++u) {
+        if (kc0 + u < kc_hi) mma1(F, u, acc);  // wave-uniform
+        load1(F, u, kc0 + D + u);
       }
-    }
-  }
-  // first group's loads: issue before anything that waits on memory
-  __device__ __forceinline__ void prefetch(Frag& A) { load(A, kc_lo); }
-  __device__ __forceinline__ void run(Frag& A, Frag& B, f32x4 (&acc)[MT]) {
-    for (int kc0 = kc_lo; kc0 < kc_hi; kc0 += 2 * U) {
-      if (kc0 + U < kc_hi) load(B, kc0 + U);
-      mma(A, kc_hi - kc0, acc);
-      if (kc0 + U >= kc_hi) break;
-      if (kc0 + 2 * U < kc_hi) load(A, kc0 + 2 * U);
-      mma(B, kc_hi - kc0 - U, acc);
     }
   }
 };
@@ -150,10 +153,9 @@ __device__ void stop_h_role(const SkJob& J, int nthr) {
 #pragma unroll
   for (int i = 0; i < 16; ++i) w[i] = J.stop_wh[lane + 64 * i];
   for (int m = wave; m < Bp; m += nw) {
-    const float* h = J.stop_h + (long)m * 1024;
     float x[16];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = h[lane + 64 * i];
+    for (int i = 0; i < 16; ++i) x[i] = J.stop_h[frag_idx(m, lane + 64 * i, 1024)];
     float s = 0.f;
 #pragma unroll
     for (int i = 0; i < 16; ++i) s = fmaf(w[i], x[i], s);
@@ -168,60 +170,73 @@ __device__ void stop_h_role(const SkJob& J, int nthr) {
 // body of one workgroup for job J (always called with a constant job index so J's fields stay
 // scalar loads from the kernarg segment; a runtime-selected reference made hipcc copy the whole
 // argument struct to scratch)
-template <int NT, int KS, int MT>
+template <int NT, int KS, int MT, int DD = 0>
 __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int jstep, int wg, float* smem) {
   constexpr int Bp = MT * 16;
   constexpr int nthr = NT * KS * 64;
-  constexpr int SITEMS = (NT * Bp * 16 + nthr - 1) / nthr;  // store items per thread (<= 4)
+  constexpr int SITEMS = (NT * Bp * 16 + nthr - 1) / nthr;  // store items per thread
+  constexpr int LITEMS = (NT * Bp * 4 + nthr - 1) / nthr;   // LSTM (utterance, unit) items per thread
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int grp = wave / KS, w = wave % KS;
   const int all_done = D.ctl->all_done;
-  if (J.stop_h && wg == J.ntiles / NT) {
-    if (!all_done) stop_h_role<MT>(J, nthr);
-    return;
-  }
   const int tile = wg * NT + grp;
-  SkPipe<MT, nthr> pipe;
-  typename SkPipe<MT, nthr>::Frag fa, fb;
+  SkPipe<MT, nthr, DD> pipe;
+  typename SkPipe<MT, nthr, DD>::Frag fa;
   pipe.init(J, tile, w, KS, lane);
   pipe.prefetch(fa);
-  // epilogue operands, fetched under the GEMM
+  // epilogue operands, fetched under the GEMM (indices clamped: no guarded loads); a 1024-thread
+  // workgroup at MT = 4 is out of registers for that and fetches them after the k-loop
+  constexpr bool EPRE = !(nthr >= 1024 && MT >= 4);
   float eb[SITEMS];
-  float lb[4] = {0.f, 0.f, 0.f, 0.f}, la[4] = {0.f, 0.f, 0.f, 0.f}, lc = 0.f;
-  float wq[4 * NT];
-  if (J.epi == EPI_STORE) {
+  float lb[LITEMS][4], la[LITEMS][4], lc[LITEMS];
+  auto load_epi = [&]() {
+    if (J.epi == EPI_STORE) {
 #pragma unroll
-    for (int i = 0; i < SITEMS; ++i) {
-      const int idx = min(tid + i * nthr, NT * Bp * 16 - 1);
-      const int g = idx / (Bp * 16), n = idx % 16;
-      eb[i] = J.bias ? J.bias[(wg * NT + g) * 16 + n] : 0.f;
-    }
-  } else {
-    const int idx = min(tid, NT * Bp * 4 - 1);
-    const int g = idx / (Bp * 4), rem = idx % (Bp * 4);
-    const int m = rem / 4, u = rem % 4;
-    const int tl = wg * NT + g;
+      for (int i = 0; i < SITEMS; ++i) {
+        const int idx = min(tid + i * nthr, NT * Bp * 16 - 1);
+        const int g = idx / (Bp * 16), n = idx % 16;
+        eb[i] = J.bias ? J.bias[(wg * NT + g) * 16 + n] : 0.f;
+      }
+    } else {
 #pragma unroll
-    for (int q = 0; q < 4; ++q) {
-      const int col = tl * 16 + q * 4 + u;
-      if (J.bias) lb[q] = J.bias[col];
-      if (J.addin) la[q] = J.addin[(long)m * J.addin_ld + col];
+      for (int i = 0; i < LITEMS; ++i) {
+        const int idx = min(tid + i * nthr, NT * Bp * 4 - 1);
+        const int g = idx / (Bp * 4), rem = idx % (Bp * 4);
+        const int m = rem / 4, u = rem % 4;
+        const int tl = wg * NT + g;
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int col = tl * 16 + q * 4 + u;
+          lb[i][q] = J.bias ? J.bias[col] : 0.f;
+          la[i][q] = J.addin ? J.addin[(long)m * J.addin_ld + col] : 0.f;
+        }
+        lc[i] = J.c_state[(long)m * J.hc_ld + tl * 4 + u];
+      }
     }
-    lc = J.c_state[(long)m * J.hc_ld + tl * 4 + u];
+  };
+  if (EPRE) load_epi();
+  // query-projection weights of this workgroup's 4*NT units for attention dim tid % 128
+  float wqv[4 * NT];
+  auto load_wq = [&]() {
     if (J.pq_part) {
-      const int a = tid % 128;
+      const float* wq = J.WqT + (long)(wg * NT * 4) * 128 + tid % 128;
 #pragma unroll
-      for (int u2 = 0; u2 < 4 * NT; ++u2) wq[u2] = J.WqT[(long)(wg * NT * 4 + u2) * 128 + a];
+      for (int u = 0; u < 4 * NT; ++u) wqv[u] = wq[(long)u * 128];
     }
-  }
+  };
+  if (EPRE) load_wq();
   if (all_done) return;
   const int t = D.ctl->base + jstep;
 
   f32x4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  pipe.run(fa, fb, acc);
+  pipe.run(fa, acc);
+  if (!EPRE) {
+    load_epi();
+    load_wq();
+  }
   float* part = smem + (long)grp * KS * Bp * 17;
   float* extra = smem + (long)NT * KS * Bp * 17;  // [NT][Bp][16]
   skinny_to_lds<MT>(part, w, lane, acc);
@@ -237,7 +252,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
       const int col = (wg * NT + g) * 16 + n;
       float v = skinny_sum<KS, Bp>(smem + (long)g * KS * Bp * 17, m, n) + eb[i];
       if (J.act == 1) v = fmaxf(v, 0.f);
-      J.out[(long)m * J.out_ld + col] = v;
+      J.out[J.out_frag ? frag_idx(m, col, J.out_ld) : (long)m * J.out_ld + col] = v;
       if (J.frames_r > 0 && m < D.B && col < 80 * J.frames_r && t < D.S_cap && !D.done[m])
         D.dec_out[((long)m * D.S_cap + t) * J.frames_r * 80 + col] = v;
       if (J.stop_part) extra[idx] = v * J.stop_wy[col];
@@ -255,62 +270,77 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
     }
   } else {  // EPI_LSTM: tile rows are gate-major [i0..i3 f0..f3 g0..g3 o0..o3] of 4 units
     float* hs = extra;  // [Bp][4*NT]
-    if (tid < NT * Bp * 4) {
-      const int g = tid / (Bp * 4), rem = tid % (Bp * 4);
+#pragma unroll
+    for (int i = 0; i < LITEMS; ++i) {
+      const int idx = tid + i * nthr;
+      if (idx >= NT * Bp * 4) break;
+      const int g = idx / (Bp * 4), rem = idx % (Bp * 4);
       const int m = rem / 4, u = rem % 4;
       const int tl = wg * NT + g;
       const float* pg = smem + (long)g * KS * Bp * 17;
       float pre[4];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) pre[q] = skinny_sum<KS, Bp>(pg, m, q * 4 + u) + lb[q] + la[q];
+      for (int q = 0; q < 4; ++q) pre[q] = skinny_sum<KS, Bp>(pg, m, q * 4 + u) + lb[i][q] + la[i][q];
       const long ci = (long)m * J.hc_ld + tl * 4 + u;
       const float ig = 1.f / (1.f + expf(-pre[0]));
       const float fg = 1.f / (1.f + expf(-pre[1]));
       const float gg = tanhf(pre[2]);
       const float og = 1.f / (1.f + expf(-pre[3]));
-      const float c = fg * lc + ig * gg;
+      const float c = fg * lc[i] + ig * gg;
       const float h = og * tanhf(c);
       J.c_state[ci] = c;
-      J.h_out[ci] = h;
+      J.h_out[frag_idx(m, tl * 4 + u, J.hc_ld)] = h;
       hs[m * 4 * NT + g * 4 + u] = h;
     }
     if (J.pq_part) {  // partial query projection over this workgroup's 4*NT hidden units
+      static_assert(nthr % 128 == 0, "pq: one attention dim per thread");
+      const int a = tid % 128;
       __syncthreads();
-      for (int idx = tid; idx < Bp * 128; idx += nthr) {
-        const int m = idx / 128, a = idx % 128;
+      for (int m = tid / 128; m < Bp; m += nthr / 128) {
         float s = 0.f;
 #pragma unroll
-        for (int u = 0; u < 4 * NT; ++u) s = fmaf(wq[u], hs[m * 4 * NT + u], s);
+        for (int u = 0; u < 4 * NT; ++u) s = fmaf(wqv[u], hs[m * 4 * NT + u], s);
         J.pq_part[((long)wg * Bp + m) * 128 + a] = s;
       }
     }
   }
 }
 
-template <int NT, int KS, int MT>
+// grid = job0 tiles/NT  [+ job1 tiles/NT]  [+ 1 stopnet-h workgroup if job0.stop_h]
+template <int NT, int KS, int MT, int DD = 0>
 __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D, int jstep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
   const int n0 = A.job[0].ntiles / NT;
-  if (A.njobs > 1 && (int)blockIdx.x >= n0)
-    skinny_body<NT, KS, MT>(A.job[1], D, jstep, (int)blockIdx.x - n0, smem);
-  else
-    skinny_body<NT, KS, MT>(A.job[0], D, jstep, (int)blockIdx.x, smem);
+  const int n1 = A.njobs > 1 ? A.job[1].ntiles / NT : 0;
+  const int bx = blockIdx.x;
+  if (bx < n0) {
+    skinny_body<NT, KS, MT, DD>(A.job[0], D, jstep, bx, smem);
+  } else if (bx < n0 + n1) {
+    skinny_body<NT, KS, MT, DD>(A.job[1], D, jstep, bx - n0, smem);
+  } else if (A.job[0].stop_h) {
+    if (!D.ctl->all_done) stop_h_role<MT>(A.job[0], NT * KS * 64);
+  }
 }
 
 // --------------------------------------------------------------------------------------
-// K1a: stop decision for step t-1 (one workgroup) || prenet layer 1 (16 workgroups)
+// K1: prenet (both layers) || stop decision for step t-1.
+//   Workgroups 0..15: each recomputes prenet layer 1 for all utterances (16 waves, one 16-wide
+//   tile each, K = 80) into LDS, then its own 16 columns of layer 2 (K = 256 split over the 16
+//   waves, operand from LDS). Recomputing layer 1 (0.65 M MAC) per workgroup is cheaper than the
+//   launch boundary it removes.
+//   Workgroup 16: stop logit = sum of the projection kernel's partial dots + b_s; sigma;
+//   reference stop rule (tacotron2.py:357-366): stop iff sigma > thr and t > 0, else stop when
+//   max_decoder_steps outputs exist.
 // --------------------------------------------------------------------------------------
 constexpr int NPARTS_MAX = 64;
+constexpr int P1LD = 260;  // LDS row stride of the layer-1 activations (bank-conflict padding)
 
 template <int MT>
-__global__ __launch_bounds__(256) void prenet1_stop_kernel(SkArgs A, DecDev D, StopArgs S, int jstep) {
+__global__ __launch_bounds__(1024) void prenet_stop_kernel(SkArgs A, DecDev D, StopArgs S, int jstep) {
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   extern __shared__ __attribute__((aligned(16))) float smem[];
   constexpr int Bp = MT * 16;
-  if (blockIdx.x == A.job[0].ntiles) {
-    // ---- stop role: logit = sum of the projection kernel's partial dots + b_s; sigma;
-    //      reference stop rule (tacotron2.py:357-366): stop iff sigma > thr and t > 0,
-    //      else stop when max_decoder_steps outputs exist. One thread per utterance.
+  if (blockIdx.x == 16) {
     __shared__ int dflag[64];
     const int m = min(tid, Bp - 1);
     float pv[NPARTS_MAX];
@@ -349,43 +379,84 @@ __global__ __launch_bounds__(256) void prenet1_stop_kernel(SkArgs A, DecDev D, S
     }
     return;
   }
-  // ---- prenet layer 1: relu(W1 . memory) with memory = y[:, 80(r-1):80r] (go frame = 0) ----
-  const SkJob& J = A.job[0];
-  const int tile = blockIdx.x;
-  SkPipe<MT> pipe;
-  typename SkPipe<MT>::Frag fa, fb;
-  pipe.init(J, tile, wave, 4, lane);
+  const SkJob& J1 = A.job[0];  // layer 1: 16 tiles, K = 80, X = y[:, 80(r-1):80r]
+  const SkJob& J2 = A.job[1];  // layer 2: tile blockIdx.x, K = 256, X from LDS
+  float* P1 = smem;                           // [Bp][P1LD]
+  float* part = smem + Bp * P1LD;             // [16][Bp][17]
+  const int n2 = blockIdx.x;
+  // layer-2 weight fragment of this wave (one k-chunk per wave) and layer-1 pipeline, issued first
+  const f32x4 w2 = reinterpret_cast<const f32x4*>(J2.W)[((long)n2 * 16 + wave) * 64 + lane];
+  SkPipe<MT, 1024> pipe;
+  typename SkPipe<MT, 1024>::Frag fa;
+  pipe.init(J1, wave, 0, 1, lane);
   pipe.prefetch(fa);
   if (D.ctl->all_done) return;
   f32x4 acc[MT];
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
-  pipe.run(fa, fb, acc);
-  skinny_to_lds<MT>(smem, wave, lane, acc);
+  pipe.run(fa, acc);
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      P1[(mt * 16 + 4 * (lane >> 4) + j) * P1LD + wave * 16 + (lane & 15)] = fmaxf(acc[mt][j], 0.f);
   __syncthreads();
-  for (int idx = tid; idx < Bp * 16; idx += 256) {
+  // layer 2, k-chunk `wave`
+#pragma unroll
+  for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  {
+    const int row = lane & 15, kl = 4 * (lane >> 4);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const f32x4 xv = *reinterpret_cast<const f32x4*>(P1 + (mt * 16 + row) * P1LD + wave * 16 + kl);
+#pragma unroll
+      for (int s = 0; s < 4; ++s) acc[mt] = MFMA16(xv[s], w2[s], acc[mt]);
+    }
+  }
+  skinny_to_lds<MT>(part, wave, lane, acc);
+  __syncthreads();
+  for (int idx = tid; idx < Bp * 16; idx += 1024) {
     const int m = idx / 16, n = idx % 16;
-    const float v = skinny_sum<4, Bp>(smem, m, n);
-    J.out[(long)m * J.out_ld + tile * 16 + n] = fmaxf(v, 0.f);
+    const float v = skinny_sum<16, Bp>(part, m, n);
+    J2.out[frag_idx(m, n2 * 16 + n, J2.out_ld)] = fmaxf(v, 0.f);
   }
 }
 
 // --------------------------------------------------------------------------------------
-// K3a: energies e[b][t] for a chunk of TCH encoder positions
+// K3: location-sensitive attention in one launch.
+//   Workgroup (chunk of TCH encoder positions, utterance): energies e_t (common_layers.py:268-278,
+//   90-110), then chunk-local sigmoid(e) / exp(e - m_chunk), the chunk sum and the chunk's
+//   unnormalised context sum_t s_t enc_t. The last workgroup of the utterance to arrive
+//   (agent-scope release/acquire counter, cdna_hip_programming.md §6 Guideline 16 split-K recipe)
+//   combines: S = sum of chunk sums, ctx = sum U_c / S, alpha_t = s_t / S, alpha_cum += alpha,
+//   alignment row (common_layers.py:347-366).
 // --------------------------------------------------------------------------------------
 constexpr int TCH = 16;
 constexpr int LOCK = 31, LOCF = 32, ADIM = 128, NPQ = 64;
 
-__global__ __launch_bounds__(256) void attn_energy_kernel(AttnArgs P, DecDev D) {
+#ifdef ATTN_TRACE_BUF
+// phase timestamps (s_memrealtime, 100 MHz) of every workgroup, tools/skinny_bench.hip only
+__device__ unsigned long long attn_trace[64 * 64 * 9];
+#define ATTN_TRACE(k) \
+  if (threadIdx.x == 0) attn_trace[((long)blockIdx.y * gridDim.x + blockIdx.x) * 9 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define ATTN_TRACE(k)
+#endif
+
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs P, DecDev D, int jstep) {
+  ATTN_TRACE(0);
   const int b = blockIdx.y;
-  const int t0 = blockIdx.x * TCH;
+  const int ch = blockIdx.x;
+  const int t0 = ch * TCH;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int a = tid & 127, grp = tid >> 7;
   __shared__ float red[2][ADIM];
   __shared__ float A0[TCH + LOCK], A1[TCH + LOCK];
   __shared__ float Wl[LOCF * 2 * LOCK];
-  __shared__ float f[LOCF][TCH];
-  __shared__ float er[2][TCH];
+  __shared__ __attribute__((aligned(16))) float f[TCH][LOCF + 4];  // [position][filter]
+  __shared__ float zb[TCH][ADIM + 4];
+  __shared__ float sv[TCH];
+  __shared__ int is_last;
   const int Bp = P.Bp;
   const int T = D.lens[b];
   const int Tm1 = max(T - 1, 0);
@@ -403,7 +474,7 @@ __global__ __launch_bounds__(256) void attn_energy_kernel(AttnArgs P, DecDev D) 
   float pp[NPQ / 2];
 #pragma unroll
   for (int i = 0; i < NPQ / 2; ++i) pp[i] = P.pq_part[((long)(grp * (NPQ / 2) + i) * Bp + b) * ADIM + a];
-  float a0 = 0.f, a1 = 0.f;
+  float a0, a1;
   {
     const int pos = t0 - (LOCK - 1) / 2 + min(tid, TCH + LOCK - 2);
     const int pc = min(max(pos, 0), Tm1);
@@ -414,7 +485,15 @@ __global__ __launch_bounds__(256) void attn_energy_kernel(AttnArgs P, DecDev D) 
   float wl[(LOCF * 2 * LOCK + 255) / 256];
 #pragma unroll
   for (int i = 0; i < (LOCF * 2 * LOCK + 255) / 256; ++i) wl[i] = P.Wloc[min(tid + 256 * i, LOCF * 2 * LOCK - 1)];
+  // encoder rows of this chunk for the partial context: dims tid and tid + 256
+  float2 ev[TCH];  // dims 2*tid, 2*tid + 1
+#pragma unroll
+  for (int i = 0; i < TCH; ++i) {
+    const int t = min(t0 + i, Tm1);
+    ev[i] = *reinterpret_cast<const float2*>(P.enc + ((long)b * D.T_max + t) * 512 + 2 * tid);
+  }
   if (D.ctl->all_done || D.done[b] || t0 >= T) return;
+  const int t_step = D.ctl->base + jstep;
   if (tid < TCH + LOCK - 1) {
     A0[tid] = a0;
     A1[tid] = a1;
@@ -422,127 +501,179 @@ __global__ __launch_bounds__(256) void attn_energy_kernel(AttnArgs P, DecDev D) 
 #pragma unroll
   for (int i = 0; i < (LOCF * 2 * LOCK + 255) / 256; ++i)
     if (tid + 256 * i < LOCF * 2 * LOCK) Wl[tid + 256 * i] = wl[i];
-  // query projection = sum of the attention-LSTM kernel's 64 partials (fixed order)
+  // query projection = sum of the attention-LSTM kernel's partials (fixed order)
   float s = 0.f;
 #pragma unroll
   for (int i = 0; i < NPQ / 2; ++i) s += pp[i];
   red[grp][a] = s;
   __syncthreads();
+  ATTN_TRACE(1);
   const float pqa = red[0][a] + red[1][a];
-  // location conv: f[c][tt] = sum_i sum_k Wl[c][i][k] * A_i[tt + k]
-  for (int idx = tid; idx < LOCF * TCH; idx += 256) {
-    const int c = idx / TCH, tt = idx % TCH;
-    float sc = 0.f;
+  // location conv: f[tt][c] = sum_i sum_k Wl[c][i][k] * A_i[tt + k]; each thread two adjacent
+  // positions of one filter, sliding the window in registers (one A read per tap)
+  {
+    const int c = tid >> 3, tt = (tid & 7) * 2;
     const float* w0 = Wl + c * 2 * LOCK;
+    float s0 = 0.f, s1 = 0.f;
+    float an = A0[tt];
 #pragma unroll
-    for (int k = 0; k < LOCK; ++k) sc = fmaf(w0[k], A0[tt + k], sc);
+    for (int k = 0; k < LOCK; ++k) {
+      const float a_k = an;
+      an = A0[tt + k + 1];
+      s0 = fmaf(w0[k], a_k, s0);
+      s1 = fmaf(w0[k], an, s1);
+    }
+    an = A1[tt];
 #pragma unroll
-    for (int k = 0; k < LOCK; ++k) sc = fmaf(w0[LOCK + k], A1[tt + k], sc);
-    f[c][tt] = sc;
+    for (int k = 0; k < LOCK; ++k) {
+      const float a_k = an;
+      an = A1[tt + k + 1];
+      s0 = fmaf(w0[LOCK + k], a_k, s0);
+      s1 = fmaf(w0[LOCK + k], an, s1);
+    }
+    f[tt][c] = s0;
+    f[tt + 1][c] = s1;
   }
   __syncthreads();
-  // loc = W_dense . f ; e = v . tanh(pq + loc + penc) + b_v
+  ATTN_TRACE(2);
+  // loc = W_dense . f ; e = v . tanh(pq + loc + penc) + b_v. Each thread owns one attention dim
+  // for 8 positions; the sum over dims goes through LDS (position-major, 16 lanes per position)
+  // instead of 8 serial 64-lane shuffle reductions
 #pragma unroll
   for (int i = 0; i < TCH / 2; ++i) {
     const int tt = grp * (TCH / 2) + i;
     float l = 0.f;
 #pragma unroll
-    for (int c = 0; c < LOCF; ++c) l = fmaf(wd[c], f[c][tt], l);
-    float z = (t0 + tt < T) ? tanhf(pqa + l + pen[i]) * va : 0.f;
-    z = wave_sum(z);
-    if (lane == 0) er[wave & 1][tt] = z;
-  }
-  __syncthreads();
-  if (tid < TCH && t0 + tid < T) P.energy[(long)b * D.T_max + t0 + tid] = er[0][tid] + er[1][tid] + P.bv;
-}
-
-// --------------------------------------------------------------------------------------
-// K3b: normalisation, alignment, alpha_cum and the context vector (slice of 128 dims)
-// --------------------------------------------------------------------------------------
-__device__ __forceinline__ float block_reduce(float v, float* wred, bool is_max) {
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+    for (int c4 = 0; c4 < LOCF / 4; ++c4) {
+      const f32x4 fv = *reinterpret_cast<const f32x4*>(&f[tt][c4 * 4]);
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1) {
-    const float o = __shfl_xor(v, off, 64);
-    v = is_max ? fmaxf(v, o) : v + o;
+      for (int q = 0; q < 4; ++q) l = fmaf(wd[c4 * 4 + q], fv[q], l);
+    }
+    zb[tt][a] = tanhf(pqa + l + pen[i]) * va;
   }
   __syncthreads();
-  if (lane == 0) wred[wave] = v;
-  __syncthreads();
-  return is_max ? fmaxf(fmaxf(wred[0], wred[1]), fmaxf(wred[2], wred[3]))
-                : (wred[0] + wred[1]) + (wred[2] + wred[3]);
-}
-
-constexpr int CTX_PRE = 4;  // encoder rows per thread prefetched before the normalisation
-
-__global__ __launch_bounds__(256) void attn_context_kernel(AttnArgs P, DecDev D, int jstep) {
-  const int b = blockIdx.y, slice = blockIdx.x;
-  const int tid = threadIdx.x;
-  extern __shared__ __attribute__((aligned(16))) float al[];  // [T_max]
-  __shared__ float wred[4];
-  __shared__ f32x4 cr[8][32];
-  const int T = D.lens[b];
-  const int Tm1 = max(T - 1, 0);
-  const int d4 = tid & 31, g = tid >> 5;
-  const f32x4* enc = reinterpret_cast<const f32x4*>(P.enc + (long)b * D.T_max * 512 + slice * 128) + d4;
-  // prefetch: first energies and the first encoder rows of this thread's context slice
-  const float* e = P.energy + (long)b * D.T_max;
-  float e0 = e[min(tid, Tm1)];
-  f32x4 ep[CTX_PRE];
+  ATTN_TRACE(3);
+  const int nvalid = min(TCH, T - t0);
+  const long pidx = (long)b * P.nchmax + ch;
+  {
+    const int pos = tid >> 4, j = tid & 15;
+    float z = 0.f;
 #pragma unroll
-  for (int i = 0; i < CTX_PRE; ++i) ep[i] = enc[(long)min(g + 8 * i, Tm1) * 128];
-  if (D.ctl->all_done || D.done[b]) return;
-  const int t_step = D.ctl->base + jstep;
-  if (tid < T) al[tid] = e0;
-  for (int t = tid + 256; t < T; t += 256) al[t] = e[t];
-  __syncthreads();
-  float mx = 0.f;
-  if (P.softmax) {
-    float m = -INFINITY;
-    for (int t = tid; t < T; t += 256) m = fmaxf(m, al[t]);
-    mx = block_reduce(m, wred, true);
-  }
-  float s = 0.f;
-  for (int t = tid; t < T; t += 256) {
-    const float x = al[t];
-    const float v = P.softmax ? expf(x - mx) : 1.f / (1.f + expf(-x));
-    al[t] = v;
-    s += v;
-  }
-  const float S = block_reduce(s, wred, false);
-  for (int t = tid; t < T; t += 256) {
-    const float a = al[t] / S;
-    al[t] = a;
-    if (slice == 0) {
-      P.alpha[(long)b * D.T_max + t] = a;
-      P.alpha_cum[(long)b * D.T_max + t] += a;
-      if (t_step < D.S_cap) D.align_out[((long)b * D.S_cap + t_step) * D.T_max + t] = a;
+    for (int q = 0; q < ADIM / 16; ++q) z += zb[pos][j * (ADIM / 16) + q];
+#pragma unroll
+    for (int off = 8; off > 0; off >>= 1) z += __shfl_xor(z, off, 64);
+    if (j == 0) {
+      const float e = z + P.bv;
+      if (pos < nvalid)
+        __hip_atomic_store(P.energy + (long)b * D.T_max + t0 + pos, e, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      sv[pos] = e;
     }
   }
   __syncthreads();
-  // context slice: ctx[b][slice*128 + d] = sum_t a_t * enc[b][t][slice*128 + d]
-  f32x4 c = {0.f, 0.f, 0.f, 0.f};
+  ATTN_TRACE(4);
+  // chunk-local normalisation terms
+  float m_c = -INFINITY;
+  if (P.softmax)
+    for (int i = 0; i < nvalid; ++i) m_c = fmaxf(m_c, sv[i]);
+  float sl[TCH];
+  float S_c = 0.f;
 #pragma unroll
-  for (int i = 0; i < CTX_PRE; ++i)
-    if (g + 8 * i < T) c += al[g + 8 * i] * ep[i];
-  int t = g + 8 * CTX_PRE;
-  for (; t + 24 < T; t += 32) {
-    const f32x4 x0 = enc[(long)t * 128], x1 = enc[(long)(t + 8) * 128];
-    const f32x4 x2 = enc[(long)(t + 16) * 128], x3 = enc[(long)(t + 24) * 128];
-    c += al[t] * x0;
-    c += al[t + 8] * x1;
-    c += al[t + 16] * x2;
-    c += al[t + 24] * x3;
+  for (int i = 0; i < TCH; ++i) {
+    const float e = sv[i];
+    const float x = P.softmax ? expf(e - m_c) : 1.f / (1.f + expf(-e));
+    sl[i] = i < nvalid ? x : 0.f;
+    S_c += sl[i];
   }
-  for (; t < T; t += 8) c += al[t] * enc[(long)t * 128];
-  cr[g][d4] = c;
+  // unnormalised partial context of this chunk (dims 2*tid, 2*tid + 1)
+  float u0 = 0.f, u1 = 0.f;
+#pragma unroll
+  for (int i = 0; i < TCH; ++i) {
+    u0 = fmaf(sl[i], ev[i].x, u0);
+    u1 = fmaf(sl[i], ev[i].y, u1);
+  }
+  // ---- publish: sc1 (write-through) stores need no release fence (cdna_hip_programming.md
+  // §5 split-K item 2); every wave drains, barrier, then one relaxed agent-scope ticket ----
+  {
+    union {
+      float2 f;
+      unsigned long long u;
+    } pk;
+    pk.f = make_float2(u0, u1);
+    __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.part_u + pidx * 512) + tid, pk.u, __ATOMIC_RELAXED,
+                       __HIP_MEMORY_SCOPE_AGENT);
+  }
+  if (tid == 0) {
+    __hip_atomic_store(P.part_s + pidx, S_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(P.part_m + pidx, m_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
-  if (tid < 32) {
-    f32x4 r = cr[0][tid];
-#pragma unroll
-    for (int k = 1; k < 8; ++k) r += cr[k][tid];
-    *reinterpret_cast<f32x4*>(P.ctx + (long)b * 512 + slice * 128 + 4 * tid) = r;
+  ATTN_TRACE(5);
+  const int nch = (T + TCH - 1) / TCH;
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(&P.counter[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    is_last = (prev == (unsigned)(nch - 1));
+    if (is_last) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
   }
+  __syncthreads();
+  ATTN_TRACE(6);
+  if (!is_last) return;
+  // ---- combine (one workgroup per utterance): chunk partials in batches of CB, all loads of a
+  // batch in flight together (clamped), online rescaling for softmax ----
+  const long pb = (long)b * P.nchmax;
+  constexpr int CB = 16;
+  float m = -INFINITY, S = 0.f, c0 = 0.f, c1 = 0.f;
+  for (int cb = 0; cb < nch; cb += CB) {
+    float pm[CB], ps[CB], pu0[CB], pu1[CB];
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const long c = pb + min(cb + i, nch - 1);
+      pm[i] = P.part_m[c];
+      ps[i] = P.part_s[c];
+      const float2 pu = *reinterpret_cast<const float2*>(P.part_u + c * 512 + 2 * tid);
+      pu0[i] = pu.x;
+      pu1[i] = pu.y;
+    }
+    float wc[CB];
+    if (P.softmax) {
+      float mb = m;
+#pragma unroll
+      for (int i = 0; i < CB; ++i)
+        if (cb + i < nch) mb = fmaxf(mb, pm[i]);
+      const float sc = (m == -INFINITY) ? 0.f : expf(m - mb);
+      S *= sc;
+      c0 *= sc;
+      c1 *= sc;
+      m = mb;
+#pragma unroll
+      for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch) ? expf(pm[i] - m) : 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch) ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      S = fmaf(ps[i], wc[i], S);
+      c0 = fmaf(pu0[i], wc[i], c0);
+      c1 = fmaf(pu1[i], wc[i], c1);
+    }
+  }
+  ATTN_TRACE(7);
+  P.ctx[frag_idx(b, 2 * tid, 512)] = c0 / S;
+  P.ctx[frag_idx(b, 2 * tid + 1, 512)] = c1 / S;
+  const float* en = P.energy + (long)b * D.T_max;
+  for (int t = tid; t < T; t += 256) {
+    const float e = en[t];
+    const float al = (P.softmax ? expf(e - m) : 1.f / (1.f + expf(-e))) / S;
+    P.alpha[(long)b * D.T_max + t] = al;
+    P.alpha_cum[(long)b * D.T_max + t] += al;
+    if (t_step < D.S_cap) D.align_out[((long)b * D.S_cap + t_step) * D.T_max + t] = al;
+  }
+  if (tid == 0) P.counter[b] = 0u;  // next step (ordered by the kernel boundary)
+  ATTN_TRACE(8);
 }
 
 __global__ void dec_advance_kernel(DecCtl* ctl, int n) {
@@ -569,40 +700,38 @@ static void launch_skinny_nt(const SkArgs& a, const DecDev& d, int jstep, int nw
 
 void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s) {
   TTS_CHECK(a.MT >= 1 && a.MT <= 4, "skinny: MT in [1,4]");
-  for (int j = 0; j < a.njobs; ++j) {
-    TTS_CHECK(a.job[j].ntiles % NT == 0, "skinny: ntiles % NT");
-    if (a.job[j].epi == EPI_LSTM) TTS_CHECK(NT * a.MT * 16 * 4 <= NT * KS * 64, "skinny: LSTM items per thread");
-  }
+  for (int j = 0; j < a.njobs; ++j) TTS_CHECK(a.job[j].ntiles % NT == 0, "skinny: ntiles % NT");
   int nwg = a.job[0].ntiles / NT + (a.njobs > 1 ? a.job[1].ntiles / NT : 0);
-  if (a.njobs == 1 && a.job[0].stop_h) nwg += 1;
+  if (a.job[0].stop_h) nwg += 1;
   if (NT == 1 && KS == 4) launch_skinny_nt<1, 4>(a, d, jstep, nwg, s);
+  else if (NT == 1 && KS == 8) launch_skinny_nt<1, 8>(a, d, jstep, nwg, s);
   else if (NT == 1 && KS == 16) launch_skinny_nt<1, 16>(a, d, jstep, nwg, s);
   else if (NT == 4 && KS == 4) launch_skinny_nt<4, 4>(a, d, jstep, nwg, s);
   else TTS_CHECK(false, "skinny: unsupported tile config");
   HIP_OK(hipGetLastError());
 }
 
-void launch_prenet1_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s) {
+void launch_prenet_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s) {
   TTS_CHECK(a.MT >= 1 && a.MT <= 4, "prenet: MT in [1,4]");
+  TTS_CHECK(a.njobs == 2 && a.job[0].ntiles == 16 && a.job[1].ntiles == 16 && a.job[1].K == 256,
+            "prenet: expects 256-wide layers");
   TTS_CHECK(st.nparts >= 1 && st.nparts <= NPARTS_MAX, "stop: too many partials (r_init <= 12)");
-  const size_t lds = skinny_lds(1, 4, a.MT * 16);
-  const int g = a.job[0].ntiles + 1;
+  const int Bp = a.MT * 16;
+  const size_t lds = ((size_t)Bp * P1LD + (size_t)16 * Bp * 17) * 4;
   switch (a.MT) {
-    case 1: prenet1_stop_kernel<1><<<g, 256, lds, s>>>(a, d, st, jstep); break;
-    case 2: prenet1_stop_kernel<2><<<g, 256, lds, s>>>(a, d, st, jstep); break;
-    case 3: prenet1_stop_kernel<3><<<g, 256, lds, s>>>(a, d, st, jstep); break;
-    default: prenet1_stop_kernel<4><<<g, 256, lds, s>>>(a, d, st, jstep); break;
+    case 1: prenet_stop_kernel<1><<<17, 1024, lds, s>>>(a, d, st, jstep); break;
+    case 2: prenet_stop_kernel<2><<<17, 1024, lds, s>>>(a, d, st, jstep); break;
+    case 3: prenet_stop_kernel<3><<<17, 1024, lds, s>>>(a, d, st, jstep); break;
+    default: prenet_stop_kernel<4><<<17, 1024, lds, s>>>(a, d, st, jstep); break;
   }
   HIP_OK(hipGetLastError());
 }
 
 void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t s) {
   TTS_CHECK(p.npq == NPQ, "attention: expects 64 query partials");
-  dim3 g1((d.T_max + TCH - 1) / TCH, d.B);
-  attn_energy_kernel<<<g1, 256, 0, s>>>(p, d);
-  HIP_OK(hipGetLastError());
-  dim3 g2(4, d.B);
-  attn_context_kernel<<<g2, 256, (size_t)d.T_max * 4, s>>>(p, d, jstep);
+  TTS_CHECK(p.nchmax * TCH >= d.T_max, "attention: partial buffers too small");
+  dim3 g((d.T_max + TCH - 1) / TCH, d.B);
+  attn_kernel<<<g, 256, 0, s>>>(p, d, jstep);
   HIP_OK(hipGetLastError());
 }
 
