@@ -266,28 +266,27 @@ int main(int argc, char** argv) {
     k4(skinny_kernel<1, 8, 2, 8>, 8, "K4 store-epi <1,8> U=2");
     a4 = keep;
   }
-  // K5: projection (35 tiles + stop-h WG) || att-pre store (256 tiles), K = 1536
-  SkArgs a5{};
-  a5.njobs = 2;
-  a5.MT = MT;
+  // K5: projection (stopnet tile + 10 frame tiles) || att-pre store (256 tiles), K = 1536
+  SkArgs pj{}, ap{};
+  pj.njobs = ap.njobs = 1;
+  pj.MT = ap.MT = MT;
   {
-    SkJob& J = a5.job[0];
+    SkJob& J = pj.job[0];
     J.seg[0] = {hd1, 16 * 1024, 1024};
     J.seg[1] = {ctx, 16 * 512, 512};
     J.nseg = 2;
     J.K = 1536;
     J.W = Wproj;
-    J.ntiles = 35;
+    J.ntiles = 11;
     J.epi = EPI_STORE;
     J.bias = bias;
     J.out = y;
     J.out_ld = 560;
+    J.out_frag = 1;
     J.frames_r = 2;
-    J.stop_wy = stw + 1024;
-    J.stop_wh = stw;
-    J.stop_h = hd1;
+    J.lead_stop = 1;
     J.stop_part = spart;
-    SkJob& J2 = a5.job[1];
+    SkJob& J2 = ap.job[0];
     J2.seg[0] = {ctx, 16 * 512, 512};
     J2.seg[1] = {hatt, 16 * 1024, 1024};
     J2.nseg = 2;
@@ -299,43 +298,34 @@ int main(int argc, char** argv) {
     J2.out = gatt;
     J2.out_ld = 4096;
   }
-  const double b5 = (35.0 + 256) * 16 * 1536 * 4;
-  auto k5 = [&](auto kern, int KS, const char* name) {
-    const size_t lds = skinny_lds(1, KS, Bp);
-    rep(name, time_graph([&] { kern<<<292, KS * 64, lds, S>>>(a5, d, 0); }), b5);
-  };
+  SkArgs both5 = pj;
+  both5.njobs = 2;
+  both5.job[1] = ap.job[0];
+  SkArgs both4 = a4;
+  both4.njobs = 2;
+  both4.job[1] = ap.job[0];
+  const double bpj = 11.0 * 16 * 1536 * 4, bap = 256.0 * 16 * 1536 * 4;
   if (MT == 2) {
-    k5(skinny_kernel<1, 4, 2, 8>, 4, "K5 <1,4> D=8");
-    k5(skinny_kernel<1, 4, 2, 12>, 4, "K5 <1,4> D=12");
-    k5(skinny_kernel<1, 8, 2, 4>, 8, "K5 <1,8> D=4");
-    k5(skinny_kernel<1, 8, 2, 6>, 8, "K5 <1,8> D=6");
-    k5(skinny_kernel<1, 16, 2, 3>, 16, "K5 <1,16> D=3");
-    k5(skinny_kernel<1, 16, 2, 6>, 16, "K5 <1,16> D=6");
-    SkArgs keep = a5;
-    a5.job[0].stop_h = nullptr;
-    auto k5b = [&](auto kern, int KS, const char* name, int nwg) {
-      const size_t lds = skinny_lds(1, KS, Bp);
-      rep(name, time_graph([&] { kern<<<nwg, KS * 64, lds, S>>>(a5, d, 0); }), b5);
-    };
-    k5b(skinny_kernel<1, 4, 2, 12>, 4, "K5 no-stop-h <1,4> U=4", 291);
-    k5b(skinny_kernel<1, 8, 2, 4>, 8, "K5 no-stop-h <1,8> U=2", 291);
-    a5.njobs = 1;
-    a5.job[0] = keep.job[0];
-    k5b(skinny_kernel<1, 4, 2, 12>, 4, "K5 proj only <1,4> U=4", 36);
-    a5.job[0].stop_h = nullptr;
-    a5.job[0].stop_part = nullptr;
-    a5.job[0].frames_r = 0;
-    k5b(skinny_kernel<1, 4, 2, 12>, 4, "K5 proj plain store <1,4> U=4", 35);
-    a5.njobs = 2;
-    a5.job[0] = keep.job[1];
-    a5.job[1] = keep.job[0];
-    a5.job[1].stop_h = nullptr;
-    k5b(skinny_kernel<1, 4, 2, 12>, 4, "K5 att-pre first <1,4> U=4", 291);
-    a5.njobs = 1;
-    a5.job[0] = keep.job[1];
-    k5b(skinny_kernel<1, 4, 2, 12>, 4, "K5 att-pre only <1,4> U=4", 256);
-    k5b(skinny_kernel<1, 8, 2, 4>, 8, "K5 att-pre only <1,8> U=2", 256);
-    a5 = keep;
+    rep("proj <1,4>", time_graph([&] { skinny_kernel<1, 4, 2, 0><<<11, 256, skinny_lds(1, 4, Bp), S>>>(pj, d, 0); }), bpj);
+    rep("proj <1,8>", time_graph([&] { skinny_kernel<1, 8, 2, 0><<<11, 512, skinny_lds(1, 8, Bp), S>>>(pj, d, 0); }), bpj);
+    rep("proj <1,16>", time_graph([&] { skinny_kernel<1, 16, 2, 0><<<11, 1024, skinny_lds(1, 16, Bp), S>>>(pj, d, 0); }), bpj);
+    rep("att-pre <1,4>", time_graph([&] { skinny_kernel<1, 4, 2, 0><<<256, 256, skinny_lds(1, 4, Bp), S>>>(ap, d, 0); }), bap);
+    rep("att-pre <1,8>", time_graph([&] { skinny_kernel<1, 8, 2, 0><<<256, 512, skinny_lds(1, 8, Bp), S>>>(ap, d, 0); }), bap);
+    rep("proj + att-pre <1,8>", time_graph([&] { skinny_kernel<1, 8, 2, 0><<<267, 512, skinny_lds(1, 8, Bp), S>>>(both5, d, 0); }), bpj + bap);
+    rep("proj + att-pre <1,4>", time_graph([&] { skinny_kernel<1, 4, 2, 0><<<267, 256, skinny_lds(1, 4, Bp), S>>>(both5, d, 0); }), bpj + bap);
+    rep("K4 + att-pre <1,4>", time_graph([&] { skinny_kernel<1, 4, 2, 0><<<512, 256, skinny_lds(1, 4, Bp), S>>>(both4, d, 0); }), wbytes + bap);
+    rep("K4 ; proj+att-pre <1,8>", time_graph([&] {
+          skinny_kernel<1, 4, 2, 0><<<256, 256, skinny_lds(1, 4, Bp), S>>>(a4, d, 0);
+          skinny_kernel<1, 8, 2, 0><<<267, 512, skinny_lds(1, 8, Bp), S>>>(both5, d, 0);
+        }), wbytes + bpj + bap);
+    rep("K4+att-pre ; proj <1,16>", time_graph([&] {
+          skinny_kernel<1, 4, 2, 0><<<512, 256, skinny_lds(1, 4, Bp), S>>>(both4, d, 0);
+          skinny_kernel<1, 16, 2, 0><<<11, 1024, skinny_lds(1, 16, Bp), S>>>(pj, d, 0);
+        }), wbytes + bpj + bap);
+    rep("K4+att-pre ; proj <1,8>", time_graph([&] {
+          skinny_kernel<1, 4, 2, 0><<<512, 256, skinny_lds(1, 4, Bp), S>>>(both4, d, 0);
+          skinny_kernel<1, 8, 2, 0><<<11, 512, skinny_lds(1, 8, Bp), S>>>(pj, d, 0);
+        }), wbytes + bpj + bap);
   }
   // K2: attention LSTM prenet part K = 256 + pq partials
   SkArgs a2{};

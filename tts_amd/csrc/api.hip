@@ -177,8 +177,8 @@ struct TacoModel {
   DevBuf emb;
   ConvLayer enc[3], lstm_in, penc, post[5];
   DevBuf whhT;
-  DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b, stop_w;
-  float bv = 0.f, stop_b = 0.f;
+  DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b;
+  float bv = 0.f;
 };
 
 struct TacoWS {
@@ -390,10 +390,28 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
   }
   {
     const int NP = F * r_init;
-    M.proj_w.upload(swz(need(h, "decoder.linear_projection.linear_layer.weight", {NP, D + E}).d, NP, D + E));
-    M.proj_b.upload(need(h, "decoder.linear_projection.linear_layer.bias", {NP}).d);
-    M.stop_w.upload(need(h, "decoder.stopnet.1.linear_layer.weight", {1, D + NP}).d);
-    M.stop_b = need(h, "decoder.stopnet.1.linear_layer.bias", {1}).d[0];
+    const auto& wp = need(h, "decoder.linear_projection.linear_layer.weight", {NP, D + E}).d;
+    const auto& bp = need(h, "decoder.linear_projection.linear_layer.bias", {NP}).d;
+    const auto& ws = need(h, "decoder.stopnet.1.linear_layer.weight", {1, D + NP}).d;
+
+    // stopnet folded through the projection (tacotron2.py:286-295, the stopnet sees all r_init
+    // frames): stop = [w_h + W_p,h^T w_y | W_p,ctx^T w_y] . [h | ctx] + (b_s + w_y . b_p)
+    std::vector<double> sw(D + E, 0.0);
+    for (int k = 0; k < D; ++k) sw[k] = ws[k];
+    double sb = need(h, "decoder.stopnet.1.linear_layer.bias", {1}).d[0];
+    for (int o = 0; o < NP; ++o) {
+      const double wy = ws[D + o];
+      for (int k = 0; k < D + E; ++k) sw[k] += wy * wp[(size_t)o * (D + E) + k];
+      sb += wy * bp[o];
+    }
+    // projection weight with the stopnet tile in front: rows [w_stop, 0 x 15, W_p]
+    std::vector<float> wx((size_t)(16 + NP) * (D + E), 0.f), bx(16 + NP, 0.f);
+    for (int k = 0; k < D + E; ++k) wx[k] = (float)sw[k];
+    std::copy(wp.begin(), wp.end(), wx.begin() + (size_t)16 * (D + E));
+    bx[0] = (float)sb;
+    std::copy(bp.begin(), bp.end(), bx.begin() + 16);
+    M.proj_w.upload(swz(wx, 16 + NP, D + E));
+    M.proj_b.upload(bx);
   }
   const int pc[6] = {F, 512, 512, 512, 512, F};
   for (int i = 0; i < 5; ++i) {
@@ -438,7 +456,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.ctx, (size_t)Bp * 512, g);
   grow<float>(W.y, (size_t)Bp * 80 * c->taco.r_init, g);
   grow<float>(W.pq, (size_t)64 * Bp * 128, g);
-  grow<float>(W.spart, (size_t)(5 * c->taco.r_init + 1) * Bp, g);
+  grow<float>(W.spart, (size_t)Bp, g);
   grow<float>(W.alpha, (size_t)B * T_max, g);
   grow<float>(W.acum, (size_t)B * T_max, g);
   grow<float>(W.energy, (size_t)B * T_max, g);
@@ -521,9 +539,6 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J2.out_frag = 1;
     StopArgs st{};
     st.part = W.spart.f();
-    st.nparts = 5 * M.r_init + 1;
-    st.Bp = MT * 16;
-    st.bs = M.stop_b;
     st.threshold = W.thr;
     launch_prenet_stop(a, d, st, j, s);
   }
@@ -589,7 +604,7 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.hc_ld = 1024;
     launch_skinny(a, d, j, 1, 4, s);
   }
-  if (which_only < 0 || which_only == 5) {  // K5: projection + stop partials || next attention_rnn ctx/h part
+  if (which_only < 0 || which_only == 5) {  // K5: projection + stop logit || next attention_rnn ctx/h part
     SkArgs a{};
     a.njobs = 2;
     a.MT = MT;
@@ -599,16 +614,14 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.nseg = 2;
     J.K = 1536;
     J.W = M.proj_w.f();
-    J.ntiles = 5 * M.r_init;
+    J.ntiles = 1 + 5 * r;  // stopnet tile + the first r frames (tacotron2.py:297)
     J.epi = EPI_STORE;
     J.bias = M.proj_b.f();
     J.out = W.y.f();
     J.out_ld = YLD;
     J.out_frag = 1;
     J.frames_r = r;
-    J.stop_wy = M.stop_w.f() + 1024;
-    J.stop_wh = M.stop_w.f();
-    J.stop_h = hd_nxt;
+    J.lead_stop = 1;
     J.stop_part = W.spart.f();
     SkJob& J2 = a.job[1] = job0();  // (+ biases)
     J2.seg[0] = seg(W.ctx.f(), 512, 0, 512);
@@ -621,7 +634,7 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J2.bias = M.att_bias.f();
     J2.out = W.gatt.f();
     J2.out_ld = 4096;
-    launch_skinny(a, d, j, 1, 8, s);  // 292 workgroups: 512 threads lets two share a CU
+    launch_skinny(a, d, j, 1, 4, s);
   }
 }
 

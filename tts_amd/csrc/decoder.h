@@ -39,12 +39,11 @@ struct SkJob {
   const float* WqT;    // optional: W_query^T [units][128] for partial query projection
   float* pq_part;      // [workgroup][Bp][128]
   int frames_r;        // projection: write the first 80*r columns as frames of active utts
-  // projection only: stopnet partial dot products, stop_part[tile][Bp]; tile == ntiles holds
-  // w_h . h_dec (computed by one extra workgroup), tiles < ntiles hold w_y[cols] . y[cols]
-  const float* stop_wy;  // [ntiles*16]
-  const float* stop_wh;  // [1024]
-  const float* stop_h;   // h_dec, fragment order (1024 columns)
-  float* stop_part;
+  // projection only: the stopnet logit is linear in [h_dec | ctx] once the projection is folded
+  // in (stop = w_h.h + w_y.(W_p [h|ctx] + b_p) + b_s), so the folded 1536-vector is row 0 of a
+  // leading weight tile (rows 1-15 zero) and its output, bias included, is the logit
+  int lead_stop;         // tile 0 is the stopnet tile; outputs of later tiles shift by 16 rows
+  float* stop_part;      // [Bp] stop logits
 };
 
 struct SkArgs {
@@ -75,10 +74,7 @@ struct DecDev {
 };
 
 struct StopArgs {
-  const float* part;  // stop_part [nparts][Bp] written by the projection kernel
-  int nparts;
-  int Bp;
-  float bs;
+  const float* part;  // stop logits [Bp] written by the projection kernel
   float threshold;
 };
 

@@ -144,26 +144,6 @@ __device__ __forceinline__ float wave_sum(float v) {
   return v;
 }
 
-// stopnet h-part: stop_part[ntiles][m] = w_h . h_dec[m]   (one extra workgroup of the projection)
-template <int MT>
-__device__ void stop_h_role(const SkJob& J, int nthr) {
-  constexpr int Bp = MT * 16;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = nthr / 64;
-  float w[16];
-#pragma unroll
-  for (int i = 0; i < 16; ++i) w[i] = J.stop_wh[lane + 64 * i];
-  for (int m = wave; m < Bp; m += nw) {
-    float x[16];
-#pragma unroll
-    for (int i = 0; i < 16; ++i) x[i] = J.stop_h[frag_idx(m, lane + 64 * i, 1024)];
-    float s = 0.f;
-#pragma unroll
-    for (int i = 0; i < 16; ++i) s = fmaf(w[i], x[i], s);
-    s = wave_sum(s);
-    if (lane == 0) J.stop_part[(long)J.ntiles * Bp + m] = s;
-  }
-}
-
 // --------------------------------------------------------------------------------------
 // generic skinny kernel: NT tiles per workgroup, KS waves per tile, MT batch tiles of 16
 // --------------------------------------------------------------------------------------
@@ -249,24 +229,19 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
       if (idx >= NT * Bp * 16) break;
       const int g = idx / (Bp * 16), rem = idx % (Bp * 16);
       const int m = rem / 16, n = rem % 16;
-      const int col = (wg * NT + g) * 16 + n;
+      int col = (wg * NT + g) * 16 + n;
       float v = skinny_sum<KS, Bp>(smem + (long)g * KS * Bp * 17, m, n) + eb[i];
       if (J.act == 1) v = fmaxf(v, 0.f);
+      if (J.lead_stop) {
+        if (col < 16) {
+          if (n == 0) J.stop_part[m] = v;
+          continue;
+        }
+        col -= 16;
+      }
       J.out[J.out_frag ? frag_idx(m, col, J.out_ld) : (long)m * J.out_ld + col] = v;
       if (J.frames_r > 0 && m < D.B && col < 80 * J.frames_r && t < D.S_cap && !D.done[m])
         D.dec_out[((long)m * D.S_cap + t) * J.frames_r * 80 + col] = v;
-      if (J.stop_part) extra[idx] = v * J.stop_wy[col];
-    }
-    if (J.stop_part) {
-      __syncthreads();
-      for (int idx = tid; idx < NT * Bp; idx += nthr) {
-        const int g = idx / Bp, m = idx % Bp;
-        const float* e = extra + ((long)g * Bp + m) * 16;
-        float s = e[0];
-#pragma unroll
-        for (int n = 1; n < 16; ++n) s += e[n];
-        J.stop_part[(long)(wg * NT + g) * Bp + m] = s;
-      }
     }
   } else {  // EPI_LSTM: tile rows are gate-major [i0..i3 f0..f3 g0..g3 o0..o3] of 4 units
     float* hs = extra;  // [Bp][4*NT]
@@ -306,7 +281,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
   }
 }
 
-// grid = job0 tiles/NT  [+ job1 tiles/NT]  [+ 1 stopnet-h workgroup if job0.stop_h]
+// grid = job0 tiles/NT  [+ job1 tiles/NT]
 template <int NT, int KS, int MT, int DD = 0>
 __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D, int jstep) {
   extern __shared__ __attribute__((aligned(16))) float smem[];
@@ -317,8 +292,6 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
     skinny_body<NT, KS, MT, DD>(A.job[0], D, jstep, bx, smem);
   } else if (bx < n0 + n1) {
     skinny_body<NT, KS, MT, DD>(A.job[1], D, jstep, bx - n0, smem);
-  } else if (A.job[0].stop_h) {
-    if (!D.ctl->all_done) stop_h_role<MT>(A.job[0], NT * KS * 64);
   }
 }
 
@@ -328,11 +301,10 @@ __global__ __launch_bounds__(NT * KS * 64) void skinny_kernel(SkArgs A, DecDev D
 //   tile each, K = 80) into LDS, then its own 16 columns of layer 2 (K = 256 split over the 16
 //   waves, operand from LDS). Recomputing layer 1 (0.65 M MAC) per workgroup is cheaper than the
 //   launch boundary it removes.
-//   Workgroup 16: stop logit = sum of the projection kernel's partial dots + b_s; sigma;
+//   Workgroup 16: stop logit from the projection launch's stopnet tile; sigma;
 //   reference stop rule (tacotron2.py:357-366): stop iff sigma > thr and t > 0, else stop when
 //   max_decoder_steps outputs exist.
 // --------------------------------------------------------------------------------------
-constexpr int NPARTS_MAX = 64;
 constexpr int P1LD = 260;  // LDS row stride of the layer-1 activations (bank-conflict padding)
 
 template <int MT>
@@ -343,9 +315,7 @@ __global__ __launch_bounds__(1024) void prenet_stop_kernel(SkArgs A, DecDev D, S
   if (blockIdx.x == 16) {
     __shared__ int dflag[64];
     const int m = min(tid, Bp - 1);
-    float pv[NPARTS_MAX];
-#pragma unroll
-    for (int p = 0; p < NPARTS_MAX; ++p) pv[p] = S.part[(long)min(p, S.nparts - 1) * S.Bp + m];
+    const float pv = S.part[m];
     const int dn0 = D.done[m];
     const int mx = D.max_steps[m];
     const int all_done = D.ctl->all_done;
@@ -354,11 +324,7 @@ __global__ __launch_bounds__(1024) void prenet_stop_kernel(SkArgs A, DecDev D, S
     if (tid < D.B) {
       int dn = dn0;
       if (t >= 1 && !dn) {
-        float s = 0.f;
-#pragma unroll
-        for (int p = 0; p < NPARTS_MAX; ++p)
-          if (p < S.nparts) s += pv[p];
-        const float logit = s + S.bs;
+        const float logit = pv;
         const float sg = 1.f / (1.f + expf(-logit));
         if (t - 1 < D.S_cap) D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
         const bool st = (sg > S.threshold) && (t - 1) > 0;
@@ -702,7 +668,6 @@ void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, 
   TTS_CHECK(a.MT >= 1 && a.MT <= 4, "skinny: MT in [1,4]");
   for (int j = 0; j < a.njobs; ++j) TTS_CHECK(a.job[j].ntiles % NT == 0, "skinny: ntiles % NT");
   int nwg = a.job[0].ntiles / NT + (a.njobs > 1 ? a.job[1].ntiles / NT : 0);
-  if (a.job[0].stop_h) nwg += 1;
   if (NT == 1 && KS == 4) launch_skinny_nt<1, 4>(a, d, jstep, nwg, s);
   else if (NT == 1 && KS == 8) launch_skinny_nt<1, 8>(a, d, jstep, nwg, s);
   else if (NT == 1 && KS == 16) launch_skinny_nt<1, 16>(a, d, jstep, nwg, s);
@@ -715,7 +680,6 @@ void launch_prenet_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, in
   TTS_CHECK(a.MT >= 1 && a.MT <= 4, "prenet: MT in [1,4]");
   TTS_CHECK(a.njobs == 2 && a.job[0].ntiles == 16 && a.job[1].ntiles == 16 && a.job[1].K == 256,
             "prenet: expects 256-wide layers");
-  TTS_CHECK(st.nparts >= 1 && st.nparts <= NPARTS_MAX, "stop: too many partials (r_init <= 12)");
   const int Bp = a.MT * 16;
   const size_t lds = ((size_t)Bp * P1LD + (size_t)16 * Bp * 17) * 4;
   switch (a.MT) {
