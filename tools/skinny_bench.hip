@@ -392,6 +392,18 @@ int main(int argc, char** argv) {
       char name[64];
       snprintf(name, sizeof(name), "K3 attention T=%d %s", T, sm ? "softmax" : "sigmoid");
       rep(name, time_graph([&] { launch_attention(p, da, 0, S); }), 1.0);
+      if (T == 168 && MT == 2) {
+        SkArgs one = a4;
+        rep("   attention + K4 (K=2560) one launch", time_graph([&] { launch_attn_gemm(p, one, da, 0, S); }), 1.0);
+        SkArgs two = a4;
+        two.njobs = 2;
+        two.job[1] = ap.job[0];
+        rep("   attention + K4 + att-pre one launch", time_graph([&] { launch_attn_gemm(p, two, da, 0, S); }), 1.0);
+        rep("   attention ; K4 serial", time_graph([&] {
+              launch_attention(p, da, 0, S);
+              skinny_kernel<1, 4, 2, 0><<<256, 256, skinny_lds(1, 4, Bp), S>>>(a4, d, 0);
+            }), 1.0);
+      }
       // one traced launch: phase durations (us) averaged over workgroups
       std::vector<unsigned long long> tr(64 * 64 * 9, 0);
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(attn_trace), tr.data(), tr.size() * 8));

@@ -104,4 +104,6 @@ void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, 
 // prenet layer 1 + layer 2 in one launch (16 workgroups) plus the stop workgroup
 void launch_prenet_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s);
 void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t s);
+// attention (grid flattened: utterance-major chunks) + <1,4> skinny GEMM jobs in one launch
+void launch_attn_gemm(const AttnArgs& p, const SkArgs& a, const DecDev& d, int jstep, hipStream_t s);
 void launch_dec_advance(DecCtl* ctl, int n, hipStream_t s);

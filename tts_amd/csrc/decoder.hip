@@ -404,15 +404,14 @@ constexpr int LOCK = 31, LOCF = 32, ADIM = 128, NPQ = 64;
 // phase timestamps (s_memrealtime, 100 MHz) of every workgroup, tools/skinny_bench.hip only
 __device__ unsigned long long attn_trace[64 * 64 * 9];
 #define ATTN_TRACE(k) \
-  if (threadIdx.x == 0) attn_trace[((long)blockIdx.y * gridDim.x + blockIdx.x) * 9 + (k)] = __builtin_amdgcn_s_memrealtime()
+  if (threadIdx.x == 0) attn_trace[((long)b * P.nchmax + ch) * 9 + (k)] = __builtin_amdgcn_s_memrealtime()
 #else
 #define ATTN_TRACE(k)
 #endif
 
-__global__ __launch_bounds__(256) void attn_kernel(AttnArgs P, DecDev D, int jstep) {
+// one workgroup (256 threads): utterance b, positions [16 ch, 16 ch + 16)
+__device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, int jstep, int b, int ch) {
   ATTN_TRACE(0);
-  const int b = blockIdx.y;
-  const int ch = blockIdx.x;
   const int t0 = ch * TCH;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int a = tid & 127, grp = tid >> 7;
@@ -642,6 +641,31 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs P, DecDev D, int jst
   ATTN_TRACE(8);
 }
 
+__global__ __launch_bounds__(256) void attn_kernel(AttnArgs P, DecDev D, int jstep) {
+  attn_body(P, D, jstep, blockIdx.y, blockIdx.x);
+}
+
+// attention workgroups first (the step's critical path), then <1,4> skinny GEMM workgroups of
+// up to two jobs that do not depend on the context (they stream beside the latency-bound
+// attention instead of after it)
+template <int MT>
+__global__ __launch_bounds__(256) void attn_gemm_kernel(AttnArgs P, SkArgs A, DecDev D, int jstep) {
+  extern __shared__ __attribute__((aligned(16))) float smem[];
+  const int nattn = P.nchmax * D.B;
+  const int bx = blockIdx.x;
+  if (bx < nattn) {
+    attn_body(P, D, jstep, bx / P.nchmax, bx % P.nchmax);
+    return;
+  }
+  const int g = bx - nattn;
+  const int n0 = A.job[0].ntiles;
+  if (g < n0) {
+    skinny_body<1, 4, MT>(A.job[0], D, jstep, g, smem);
+  } else {
+    skinny_body<1, 4, MT>(A.job[1], D, jstep, g - n0, smem);
+  }
+}
+
 __global__ void dec_advance_kernel(DecCtl* ctl, int n) {
   if (threadIdx.x == 0) ctl->base += n;
 }
@@ -696,6 +720,21 @@ void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t
   TTS_CHECK(p.nchmax * TCH >= d.T_max, "attention: partial buffers too small");
   dim3 g((d.T_max + TCH - 1) / TCH, d.B);
   attn_kernel<<<g, 256, 0, s>>>(p, d, jstep);
+  HIP_OK(hipGetLastError());
+}
+
+void launch_attn_gemm(const AttnArgs& p, const SkArgs& a, const DecDev& d, int jstep, hipStream_t s) {
+  TTS_CHECK(p.npq == NPQ, "attention: expects 64 query partials");
+  TTS_CHECK(p.nchmax * TCH >= d.T_max, "attention: partial buffers too small");
+  TTS_CHECK(a.MT >= 1 && a.MT <= 4, "skinny: MT in [1,4]");
+  const int nwg = p.nchmax * d.B + a.job[0].ntiles + (a.njobs > 1 ? a.job[1].ntiles : 0);
+  const size_t lds = skinny_lds(1, 4, a.MT * 16);
+  switch (a.MT) {
+    case 1: attn_gemm_kernel<1><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
+    case 2: attn_gemm_kernel<2><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
+    case 3: attn_gemm_kernel<3><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
+    default: attn_gemm_kernel<4><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
+  }
   HIP_OK(hipGetLastError());
 }
 
