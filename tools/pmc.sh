@@ -10,4 +10,4 @@ export TMPDIR=/tmp
 rm -rf gpurun_out/pmc_fetch gpurun_out/pmc_write
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --kernel-trace -d gpurun_out/pmc_fetch -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --kernel-iters 20 > gpurun_out/pmc_fetch.log 2>&1 &&
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --kernel-trace -d gpurun_out/pmc_write -o run --output-format csv -- python3 bench.py --steps 1 --warmup 1 --no-cpu-baseline --kernel-iters 20 > gpurun_out/pmc_write.log 2>&1 &&
-python3 tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write profiles/k4_pmc.json
+python3 tools/pmc_summary.py gpurun_out/pmc_fetch gpurun_out/pmc_write gpurun_out/k4_pmc.json  # copy into profiles/ here
