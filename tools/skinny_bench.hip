@@ -2,6 +2,7 @@
 // weight-stream rate, timed as graph replays of back-to-back launches. Not part of the library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I../tts_amd/csrc tools/skinny_bench.hip -o /tmp/sb
 #define ATTN_TRACE_BUF 1
+#define SK_TRACE_BUF 1
 #include "../tts_amd/csrc/decoder.hip"
 #include <algorithm>
 
@@ -153,7 +154,36 @@ static float time_graph(const std::function<void()>& body, int per_graph = 40, i
   return ms * 1000.f / (per_graph * reps);
 }
 
+// one traced launch: per-phase averages over workgroups (us)
+static void sk_report(const char* name, int nwg, const std::function<void()>& launch) {
+  std::vector<unsigned long long> tr(1024 * 8, 0);
+  HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(sk_trace), tr.data(), tr.size() * 8));
+  time_graph(launch, 20, 2);  // warm replays; the buffer keeps the last launch
+  HIP_OK(hipStreamSynchronize(S));
+  HIP_OK(hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(sk_trace), tr.size() * 8));
+  unsigned long long tmin = ~0ull, tmax = 0;
+  for (int w = 0; w < nwg; ++w) tmin = std::min(tmin, tr[w * 8]);
+  double ph[6] = {0};
+  int n = 0;
+  for (int w = 0; w < nwg; ++w) {
+    const unsigned long long* t = &tr[w * 8];
+    if (!t[5]) continue;
+    ++n;
+    ph[0] += (double)(t[0] - tmin);
+    ph[1] += (double)(t[1] - t[0]);
+    ph[2] += (double)(t[2] - t[1]);
+    ph[3] += (double)(t[3] - t[2]);
+    ph[4] += (double)((t[4] ? t[4] : t[5]) - t[3]);
+    ph[5] += (double)(t[5] - (t[4] ? t[4] : t[3]));
+    tmax = std::max(tmax, t[5]);
+  }
+  printf("   %s: start %.2f | issue %.2f gemm %.2f reduce %.2f epi %.2f pq/tail %.2f | span %.2f us (%d wg)\n", name,
+         ph[0] / n / 100, ph[1] / n / 100, ph[2] / n / 100, ph[3] / n / 100, ph[4] / n / 100, ph[5] / n / 100,
+         (double)(tmax - tmin) / 100, n);
+}
+
 int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IONBF, 0);
   HIP_OK(hipStreamCreate(&S));
   const int B = argc > 1 ? atoi(argv[1]) : 32;
   const int MT = (B + 15) / 16, Bp = MT * 16;
@@ -182,7 +212,7 @@ int main(int argc, char** argv) {
   float* gatt = dalloc((size_t)Bp * 4096);
   float* pb = dalloc((size_t)Bp * 256);
   float* y = dalloc((size_t)Bp * 560);
-  float* pq = dalloc((size_t)64 * Bp * 128);
+  float* pq = dalloc((size_t)256 * Bp * 128);
   float* spart = dalloc((size_t)64 * Bp);
   float* Wdec = dalloc((size_t)4096 * 2560);
   float* Wpre = dalloc((size_t)4096 * 1536);
@@ -346,9 +376,19 @@ int main(int argc, char** argv) {
     J.hc_ld = 1024;
     J.WqT = WqT;
     J.pq_part = pq;
+    J.pq_cap = 256;
   }
   const double b2 = 4096.0 * 256 * 4;
   if (MT == 2) {
+    sk_report("K2 <4,4>", 64, [&] { skinny_kernel<4, 4, 2, 0><<<64, 1024, skinny_lds(4, 4, Bp), S>>>(a2, d, 0); });
+    sk_report("K4 <1,4>", 256, [&] { skinny_kernel<1, 4, 2, 0><<<256, 256, skinny_lds(1, 4, Bp), S>>>(a4, d, 0); });
+    sk_report("proj <1,4>", 11, [&] { skinny_kernel<1, 4, 2, 0><<<11, 256, skinny_lds(1, 4, Bp), S>>>(pj, d, 0); });
+    sk_report("proj+att-pre <1,4>", 267, [&] { skinny_kernel<1, 4, 2, 0><<<267, 256, skinny_lds(1, 4, Bp), S>>>(both5, d, 0); });
+    rep("K2 <1,4> D=4 (pq 256)", time_graph([&] { skinny_kernel<1, 4, 2, 4><<<256, 256, skinny_lds(1, 4, Bp), S>>>(a2, d, 0); }), b2);
+    rep("K2 <2,4> D=4 (pq 128)", time_graph([&] { skinny_kernel<2, 4, 2, 4><<<128, 512, skinny_lds(2, 4, Bp), S>>>(a2, d, 0); }), b2);
+    rep("K2 <4,2> D=4", time_graph([&] { skinny_kernel<4, 2, 2, 4><<<64, 512, skinny_lds(4, 2, Bp), S>>>(a2, d, 0); }), b2);
+    rep("K2 <4,2> D=8", time_graph([&] { skinny_kernel<4, 2, 2, 8><<<64, 512, skinny_lds(4, 2, Bp), S>>>(a2, d, 0); }), b2);
+    rep("K2 <4,1> D=16", time_graph([&] { skinny_kernel<4, 1, 2, 16><<<64, 256, skinny_lds(4, 1, Bp), S>>>(a2, d, 0); }), b2);
     rep("K2 <4,4> D=4", time_graph([&] { skinny_kernel<4, 4, 2, 4><<<64, 1024, skinny_lds(4, 4, Bp), S>>>(a2, d, 0); }), b2);
     rep("K2 <4,4> D=2", time_graph([&] { skinny_kernel<4, 4, 2, 2><<<64, 1024, skinny_lds(4, 4, Bp), S>>>(a2, d, 0); }), b2);
   }
@@ -366,7 +406,7 @@ int main(int argc, char** argv) {
     da.align_out = align;
     AttnArgs p{};
     p.pq_part = pq;
-    p.npq = 64;
+    p.npq = 128;
     p.Bp = Bp;
     p.alpha = dalloc((size_t)B * T);
     p.alpha_cum = dalloc((size_t)B * T);
@@ -392,22 +432,10 @@ int main(int argc, char** argv) {
       char name[64];
       snprintf(name, sizeof(name), "K3 attention T=%d %s", T, sm ? "softmax" : "sigmoid");
       rep(name, time_graph([&] { launch_attention(p, da, 0, S); }), 1.0);
-      if (T == 168 && MT == 2) {
-        SkArgs one = a4;
-        rep("   attention + K4 (K=2560) one launch", time_graph([&] { launch_attn_gemm(p, one, da, 0, S); }), 1.0);
-        SkArgs two = a4;
-        two.njobs = 2;
-        two.job[1] = ap.job[0];
-        rep("   attention + K4 + att-pre one launch", time_graph([&] { launch_attn_gemm(p, two, da, 0, S); }), 1.0);
-        rep("   attention ; K4 serial", time_graph([&] {
-              launch_attention(p, da, 0, S);
-              skinny_kernel<1, 4, 2, 0><<<256, 256, skinny_lds(1, 4, Bp), S>>>(a4, d, 0);
-            }), 1.0);
-      }
       // one traced launch: phase durations (us) averaged over workgroups
       std::vector<unsigned long long> tr(64 * 64 * 9, 0);
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(attn_trace), tr.data(), tr.size() * 8));
-      launch_attention(p, da, 0, S);
+      time_graph([&] { launch_attention(p, da, 0, S); }, 20, 2);
       HIP_OK(hipStreamSynchronize(S));
       HIP_OK(hipMemcpyFromSymbol(tr.data(), HIP_SYMBOL(attn_trace), tr.size() * 8));
       const int nwg = nch * B;

@@ -455,7 +455,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.cdec, (size_t)Bp * 1024, g);
   grow<float>(W.ctx, (size_t)Bp * 512, g);
   grow<float>(W.y, (size_t)Bp * 80 * c->taco.r_init, g);
-  grow<float>(W.pq, (size_t)64 * Bp * 128, g);
+  grow<float>(W.pq, (size_t)128 * Bp * 128, g);
   grow<float>(W.spart, (size_t)Bp, g);
   grow<float>(W.alpha, (size_t)B * T_max, g);
   grow<float>(W.acum, (size_t)B * T_max, g);
@@ -560,12 +560,13 @@ void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
     J.hc_ld = 1024;
     J.WqT = M.WqT.f();
     J.pq_part = W.pq.f();
-    launch_skinny(a, d, j, 4, 4, s);
+    J.pq_cap = 128;
+    launch_skinny(a, d, j, 2, 4, s);  // 128 workgroups of 8 units: 128 query partials
   }
   if (which_only < 0 || which_only == 4) {  // K3: attention
     AttnArgs p{};
     p.pq_part = W.pq.f();
-    p.npq = 64;
+    p.npq = 128;
     p.Bp = MT * 16;
     p.alpha = W.alpha.f();
     p.alpha_cum = W.acum.f();

@@ -38,6 +38,7 @@ struct SkJob {
   int hc_ld;
   const float* WqT;    // optional: W_query^T [units][128] for partial query projection
   float* pq_part;      // [workgroup][Bp][128]
+  int pq_cap;          // workgroup slots in pq_part (checked at launch)
   int frames_r;        // projection: write the first 80*r columns as frames of active utts
   // projection only: the stopnet logit is linear in [h_dec | ctx] once the projection is folded
   // in (stop = w_h.h + w_y.(W_p [h|ctx] + b_p) + b_s), so the folded 1536-vector is row 0 of a
@@ -104,6 +105,4 @@ void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, 
 // prenet layer 1 + layer 2 in one launch (16 workgroups) plus the stop workgroup
 void launch_prenet_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s);
 void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t s);
-// attention (grid flattened: utterance-major chunks) + <1,4> skinny GEMM jobs in one launch
-void launch_attn_gemm(const AttnArgs& p, const SkArgs& a, const DecDev& d, int jstep, hipStream_t s);
 void launch_dec_advance(DecCtl* ctl, int n, hipStream_t s);

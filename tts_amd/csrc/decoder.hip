@@ -31,6 +31,15 @@
 #include "common.h"
 #include "decoder.h"
 
+#ifdef SK_TRACE_BUF
+// phase timestamps (s_memrealtime, 100 MHz) per workgroup of skinny launches: bench tool only
+__device__ unsigned long long sk_trace[1024 * 8];
+#define SK_TRACE(k) \
+  if (threadIdx.x == 0) sk_trace[(long)blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define SK_TRACE(k)
+#endif
+
 template <int MT, int D>
 struct SkFrag {
   f32x4 w[D];
@@ -164,6 +173,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
   SkPipe<MT, nthr, DD> pipe;
   typename SkPipe<MT, nthr, DD>::Frag fa;
   pipe.init(J, tile, w, KS, lane);
+  SK_TRACE(0);
   pipe.prefetch(fa);
   // epilogue operands, fetched under the GEMM (indices clamped: no guarded loads); a 1024-thread
   // workgroup at MT = 4 is out of registers for that and fetches them after the k-loop
@@ -206,6 +216,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
     }
   };
   if (EPRE) load_wq();
+  SK_TRACE(1);
   if (all_done) return;
   const int t = D.ctl->base + jstep;
 
@@ -213,6 +224,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
 #pragma unroll
   for (int i = 0; i < MT; ++i) acc[i] = f32x4{0.f, 0.f, 0.f, 0.f};
   pipe.run(fa, acc);
+  SK_TRACE(2);
   if (!EPRE) {
     load_epi();
     load_wq();
@@ -221,6 +233,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
   float* extra = smem + (long)NT * KS * Bp * 17;  // [NT][Bp][16]
   skinny_to_lds<MT>(part, w, lane, acc);
   __syncthreads();
+  SK_TRACE(3);
 
   if (J.epi == EPI_STORE) {
 #pragma unroll
@@ -267,6 +280,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
       J.h_out[frag_idx(m, tl * 4 + u, J.hc_ld)] = h;
       hs[m * 4 * NT + g * 4 + u] = h;
     }
+    SK_TRACE(4);
     if (J.pq_part) {  // partial query projection over this workgroup's 4*NT hidden units
       static_assert(nthr % 128 == 0, "pq: one attention dim per thread");
       const int a = tid % 128;
@@ -279,6 +293,7 @@ __device__ __forceinline__ void skinny_body(const SkJob& J, const DecDev& D, int
       }
     }
   }
+  SK_TRACE(5);
 }
 
 // grid = job0 tiles/NT  [+ job1 tiles/NT]
@@ -398,7 +413,7 @@ __global__ __launch_bounds__(1024) void prenet_stop_kernel(SkArgs A, DecDev D, S
 //   alignment row (common_layers.py:347-366).
 // --------------------------------------------------------------------------------------
 constexpr int TCH = 16;
-constexpr int LOCK = 31, LOCF = 32, ADIM = 128, NPQ = 64;
+constexpr int LOCK = 31, LOCF = 32, ADIM = 128, NPQ = 128;
 
 #ifdef ATTN_TRACE_BUF
 // phase timestamps (s_memrealtime, 100 MHz) of every workgroup, tools/skinny_bench.hip only
@@ -645,27 +660,6 @@ __global__ __launch_bounds__(256) void attn_kernel(AttnArgs P, DecDev D, int jst
   attn_body(P, D, jstep, blockIdx.y, blockIdx.x);
 }
 
-// attention workgroups first (the step's critical path), then <1,4> skinny GEMM workgroups of
-// up to two jobs that do not depend on the context (they stream beside the latency-bound
-// attention instead of after it)
-template <int MT>
-__global__ __launch_bounds__(256) void attn_gemm_kernel(AttnArgs P, SkArgs A, DecDev D, int jstep) {
-  extern __shared__ __attribute__((aligned(16))) float smem[];
-  const int nattn = P.nchmax * D.B;
-  const int bx = blockIdx.x;
-  if (bx < nattn) {
-    attn_body(P, D, jstep, bx / P.nchmax, bx % P.nchmax);
-    return;
-  }
-  const int g = bx - nattn;
-  const int n0 = A.job[0].ntiles;
-  if (g < n0) {
-    skinny_body<1, 4, MT>(A.job[0], D, jstep, g, smem);
-  } else {
-    skinny_body<1, 4, MT>(A.job[1], D, jstep, g - n0, smem);
-  }
-}
-
 __global__ void dec_advance_kernel(DecCtl* ctl, int n) {
   if (threadIdx.x == 0) ctl->base += n;
 }
@@ -690,12 +684,15 @@ static void launch_skinny_nt(const SkArgs& a, const DecDev& d, int jstep, int nw
 
 void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s) {
   TTS_CHECK(a.MT >= 1 && a.MT <= 4, "skinny: MT in [1,4]");
-  for (int j = 0; j < a.njobs; ++j) TTS_CHECK(a.job[j].ntiles % NT == 0, "skinny: ntiles % NT");
+  for (int j = 0; j < a.njobs; ++j) {
+    TTS_CHECK(a.job[j].ntiles % NT == 0, "skinny: ntiles % NT");
+    TTS_CHECK(!a.job[j].pq_part || a.job[j].ntiles / NT <= a.job[j].pq_cap, "skinny: query partial buffer too small");
+  }
   int nwg = a.job[0].ntiles / NT + (a.njobs > 1 ? a.job[1].ntiles / NT : 0);
   if (NT == 1 && KS == 4) launch_skinny_nt<1, 4>(a, d, jstep, nwg, s);
   else if (NT == 1 && KS == 8) launch_skinny_nt<1, 8>(a, d, jstep, nwg, s);
   else if (NT == 1 && KS == 16) launch_skinny_nt<1, 16>(a, d, jstep, nwg, s);
-  else if (NT == 4 && KS == 4) launch_skinny_nt<4, 4>(a, d, jstep, nwg, s);
+  else if (NT == 2 && KS == 4) launch_skinny_nt<2, 4>(a, d, jstep, nwg, s);
   else TTS_CHECK(false, "skinny: unsupported tile config");
   HIP_OK(hipGetLastError());
 }
@@ -716,25 +713,10 @@ void launch_prenet_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, in
 }
 
 void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t s) {
-  TTS_CHECK(p.npq == NPQ, "attention: expects 64 query partials");
+  TTS_CHECK(p.npq == NPQ, "attention: expects 128 query partials");
   TTS_CHECK(p.nchmax * TCH >= d.T_max, "attention: partial buffers too small");
   dim3 g((d.T_max + TCH - 1) / TCH, d.B);
   attn_kernel<<<g, 256, 0, s>>>(p, d, jstep);
-  HIP_OK(hipGetLastError());
-}
-
-void launch_attn_gemm(const AttnArgs& p, const SkArgs& a, const DecDev& d, int jstep, hipStream_t s) {
-  TTS_CHECK(p.npq == NPQ, "attention: expects 64 query partials");
-  TTS_CHECK(p.nchmax * TCH >= d.T_max, "attention: partial buffers too small");
-  TTS_CHECK(a.MT >= 1 && a.MT <= 4, "skinny: MT in [1,4]");
-  const int nwg = p.nchmax * d.B + a.job[0].ntiles + (a.njobs > 1 ? a.job[1].ntiles : 0);
-  const size_t lds = skinny_lds(1, 4, a.MT * 16);
-  switch (a.MT) {
-    case 1: attn_gemm_kernel<1><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
-    case 2: attn_gemm_kernel<2><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
-    case 3: attn_gemm_kernel<3><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
-    default: attn_gemm_kernel<4><<<nwg, 256, lds, s>>>(p, a, d, jstep); break;
-  }
   HIP_OK(hipGetLastError());
 }
 
