@@ -432,6 +432,7 @@ int main(int argc, char** argv) {
       char name[64];
       snprintf(name, sizeof(name), "K3 attention T=%d %s", T, sm ? "softmax" : "sigmoid");
       rep(name, time_graph([&] { launch_attention(p, da, 0, S); }), 1.0);
+      rep("   same, 256-thread workgroups", time_graph([&] { attn_kernel<256><<<dim3(nch, B), 256, 0, S>>>(p, da, 0); }), 1.0);
       // one traced launch: phase durations (us) averaged over workgroups
       std::vector<unsigned long long> tr(64 * 64 * 9, 0);
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(attn_trace), tr.data(), tr.size() * 8));

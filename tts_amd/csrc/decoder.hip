@@ -424,13 +424,21 @@ __device__ unsigned long long attn_trace[64 * 64 * 9];
 #define ATTN_TRACE(k)
 #endif
 
-// one workgroup (256 threads): utterance b, positions [16 ch, 16 ch + 16)
+// one workgroup of NT threads (256 or 512): utterance b, positions [16 ch, 16 ch + 16)
+template <int NT>
 __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, int jstep, int b, int ch) {
+  constexpr int NG = NT / ADIM;           // thread groups over the attention dims
+  constexpr int PPG = TCH / NG;           // positions per group in the energy phase
+  constexpr int DPT = 512 / NT;           // encoder dims per thread (context)
+  constexpr int OPT = (LOCF * TCH) / NT;  // location-conv outputs per thread
+  constexpr int LPP = NT / TCH;           // lanes per position in the energy reduction
+  constexpr int NWL = (LOCF * 2 * LOCK + NT - 1) / NT;
+  static_assert(NG >= 2 && OPT >= 1 && OPT <= 2 && LPP <= 64, "attention geometry");
   ATTN_TRACE(0);
   const int t0 = ch * TCH;
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int a = tid & 127, grp = tid >> 7;
-  __shared__ float red[2][ADIM];
+  const int tid = threadIdx.x;
+  const int a = tid % ADIM, grp = tid / ADIM;
+  __shared__ float red[NG][ADIM];
   __shared__ float A0[TCH + LOCK], A1[TCH + LOCK];
   __shared__ float Wl[LOCF * 2 * LOCK];
   __shared__ __attribute__((aligned(16))) float f[TCH][LOCF + 4];  // [position][filter]
@@ -441,19 +449,19 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   const int T = D.lens[b];
   const int Tm1 = max(T - 1, 0);
   // -- every independent global load up front (clamped indices, no guarded loads) --
-  float pen[TCH / 2];
+  float pen[PPG];
 #pragma unroll
-  for (int i = 0; i < TCH / 2; ++i) {
-    const int t = min(t0 + grp * (TCH / 2) + i, Tm1);
+  for (int i = 0; i < PPG; ++i) {
+    const int t = min(t0 + grp * PPG + i, Tm1);
     pen[i] = P.penc[((long)b * D.T_max + t) * ADIM + a];
   }
   float wd[LOCF];
 #pragma unroll
   for (int c = 0; c < LOCF; ++c) wd[c] = P.WdT[c * ADIM + a];
   const float va = P.v[a];
-  float pp[NPQ / 2];
+  float pp[NPQ / NG];
 #pragma unroll
-  for (int i = 0; i < NPQ / 2; ++i) pp[i] = P.pq_part[((long)(grp * (NPQ / 2) + i) * Bp + b) * ADIM + a];
+  for (int i = 0; i < NPQ / NG; ++i) pp[i] = P.pq_part[((long)(grp * (NPQ / NG) + i) * Bp + b) * ADIM + a];
   float a0, a1;
   {
     const int pos = t0 - (LOCK - 1) / 2 + min(tid, TCH + LOCK - 2);
@@ -462,15 +470,21 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
     a1 = P.alpha_cum[(long)b * D.T_max + pc];
     if (pos < 0 || pos >= T) a0 = a1 = 0.f;
   }
-  float wl[(LOCF * 2 * LOCK + 255) / 256];
+  float wl[NWL];
 #pragma unroll
-  for (int i = 0; i < (LOCF * 2 * LOCK + 255) / 256; ++i) wl[i] = P.Wloc[min(tid + 256 * i, LOCF * 2 * LOCK - 1)];
-  // encoder rows of this chunk for the partial context: dims tid and tid + 256
-  float2 ev[TCH];  // dims 2*tid, 2*tid + 1
+  for (int i = 0; i < NWL; ++i) wl[i] = P.Wloc[min(tid + NT * i, LOCF * 2 * LOCK - 1)];
+  // encoder rows of this chunk for the partial context: dims DPT*tid .. DPT*tid + DPT-1
+  float ev[TCH][DPT];
 #pragma unroll
   for (int i = 0; i < TCH; ++i) {
-    const int t = min(t0 + i, Tm1);
-    ev[i] = *reinterpret_cast<const float2*>(P.enc + ((long)b * D.T_max + t) * 512 + 2 * tid);
+    const float* er = P.enc + ((long)b * D.T_max + min(t0 + i, Tm1)) * 512 + DPT * tid;
+    if constexpr (DPT == 2) {
+      const float2 v2 = *reinterpret_cast<const float2*>(er);
+      ev[i][0] = v2.x;
+      ev[i][1] = v2.y;
+    } else {
+      ev[i][0] = er[0];
+    }
   }
   if (D.ctl->all_done || D.done[b] || t0 >= T) return;
   const int t_step = D.ctl->base + jstep;
@@ -479,49 +493,53 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
     A1[tid] = a1;
   }
 #pragma unroll
-  for (int i = 0; i < (LOCF * 2 * LOCK + 255) / 256; ++i)
-    if (tid + 256 * i < LOCF * 2 * LOCK) Wl[tid + 256 * i] = wl[i];
+  for (int i = 0; i < NWL; ++i)
+    if (tid + NT * i < LOCF * 2 * LOCK) Wl[tid + NT * i] = wl[i];
   // query projection = sum of the attention-LSTM kernel's partials (fixed order)
   float s = 0.f;
 #pragma unroll
-  for (int i = 0; i < NPQ / 2; ++i) s += pp[i];
+  for (int i = 0; i < NPQ / NG; ++i) s += pp[i];
   red[grp][a] = s;
   __syncthreads();
   ATTN_TRACE(1);
-  const float pqa = red[0][a] + red[1][a];
-  // location conv: f[tt][c] = sum_i sum_k Wl[c][i][k] * A_i[tt + k]; each thread two adjacent
-  // positions of one filter, sliding the window in registers (one A read per tap)
+  float pqa = red[0][a];
+#pragma unroll
+  for (int g = 1; g < NG; ++g) pqa += red[g][a];
+  // location conv: f[tt][c] = sum_i sum_k Wl[c][i][k] * A_i[tt + k]; OPT adjacent positions of
+  // one filter per thread, the window sliding in registers (one A read per tap)
   {
-    const int c = tid >> 3, tt = (tid & 7) * 2;
+    const int c = tid / (TCH / OPT), tt = (tid % (TCH / OPT)) * OPT;
     const float* w0 = Wl + c * 2 * LOCK;
-    float s0 = 0.f, s1 = 0.f;
-    float an = A0[tt];
+    float acc[OPT];
 #pragma unroll
-    for (int k = 0; k < LOCK; ++k) {
-      const float a_k = an;
-      an = A0[tt + k + 1];
-      s0 = fmaf(w0[k], a_k, s0);
-      s1 = fmaf(w0[k], an, s1);
-    }
-    an = A1[tt];
+    for (int o = 0; o < OPT; ++o) acc[o] = 0.f;
 #pragma unroll
-    for (int k = 0; k < LOCK; ++k) {
-      const float a_k = an;
-      an = A1[tt + k + 1];
-      s0 = fmaf(w0[LOCK + k], a_k, s0);
-      s1 = fmaf(w0[LOCK + k], an, s1);
+    for (int ci = 0; ci < 2; ++ci) {
+      const float* Ai = ci ? A1 : A0;
+      float win[OPT];
+#pragma unroll
+      for (int o = 0; o < OPT; ++o) win[o] = Ai[tt + o];
+#pragma unroll
+      for (int k = 0; k < LOCK; ++k) {
+        const float w = w0[ci * LOCK + k];
+#pragma unroll
+        for (int o = 0; o < OPT; ++o) acc[o] = fmaf(w, win[o], acc[o]);
+#pragma unroll
+        for (int o = 0; o + 1 < OPT; ++o) win[o] = win[o + 1];
+        win[OPT - 1] = Ai[tt + k + OPT];
+      }
     }
-    f[tt][c] = s0;
-    f[tt + 1][c] = s1;
+#pragma unroll
+    for (int o = 0; o < OPT; ++o) f[tt + o][c] = acc[o];
   }
   __syncthreads();
   ATTN_TRACE(2);
   // loc = W_dense . f ; e = v . tanh(pq + loc + penc) + b_v. Each thread owns one attention dim
-  // for 8 positions; the sum over dims goes through LDS (position-major, 16 lanes per position)
-  // instead of 8 serial 64-lane shuffle reductions
+  // for PPG positions; the sum over dims goes through LDS (position-major, LPP lanes per
+  // position) instead of serial 64-lane shuffle reductions
 #pragma unroll
-  for (int i = 0; i < TCH / 2; ++i) {
-    const int tt = grp * (TCH / 2) + i;
+  for (int i = 0; i < PPG; ++i) {
+    const int tt = grp * PPG + i;
     float l = 0.f;
 #pragma unroll
     for (int c4 = 0; c4 < LOCF / 4; ++c4) {
@@ -536,12 +554,12 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   const int nvalid = min(TCH, T - t0);
   const long pidx = (long)b * P.nchmax + ch;
   {
-    const int pos = tid >> 4, j = tid & 15;
+    const int pos = tid / LPP, j = tid % LPP;
     float z = 0.f;
 #pragma unroll
-    for (int q = 0; q < ADIM / 16; ++q) z += zb[pos][j * (ADIM / 16) + q];
+    for (int q = 0; q < ADIM / LPP; ++q) z += zb[pos][j * (ADIM / LPP) + q];
 #pragma unroll
-    for (int off = 8; off > 0; off >>= 1) z += __shfl_xor(z, off, 64);
+    for (int off = LPP / 2; off > 0; off >>= 1) z += __shfl_xor(z, off, 64);
     if (j == 0) {
       const float e = z + P.bv;
       if (pos < nvalid)
@@ -564,23 +582,26 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
     sl[i] = i < nvalid ? x : 0.f;
     S_c += sl[i];
   }
-  // unnormalised partial context of this chunk (dims 2*tid, 2*tid + 1)
-  float u0 = 0.f, u1 = 0.f;
+  // unnormalised partial context of this chunk
+  float u[DPT];
 #pragma unroll
-  for (int i = 0; i < TCH; ++i) {
-    u0 = fmaf(sl[i], ev[i].x, u0);
-    u1 = fmaf(sl[i], ev[i].y, u1);
+  for (int q = 0; q < DPT; ++q) {
+    u[q] = 0.f;
+#pragma unroll
+    for (int i = 0; i < TCH; ++i) u[q] = fmaf(sl[i], ev[i][q], u[q]);
   }
   // ---- publish: sc1 (write-through) stores need no release fence (cdna_hip_programming.md
   // §5 split-K item 2); every wave drains, barrier, then one relaxed agent-scope ticket ----
-  {
+  if constexpr (DPT == 2) {
     union {
       float2 f;
       unsigned long long u;
     } pk;
-    pk.f = make_float2(u0, u1);
+    pk.f = make_float2(u[0], u[1]);
     __hip_atomic_store(reinterpret_cast<unsigned long long*>(P.part_u + pidx * 512) + tid, pk.u, __ATOMIC_RELAXED,
                        __HIP_MEMORY_SCOPE_AGENT);
+  } else {
+    __hip_atomic_store(P.part_u + pidx * 512 + tid, u[0], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
   if (tid == 0) {
     __hip_atomic_store(P.part_s + pidx, S_c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -605,17 +626,24 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   // batch in flight together (clamped), online rescaling for softmax ----
   const long pb = (long)b * P.nchmax;
   constexpr int CB = 16;
-  float m = -INFINITY, S = 0.f, c0 = 0.f, c1 = 0.f;
+  float m = -INFINITY, S = 0.f;
+  float cx[DPT];
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) cx[q] = 0.f;
   for (int cb = 0; cb < nch; cb += CB) {
-    float pm[CB], ps[CB], pu0[CB], pu1[CB];
+    float pm[CB], ps[CB], pu[CB][DPT];
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
       const long c = pb + min(cb + i, nch - 1);
       pm[i] = P.part_m[c];
       ps[i] = P.part_s[c];
-      const float2 pu = *reinterpret_cast<const float2*>(P.part_u + c * 512 + 2 * tid);
-      pu0[i] = pu.x;
-      pu1[i] = pu.y;
+      if constexpr (DPT == 2) {
+        const float2 v2 = *reinterpret_cast<const float2*>(P.part_u + c * 512 + 2 * tid);
+        pu[i][0] = v2.x;
+        pu[i][1] = v2.y;
+      } else {
+        pu[i][0] = P.part_u[c * 512 + tid];
+      }
     }
     float wc[CB];
     if (P.softmax) {
@@ -625,8 +653,8 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
         if (cb + i < nch) mb = fmaxf(mb, pm[i]);
       const float sc = (m == -INFINITY) ? 0.f : expf(m - mb);
       S *= sc;
-      c0 *= sc;
-      c1 *= sc;
+#pragma unroll
+      for (int q = 0; q < DPT; ++q) cx[q] *= sc;
       m = mb;
 #pragma unroll
       for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch) ? expf(pm[i] - m) : 0.f;
@@ -637,15 +665,15 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
       S = fmaf(ps[i], wc[i], S);
-      c0 = fmaf(pu0[i], wc[i], c0);
-      c1 = fmaf(pu1[i], wc[i], c1);
+#pragma unroll
+      for (int q = 0; q < DPT; ++q) cx[q] = fmaf(pu[i][q], wc[i], cx[q]);
     }
   }
   ATTN_TRACE(7);
-  P.ctx[frag_idx(b, 2 * tid, 512)] = c0 / S;
-  P.ctx[frag_idx(b, 2 * tid + 1, 512)] = c1 / S;
+#pragma unroll
+  for (int q = 0; q < DPT; ++q) P.ctx[frag_idx(b, DPT * tid + q, 512)] = cx[q] / S;
   const float* en = P.energy + (long)b * D.T_max;
-  for (int t = tid; t < T; t += 256) {
+  for (int t = tid; t < T; t += NT) {
     const float e = en[t];
     const float al = (P.softmax ? expf(e - m) : 1.f / (1.f + expf(-e))) / S;
     P.alpha[(long)b * D.T_max + t] = al;
@@ -656,8 +684,9 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   ATTN_TRACE(8);
 }
 
-__global__ __launch_bounds__(256) void attn_kernel(AttnArgs P, DecDev D, int jstep) {
-  attn_body(P, D, jstep, blockIdx.y, blockIdx.x);
+template <int NT>
+__global__ __launch_bounds__(NT) void attn_kernel(AttnArgs P, DecDev D, int jstep) {
+  attn_body<NT>(P, D, jstep, blockIdx.y, blockIdx.x);
 }
 
 __global__ void dec_advance_kernel(DecCtl* ctl, int n) {
@@ -716,7 +745,12 @@ void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t
   TTS_CHECK(p.npq == NPQ, "attention: expects 128 query partials");
   TTS_CHECK(p.nchmax * TCH >= d.T_max, "attention: partial buffers too small");
   dim3 g((d.T_max + TCH - 1) / TCH, d.B);
-  attn_kernel<<<g, 256, 0, s>>>(p, d, jstep);
+  // 512-thread workgroups shorten the chain when few chunks run; past ~200 workgroups the
+  // 256-thread form is faster (tools/skinny_bench.hip, B = 32: T 64 11.7 vs 12.3 us, T 168 15.8 vs 14.9)
+  if ((long)g.x * g.y <= 200)
+    attn_kernel<512><<<g, 512, 0, s>>>(p, d, jstep);
+  else
+    attn_kernel<256><<<g, 256, 0, s>>>(p, d, jstep);
   HIP_OK(hipGetLastError());
 }
 
