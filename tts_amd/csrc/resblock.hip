@@ -11,13 +11,14 @@
 constexpr int RB_DMAX = 27;  // largest dilation (3^3, num_res_blocks <= 4)
 
 template <int C, int TQ, int WM, int WN>
-__global__ __launch_bounds__(256) void resblock_kernel(ResArgs a) {
-  static_assert(WM * WN == 4, "4 waves");
+__global__ __launch_bounds__(64 * WM * WN) void resblock_kernel(ResArgs a) {
+  constexpr int NTHR = 64 * WM * WN;
+  static_assert(WM * WN == 4 || WM * WN == 8, "4 or 8 waves");
   constexpr int MI = C / 16 / WM;
   constexpr int NI = TQ / 16 / WN;
   static_assert(MI * 16 * WM == C && NI * 16 * WN == TQ, "tile split");
   constexpr int ROWMAX = TQ + 2 * RB_DMAX + 1;
-  constexpr int SPT = (16 * ROWMAX + 255) / 256;
+  constexpr int SPT = (16 * ROWMAX + NTHR - 1) / NTHR;
   extern __shared__ __attribute__((aligned(16))) float smem[];
 
   const int b = blockIdx.y;
@@ -46,7 +47,7 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs a) {
   int sc_[SPT], sp_[SPT];
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
-    const int e = tid + 256 * j;
+    const int e = tid + NTHR * j;
     sc_[j] = e / ROW;
     sp_[j] = e - sc_[j] * ROW;
   }
@@ -72,7 +73,7 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs a) {
   auto stage_store = [&](float* X, int chunk) {
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
-      const int e = tid + 256 * j;
+      const int e = tid + NTHR * j;
       if (e < 16 * ROW) {
         X[e] = lrelu02(st[j]);
         const int p = sp_[j] - d;
@@ -81,18 +82,33 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs a) {
     }
   };
 
-  // ---------------- phase 1: h = Wd . lrelu(x) (K = 3C) ----------------
+  // Weight fragments come from L2 (every workgroup streams all of Wd and Wf): a ring of 3
+  // k-chunks per wave keeps one whole staging chunk of weights in flight. The ring runs over
+  // the concatenated sequence [Wd chunks 0..NKC1) [Wf chunks 0..NKC2), so phase 2's first
+  // weights are already loaded when phase 1 ends.
   constexpr int NKC1 = 3 * C / 16;
+  constexpr int NKC2 = 2 * C / 16;
   const f32x4* Wd = reinterpret_cast<const f32x4*>(a.Wd);
+  const f32x4* Wf = reinterpret_cast<const f32x4*>(a.Wf);
+  f32x4 ring[3][MI];
+  auto wload = [&](f32x4 (&r)[MI], int seq) {
+    const bool p1 = seq < NKC1;
+    const f32x4* base = p1 ? Wd : Wf;
+    const int nk = p1 ? NKC1 : NKC2;
+    const int kc = p1 ? seq : min(seq - NKC1, NKC2 - 1);
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) r[mi] = base[((long)(mt0 + mi) * nk + kc) * 64 + lane];
+  };
+
+  // ---------------- phase 1: h = Wd . lrelu(x) (K = 3C) ----------------
   f32x4 acc[MI][NI];
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
   stage_load(0);
-  f32x4 An[MI];
 #pragma unroll
-  for (int mi = 0; mi < MI; ++mi) An[mi] = Wd[((long)(mt0 + mi) * NKC1) * 64 + lane];
+  for (int u = 0; u < 3; ++u) wload(ring[u], u);
   stage_store(X0, 0);
   __syncthreads();
   constexpr int NCH = C / 16;
@@ -101,13 +117,10 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs a) {
     if (chunk + 1 < NCH) stage_load(chunk + 1);
 #pragma unroll
     for (int kq = 0; kq < 3; ++kq) {
-      const int kc = chunk * 3 + kq;
       f32x4 A[MI];
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) A[mi] = An[mi];
-      const int kn = min(kc + 1, NKC1 - 1);
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) An[mi] = Wd[((long)(mt0 + mi) * NKC1 + kn) * 64 + lane];
+      for (int mi = 0; mi < MI; ++mi) A[mi] = ring[kq][mi];
+      wload(ring[kq], (chunk + 1) * 3 + kq);
       const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
       const int ov[4] = {o.x, o.y, o.z, o.w};
 #pragma unroll
@@ -125,10 +138,6 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs a) {
     __syncthreads();
   }
   // h -> lrelu(h + b_d) into HX[0:C)
-  constexpr int NKC2 = 2 * C / 16;
-  const f32x4* Wf = reinterpret_cast<const f32x4*>(a.Wf);
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi) An[mi] = Wf[((long)(mt0 + mi) * NKC2) * 64 + lane];
 #pragma unroll
   for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
@@ -145,23 +154,26 @@ __global__ __launch_bounds__(256) void resblock_kernel(ResArgs a) {
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-  for (int kc = 0; kc < NKC2; ++kc) {
-    f32x4 A[MI];
+  for (int kc0 = 0; kc0 < NKC2; kc0 += 3) {
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) A[mi] = An[mi];
-    const int kn = min(kc + 1, NKC2 - 1);
+    for (int u = 0; u < 3; ++u) {
+      const int kc = kc0 + u;
+      if (kc >= NKC2) break;  // C/8 chunks need not be a multiple of 3 (wave-uniform)
+      f32x4 A[MI];
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) An[mi] = Wf[((long)(mt0 + mi) * NKC2 + kn) * 64 + lane];
-    const float* hrow = HX + (kc * 16 + g4) * TQ + qb;
+      for (int mi = 0; mi < MI; ++mi) A[mi] = ring[u][mi];
+      wload(ring[u], NKC1 + kc + 3);
+      const float* hrow = HX + (kc * 16 + g4) * TQ + qb;
 #pragma unroll
-    for (int s = 0; s < 4; ++s) {
-      float bv[NI];
+      for (int s = 0; s < 4; ++s) {
+        float bv[NI];
 #pragma unroll
-      for (int ni = 0; ni < NI; ++ni) bv[ni] = hrow[s * TQ + ni * 16];
+        for (int ni = 0; ni < NI; ++ni) bv[ni] = hrow[s * TQ + ni * 16];
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
+        for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
+          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
+      }
     }
   }
   float* yb = a.y + (long)b * a.sb;
@@ -185,20 +197,21 @@ static void launch_rb(const ResArgs& a, hipStream_t s) {
   const int ROW = TQ + 2 * a.dil + 1;
   const size_t lds = ((size_t)2 * ((16 * ROW + 3) & ~3) + (size_t)2 * C * TQ + 48) * 4;
   dim3 grid((a.max_q + TQ - 1) / TQ, a.B);
-  resblock_kernel<C, TQ, WM, WN><<<grid, 256, lds, s>>>(a);
+  resblock_kernel<C, TQ, WM, WN><<<grid, 64 * WM * WN, lds, s>>>(a);
 }
 
 void launch_resblock(const ResArgs& a, int C, hipStream_t s) {
   TTS_CHECK(a.dil >= 1 && a.dil <= RB_DMAX, "resblock: dilation must be in [1, 27] (num_res_blocks <= 4)");
   if (a.max_q <= 0 || a.B <= 0) return;
+  // tiles from tools/voc_bench.hip (C2 shapes): 8 waves at C >= 96, TQ = 64 below
   switch (C) {
-    case 192: launch_rb<192, 32, 4, 1>(a, s); break;
-    case 96: launch_rb<96, 64, 2, 2>(a, s); break;
-    case 48: launch_rb<48, 128, 1, 4>(a, s); break;
-    case 256: launch_rb<256, 32, 4, 1>(a, s); break;
-    case 128: launch_rb<128, 64, 2, 2>(a, s); break;
-    case 64: launch_rb<64, 64, 2, 2>(a, s); break;
-    case 32: launch_rb<32, 128, 1, 4>(a, s); break;
+    case 192: launch_rb<192, 32, 4, 2>(a, s); break;
+    case 96: launch_rb<96, 64, 2, 4>(a, s); break;
+    case 48: launch_rb<48, 64, 1, 4>(a, s); break;
+    case 256: launch_rb<256, 32, 4, 2>(a, s); break;
+    case 128: launch_rb<128, 64, 2, 4>(a, s); break;
+    case 64: launch_rb<64, 64, 1, 4>(a, s); break;
+    case 32: launch_rb<32, 64, 1, 4>(a, s); break;
     default: TTS_CHECK(false, "resblock: unsupported channel count");
   }
   HIP_OK(hipGetLastError());
