@@ -202,6 +202,16 @@ struct MelganModel {
   std::vector<ConvLayer> convT;
   std::vector<ConvLayer> dconv, fused;  // [stage*nres + block]
   DevBuf G;
+  DevBuf out_w, out_b;  // conv_out as [c][k][o] for the fused output + PQMF kernel
+  int C_last = 0;
+};
+
+// what run_generator leaves when the output conv is left to the fused PQMF kernel
+struct GenTail {
+  const float* x = nullptr;  // last ResidualStack output (B, C, Ls), before LReLU
+  int C = 0;
+  long Ls = 0;
+  int mul = 1;
 };
 
 struct MelganWS {
@@ -926,7 +936,17 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
   {
     const std::string nm = "layers." + std::to_string(idx + 2);
     auto w = wn_weight(m, nm, {out_ch, C, 7});
-    pack_conv(G.conv_out, w, need(m, nm + ".bias", {out_ch}).d, C, out_ch, 7, 1, 1, pl3);
+    const auto& bo = need(m, nm + ".bias", {out_ch}).d;
+    pack_conv(G.conv_out, w, bo, C, out_ch, 7, 1, 1, pl3);
+    G.C_last = C;
+    if (out_ch == 4) {
+      std::vector<float> wo((size_t)C * 7 * 4);
+      for (int o = 0; o < 4; ++o)
+        for (int ci = 0; ci < C; ++ci)
+          for (int k = 0; k < 7; ++k) wo[((size_t)ci * 7 + k) * 4 + o] = w[((size_t)o * C + ci) * 7 + k];
+      G.out_w.upload(wo);
+      G.out_b.upload(bo);
+    }
   }
   if (use_pqmf) {
     const auto& g = need(m, "pqmf_layer.G", {}).d;
@@ -941,7 +961,7 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
 
 // returns total upsampling factor; writes bands (B, out_ch, up*(M_max+2pad)) into `out`
 int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int M_max, int pad, float* out,
-                  hipStream_t s) {
+                  hipStream_t s, GenTail* tail = nullptr) {
   auto& G = c->mg;
   auto& W = c->mws;
   TTS_CHECK(G.ready, "melgan weights not finalized");
@@ -1028,6 +1048,13 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
       launch_resblock(ra, C, s);
       std::swap(x, xo);
     }
+  }
+  if (tail) {
+    tail->x = x;
+    tail->C = C;
+    tail->Ls = Ls;
+    tail->mul = mul;
+    return up;
   }
   ConvCall o = cc;
   o.s[0] = src_of(x, (long)C * Ls, Ls, 1, C, 1);
@@ -1236,11 +1263,21 @@ int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int 
     int up = 1;
     for (int u : G.ups) up *= u;
     const long Ls = (long)(M_max + 2 * pad) * up;
-    c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
-    run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s);
     HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
-    launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
-                          2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
+    const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
+    if (fused) {
+      GenTail t;
+      run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t);
+      TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
+      TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
+                                G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
+                "fused output/PQMF shape not covered");
+    } else {
+      c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
+      run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s);
+      launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
+                            2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
+    }
     leave(c, stream);
   });
 }

@@ -106,3 +106,9 @@ struct ResArgs {
   int max_q, B;
 };
 void launch_resblock(const ResArgs& a, int C, hipStream_t s);
+
+// fused MB-MelGAN output conv (C -> 4, k7, LReLU + reflect pad 3 + tanh) and PQMF synthesis
+// (melgan_out.hip); returns false when the shape is not covered (N != 4, 63 taps, C not 32/48)
+bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, const float* bo, const float* G,
+                     int N, int taps, const int* lens, int len_add, int L_mul, int maxL, int B, float* y, long yb,
+                     hipStream_t s);
