@@ -232,6 +232,43 @@ def test_tacotron2_random_batch_vs_oracle():
         assert not align[i, :, L:].any()
 
 
+def test_tacotron2_batch_tiles_shrink_vs_oracle():
+    """37 utterances (3 batch tiles) in caller order with the long ones scattered: the decoder
+    decodes longest-first and drops to 2 and then 1 batch tile as rows finish; every row must
+    still equal its B=1 oracle run, in the caller's order."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=13, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    r = 2
+    m.decoder.set_r(r)
+    rs = np.random.RandomState(9)
+    B = 37
+    lens = [int(x) for x in rs.randint(2, 24, B)]
+    steps = [int(x) for x in rs.randint(2, 9, B)]
+    for i in (3, 20, 31):  # a few long rows, not in front
+        steps[i] = 41
+    for i in (7, 11, 26, 35):
+        steps[i] = 23
+    T = max(lens)
+    batch = np.zeros((B, T), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, L)
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=lens, max_decoder_steps=steps)
+    assert list(m.last_steps) == steps
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    dec, post, align = dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy()
+    for i, L in enumerate(lens):
+        d, p, a, s = orc.inference(batch[i, :L], r, steps[i])
+        M = steps[i] * r
+        assert np.abs(dec[i, :M] - d).max() <= MEL_TOL, i
+        assert np.abs(post[i, :M] - p).max() <= MEL_TOL, i
+        assert np.abs(align[i, :steps[i], :L] - a).max() <= 1e-5, i
+        assert not dec[i, M:].any() and not post[i, M:].any()
+
+
 def test_tacotron2_deterministic():
     _dev()
     fx = load_fixture("taco_sigmoid")

@@ -188,7 +188,10 @@ struct TacoWS {
   DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, spart, alpha, acum, energy, ctl;
   DevBuf dec, align, stop, pa, pbb;
   DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
-  hipGraphExec_t graph = nullptr;
+  DevBuf ids, post, map;       // rows in decode order (longest first), output scatter map
+  // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
+  // longest-first rows finish); all share one configuration key
+  hipGraphExec_t graphs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
   long graph_gen = -1;
   int gB = -1, gT = -1, gS = -1, gr = -1;
   float thr = 0.5f, gthr = -1.f;
@@ -481,6 +484,9 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.stop, (size_t)B * S_cap, g);
   grow<float>(W.pa, (size_t)B * 512 * S_cap * r, g);
   grow<float>(W.pbb, (size_t)B * 512 * S_cap * r, g);
+  grow<int64_t>(W.ids, (size_t)B * T_max, g);
+  grow<float>(W.post, (size_t)B * S_cap * r * 80, g);
+  grow<int>(W.map, BMAX, g);
   W.B = B;
   W.T_max = T_max;
   W.S_cap = S_cap;
@@ -488,7 +494,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   W.MT = Bp / 16;
 }
 
-DecDev make_dev(tts_ctx* c) {
+DecDev make_dev(tts_ctx* c, int Bact) {
   auto& W = c->tws;
   DecDev d{};
   int* ci = W.ctl.i();
@@ -503,7 +509,7 @@ DecDev make_dev(tts_ctx* c) {
   d.stop_out = W.stop.f();
   d.S_cap = W.S_cap;
   d.T_max = W.T_max;
-  d.B = W.B;
+  d.B = Bact;
   return d;
 }
 
@@ -522,12 +528,13 @@ SkJob job0() {
   return j;
 }
 
-// the 7 launches of decoder step j of a chunk (parity j & 1 selects the h_dec buffer)
-void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s) {
+// the 5 launches of decoder step j of a chunk (parity j & 1 selects the h_dec buffer) over the
+// first MT batch tiles (rows >= 16*MT must all be finished)
+void enqueue_step(tts_ctx* c, int j, int which_only, hipStream_t s, int MT) {
   auto& M = c->taco;
   auto& W = c->tws;
-  const DecDev d = make_dev(c);
-  const int r = W.r, MT = W.MT, YLD = 80 * M.r_init;
+  const DecDev d = make_dev(c, std::min(W.B, 16 * MT));
+  const int r = W.r, YLD = 80 * M.r_init;
   float* hd_cur = (j & 1) ? W.hdec1.f() : W.hdec0.f();
   float* hd_nxt = (j & 1) ? W.hdec0.f() : W.hdec1.f();
   if (which_only < 0 || which_only == 1) {  // K1: prenet layers 1+2 || stop(t-1)
@@ -723,6 +730,44 @@ void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int
   run_conv(M.post[4], cc, s);
 }
 
+template <class T>
+__global__ void gather_rows_kernel(const T* __restrict__ src, T* __restrict__ dst, const int* __restrict__ map,
+                                   long row) {
+  const long i = blockIdx.y;
+  const T* sr = src + (long)map[i] * row;
+  T* dr = dst + i * row;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < row; e += (long)gridDim.x * blockDim.x) dr[e] = sr[e];
+}
+
+// dst row i <- src row map[i], i < B
+template <class T>
+void gather_rows(const T* src, T* dst, const int* d_map, long row, int B, hipStream_t s) {
+  if (row <= 0 || B <= 0) return;
+  dim3 g((unsigned)std::min<long>((row + 255) / 256, 64), B);
+  gather_rows_kernel<T><<<g, 256, 0, s>>>(src, dst, d_map, row);
+  HIP_OK(hipGetLastError());
+}
+
+// CHUNK-step graph for batch tile count MT (captured once per configuration)
+hipGraphExec_t step_graph(tts_ctx* c, int MT, hipStream_t s) {
+  auto& W = c->tws;
+  if (W.graphs[MT]) return W.graphs[MT];
+  hipGraph_t g;
+  HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  try {
+    for (int j = 0; j < CHUNK; ++j) enqueue_step(c, j, -1, s, MT);
+    launch_dec_advance(reinterpret_cast<DecCtl*>(W.ctl.p), CHUNK, s);
+  } catch (...) {
+    hipGraph_t tmp;
+    (void)hipStreamEndCapture(s, &tmp);
+    throw;
+  }
+  HIP_OK(hipStreamEndCapture(s, &g));
+  HIP_OK(hipGraphInstantiate(&W.graphs[MT], g, nullptr, nullptr, 0));
+  HIP_OK(hipGraphDestroy(g));
+  return W.graphs[MT];
+}
+
 void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, int T_max, int r,
                 const int32_t* h_max_steps, int S_cap, float thr, float* d_dec, float* d_post, float* d_align,
                 float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream) {
@@ -742,15 +787,30 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   auto& W = c->tws;
   hipStream_t s = c->s;
   enter(c, stream);
-  // control block: base = 0, all_done = 0, done/steps/status = 0, max_steps
+  // Decode order: longest expected first (max_decoder_steps, then text length), so the rows still
+  // decoding at the end sit in the first batch tiles and the step can shrink to fewer tiles.
+  // Every row is independent, so the order changes nothing but speed; outputs are scattered back.
+  std::vector<int> perm(B), inv(B);
+  for (int b = 0; b < B; ++b) perm[b] = b;
+  std::stable_sort(perm.begin(), perm.end(), [&](int x, int y) {
+    if (h_max_steps[x] != h_max_steps[y]) return h_max_steps[x] > h_max_steps[y];
+    return h_lens[x] > h_lens[y];
+  });
+  for (int i = 0; i < B; ++i) inv[perm[i]] = i;
+  int* d_map = W.map.i();
+  HIP_OK(hipMemcpyAsync(d_map, perm.data(), B * 4, hipMemcpyHostToDevice, s));
+  gather_rows<int64_t>(ids, reinterpret_cast<int64_t*>(W.ids.p), d_map, T_max, B, s);
+  // control block: base = 0, all_done = 0, active_tiles = MT, done/steps/status = 0, max_steps
   std::vector<int> ctl(4 + 4 * BMAX, 0);
-  for (int b = 0; b < B; ++b) ctl[4 + 3 * BMAX + b] = h_max_steps[b];
+  ctl[2] = W.MT;
+  for (int i = 0; i < B; ++i) ctl[4 + 3 * BMAX + i] = h_max_steps[perm[i]];
   HIP_OK(hipMemcpyAsync(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice, s));
-  std::vector<int> lens(h_lens, h_lens + B);
+  std::vector<int> lens(B);
+  for (int i = 0; i < B; ++i) lens[i] = h_lens[perm[i]];
   HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
   W.thr = thr;
   // encoder + processed inputs
-  run_encoder(c, ids, B, T_max, W.enc.f(), s);
+  run_encoder(c, reinterpret_cast<const int64_t*>(W.ids.p), B, T_max, W.enc.f(), s);
   {
     ConvCall cc;
     cc.lens = W.lens.i();
@@ -780,25 +840,13 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   HIP_OK(hipMemsetAsync(W.acnt.p, 0, BMAX * sizeof(unsigned), s));
   bcast_rows_kernel<<<256, 256, 0, s>>>(M.att_bias.f(), 4096, W.gatt.f(), Bp);
   HIP_OK(hipGetLastError());
-  // graph for CHUNK steps (+ base advance), cached per configuration / buffer generation
-  if (!W.graph || W.graph_gen != W.gen || W.gB != B || W.gT != T_max || W.gS != S_cap || W.gr != r || W.gthr != thr) {
-    if (W.graph) {
-      HIP_OK(hipGraphExecDestroy(W.graph));
-      W.graph = nullptr;
-    }
-    hipGraph_t g;
-    HIP_OK(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
-    try {
-      for (int j = 0; j < CHUNK; ++j) enqueue_step(c, j, -1, s);
-      launch_dec_advance(reinterpret_cast<DecCtl*>(W.ctl.p), CHUNK, s);
-    } catch (...) {
-      hipGraph_t tmp;
-      (void)hipStreamEndCapture(s, &tmp);
-      throw;
-    }
-    HIP_OK(hipStreamEndCapture(s, &g));
-    HIP_OK(hipGraphInstantiate(&W.graph, g, nullptr, nullptr, 0));
-    HIP_OK(hipGraphDestroy(g));
+  // step graphs, cached per configuration / buffer generation
+  if (W.graph_gen != W.gen || W.gB != B || W.gT != T_max || W.gS != S_cap || W.gr != r || W.gthr != thr) {
+    for (auto& ge : W.graphs)
+      if (ge) {
+        HIP_OK(hipGraphExecDestroy(ge));
+        ge = nullptr;
+      }
     W.graph_gen = W.gen;
     W.gB = B;
     W.gT = T_max;
@@ -806,17 +854,22 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     W.gr = r;
     W.gthr = thr;
   }
-  // run chunks until every utterance is done (checked one chunk behind) or t > max steps
+  for (int mt = 1; mt <= W.MT; ++mt) step_graph(c, mt, s);
+  // run chunks until every utterance is done (checked one chunk behind) or t > max steps; drop
+  // to fewer batch tiles once the trailing rows have all finished
   const int chunks_max = max_ms / CHUNK + 1;  // covers t = max_ms (stop of the last step)
   bool done = false;
+  int mt = W.MT;
   for (int ch = 0; ch < chunks_max && !done; ++ch) {
-    HIP_OK(hipGraphLaunch(W.graph, s));
-    HIP_OK(hipMemcpyAsync(&c->pinned[ch & 1], &reinterpret_cast<DecCtl*>(W.ctl.p)->all_done, 4,
+    HIP_OK(hipGraphLaunch(W.graphs[mt], s));
+    HIP_OK(hipMemcpyAsync(&c->pinned[2 * (ch & 1)], &reinterpret_cast<DecCtl*>(W.ctl.p)->all_done, 8,
                           hipMemcpyDeviceToHost, s));
     HIP_OK(hipEventRecord(c->ev_chunk[ch & 1], s));
     if (ch >= 1) {
       HIP_OK(hipEventSynchronize(c->ev_chunk[(ch - 1) & 1]));
-      if (c->pinned[(ch - 1) & 1]) done = true;
+      const int* pv = &c->pinned[2 * ((ch - 1) & 1)];
+      if (pv[0]) done = true;
+      else if (pv[1] >= 1 && pv[1] < mt) mt = pv[1];
     }
   }
   HIP_OK(hipStreamSynchronize(s));
@@ -824,20 +877,24 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   HIP_OK(hipMemcpy(res.data(), W.ctl.i() + 4, 3 * BMAX * 4, hipMemcpyDeviceToHost));
   int maxM = 0;
   std::vector<int> mlens(B);
-  for (int b = 0; b < B; ++b) {
-    TTS_CHECK(res[b] == 1, "decoder did not finish an utterance (internal error)");
-    h_steps[b] = res[BMAX + b];
-    h_status[b] = res[2 * BMAX + b];
-    mlens[b] = h_steps[b] * r;
-    maxM = std::max(maxM, mlens[b]);
+  for (int i = 0; i < B; ++i) {
+    TTS_CHECK(res[i] == 1, "decoder did not finish an utterance (internal error)");
+    const int b = perm[i];
+    h_steps[b] = res[BMAX + i];
+    h_status[b] = res[2 * BMAX + i];
+    mlens[i] = h_steps[b] * r;
+    maxM = std::max(maxM, mlens[i]);
   }
   HIP_OK(hipMemcpyAsync(W.mlens.p, mlens.data(), B * 4, hipMemcpyHostToDevice, s));
   const long fb = (long)S_cap * r * 80;
-  HIP_OK(hipMemsetAsync(d_post, 0, (size_t)B * fb * 4, s));
-  run_postnet(c, W.dec.f(), fb, W.mlens.i(), B, S_cap * r, maxM, d_post, fb, s);
-  HIP_OK(hipMemcpyAsync(d_dec, W.dec.p, (size_t)B * fb * 4, hipMemcpyDeviceToDevice, s));
-  HIP_OK(hipMemcpyAsync(d_align, W.align.p, (size_t)B * S_cap * T_max * 4, hipMemcpyDeviceToDevice, s));
-  HIP_OK(hipMemcpyAsync(d_stop, W.stop.p, (size_t)B * S_cap * 4, hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemsetAsync(W.post.p, 0, (size_t)B * fb * 4, s));
+  run_postnet(c, W.dec.f(), fb, W.mlens.i(), B, S_cap * r, maxM, W.post.f(), fb, s);
+  // scatter back to the caller's row order: output row b <- decode row inv[b]
+  HIP_OK(hipMemcpyAsync(d_map, inv.data(), B * 4, hipMemcpyHostToDevice, s));
+  gather_rows<float>(W.post.f(), d_post, d_map, fb, B, s);
+  gather_rows<float>(W.dec.f(), d_dec, d_map, fb, B, s);
+  gather_rows<float>(W.align.f(), d_align, d_map, (long)S_cap * T_max, B, s);
+  gather_rows<float>(W.stop.f(), d_stop, d_map, S_cap, B, s);
   leave(c, stream);
   c->last_B = B;
   c->last_T = T_max;
@@ -1131,8 +1188,11 @@ int tts_ctx_destroy(tts_ctx* c) {
     {
       DeviceGuard g(c->device);
       (void)hipStreamSynchronize(c->s);
-      if (c->tws.graph) (void)hipGraphExecDestroy(c->tws.graph);
-      c->tws.graph = nullptr;
+      for (auto& ge : c->tws.graphs)
+        if (ge) {
+          (void)hipGraphExecDestroy(ge);
+          ge = nullptr;
+        }
     }
     int dev = c->device;
     {
@@ -1301,7 +1361,7 @@ int tts_pqmf_synthesis(tts_ctx* c, const float* d_x, int B, int N, int L, const 
 int tts_time_decoder_kernel(tts_ctx* c, int which, int iters, float* ms_out) {
   return guarded([&] {
     TTS_CHECK(c && ms_out && iters >= 1, "bad arguments");
-    TTS_CHECK(c->last_B > 0 && c->tws.graph, "run tts_taco_infer first");
+    TTS_CHECK(c->last_B > 0 && c->tws.graphs[c->tws.MT], "run tts_taco_infer first");
     TTS_CHECK(c->tws.S_cap >= CHUNK + 2, "S_cap too small for timing");
     DeviceGuard g(c->device);
     auto& W = c->tws;
@@ -1314,14 +1374,14 @@ int tts_time_decoder_kernel(tts_ctx* c, int which, int iters, float* ms_out) {
     HIP_OK(hipEventCreate(&e0));
     HIP_OK(hipEventCreate(&e1));
     HIP_OK(hipMemcpyAsync(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice, s));
-    if (which == 0) enqueue_step(c, 0, 0, s);  // warm-up
-    else HIP_OK(hipGraphLaunch(W.graph, s));
+    if (which == 0) enqueue_step(c, 0, 0, s, W.MT);  // warm-up
+    else HIP_OK(hipGraphLaunch(W.graphs[W.MT], s));
     HIP_OK(hipMemcpyAsync(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice, s));
     HIP_OK(hipEventRecord(e0, s));
     for (int i = 0; i < iters; ++i) {
-      if (which == 0) enqueue_step(c, 0, 0, s);
+      if (which == 0) enqueue_step(c, 0, 0, s, W.MT);
       else {
-        HIP_OK(hipGraphLaunch(W.graph, s));
+        HIP_OK(hipGraphLaunch(W.graphs[W.MT], s));
       }
     }
     HIP_OK(hipEventRecord(e1, s));

@@ -54,9 +54,10 @@ struct SkArgs {
 };
 
 struct DecCtl {
-  int base;      // step index of j = 0 in the current chunk
-  int all_done;  // every utterance finished: all later kernels exit at entry
-  int pad0, pad1;
+  int base;          // step index of j = 0 in the current chunk
+  int all_done;      // every utterance finished: all later kernels exit at entry
+  int active_tiles;  // 1 + (largest unfinished row) / 16: the host drops to a smaller batch tile
+  int pad1;
 };
 
 struct DecDev {

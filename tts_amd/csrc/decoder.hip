@@ -354,9 +354,11 @@ __global__ __launch_bounds__(1024) void prenet_stop_kernel(SkArgs A, DecDev D, S
     }
     __syncthreads();
     if (tid == 0) {
-      int all = 1;
-      for (int k = 0; k < D.B; ++k) all &= dflag[k];
-      D.ctl->all_done = all;
+      int last = -1;
+      for (int k = 0; k < D.B; ++k)
+        if (!dflag[k]) last = k;
+      D.ctl->all_done = last < 0;
+      D.ctl->active_tiles = last / 16 + 1;
     }
     return;
   }
