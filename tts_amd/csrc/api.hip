@@ -15,7 +15,8 @@
 
 void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int num_rows, int D,
                          const int* lens, int B, float* out, hipStream_t s);
-void launch_bilstm_rec(const float* Gin, const float* WhhT, const int* lens, int T_max, int B, float* out,
+void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
+                   float* out,
                        hipStream_t s);
 
 static thread_local std::string g_err;
@@ -185,6 +186,7 @@ struct TacoWS {
   int B = 0, T_max = 0, S_cap = 0, r = 0, MT = 0;
   long gen = 0;
   DevBuf lens, mlens, x0, ca, cb, gin, enc, penc;
+  DevBuf lh, lc;  // BiLSTM h (2 buffers x 2 directions, fragment order) and c
   DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, spart, alpha, acum, energy, ctl;
   DevBuf dec, align, stop, pa, pbb;
   DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
@@ -334,24 +336,27 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     pack_conv(M.enc[i], Wm, b, E, E, 5, 1, 1, pl2);
   }
   {  // BiLSTM input projection for both directions as one K=1 conv (Cout 2048), b_ih + b_hh folded
+    // gate rows of both the input projection and W_hh in gate-interleaved tile order:
+    // column dir*1024 + tile*16 + gate*4 + unit  (unit = 4*tile + u)
     std::vector<float> Wm((size_t)2048 * E), b(2048);
-    std::vector<float> whhT((size_t)2 * 4 * 64 * 256 * 4);
+    std::vector<float> whh_all;
     for (int dir = 0; dir < 2; ++dir) {
       const std::string sfx = dir ? "_reverse" : "";
       const auto& wih = need(h, "encoder.lstm.weight_ih_l0" + sfx, {4 * H, E}).d;
       const auto& whh = need(h, "encoder.lstm.weight_hh_l0" + sfx, {4 * H, H}).d;
       const auto& bih = need(h, "encoder.lstm.bias_ih_l0" + sfx, {4 * H}).d;
       const auto& bhh = need(h, "encoder.lstm.bias_hh_l0" + sfx, {4 * H}).d;
-      std::memcpy(&Wm[(size_t)dir * 1024 * E], wih.data(), (size_t)1024 * E * 4);
-      for (int i = 0; i < 1024; ++i) b[dir * 1024 + i] = bih[i] + bhh[i];
-      for (int g = 0; g < 4; ++g)
-        for (int k4 = 0; k4 < 64; ++k4)
-          for (int j = 0; j < 256; ++j)
-            for (int e = 0; e < 4; ++e)
-              whhT[((((size_t)dir * 4 + g) * 64 + k4) * 256 + j) * 4 + e] = whh[(size_t)(g * 256 + j) * H + 4 * k4 + e];
+      const auto wt = lstm_tile_rows(wih, H, E);
+      std::memcpy(&Wm[(size_t)dir * 1024 * E], wt.data(), (size_t)1024 * E * 4);
+      std::vector<float> bs(4 * H);
+      for (int i = 0; i < 4 * H; ++i) bs[i] = bih[i] + bhh[i];
+      const auto bt = lstm_tile_rows(bs, H, 1);
+      std::copy(bt.begin(), bt.end(), b.begin() + dir * 1024);
+      const auto hs = swz(lstm_tile_rows(whh, H, H), 4 * H, H);
+      whh_all.insert(whh_all.end(), hs.begin(), hs.end());
     }
     pack_conv(M.lstm_in, Wm, b, E, 2048, 1, 1, 1, pl0);
-    M.whhT.upload(whhT);
+    M.whhT.upload(whh_all);
   }
   {  // processed_inputs = inputs_layer(enc)  (common_layers.py:262-263), K=1 conv, no bias
     const auto& win = need(h, "decoder.attention.inputs_layer.linear_layer.weight", {A, E}).d;
@@ -456,6 +461,8 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.ca, (size_t)B * T_max * 512, g);
   grow<float>(W.cb, (size_t)B * T_max * 512, g);
   grow<float>(W.gin, (size_t)B * T_max * 2048, g);
+  grow<float>(W.lh, (size_t)2 * 2 * 64 * 256, g);
+  grow<float>(W.lc, (size_t)2 * 64 * 256, g);
   grow<float>(W.enc, (size_t)B * T_max * 512, g);
   grow<float>(W.penc, (size_t)B * T_max * 128, g);
   grow<float>(W.p1, (size_t)Bp * 256, g);
@@ -685,14 +692,14 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
   cc.out = W.ca.f();
   run_conv(M.enc[2], cc, s);
   cc.s[0] = src_of(W.ca.f(), (long)512 * T_max, T_max, 1, 512, 0);
-  cc.out = W.gin.f();
+  cc.out = W.gin.f();  // (B, T_max, 2048): time-major, so one step's gates of a tile are contiguous
   cc.ob = (long)2048 * T_max;
-  cc.oc = T_max;
-  cc.ot = 1;
+  cc.oc = 1;
+  cc.ot = 2048;
   cc.epi = 0;
   run_conv(M.lstm_in, cc, s);
   HIP_OK(hipMemsetAsync(enc_out, 0, (size_t)B * T_max * 512 * 4, s));
-  launch_bilstm_rec(W.gin.f(), M.whhT.f(), lens, T_max, B, enc_out, s);
+  launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
 }
 
 void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int B, int Mmax_alloc, int max_q,

@@ -2,10 +2,11 @@
 //  * embedding gather  (TTS/tts/models/tacotron2.py:61,144)
 //  * BiLSTM recurrence (TTS/tts/layers/tacotron2.py:91-96,116-118, nn.LSTM bidirectional,
 //    no packing at inference). The input projection x.W_ih^T + b_ih + b_hh for both directions
-//    runs beforehand as one MFMA conv (K=1, Cout=2048); this kernel does the T sequential
-//    steps with per-utterance lengths: the reverse direction starts at T_b - 1, never in the
-//    padding (a padded reverse pass differs by 0.29 L-inf).
+//    runs beforehand as one MFMA conv (K=1, Cout=2048); the step kernel below does the T
+//    sequential steps with per-utterance lengths: the reverse direction starts at T_b - 1, never
+//    in the padding (a padded reverse pass differs by 0.29 L-inf).
 #include "common.h"
+#include "decoder.h"  // frag_idx
 
 __global__ __launch_bounds__(256) void embed_gather_kernel(const int64_t* __restrict__ ids, int T_max,
                                                            const float* __restrict__ table, int num_rows,
@@ -26,60 +27,97 @@ void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int 
   HIP_OK(hipGetLastError());
 }
 
-// Gin: (B, 2048, T_max) channel-major gate pre-activations incl. b_ih + b_hh
-//      rows [dir*1024 + gate*256 + j], gate order i, f, g, o.
-// WhhT: per dir [gate][k/4][j][4] so thread j's float4 loads are contiguous across the wave.
-// out: (B, T_max, 512) = [fwd h | bwd h]
-__global__ __launch_bounds__(256) void bilstm_rec_kernel(const float* __restrict__ Gin,
-                                                         const float* __restrict__ WhhT,
-                                                         const int* lens, int T_max,
-                                                         float* __restrict__ out) {
-  const int b = blockIdx.x >> 1, dir = blockIdx.x & 1;
-  const int j = threadIdx.x;
-  const int T = lens[b];
-  __shared__ __attribute__((aligned(16))) float h[256];
-  h[j] = 0.f;
-  float c = 0.f;
-  __syncthreads();
-  const f32x4* W = reinterpret_cast<const f32x4*>(WhhT) + (long)dir * 4 * 64 * 256 + j;
-  const float* gbase = Gin + (long)b * 2048 * T_max + (long)dir * 1024 * T_max;
-  for (int step = 0; step < T; ++step) {
-    const int t = dir ? (T - 1 - step) : step;
-    float a0 = gbase[(long)(0 * 256 + j) * T_max + t];
-    float a1 = gbase[(long)(1 * 256 + j) * T_max + t];
-    float a2 = gbase[(long)(2 * 256 + j) * T_max + t];
-    float a3 = gbase[(long)(3 * 256 + j) * T_max + t];
-#pragma unroll 8
-    for (int k4 = 0; k4 < 64; ++k4) {
-      const f32x4 hv = *reinterpret_cast<const f32x4*>(h + 4 * k4);
-      const f32x4 w0 = W[(long)(0 * 64 + k4) * 256];
-      const f32x4 w1 = W[(long)(1 * 64 + k4) * 256];
-      const f32x4 w2 = W[(long)(2 * 64 + k4) * 256];
-      const f32x4 w3 = W[(long)(3 * 64 + k4) * 256];
+// One BiLSTM time step for every utterance and both directions. The recurrent GEMM
+// gates = h W_hh^T runs on MFMA over all B utterances at once (M = 16-row batch tiles), split by
+// hidden units across 128 workgroups: workgroup (dir, tile) owns 4 hidden units = the i, f, g, o
+// rows of one 16-row tile (gate-interleaved like the decoder LSTMs), so the cell update is its
+// epilogue and W_hh is spread over the chip instead of streamed by one CU per utterance. One
+// launch per step; h ping-pongs between two fragment-order buffers.
+//   Whh : per dir, gate-interleaved tiles, swizzled [64 tiles][16 k-chunks][64 lanes][4]
+//   Gin : (B, T_max, 2048) x W_ih^T + b_ih + b_hh, columns [dir][tile][gate][unit]
+//   h   : [dir][Bp x 256] fragment order (frag_idx), c: [dir][Bp][256]
+//   out : (B, T_max, 512) = [fwd h | bwd h]
+template <int MT>
+__global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restrict__ Whh,
+                                                          const float* __restrict__ Gin, const int* lens,
+                                                          int T_max, int B, int step,
+                                                          const float* __restrict__ h_in, float* __restrict__ h_out,
+                                                          float* __restrict__ c, float* __restrict__ out) {
+  constexpr int Bp = MT * 16;
+  constexpr int H = 256, NKC = H / 16, KPW = NKC / 4;  // 4 k-chunks per wave
+  __shared__ float part[4 * Bp * 17];
+  const int dir = blockIdx.x >> 6, tl = blockIdx.x & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const f32x4* Wv = reinterpret_cast<const f32x4*>(Whh) + ((long)(dir * 64 + tl) * NKC + wave * KPW) * 64 + lane;
+  const float* hx = h_in + (long)dir * Bp * H + (long)(wave * KPW) * 256 + 4 * lane;
+  f32x4 w[KPW], x[KPW][MT];
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        a0 = fmaf(w0[e], hv[e], a0);
-        a1 = fmaf(w1[e], hv[e], a1);
-        a2 = fmaf(w2[e], hv[e], a2);
-        a3 = fmaf(w3[e], hv[e], a3);
-      }
-    }
-    const float ig = 1.f / (1.f + expf(-a0));
-    const float fg = 1.f / (1.f + expf(-a1));
-    const float gg = tanhf(a2);
-    const float og = 1.f / (1.f + expf(-a3));
-    c = fg * c + ig * gg;
-    const float hn = og * tanhf(c);
-    __syncthreads();
-    h[j] = hn;
-    __syncthreads();
-    out[((long)b * T_max + t) * 512 + dir * 256 + j] = hn;
+  for (int k = 0; k < KPW; ++k) {
+    w[k] = Wv[(long)k * 64];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) x[k][mt] = *reinterpret_cast<const f32x4*>(hx + (long)mt * 16 * H + k * 256);
   }
+  // epilogue operands (clamped indices; validity applied at the stores)
+  const int m = min(tid >> 2, Bp - 1), u = tid & 3;
+  const int Tm = lens[min(m, B - 1)];
+  const bool valid = (tid >> 2) < Bp && m < B && step < Tm;
+  const int t = min(max(dir ? Tm - 1 - step : step, 0), T_max - 1);
+  const float* gp = Gin + ((long)min(m, B - 1) * T_max + t) * 2048 + dir * 1024 + tl * 16 + u;
+  float gin[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gin[q] = gp[q * 4];
+  const long ci = ((long)dir * Bp + m) * H + tl * 4 + u;
+  const float cprev = c[ci];
+  f32x4 acc[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < KPW; ++k)
+#pragma unroll
+    for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[k][mt][s4], w[k][s4], acc[mt]);
+  float* p = part + wave * Bp * 17;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
+  __syncthreads();
+  if (!valid) return;
+  float pre[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const int n = q * 4 + u;
+    pre[q] = part[m * 17 + n] + part[(Bp + m) * 17 + n] + part[(2 * Bp + m) * 17 + n] + part[(3 * Bp + m) * 17 + n] +
+             gin[q];
+  }
+  const float ig = 1.f / (1.f + expf(-pre[0]));
+  const float fg = 1.f / (1.f + expf(-pre[1]));
+  const float gg = tanhf(pre[2]);
+  const float og = 1.f / (1.f + expf(-pre[3]));
+  const float cn = fg * cprev + ig * gg;
+  const float hn = og * tanhf(cn);
+  c[ci] = cn;
+  h_out[(long)dir * Bp * H + frag_idx(m, tl * 4 + u, H)] = hn;
+  out[((long)m * T_max + t) * 512 + dir * 256 + tl * 4 + u] = hn;
 }
 
-void launch_bilstm_rec(const float* Gin, const float* WhhT, const int* lens, int T_max, int B, float* out,
-                       hipStream_t s) {
+void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
+                   float* out, hipStream_t s) {
   if (B <= 0 || T_max <= 0) return;
-  bilstm_rec_kernel<<<2 * B, 256, 0, s>>>(Gin, WhhT, lens, T_max, out);
+  TTS_CHECK(B <= 64, "bilstm: B <= 64");
+  const int MT = (B + 15) / 16, Bp = MT * 16;
+  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * 2 * Bp * 256 * 4, s));
+  HIP_OK(hipMemsetAsync(cbuf, 0, (size_t)2 * Bp * 256 * 4, s));
+  for (int step = 0; step < T_max; ++step) {
+    const float* hi = hbuf + (size_t)(step & 1) * 2 * Bp * 256;
+    float* ho = hbuf + (size_t)((step + 1) & 1) * 2 * Bp * 256;
+    switch (MT) {
+      case 1: bilstm_step_kernel<1><<<128, 256, 0, s>>>(Whh, Gin, lens, T_max, B, step, hi, ho, cbuf, out); break;
+      case 2: bilstm_step_kernel<2><<<128, 256, 0, s>>>(Whh, Gin, lens, T_max, B, step, hi, ho, cbuf, out); break;
+      case 3: bilstm_step_kernel<3><<<128, 256, 0, s>>>(Whh, Gin, lens, T_max, B, step, hi, ho, cbuf, out); break;
+      default: bilstm_step_kernel<4><<<128, 256, 0, s>>>(Whh, Gin, lens, T_max, B, step, hi, ho, cbuf, out); break;
+    }
+  }
   HIP_OK(hipGetLastError());
 }
