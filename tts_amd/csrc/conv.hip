@@ -39,7 +39,10 @@ struct ConvTileCfg {
   static constexpr int SPT = (16 * ROWMAX + 255) / 256;  // staged elements per thread
 };
 
-template <int MI, int NI, int WM, int WN>
+// KT > 0: the tap count is a compile-time constant and the weight fragments run in a ring of KT
+// k-chunks (one staging chunk ahead, like the ResidualStack kernel); KT = 0: runtime taps, one
+// k-chunk ahead.
+template <int MI, int NI, int WM, int WN, int KT = 0>
 __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   using Cfg = ConvTileCfg<MI, NI, WM, WN>;
   constexpr int TC = Cfg::TC, TQ = Cfg::TQ, SPT = Cfg::SPT;
@@ -54,7 +57,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   if (q0 >= Lq) return;
   const int co0 = blockIdx.y * TC;
   const int Lin = base * a.in_mul;
-  const int K = a.K, dil = a.dil;
+  const int K = KT > 0 ? KT : a.K, dil = a.dil;
   const int span = (K - 1) * dil;
   const int ROW = TQ + span + 1;
   const int XS = (16 * ROW + 3) & ~3;  // one LDS X buffer (floats)
@@ -132,37 +135,75 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 
   stage_load(0);
-  f32x4 Anext[MI];
+  if constexpr (KT > 0) {
+    f32x4 ring[KT][MI];
+    auto wload = [&](f32x4 (&r)[MI], int kc) {
+      kc = min(kc, nkc_total - 1);
 #pragma unroll
-  for (int mi = 0; mi < MI; ++mi) Anext[mi] = Wv[((long)(mt0 + mi) * nkc_total + 0) * 64 + lane];
-  stage_store(X0, 0);
-  __syncthreads();
-  for (int chunk = 0; chunk < nchunks; ++chunk) {
-    float* X = (chunk & 1) ? X1 : X0;
-    if (chunk + 1 < nchunks) stage_load(chunk + 1);  // in flight during this chunk's MFMAs
-    for (int kq = 0; kq < K; ++kq) {
-      const int kc = chunk * K + kq;
-      f32x4 A[MI];
+      for (int mi = 0; mi < MI; ++mi) r[mi] = Wv[((long)(mt0 + mi) * nkc_total + kc) * 64 + lane];
+    };
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) A[mi] = Anext[mi];
-      const int kn = min(kc + 1, nkc_total - 1);
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) Anext[mi] = Wv[((long)(mt0 + mi) * nkc_total + kn) * 64 + lane];
-      const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
-      const int ov[4] = {o.x, o.y, o.z, o.w};
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float bv[NI];
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) bv[ni] = X[ov[s] + qb + ni * 16];
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
-      }
-    }
-    if (chunk + 1 < nchunks) stage_store((chunk & 1) ? X0 : X1, chunk + 1);
+    for (int kq = 0; kq < KT; ++kq) wload(ring[kq], kq);
+    stage_store(X0, 0);
     __syncthreads();
+    for (int chunk = 0; chunk < nchunks; ++chunk) {
+      float* X = (chunk & 1) ? X1 : X0;
+      if (chunk + 1 < nchunks) stage_load(chunk + 1);  // in flight during this chunk's MFMAs
+#pragma unroll
+      for (int kq = 0; kq < KT; ++kq) {
+        f32x4 A[MI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) A[mi] = ring[kq][mi];
+        wload(ring[kq], (chunk + 1) * KT + kq);
+        const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
+        const int ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float bv[NI];
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) bv[ni] = X[ov[s] + qb + ni * 16];
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
+        }
+      }
+      if (chunk + 1 < nchunks) stage_store((chunk & 1) ? X0 : X1, chunk + 1);
+      __syncthreads();
+    }
+  } else {
+    f32x4 Anext[MI];
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) Anext[mi] = Wv[((long)(mt0 + mi) * nkc_total + 0) * 64 + lane];
+    stage_store(X0, 0);
+    __syncthreads();
+    for (int chunk = 0; chunk < nchunks; ++chunk) {
+      float* X = (chunk & 1) ? X1 : X0;
+      if (chunk + 1 < nchunks) stage_load(chunk + 1);  // in flight during this chunk's MFMAs
+      for (int kq = 0; kq < K; ++kq) {
+        const int kc = chunk * K + kq;
+        f32x4 A[MI];
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) A[mi] = Anext[mi];
+        const int kn = min(kc + 1, nkc_total - 1);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi) Anext[mi] = Wv[((long)(mt0 + mi) * nkc_total + kn) * 64 + lane];
+        const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
+        const int ov[4] = {o.x, o.y, o.z, o.w};
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          float bv[NI];
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) bv[ni] = X[ov[s] + qb + ni * 16];
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
+        }
+      }
+      if (chunk + 1 < nchunks) stage_store((chunk & 1) ? X0 : X1, chunk + 1);
+      __syncthreads();
+    }
   }
 
   // epilogue: bias, activation, optional residual, strided store
@@ -236,19 +277,31 @@ void launch_conv(const ConvArgs& a, int tile, hipStream_t s) {
   TTS_CHECK(a.nphase >= 1 && a.nphase <= 8, "conv: nphase");
   TTS_CHECK((a.K - 1) * a.dil <= CONV_MAX_SPAN, "conv: receptive span too large for the generic kernel");
   if (a.max_q <= 0 || a.B <= 0) return;
-  const int TQ = conv_tile_tq(tile);
+  int TQ = conv_tile_tq(tile), TC = conv_tile_tc(tile);
+  // compile-time-tap variants with a weight ring (tools/conv_bench.hip, postnet 512->512 k5:
+  // 128x64 one-ahead 642 us, 64x64 ring5 557 us)
+  int variant = -1;
+  if (a.K == 5 && tile == TILE_128x64) variant = 0, TC = 64;
+  else if (a.K == 5 && tile == TILE_80x64) variant = 1;
+  else if (a.K == 2 && tile == TILE_192x64) variant = 3;
   const int span = (a.K - 1) * a.dil;
   const int ROW = TQ + span + 1;
   const size_t lds = (size_t)(2 * ((16 * ROW + 3) & ~3) + 16 * a.K) * 4;
-  dim3 grid((a.max_q + TQ - 1) / TQ, a.Cout_pad / conv_tile_tc(tile), a.B * a.nphase);
-  switch (tile) {
-    case TILE_128x64: conv_mfma_kernel<4, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
-    case TILE_64x64: conv_mfma_kernel<2, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
-    case TILE_192x64: conv_mfma_kernel<3, 4, 4, 1><<<grid, 256, lds, s>>>(a); break;
-    case TILE_96x64: conv_mfma_kernel<3, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
-    case TILE_48x128: conv_mfma_kernel<3, 2, 1, 4><<<grid, 256, lds, s>>>(a); break;
-    case TILE_80x64: conv_mfma_kernel<5, 1, 1, 4><<<grid, 256, lds, s>>>(a); break;
-    default: conv_mfma_kernel<1, 4, 1, 4><<<grid, 256, lds, s>>>(a); break;
+  dim3 grid((a.max_q + TQ - 1) / TQ, a.Cout_pad / TC, a.B * a.nphase);
+  switch (variant) {
+    case 0: conv_mfma_kernel<2, 2, 2, 2, 5><<<grid, 256, lds, s>>>(a); break;
+    case 1: conv_mfma_kernel<5, 1, 1, 4, 5><<<grid, 256, lds, s>>>(a); break;
+    case 3: conv_mfma_kernel<3, 4, 4, 1, 2><<<grid, 256, lds, s>>>(a); break;
+    default:
+      switch (tile) {
+        case TILE_128x64: conv_mfma_kernel<4, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
+        case TILE_64x64: conv_mfma_kernel<2, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
+        case TILE_192x64: conv_mfma_kernel<3, 4, 4, 1><<<grid, 256, lds, s>>>(a); break;
+        case TILE_96x64: conv_mfma_kernel<3, 2, 2, 2><<<grid, 256, lds, s>>>(a); break;
+        case TILE_48x128: conv_mfma_kernel<3, 2, 1, 4><<<grid, 256, lds, s>>>(a); break;
+        case TILE_80x64: conv_mfma_kernel<5, 1, 1, 4><<<grid, 256, lds, s>>>(a); break;
+        default: conv_mfma_kernel<1, 4, 1, 4><<<grid, 256, lds, s>>>(a); break;
+      }
   }
   HIP_OK(hipGetLastError());
 }
