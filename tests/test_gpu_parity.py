@@ -319,3 +319,70 @@ def test_postnet_vs_oracle():
     for i, L in enumerate(lens):
         assert np.abs(out[i, :L] - orc.postnet(dec[i, :L])).max() <= 1e-4
         assert not out[i, L:].any()
+
+
+def _synth_files(tmp_path, with_vocoder=True):
+    import json as _json
+    from tts_amd.spec import MelganConfig, TacotronConfig
+    from tts_amd.text import symbols
+    cfg = TacotronConfig(num_chars=len(symbols))
+    _, sd = taco_state_dict(None, seed=21, overrides={}, stop_bias=-1e4, cfg=cfg)
+    audio = dict(fft_size=1024, win_length=1024, hop_length=256, sample_rate=22050, preemphasis=0.0,
+                 ref_level_db=20, power=1.5, griffin_lim_iters=4, num_mels=80, mel_fmin=50.0, mel_fmax=7600.0,
+                 spec_gain=1, signal_norm=True, min_level_db=-100, symmetric_norm=True, max_norm=4.0,
+                 clip_norm=True)
+    tcfg = {"model": "Tacotron2", "r": 7, "use_phonemes": False, "text_cleaner": "english_cleaners",
+            "audio": audio, "attention_norm": "sigmoid", "double_decoder_consistency": True, "ddc_r": 7,
+            "prenet_dropout": False, "separate_stopnet": True, "location_attn": True}
+    (tmp_path / "tts.json").write_text(_json.dumps(tcfg))
+    torch.save({"model": {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, "r": 2},
+               str(tmp_path / "tts.pth"))
+    conf = {"use_cuda": True, "tts_checkpoint": str(tmp_path / "tts.pth"), "tts_config": str(tmp_path / "tts.json"),
+            "tts_speakers": None, "vocoder_checkpoint": None, "vocoder_config": None, "wavernn_lib_path": None}
+    if with_vocoder:
+        mcfg, msd = melgan_state_dict(seed=5, cfg=MelganConfig())
+        vcfg = {"generator_model": "multiband_melgan_generator", "audio": audio,
+                "generator_model_params": {"upsample_factors": list(mcfg.upsample_factors),
+                                           "num_res_blocks": mcfg.num_res_blocks}}
+        (tmp_path / "voc.json").write_text(_json.dumps(vcfg))
+        from tts_amd import MultibandMelganGenerator
+        full = MultibandMelganGenerator(in_channels=mcfg.in_channels, out_channels=mcfg.out_channels,
+                                        base_channels=mcfg.base_channels, upsample_factors=mcfg.upsample_factors,
+                                        num_res_blocks=mcfg.num_res_blocks).state_dict()  # + PQMF buffers
+        full.update({k: torch.from_numpy(np.asarray(v)) for k, v in msd.items()})
+        torch.save({"model": full}, str(tmp_path / "voc.pth"))
+        conf["vocoder_checkpoint"] = str(tmp_path / "voc.pth")
+        conf["vocoder_config"] = str(tmp_path / "voc.json")
+    return conf
+
+
+def test_synthesizer_batched_sentences_equal_single(tmp_path):
+    """Synthesizer.tts batches all sentences into one Tacotron2 and one vocoder call; each
+    sentence must equal its own B=1 synthesis, and tts() must return a readable 16-bit wav."""
+    import io
+    import scipy.io.wavfile
+    from tts_amd.synthesizer import Synthesizer
+    _dev()
+    synth = Synthesizer(_synth_files(tmp_path))
+    synth.tts_model.decoder.max_decoder_steps = 24
+    sens = ["Hello world.", "This is a longer test of the batched path, with 2 numbers!", "Short one?"]
+    wavs = synth.synthesize_batch(sens)
+    assert len(wavs) == 3
+    for s, w in zip(sens, wavs):
+        ref = synth.synthesize_batch([s])[0]
+        assert w.shape == ref.shape == (24 * 2 * 256,)
+        assert np.abs(w - ref).max() <= 1e-4
+    buf = synth.tts(" ".join(sens))
+    sr, x = scipy.io.wavfile.read(io.BytesIO(buf.getvalue()))
+    assert sr == 22050 and x.dtype == np.int16 and len(x) >= 3 * 10000
+
+
+def test_synthesizer_griffin_lim_fallback(tmp_path):
+    """No vocoder checkpoint: mel on the GPU, Griffin-Lim on the CPU (config C1's fallback)."""
+    from tts_amd.synthesizer import Synthesizer
+    _dev()
+    synth = Synthesizer(_synth_files(tmp_path, with_vocoder=False))
+    synth.tts_model.decoder.max_decoder_steps = 10
+    wavs = synth.synthesize_batch(["Griffin and Lim.", "Phase from noise."])
+    for w in wavs:
+        assert np.isfinite(w).all() and abs(len(w) - 20 * 256) <= 256

@@ -432,7 +432,9 @@ int main(int argc, char** argv) {
       char name[64];
       snprintf(name, sizeof(name), "K3 attention T=%d %s", T, sm ? "softmax" : "sigmoid");
       rep(name, time_graph([&] { launch_attention(p, da, 0, S); }), 1.0);
-      rep("   same, 256-thread workgroups", time_graph([&] { attn_kernel<256><<<dim3(nch, B), 256, 0, S>>>(p, da, 0); }), 1.0);
+      rep("   256 thr, 16 pos", time_graph([&] { attn_kernel<256, 16><<<dim3(nch, B), 256, 0, S>>>(p, da, 0); }), 1.0);
+      rep("   512 thr, 16 pos", time_graph([&] { attn_kernel<512, 16><<<dim3(nch, B), 512, 0, S>>>(p, da, 0); }), 1.0);
+      rep("   512 thr, 32 pos", time_graph([&] { attn_kernel<512, 32><<<dim3((T + 31) / 32, B), 512, 0, S>>>(p, da, 0); }), 1.0);
       // one traced launch: phase durations (us) averaged over workgroups
       std::vector<unsigned long long> tr(64 * 64 * 9, 0);
       HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(attn_trace), tr.data(), tr.size() * 8));

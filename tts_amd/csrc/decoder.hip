@@ -426,26 +426,26 @@ __device__ unsigned long long attn_trace[64 * 64 * 9];
 #define ATTN_TRACE(k)
 #endif
 
-// one workgroup of NT threads (256 or 512): utterance b, positions [16 ch, 16 ch + 16)
-template <int NT>
+// one workgroup of NT threads (256 or 512): utterance b, positions [TC ch, TC ch + TC)
+template <int NT, int TC>
 __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, int jstep, int b, int ch) {
   constexpr int NG = NT / ADIM;           // thread groups over the attention dims
-  constexpr int PPG = TCH / NG;           // positions per group in the energy phase
+  constexpr int PPG = TC / NG;           // positions per group in the energy phase
   constexpr int DPT = 512 / NT;           // encoder dims per thread (context)
-  constexpr int OPT = (LOCF * TCH) / NT;  // location-conv outputs per thread
-  constexpr int LPP = NT / TCH;           // lanes per position in the energy reduction
+  constexpr int OPT = (LOCF * TC) / NT;  // location-conv outputs per thread
+  constexpr int LPP = NT / TC;           // lanes per position in the energy reduction
   constexpr int NWL = (LOCF * 2 * LOCK + NT - 1) / NT;
   static_assert(NG >= 2 && OPT >= 1 && OPT <= 2 && LPP <= 64, "attention geometry");
   ATTN_TRACE(0);
-  const int t0 = ch * TCH;
+  const int t0 = ch * TC;
   const int tid = threadIdx.x;
   const int a = tid % ADIM, grp = tid / ADIM;
   __shared__ float red[NG][ADIM];
-  __shared__ float A0[TCH + LOCK], A1[TCH + LOCK];
+  __shared__ float A0[TC + LOCK], A1[TC + LOCK];
   __shared__ float Wl[LOCF * 2 * LOCK];
-  __shared__ __attribute__((aligned(16))) float f[TCH][LOCF + 4];  // [position][filter]
-  __shared__ float zb[TCH][ADIM + 4];
-  __shared__ float sv[TCH];
+  __shared__ __attribute__((aligned(16))) float f[TC][LOCF + 4];  // [position][filter]
+  __shared__ float zb[TC][ADIM + 4];
+  __shared__ float sv[TC];
   __shared__ int is_last;
   const int Bp = P.Bp;
   const int T = D.lens[b];
@@ -466,7 +466,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   for (int i = 0; i < NPQ / NG; ++i) pp[i] = P.pq_part[((long)(grp * (NPQ / NG) + i) * Bp + b) * ADIM + a];
   float a0, a1;
   {
-    const int pos = t0 - (LOCK - 1) / 2 + min(tid, TCH + LOCK - 2);
+    const int pos = t0 - (LOCK - 1) / 2 + min(tid, TC + LOCK - 2);
     const int pc = min(max(pos, 0), Tm1);
     a0 = P.alpha[(long)b * D.T_max + pc];
     a1 = P.alpha_cum[(long)b * D.T_max + pc];
@@ -476,9 +476,9 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
 #pragma unroll
   for (int i = 0; i < NWL; ++i) wl[i] = P.Wloc[min(tid + NT * i, LOCF * 2 * LOCK - 1)];
   // encoder rows of this chunk for the partial context: dims DPT*tid .. DPT*tid + DPT-1
-  float ev[TCH][DPT];
+  float ev[TC][DPT];
 #pragma unroll
-  for (int i = 0; i < TCH; ++i) {
+  for (int i = 0; i < TC; ++i) {
     const float* er = P.enc + ((long)b * D.T_max + min(t0 + i, Tm1)) * 512 + DPT * tid;
     if constexpr (DPT == 2) {
       const float2 v2 = *reinterpret_cast<const float2*>(er);
@@ -490,7 +490,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   }
   if (D.ctl->all_done || D.done[b] || t0 >= T) return;
   const int t_step = D.ctl->base + jstep;
-  if (tid < TCH + LOCK - 1) {
+  if (tid < TC + LOCK - 1) {
     A0[tid] = a0;
     A1[tid] = a1;
   }
@@ -510,7 +510,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   // location conv: f[tt][c] = sum_i sum_k Wl[c][i][k] * A_i[tt + k]; OPT adjacent positions of
   // one filter per thread, the window sliding in registers (one A read per tap)
   {
-    const int c = tid / (TCH / OPT), tt = (tid % (TCH / OPT)) * OPT;
+    const int c = tid / (TC / OPT), tt = (tid % (TC / OPT)) * OPT;
     const float* w0 = Wl + c * 2 * LOCK;
     float acc[OPT];
 #pragma unroll
@@ -553,7 +553,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   }
   __syncthreads();
   ATTN_TRACE(3);
-  const int nvalid = min(TCH, T - t0);
+  const int nvalid = min(TC, T - t0);
   const long pidx = (long)b * P.nchmax + ch;
   {
     const int pos = tid / LPP, j = tid % LPP;
@@ -575,10 +575,10 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   float m_c = -INFINITY;
   if (P.softmax)
     for (int i = 0; i < nvalid; ++i) m_c = fmaxf(m_c, sv[i]);
-  float sl[TCH];
+  float sl[TC];
   float S_c = 0.f;
 #pragma unroll
-  for (int i = 0; i < TCH; ++i) {
+  for (int i = 0; i < TC; ++i) {
     const float e = sv[i];
     const float x = P.softmax ? expf(e - m_c) : 1.f / (1.f + expf(-e));
     sl[i] = i < nvalid ? x : 0.f;
@@ -590,7 +590,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   for (int q = 0; q < DPT; ++q) {
     u[q] = 0.f;
 #pragma unroll
-    for (int i = 0; i < TCH; ++i) u[q] = fmaf(sl[i], ev[i][q], u[q]);
+    for (int i = 0; i < TC; ++i) u[q] = fmaf(sl[i], ev[i][q], u[q]);
   }
   // ---- publish: sc1 (write-through) stores need no release fence (cdna_hip_programming.md
   // §5 split-K item 2); every wave drains, barrier, then one relaxed agent-scope ticket ----
@@ -612,7 +612,7 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ATTN_TRACE(5);
-  const int nch = (T + TCH - 1) / TCH;
+  const int nch = (T + TC - 1) / TC;
   if (tid == 0) {
     const unsigned prev = __hip_atomic_fetch_add(&P.counter[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     is_last = (prev == (unsigned)(nch - 1));
@@ -686,9 +686,9 @@ __device__ __forceinline__ void attn_body(const AttnArgs& P, const DecDev& D, in
   ATTN_TRACE(8);
 }
 
-template <int NT>
+template <int NT, int TC>
 __global__ __launch_bounds__(NT) void attn_kernel(AttnArgs P, DecDev D, int jstep) {
-  attn_body<NT>(P, D, jstep, blockIdx.y, blockIdx.x);
+  attn_body<NT, TC>(P, D, jstep, blockIdx.y, blockIdx.x);
 }
 
 __global__ void dec_advance_kernel(DecCtl* ctl, int n) {
@@ -750,9 +750,9 @@ void launch_attention(const AttnArgs& p, const DecDev& d, int jstep, hipStream_t
   // 512-thread workgroups shorten the chain when few chunks run; past ~200 workgroups the
   // 256-thread form is faster (tools/skinny_bench.hip, B = 32: T 64 11.7 vs 12.3 us, T 168 15.8 vs 14.9)
   if ((long)g.x * g.y <= 200)
-    attn_kernel<512><<<g, 512, 0, s>>>(p, d, jstep);
+    attn_kernel<512, TCH><<<g, 512, 0, s>>>(p, d, jstep);
   else
-    attn_kernel<256><<<g, 256, 0, s>>>(p, d, jstep);
+    attn_kernel<256, TCH><<<g, 256, 0, s>>>(p, d, jstep);
   HIP_OK(hipGetLastError());
 }
 

@@ -1,0 +1,115 @@
+"""Batched `Synthesizer.tts` with the reference's constructor, loaders and output.
+
+Follows `TTS/server/synthesizer.py:21-193`. What differs on purpose:
+  * all sentences of one `tts()` call decode in ONE batched Tacotron2 call and ONE batched
+    vocoder call (the reference loops B=1 per sentence, because its decoder cannot batch,
+    `TTS/tts/layers/tacotron2.py:362`); per-sentence outputs are cut back to each sentence's
+    own mel length, so every sentence equals its B=1 synthesis;
+  * without a vocoder checkpoint the Griffin-Lim fallback runs on the CPU (`tts_amd.audio`);
+  * checkpoints load with `torch.load(..., weights_only=True)`;
+  * sentence splitting and the text front end are the stand-ins of `tts_amd.text` (pysbd,
+    phonemizer, unidecode and inflect are not in this image); phoneme configs need a
+    `phonemize` callable.
+"""
+import time
+
+import numpy as np
+import torch
+
+from .audio import AudioProcessor, wav_bytes
+from .factories import load_config, setup_generator, setup_model
+from .text import make_symbols, phonemes, split_into_sentences, symbols, text_to_seqvec
+
+
+class Synthesizer:
+    def __init__(self, config, phonemize=None):
+        self.wavernn = None
+        self.vocoder_model = None
+        self.config = config
+        self.phonemize = phonemize
+        self.use_cuda = config["use_cuda"]
+        if self.use_cuda:
+            assert torch.cuda.is_available(), "CUDA is not availabe on this machine."
+        self.load_tts(config["tts_checkpoint"], config["tts_config"], self.use_cuda)
+        if config.get("vocoder_checkpoint"):
+            self.load_vocoder(config["vocoder_checkpoint"], config["vocoder_config"], self.use_cuda)
+        if config.get("wavernn_lib_path"):
+            raise NotImplementedError("WaveRNN is outside the MI355X hot path (SURVEY.md §8f)")
+
+    def load_tts(self, tts_checkpoint, tts_config, use_cuda):
+        """synthesizer.py:44-82"""
+        self.tts_config = load_config(tts_config) if isinstance(tts_config, str) else tts_config
+        self.use_phonemes = self.tts_config["use_phonemes"]
+        self.ap = AudioProcessor(**self.tts_config["audio"])
+        syms, phs = symbols, phonemes
+        if "characters" in self.tts_config:
+            syms, phs = make_symbols(**self.tts_config["characters"])
+        self.input_size = len(phs) if self.use_phonemes else len(syms)
+        if self.config.get("tts_speakers") is not None:
+            raise NotImplementedError("multi-speaker Tacotron2 is SURVEY.md §8f rank 2")
+        self.tts_model = setup_model(self.input_size, num_speakers=0, c=self.tts_config)
+        cp = torch.load(tts_checkpoint, map_location=torch.device("cpu"), weights_only=True)
+        self.tts_model.load_state_dict(cp["model"])
+        if use_cuda:
+            self.tts_model.cuda()
+        self.tts_model.eval()
+        self.tts_model.decoder.max_decoder_steps = 3000
+        if "r" in cp:
+            self.tts_model.decoder.set_r(int(cp["r"]))
+            print(f" > model reduction factor: {int(cp['r'])}")
+
+    def load_vocoder(self, model_file, model_config, use_cuda):
+        """synthesizer.py:84-94"""
+        self.vocoder_config = load_config(model_config) if isinstance(model_config, str) else model_config
+        self.vocoder_model = setup_generator(self.vocoder_config)
+        self.vocoder_model.load_state_dict(torch.load(model_file, map_location="cpu", weights_only=True)["model"])
+        self.vocoder_model.remove_weight_norm()
+        self.vocoder_model.inference_padding = 0
+        if use_cuda:
+            self.vocoder_model.cuda()
+        self.vocoder_model.eval()
+
+    def save_wav(self, wav, path):
+        self.ap.save_wav(np.array(wav), path)
+
+    @staticmethod
+    def split_into_sentences(text):
+        return split_into_sentences(text)
+
+    def synthesize_batch(self, sentences):
+        """Sentences -> list of per-sentence waveforms (float32 numpy), one GPU call per model."""
+        seqs = [text_to_seqvec(s, self.tts_config, self.phonemize) for s in sentences]
+        lens = [max(1, len(q)) for q in seqs]
+        dev = "cuda" if self.use_cuda else "cpu"
+        batch = np.zeros((len(seqs), max(lens)), np.int64)
+        for i, q in enumerate(seqs):
+            batch[i, :len(q)] = q
+        with torch.no_grad():
+            _, post, _, _ = self.tts_model.inference(torch.from_numpy(batch).to(dev), text_lengths=lens)
+            mel_lens = [int(m) for m in self.tts_model.last_mel_lengths]
+            if self.vocoder_model is not None:
+                wav = self.vocoder_model.inference(post.transpose(1, 2).contiguous(), lengths=mel_lens)
+                hop = wav.shape[-1] // post.shape[1]
+                wav = wav.reshape(len(seqs), -1).cpu().numpy()
+                return [wav[i, :mel_lens[i] * hop] for i in range(len(seqs))]
+        post = post.cpu().numpy()
+        return [self.ap.inv_melspectrogram(post[i, :mel_lens[i]].T).astype(np.float32) for i in range(len(seqs))]
+
+    def tts(self, text, speaker_id=None):
+        """synthesizer.py:134-193"""
+        if speaker_id is not None:
+            raise NotImplementedError("multi-speaker Tacotron2 is SURVEY.md §8f rank 2")
+        start_time = time.time()
+        sens = self.split_into_sentences(text)
+        print(sens)
+        wavs = []
+        for wav in self.synthesize_batch(sens):
+            wav = wav[:self.ap.find_endpoint(wav)]  # synthesis.py:130-131
+            wavs += list(wav)
+            wavs += [0] * 10000
+        out = wav_bytes(self.ap, np.asarray(wavs, np.float32))
+        process_time = time.time() - start_time
+        audio_time = len(wavs) / self.tts_config["audio"]["sample_rate"]
+        print(f" > Processing time: {process_time}")
+        print(f" > Real-time factor: {process_time / audio_time}")
+        return out
