@@ -112,6 +112,7 @@ def main():
     taco, tsd, voc, vsd, tcfg, vcfg = build_models(dev)
     r = args.r
     taco.decoder.set_r(r)
+    taco.decoder.verbose = False  # forced lengths end every utterance at max_decoder_steps
     T_all, M_all, shards = replicated_workload(world, args.per_gpu_batch)
     mine = shards[rank]
     T_prof, M_prof = lj_profile()

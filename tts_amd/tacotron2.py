@@ -157,9 +157,10 @@ class Tacotron2(nn.Module):
             outs.append((dec, post, align, stop, steps, status, Tn))
         steps = np.concatenate([o[4] for o in outs])
         status = np.concatenate([o[5] for o in outs])
-        for s in status:
-            if s == 2:
-                print("   | > Decoder stopped with 'max_decoder_steps")
+        if getattr(self.decoder, "verbose", True):  # reference behaviour (tacotron2.py:365); bench.py mutes it
+            for s in status:
+                if s == 2:
+                    print("   | > Decoder stopped with 'max_decoder_steps")
         S = int(steps.max())
         M = S * r
         dec = torch.cat([o[0][:, :M] for o in outs]) if len(outs) > 1 else outs[0][0][:, :M]
