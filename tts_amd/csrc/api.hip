@@ -98,9 +98,16 @@ void pack_conv(ConvLayer& L, const std::vector<float>& Wm, const std::vector<flo
   L.Cout_pad = (Cout + TC - 1) / TC * TC;
   const int Kdim = Cin * K;
   const size_t per = (size_t)L.Cout_pad * Kdim;
+  // k order inside each 16-input-channel chunk: tap-major (k' = tap * 16 + ci % 16), so k-chunk
+  // `tap` of a staging chunk reads LDS rows ci at column offset tap * dil (no offset table)
+  std::vector<float> Wt(Wm.size());
+  for (size_t r = 0; r < (size_t)nphase * Cout; ++r)
+    for (int ci = 0; ci < Cin; ++ci)
+      for (int k = 0; k < K; ++k)
+        Wt[r * Kdim + (size_t)(ci / 16) * 16 * K + k * 16 + ci % 16] = Wm[r * Kdim + (size_t)ci * K + k];
   std::vector<float> sw(per * nphase);
   for (int ph = 0; ph < nphase; ++ph)
-    swizzle_rows16(Wm.data() + (size_t)ph * Cout * Kdim, Cout, L.Cout_pad, Kdim, sw.data() + ph * per);
+    swizzle_rows16(Wt.data() + (size_t)ph * Cout * Kdim, Cout, L.Cout_pad, Kdim, sw.data() + ph * per);
   L.phase_stride = (long)per;
   L.W.upload(sw);
   L.bias.upload(bias);

@@ -9,8 +9,9 @@
 // v_mfma_f32_16x16x4_f32 (exact fp32). A (weights) is pre-swizzled into MFMA fragment order:
 // one contiguous 1 KiB float4 read per wave instruction, L2-resident, prefetched one k-chunk
 // ahead. B (activations) is staged per 16-input-channel chunk into LDS with padding / reflection
-// / activation resolved at staging time (read through a per-K offset table so taps and dilation
-// cost nothing in the MFMA loop); staging is register double-buffered -- the global loads of chunk
+// / activation resolved at staging time; weights are tap-major inside a chunk (k-chunk = tap,
+// see pack_conv), so a tap is a column offset tap * dil into the staged rows; staging is
+// register double-buffered -- the global loads of chunk
 // c+1 are in flight while chunk c's MFMAs issue -- into two LDS buffers (one barrier per chunk).
 // A wave owns MI x NI 16x16 tiles so each LDS read feeds MI MFMAs and each weight fragment NI.
 #include "common.h"
@@ -63,12 +64,10 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
   const int XS = (16 * ROW + 3) & ~3;  // one LDS X buffer (floats)
   float* X0 = smem;
   float* X1 = smem + XS;
-  int* offs = reinterpret_cast<int*>(smem + 2 * XS);
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
   const int wm = wave / WN, wn = wave % WN;
-  for (int i = tid; i < 16 * K; i += 256) offs[i] = (i / K) * ROW + (i % K) * dil;
 
   const int i0 = q0 - a.pad_left[ph];
   const int nchunks = a.Cin / 16;
@@ -90,6 +89,8 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     sp_[j] = e - sc_[j] * ROW;
   }
   float st[SPT];
+  // every load address is clamped into the source (no per-element branch); zero padding is a
+  // select after the load, slots past 16 x (TQ + span) are loaded but never stored
   auto stage_load = [&](int chunk) {
     const int cbase = chunk * 16;
     const bool first = cbase < a.src[0].C;
@@ -99,23 +100,19 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     const int sst = first ? a.src[0].st : a.src[1].st;
     const int cs = first ? cbase : cbase - a.src[0].C;
     const float* bp = sp + (long)b * sb + (long)cs * ssc;
+    const int Lsrc = a.rep_pad ? rawL : Lin;
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
-      const int c = sc_[j], p = sp_[j];
-      float v = 0.f;
-      if (c < 16 && p < TQ + span) {
-        int i = i0 + p;
-        bool valid = true;
-        if (!interior) {
-          i = map_pad_index(i, Lin, a.pad_mode, valid);
-          if (a.rep_pad) {
-            i -= a.rep_pad;
-            i = i < 0 ? 0 : (i >= rawL ? rawL - 1 : i);
-          }
-        }
-        if (valid) v = bp[(long)c * ssc + (long)i * sst];
+      const int c = min(sc_[j], 15);
+      int i = i0 + sp_[j];
+      bool valid = true;
+      if (!interior) {
+        i = map_pad_index(i, Lin, a.pad_mode, valid);
+        if (a.rep_pad) i -= a.rep_pad;
       }
-      st[j] = v;
+      i = i < 0 ? 0 : (i >= Lsrc ? Lsrc - 1 : i);
+      const float v = bp[(long)c * ssc + (long)i * sst];
+      st[j] = valid ? v : 0.f;
     }
   };
   auto stage_store = [&](float* X, int chunk) {
@@ -149,24 +146,25 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
     for (int chunk = 0; chunk < nchunks; ++chunk) {
       float* X = (chunk & 1) ? X1 : X0;
       if (chunk + 1 < nchunks) stage_load(chunk + 1);  // in flight during this chunk's MFMAs
+      // keep the scheduler from sinking the staging loads down to their LDS stores
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
       for (int kq = 0; kq < KT; ++kq) {
-        f32x4 A[MI];
+        // all 4 x NI operand reads of this k-chunk first (one LDS wait), tap offsets arithmetic
+        float bv[4][NI];
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi) A[mi] = ring[kq][mi];
-        wload(ring[kq], (chunk + 1) * KT + kq);
-        const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
-        const int ov[4] = {o.x, o.y, o.z, o.w};
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          float bv[NI];
+          for (int ni = 0; ni < NI; ++ni) bv[s][ni] = X[(g4 + s) * ROW + kq * dil + qb + ni * 16];
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) bv[ni] = X[ov[s] + qb + ni * 16];
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
-        }
+            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(ring[kq][mi][s], bv[s][ni], acc[mi][ni]);
+        // reload the slot in place after its MFMAs (no register rotation, no vmcnt(0))
+        wload(ring[kq], (chunk + 1) * KT + kq);
       }
       if (chunk + 1 < nchunks) stage_store((chunk & 1) ? X0 : X1, chunk + 1);
       __syncthreads();
@@ -188,18 +186,17 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
         const int kn = min(kc + 1, nkc_total - 1);
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi) Anext[mi] = Wv[((long)(mt0 + mi) * nkc_total + kn) * 64 + lane];
-        const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
-        const int ov[4] = {o.x, o.y, o.z, o.w};
+        float bv[4][NI];
 #pragma unroll
-        for (int s = 0; s < 4; ++s) {
-          float bv[NI];
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) bv[ni] = X[ov[s] + qb + ni * 16];
+          for (int ni = 0; ni < NI; ++ni) bv[s][ni] = X[(g4 + s) * ROW + kq * dil + qb + ni * 16];
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
 #pragma unroll
           for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
-        }
+            for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[s][ni], acc[mi][ni]);
       }
       if (chunk + 1 < nchunks) stage_store((chunk & 1) ? X0 : X1, chunk + 1);
       __syncthreads();
@@ -286,7 +283,7 @@ void launch_conv(const ConvArgs& a, int tile, hipStream_t s) {
   else if (a.K == 2 && tile == TILE_192x64) variant = 3;
   const int span = (a.K - 1) * a.dil;
   const int ROW = TQ + span + 1;
-  const size_t lds = (size_t)(2 * ((16 * ROW + 3) & ~3) + 16 * a.K) * 4;
+  const size_t lds = (size_t)2 * ((16 * ROW + 3) & ~3) * 4;
   dim3 grid((a.max_q + TQ - 1) / TQ, a.Cout_pad / TC, a.B * a.nphase);
   switch (variant) {
     case 0: conv_mfma_kernel<2, 2, 2, 2, 5><<<grid, 256, lds, s>>>(a); break;

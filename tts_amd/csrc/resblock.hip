@@ -31,7 +31,6 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_kernel(ResArgs a) {
   float* X0 = smem;
   float* X1 = smem + XS;
   float* HX = smem + 2 * XS;                           // [2C][TQ]: lrelu(h) then raw x (centre)
-  int* offs = reinterpret_cast<int*>(HX + 2 * C * TQ);  // [48]
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6;
@@ -39,7 +38,6 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_kernel(ResArgs a) {
   const int qb = wn * 16 * NI + (lane & 15);
   const int g4 = 4 * (lane >> 4);
   const int mt0 = wm * MI;
-  if (tid < 48) offs[tid] = (tid / 3) * ROW + (tid % 3) * d;
 
   const float* xb = a.x + (long)b * a.sb;
   const int i0 = q0 - d;
@@ -52,22 +50,20 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_kernel(ResArgs a) {
     sp_[j] = e - sc_[j] * ROW;
   }
   float st[SPT];
+  // clamped (always valid) addresses, no per-element guard: a guarded load becomes an exec-masked
+  // branch per element; slots past 16 x (TQ + 2d) are loaded but never stored
   auto stage_load = [&](int chunk) {
     const float* bp = xb + (long)(chunk * 16) * a.Ls;
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
-      const int c = sc_[j], p = sp_[j];
-      float v = 0.f;
-      if (c < 16 && p < TQ + 2 * d) {
-        int i = i0 + p;
-        if (!interior) {  // reflection (torch ReflectionPad1d), clamped for safety
-          if (i < 0) i = -i;
-          if (i >= L) i = 2 * (L - 1) - i;
-          i = i < 0 ? 0 : (i >= L ? L - 1 : i);
-        }
-        v = bp[(long)c * a.Ls + i];
+      const int c = min(sc_[j], 15);
+      int i = i0 + sp_[j];
+      if (!interior) {  // reflection (torch ReflectionPad1d)
+        if (i < 0) i = -i;
+        if (i >= L) i = 2 * (L - 1) - i;
       }
-      st[j] = v;
+      i = i < 0 ? 0 : (i >= L ? L - 1 : i);
+      st[j] = bp[(long)c * a.Ls + i];
     }
   };
   auto stage_store = [&](float* X, int chunk) {
@@ -115,24 +111,25 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_kernel(ResArgs a) {
   for (int chunk = 0; chunk < NCH; ++chunk) {
     float* X = (chunk & 1) ? X1 : X0;
     if (chunk + 1 < NCH) stage_load(chunk + 1);
+    // keep the scheduler from sinking the staging loads to their stores (that made them synchronous)
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int kq = 0; kq < 3; ++kq) {
-      f32x4 A[MI];
+      // all 4 x NI operand reads of this k-chunk first (one LDS wait), tap offsets in registers
+      float bv[4][NI];
 #pragma unroll
-      for (int mi = 0; mi < MI; ++mi) A[mi] = ring[kq][mi];
-      wload(ring[kq], (chunk + 1) * 3 + kq);
-      const int4 o = *reinterpret_cast<const int4*>(offs + kq * 16 + g4);
-      const int ov[4] = {o.x, o.y, o.z, o.w};
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float bv[NI];
+        for (int ni = 0; ni < NI; ++ni) bv[s][ni] = X[(g4 + s) * ROW + kq * d + qb + ni * 16];
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) bv[ni] = X[ov[s] + qb + ni * 16];
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
-      }
+          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(ring[kq][mi][s], bv[s][ni], acc[mi][ni]);
+      // reload this ring slot in place, after its MFMAs (no register rotation, no vmcnt(0))
+      wload(ring[kq], (chunk + 1) * 3 + kq);
     }
     if (chunk + 1 < NCH) stage_store((chunk & 1) ? X0 : X1, chunk + 1);
     __syncthreads();
@@ -159,21 +156,20 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_kernel(ResArgs a) {
     for (int u = 0; u < 3; ++u) {
       const int kc = kc0 + u;
       if (kc >= NKC2) break;  // C/8 chunks need not be a multiple of 3 (wave-uniform)
-      f32x4 A[MI];
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) A[mi] = ring[u][mi];
-      wload(ring[u], NKC1 + kc + 3);
       const float* hrow = HX + (kc * 16 + g4) * TQ + qb;
+      float bv[4][NI];
 #pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        float bv[NI];
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) bv[ni] = hrow[s * TQ + ni * 16];
+        for (int ni = 0; ni < NI; ++ni) bv[s][ni] = hrow[s * TQ + ni * 16];
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int s = 0; s < 4; ++s)
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
-      }
+          for (int ni = 0; ni < NI; ++ni) acc[mi][ni] = MFMA16(ring[u][mi][s], bv[s][ni], acc[mi][ni]);
+      wload(ring[u], NKC1 + kc + 3);
     }
   }
   float* yb = a.y + (long)b * a.sb;
@@ -195,7 +191,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_kernel(ResArgs a) {
 template <int C, int TQ, int WM, int WN>
 static void launch_rb(const ResArgs& a, hipStream_t s) {
   const int ROW = TQ + 2 * a.dil + 1;
-  const size_t lds = ((size_t)2 * ((16 * ROW + 3) & ~3) + (size_t)2 * C * TQ + 48) * 4;
+  const size_t lds = ((size_t)2 * ((16 * ROW + 3) & ~3) + (size_t)2 * C * TQ) * 4;
   dim3 grid((a.max_q + TQ - 1) / TQ, a.B);
   resblock_kernel<C, TQ, WM, WN><<<grid, 64 * WM * WN, lds, s>>>(a);
 }
@@ -203,14 +199,14 @@ static void launch_rb(const ResArgs& a, hipStream_t s) {
 void launch_resblock(const ResArgs& a, int C, hipStream_t s) {
   TTS_CHECK(a.dil >= 1 && a.dil <= RB_DMAX, "resblock: dilation must be in [1, 27] (num_res_blocks <= 4)");
   if (a.max_q <= 0 || a.B <= 0) return;
-  // tiles from tools/voc_bench.hip (C2 shapes): 8 waves at C >= 96, TQ = 64 below
+  // tiles from tools/voc_bench.hip (C2 shapes)
   switch (C) {
-    case 192: launch_rb<192, 32, 4, 2>(a, s); break;
-    case 96: launch_rb<96, 64, 2, 4>(a, s); break;
-    case 48: launch_rb<48, 64, 1, 4>(a, s); break;
-    case 256: launch_rb<256, 32, 4, 2>(a, s); break;
-    case 128: launch_rb<128, 64, 2, 4>(a, s); break;
-    case 64: launch_rb<64, 64, 1, 4>(a, s); break;
+    case 192: launch_rb<192, 32, 4, 1>(a, s); break;
+    case 96: launch_rb<96, 64, 2, 2>(a, s); break;
+    case 48: launch_rb<48, 128, 1, 8>(a, s); break;
+    case 256: launch_rb<256, 32, 4, 1>(a, s); break;
+    case 128: launch_rb<128, 64, 2, 2>(a, s); break;
+    case 64: launch_rb<64, 128, 1, 8>(a, s); break;
     case 32: launch_rb<32, 64, 1, 4>(a, s); break;
     default: TTS_CHECK(false, "resblock: unsupported channel count");
   }
