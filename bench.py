@@ -173,21 +173,53 @@ def main():
     # dominant decoder kernel, timed live with HIP events on the library's stream
     from tts_amd._lib import get_engine
     eng = get_engine(dev)
-    k4_ms = eng.time_decoder_kernel(0, args.kernel_iters)
-    step_ms = eng.time_decoder_kernel(1, max(4, args.kernel_iters // 8))
-    Bp = 16 * ((len(mine) + 15) // 16)
-    k4_bytes = 4 * (4096 * 2560                         # decoder_rnn [W_ih | W_hh], gate-interleaved tiles
-                    + 4096                              # folded biases
-                    + Bp * 2560                         # activations read [h_att | ctx | h_dec]
-                    + Bp * 1024 * 3)                    # c read/write, h write
-    achieved = k4_bytes / (k4_ms * 1e-3) / 1e9
-    traffic = None
-    pmc = os.path.join(ROOT, "profiles", "k4_pmc.json")
-    if os.path.exists(pmc):
-        try:
-            traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
-        except Exception:
-            traffic = None
+    path, launches = eng.decoder_stats()
+    if path == 1:
+        # persistent decoder: the MT = 2 launch (32-row batch tile) carries most steps. Algorithmic
+        # work = useful row-steps (rows still decoding) x the per-row GEMM flops of one step
+        ms0, st0 = launches[0]
+        flop_row = 2 * (4096 * 2560          # decoder_rnn [W_ih | W_hh]
+                        + 4096 * 1536        # attention_rnn ctx/h part
+                        + 4096 * 256         # attention_rnn prenet part
+                        + (1 + 80 * r) * 1536  # projection (r frames) + stopnet
+                        + 80 * 256 + 256 * 256  # prenet
+                        + 1024 * 128)        # query projection
+        row_steps = sum(min(s_, st0) for s_ in steps[:16 * ((len(mine) + 15) // 16)])
+        flops = row_steps * flop_row
+        achieved = flops / (ms0 * 1e-3) / 1e12
+        step_ms = ms0 / max(st0, 1)
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "persist_pmc.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"kernel": "persist_decoder_kernel<2> (whole decoder loop, weights resident on chip)",
+                "bound": "mfma", "achieved": round(achieved, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                "frac": round(achieved / F32_PEAK_TFLOPS, 4), "traffic": traffic,
+                "avg_launch_us": round(ms0 * 1000.0, 1), "algorithmic_flops": flops,
+                "launch_steps": st0, "launches": [[round(m_, 3), s_] for m_, s_ in launches]}
+    else:
+        k4_ms = eng.time_decoder_kernel(0, args.kernel_iters)
+        step_ms = eng.time_decoder_kernel(1, max(4, args.kernel_iters // 8))
+        Bp = 16 * ((len(mine) + 15) // 16)
+        k4_bytes = 4 * (4096 * 2560                         # decoder_rnn [W_ih | W_hh], gate-interleaved tiles
+                        + 4096                              # folded biases
+                        + Bp * 2560                         # activations read [h_att | ctx | h_dec]
+                        + Bp * 1024 * 3)                    # c read/write, h write
+        achieved = k4_bytes / (k4_ms * 1e-3) / 1e9
+        traffic = None
+        pmc = os.path.join(ROOT, "profiles", "k4_pmc.json")
+        if os.path.exists(pmc):
+            try:
+                traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+            except Exception:
+                traffic = None
+        roof = {"kernel": "decoder K4 (decoder_rnn LSTMCell: K=2560 skinny GEMM + fused cell update)",
+                "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
+                "avg_launch_us": round(k4_ms * 1000.0, 2), "algorithmic_bytes": k4_bytes}
 
     out = {
         "metric": "mel-frames/s (Tacotron2-DDC + MB-MelGAN end-to-end)",
@@ -211,10 +243,8 @@ def main():
         "vocoder_ms": round(voc_ms, 3),
         "decoder_step_us": round(step_ms * 1000.0, 2),
         "decoder_steps": int(max(steps)),
-        "roofline": {"kernel": "decoder K4 (decoder_rnn LSTMCell: K=2560 skinny GEMM + fused cell update)",
-                     "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                     "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
-                     "avg_launch_us": round(k4_ms * 1000.0, 2), "algorithmic_bytes": k4_bytes},
+        "decoder_path": "persistent" if path == 1 else "step-graphs",
+        "roofline": roof,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(tsd, vsd, tcfg, vcfg, ids, forced_steps(M_prof, r), r,

@@ -94,6 +94,11 @@ int tts_pqmf_synthesis(tts_ctx* ctx, const float* d_x, int B, int N, int L, cons
    which: 0 = decoder LSTM GEMM step kernel (K4), 1 = full decoder step (all 7 kernels). */
 int tts_time_decoder_kernel(tts_ctx* ctx, int which, int iters, float* ms_out);
 
+/* Decoder launches of the last tts_taco_infer: path 1 = persistent kernel (one cooperative
+   launch per batch-tile count, nlaunch <= 2; ms[i] = hipEvent time of launch i, steps[i] =
+   decoder steps it completed), path 0 = step graphs (nlaunch = 0). */
+int tts_decoder_stats(tts_ctx* ctx, int* path, int* nlaunch, float* ms, int* steps);
+
 #ifdef __cplusplus
 }
 #endif

@@ -1,0 +1,314 @@
+// Microbenchmark for a persistent (one launch per chunk of decoder steps) design: the cost of a
+// grid-wide barrier across 256 co-resident workgroups, and of a decoder_rnn-sized GEMM phase
+// (4096 gate rows x K = 2560, B = 32) whose weight fragments stay in VGPRs across iterations.
+// Not part of the library:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/persist_bench.hip -o tools/persist_bench
+#include "../tts_amd/csrc/common.h"
+
+#include <cstdio>
+#include <vector>
+
+__device__ unsigned g_err;
+
+// mode bit 0: agent acquire fence after the barrier; bit 1: s_sleep in the spin
+__device__ __forceinline__ bool grid_sync(unsigned* ctr, unsigned& target, int mode, int* ok) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    target += gridDim.x;
+    __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    int good = 1;
+    while (__hip_atomic_load(ctr, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {  // 0.2 s: give up, every WG exits
+        atomicOr(&g_err, 1u);
+        good = 0;
+        break;
+      }
+      if (mode & 2) __builtin_amdgcn_s_sleep(1);
+    }
+    if (mode & 1) __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    *ok = good;
+  }
+  __syncthreads();
+  return *ok;
+}
+
+__global__ __launch_bounds__(256) void bar_kernel(unsigned* ctr, int iters, int mode) {
+  __shared__ int ok;
+  unsigned target = 0;
+  for (int i = 0; i < iters; ++i)
+    if (!grid_sync(ctr, target, mode, &ok)) return;
+}
+
+__device__ __forceinline__ bool spin_timeout(unsigned long long t0) {
+  if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) {
+    atomicOr(&g_err, 1u);
+    return true;
+  }
+  return false;
+}
+
+// (B) hierarchical: per-XCD counters (workgroups are dispatched round-robin over the 8 XCDs), the
+// last arriver of an XCD bumps the global counter, the last global arriver bumps a go flag
+__global__ __launch_bounds__(256) void bar_hier_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  const int xcd = blockIdx.x & 7;
+  const unsigned per = gridDim.x / 8;
+  unsigned* xc = ctr + 64 + xcd * 32;  // own 128-B line per XCD
+  unsigned* gc = ctr;
+  unsigned* go = ctr + 32;
+  for (int i = 0; i < iters; ++i) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int good = 1;
+      const unsigned old = __hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == per * (i + 1) - 1) {
+        const unsigned g = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g == 8u * (i + 1) - 1) __hip_atomic_store(go, (unsigned)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(i + 1))
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
+// (C) flag array, no atomics: each workgroup stores its generation to its own slot; wave 0 polls
+// all slots (4 per lane) until the minimum reaches the generation
+__global__ __launch_bounds__(256) void bar_flags_kernel(unsigned* flags, int iters) {
+  __shared__ int ok;
+  for (int i = 0; i < iters; ++i) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, (unsigned)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      int good = 1;
+      while (true) {
+        unsigned m = 0xffffffffu;
+        for (int j = threadIdx.x; j < (int)gridDim.x; j += 64)
+          m = min(m, __hip_atomic_load(flags + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+        for (int off = 32; off > 0; off >>= 1) m = min(m, (unsigned)__shfl_xor((int)m, off, 64));
+        if (m >= (unsigned)(i + 1)) break;
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      }
+      if (threadIdx.x == 0) ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
+// (E) one counter, but waiters poll a separate go flag written by the last arriver
+__global__ __launch_bounds__(256) void bar_go_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  unsigned* go = ctr + 32;
+  for (int i = 0; i < iters; ++i) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int good = 1;
+      const unsigned old = __hip_atomic_fetch_add(ctr, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == gridDim.x * (i + 1) - 1) __hip_atomic_store(go, (unsigned)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < (unsigned)(i + 1))
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
+__global__ void empty_kernel() {}
+
+constexpr int KC = 160;  // 2560 / 16
+constexpr int NWV = 8;   // waves per workgroup
+constexpr int NKW = KC / NWV;  // k-chunks per wave
+
+// MODE bit 2: activation loads with sc1 (device-coherent) instead of plain loads
+template <int MT, int MODE>
+__global__ __launch_bounds__(64 * NWV) void k4_kernel(const f32x4* __restrict__ W, const f32x4* act, float* out,
+                                                 unsigned* ctr, int iters) {
+  __shared__ int ok;
+  __shared__ f32x4 red[NWV][MT][64];
+  const int tile = blockIdx.x, wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  f32x4 w[NKW];
+#pragma unroll
+  for (int i = 0; i < NKW; ++i) w[i] = W[((long)tile * KC + wave * NKW + i) * 64 + lane];
+  __amdgpu_buffer_rsrc_t rs = __builtin_amdgcn_make_buffer_rsrc((void*)act, 0, 0x7fffffff, 0x00020000);
+  auto ld = [&](int i, int mt) {
+    const int idx = (mt * KC + wave * NKW + i) * 64 + lane;
+    if constexpr (MODE & 4) return __builtin_amdgcn_raw_buffer_load_b128(rs, idx * 16, 0, 16);
+    else return act[idx];
+  };
+  unsigned target = 0;
+  for (int it = 0; it < iters; ++it) {
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    constexpr int G = 4;
+    f32x4 a[2][G][MT];
+#pragma unroll
+    for (int i = 0; i < G; ++i)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) a[0][i][mt] = ld(i, mt);
+#pragma unroll
+    for (int i0 = 0; i0 < NKW; i0 += G) {
+      const int cur = (i0 / G) & 1;
+      if (i0 + G < NKW) {
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) a[cur ^ 1][i][mt] = ld(i0 + G + i, mt);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int s = 0; s < 4; ++s)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(a[cur][i][mt][s], w[i0 + i][s], acc[mt]);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) red[wave][mt][lane] = acc[mt];
+    __syncthreads();
+    if (wave < MT) {
+      f32x4 r = red[0][wave][lane];
+#pragma unroll
+      for (int v = 1; v < NWV; ++v) r += red[v][wave][lane];
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        __hip_atomic_store(out + ((long)(wave * 16 + 4 * (lane >> 4) + j) * 4096 + tile * 16 + (lane & 15)), r[j],
+                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (!grid_sync(ctr, target, MODE, &ok)) return;
+  }
+}
+
+static hipStream_t S;
+
+template <typename F>
+static float timed(F launch) {
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  launch();  // warm
+  HIP_OK(hipStreamSynchronize(S));
+  HIP_OK(hipEventRecord(e0, S));
+  launch();
+  HIP_OK(hipEventRecord(e1, S));
+  HIP_OK(hipEventSynchronize(e1));
+  float ms;
+  HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+  return ms;
+}
+
+static bool check_err(const char* what) {
+  unsigned e = 0;
+  HIP_OK(hipMemcpyFromSymbol(&e, HIP_SYMBOL(g_err), 4));
+  if (e) {
+    printf("%s: barrier timeout (not all workgroups co-resident?)\n", what);
+    unsigned z = 0;
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_err), &z, 4));
+    return false;
+  }
+  return true;
+}
+
+int main() {
+  setvbuf(stdout, nullptr, _IONBF, 0);
+  HIP_OK(hipStreamCreate(&S));
+  unsigned* ctr;
+  HIP_OK(hipMalloc(&ctr, 4));
+  const int NWG = 256;
+  const size_t lds_force = 96 * 1024;  // one workgroup per CU
+  HIP_OK(hipFuncSetAttribute((const void*)bar_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
+  for (int mode : {0, 1, 2, 3}) {
+    const int iters = 2000;
+    float ms = timed([&] {
+      HIP_OK(hipMemsetAsync(ctr, 0, 4, S));
+      int it = iters, md = mode;
+      void* args[] = {&ctr, &it, &md};
+      HIP_OK(hipLaunchCooperativeKernel((const void*)bar_kernel, dim3(NWG), dim3(256), args, lds_force, S));
+    });
+    if (!check_err("barrier")) return 1;
+    printf("grid barrier, 256 WGs, mode %d (fence %d, sleep %d): %.3f us per barrier\n", mode, mode & 1,
+           (mode >> 1) & 1, ms * 1000.f / iters);
+  }
+  unsigned* big;
+  HIP_OK(hipMalloc(&big, 4096 * 4));
+  for (int v = 0; v < 3; ++v) {
+    const void* f = v == 0 ? (const void*)bar_hier_kernel : v == 1 ? (const void*)bar_flags_kernel : (const void*)bar_go_kernel;
+    const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : "counter + go flag";
+    HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
+    for (int nwg : {256, 128}) {
+      const int iters = 2000;
+      float ms = timed([&] {
+        HIP_OK(hipMemsetAsync(big, 0, 4096 * 4, S));
+        int it = iters;
+        void* args[] = {&big, &it};
+        HIP_OK(hipLaunchCooperativeKernel(f, dim3(nwg), dim3(256), args, lds_force, S));
+      });
+      if (!check_err(nm)) return 1;
+      printf("grid barrier %-18s %d WGs: %.3f us per barrier\n", nm, nwg, ms * 1000.f / iters);
+    }
+  }
+  {
+    hipGraph_t g;
+    hipGraphExec_t ge;
+    HIP_OK(hipStreamBeginCapture(S, hipStreamCaptureModeThreadLocal));
+    for (int i = 0; i < 100; ++i) empty_kernel<<<256, 256, 0, S>>>();
+    HIP_OK(hipStreamEndCapture(S, &g));
+    HIP_OK(hipGraphInstantiate(&ge, g, nullptr, nullptr, 0));
+    float ms = timed([&] { HIP_OK(hipGraphLaunch(ge, S)); });
+    printf("empty kernel in a graph: %.3f us per launch\n", ms * 10.f);
+  }
+  // K4-sized phase with resident weights
+  const int Bp = 32;
+  std::vector<float> h((size_t)4096 * 2560);
+  for (size_t i = 0; i < h.size(); ++i) h[i] = 1e-3f * (float)((i * 2654435761u) % 1000) / 1000.f;
+  f32x4* W;
+  f32x4* act;
+  float* out;
+  HIP_OK(hipMalloc(&W, h.size() * 4));
+  HIP_OK(hipMemcpy(W, h.data(), h.size() * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMalloc(&act, (size_t)Bp * 2560 * 4));
+  HIP_OK(hipMemcpy(act, h.data(), (size_t)Bp * 2560 * 4, hipMemcpyHostToDevice));
+  HIP_OK(hipMalloc(&out, (size_t)Bp * 4096 * 4));
+  auto run_k4 = [&](const void* f, int mt, int mode) {
+    HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
+    const int iters = 500;
+    float ms = timed([&] {
+      HIP_OK(hipMemsetAsync(ctr, 0, 4, S));
+      int it = iters;
+      void* args[] = {&W, &act, &out, &ctr, &it};
+      HIP_OK(hipLaunchCooperativeKernel(f, dim3(NWG), dim3(64 * NWV), args, lds_force, S));
+    });
+    if (!check_err("k4")) exit(1);
+    printf("K4 phase resident weights MT=%d mode %d: %.3f us per phase (incl. barrier)\n", mt, mode,
+           ms * 1000.f / iters);
+  };
+  run_k4((const void*)k4_kernel<2, 1>, 2, 1);
+  run_k4((const void*)k4_kernel<2, 4>, 2, 4);
+  run_k4((const void*)k4_kernel<2, 3>, 2, 3);
+  run_k4((const void*)k4_kernel<1, 1>, 1, 1);
+  run_k4((const void*)k4_kernel<1, 4>, 1, 4);
+  printf("done\n");
+  return 0;
+}

@@ -1,0 +1,42 @@
+"""Summarise a persistent-decoder phase trace (TTS_PTRACE=<file>): [8 steps][10 stamps][256 WGs]
+of s_memrealtime ticks (100 MHz). Stamp 2k = phase k starts (barrier released), 2k+1 = its work
+ends (barrier entered); phases P1, P3, P4, P5, P6."""
+import sys
+
+import numpy as np
+
+raw = np.fromfile(sys.argv[1], dtype=np.uint64).astype(np.int64)
+a = raw[:8 * 10 * 256].reshape(8, 10, 256)
+at = raw[8 * 10 * 256:].reshape(8, 256, 8) if raw.size > 8 * 10 * 256 else None
+names = ["P1 stop+prenet2", "P3 attLSTM+pq", "P4 attention", "P5 decLSTM", "P6 attpre+proj"]
+rows = []
+for s in range(7):  # the next step's stamp 0 closes the last barrier
+    st = a[s]
+    nxt = a[s + 1]
+    r = []
+    for k in range(5):
+        start = st[2 * k].min()
+        end = st[2 * k + 1]
+        rel = (nxt[0] if k == 4 else st[2 * k + 2])
+        r.append(((end.max() - start) / 100.0, np.median(end - st[2 * k]) / 100.0, (rel.min() - end.max()) / 100.0,
+                  (rel.max() - rel.min()) / 100.0))
+    rows.append(r)
+rows = np.array(rows)  # steps x phase x 4
+med = np.median(rows, axis=0)
+print(f"{'phase':18s} {'last WG done':>12s} {'median WG':>10s} {'barrier':>8s} {'release skew':>12s}  (us)")
+for k in range(5):
+    print(f"{names[k]:18s} {med[k,0]:12.2f} {med[k,1]:10.2f} {med[k,2]:8.2f} {med[k,3]:12.2f}")
+step = np.median([(a[s + 1][0].min() - a[s][0].min()) / 100.0 for s in range(7)])
+print(f"step {step:.2f} us")
+
+if at is not None:
+    # attention items: stamps 0 start (after loads), 1 query summed, 2 location conv, 3 energies,
+    # 4 energy reduction, 5 partials published, 6 ticket, 7 combine done (last arriver only)
+    labels = ["loads", "query", "locconv", "energy", "reduce", "publish", "ticket", "combine"]
+    for s in range(3):
+        p4start = a[s][4].min()
+        items = [i for i in range(256) if at[s][i][0] > 0]
+        d = np.array([[(at[s][i][k] - p4start) / 100.0 if at[s][i][k] > 0 else np.nan for k in range(8)]
+                      for i in items])
+        print(f"step {s}: {len(items)} items; stamp times after P4 release (us): median / max")
+        print("  " + " ".join(f"{labels[k]}={np.nanmedian(d[:, k]):.2f}/{np.nanmax(d[:, k]):.2f}" for k in range(8)))

@@ -21,6 +21,7 @@ _lock = threading.Lock()
 _c_int_p = ctypes.POINTER(ctypes.c_int32)
 _c_i64_p = ctypes.POINTER(ctypes.c_int64)
 _c_f_p = ctypes.POINTER(ctypes.c_float)
+_c_i_p = ctypes.POINTER(ctypes.c_int)
 _vp = ctypes.c_void_p
 
 # (name, restype, argtypes) for every symbol declared in include/ttship.h
@@ -44,6 +45,7 @@ SIGNATURES = [
     ("tts_pqmf_synthesis", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int,
                                           _vp, _vp]),
     ("tts_time_decoder_kernel", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_f_p]),
+    ("tts_decoder_stats", ctypes.c_int, [_vp, _c_i_p, _c_i_p, _c_f_p, _c_i_p]),
 ]
 
 
@@ -158,6 +160,14 @@ class Engine:
         B, N, L = x.shape
         taps = G.shape[-1] - 1
         _check(self.lib.tts_pqmf_synthesis(self.h, _ptr(x), B, N, L, _ptr(G), taps, _ptr(y), _stream(x.device)))
+
+    def decoder_stats(self):
+        """(path, [(ms, steps) per persistent launch]) of the last Tacotron2 decode."""
+        path, n = ctypes.c_int(0), ctypes.c_int(0)
+        ms = (ctypes.c_float * 2)()
+        st = (ctypes.c_int * 2)()
+        _check(self.lib.tts_decoder_stats(self.h, ctypes.byref(path), ctypes.byref(n), ms, st))
+        return int(path.value), [(float(ms[i]), int(st[i])) for i in range(n.value)]
 
     def time_decoder_kernel(self, which: int, iters: int) -> float:
         ms = ctypes.c_float(0.0)

@@ -6,6 +6,8 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <map>
 #include <memory>
@@ -186,7 +188,13 @@ struct TacoModel {
   ConvLayer enc[3], lstm_in, penc, post[5];
   DevBuf whhT;
   DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b;
+  DevBuf Wcomb;  // location_dense . location_conv folded, [64 taps (62 used)][128 dims]
   float bv = 0.f;
+  // persistent decoder: projection rows [stop tile | W_p] (+ bias) and prenet layer 1 on the host,
+  // folded per r into pj_w / pj_b = [stop tile | first 80r rows of W_p | W1 W_p,last frame]
+  std::vector<float> proj_rows, proj_bias, pre1_host;
+  DevBuf pj_w, pj_b;
+  int pj_r = -1;
 };
 
 struct TacoWS {
@@ -198,6 +206,7 @@ struct TacoWS {
   DevBuf dec, align, stop, pa, pbb;
   DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
   DevBuf ids, post, map;       // rows in decode order (longest first), output scatter map
+  DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
   // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
   // longest-first rows finish); all share one configuration key
   hipGraphExec_t graphs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -236,7 +245,10 @@ struct tts_ctx {
   int device = 0;
   hipStream_t s = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_chunk[2] = {nullptr, nullptr};
-  int* pinned = nullptr;  // [4]
+  hipEvent_t ev_dec[3] = {nullptr, nullptr, nullptr};  // around the persistent decoder launches
+  int* pinned = nullptr;  // [16]: [0:4) chunk polling, [8:10) step index after each persistent launch
+  int dec_path = 0;       // last decode: 0 = step graphs, 1 = persistent kernel
+  int dec_nlaunch = 0;
   HostMap taco_host, mg_host;
   TacoModel taco;
   TacoWS tws;
@@ -369,7 +381,8 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     const auto& win = need(h, "decoder.attention.inputs_layer.linear_layer.weight", {A, E}).d;
     pack_conv(M.penc, win, std::vector<float>(A, 0.f), E, A, 1, 1, 1, pl0);
   }
-  M.pre1.upload(swz(need(h, "decoder.prenet.linear_layers.0.linear_layer.weight", {P, F}).d, P, F));
+  M.pre1_host = need(h, "decoder.prenet.linear_layers.0.linear_layer.weight", {P, F}).d;
+  M.pre1.upload(swz(M.pre1_host, P, F));
   M.pre2.upload(swz(need(h, "decoder.prenet.linear_layers.1.linear_layer.weight", {P, P}).d, P, P));
   {
     const auto& wih = need(h, "decoder.attention_rnn.weight_ih", {4 * Q, P + E}).d;
@@ -398,6 +411,16 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
       for (int a = 0; a < A; ++a)
         for (int c = 0; c < 32; ++c) wdT[(size_t)c * A + a] = wd[(size_t)a * 32 + c];
       M.Wdense.upload(wdT);
+      // location_dense(location_conv(.)) has no biases: one 62-tap filter per attention dim
+      const auto& wl = need(h, "decoder.attention.location_layer.location_conv1d.weight", {32, 2, 31}).d;
+      std::vector<float> wc((size_t)64 * A, 0.f);
+      for (int j = 0; j < 62; ++j)
+        for (int a = 0; a < A; ++a) {
+          double acc = 0.0;
+          for (int cf = 0; cf < 32; ++cf) acc += (double)wd[(size_t)a * 32 + cf] * wl[(size_t)cf * 62 + j];
+          wc[(size_t)j * A + a] = (float)acc;
+        }
+      M.Wcomb.upload(wc);
     }
     M.v.upload(need(h, "decoder.attention.v.linear_layer.weight", {1, A}).d);
     M.bv = need(h, "decoder.attention.v.linear_layer.bias", {1}).d[0];
@@ -437,6 +460,9 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     std::copy(bp.begin(), bp.end(), bx.begin() + 16);
     M.proj_w.upload(swz(wx, 16 + NP, D + E));
     M.proj_b.upload(bx);
+    M.proj_rows = std::move(wx);
+    M.proj_bias = std::move(bx);
+    M.pj_r = -1;
   }
   const int pc[6] = {F, 512, 512, 512, 512, F};
   for (int i = 0; i < 5; ++i) {
@@ -501,6 +527,8 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<int64_t>(W.ids, (size_t)B * T_max, g);
   grow<float>(W.post, (size_t)B * S_cap * r * 80, g);
   grow<int>(W.map, BMAX, g);
+  grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
+  grow<unsigned>(W.pbar, 512, g);
   W.B = B;
   W.T_max = T_max;
   W.S_cap = S_cap;
@@ -782,6 +810,122 @@ hipGraphExec_t step_graph(tts_ctx* c, int MT, hipStream_t s) {
   return W.graphs[MT];
 }
 
+// projection job tiles of the persistent decoder for reduction factor r: the stop tile, the
+// 5r tiles of the first r frames, and prenet layer 1 folded through the last frame's rows
+// (relu(W1 y_last) = relu(W1 W_p,last [h|ctx] + W1 b_p,last); layer 1 has no bias), fold in double
+void build_pj(tts_ctx* c, int r) {
+  auto& M = c->taco;
+  if (M.pj_r == r) return;
+  const int K = 1536, F = 80, P = 256;
+  const int rows_p = 16 + F * r;
+  std::vector<float> rows((size_t)(rows_p + P) * K), bias(rows_p + P);
+  std::memcpy(rows.data(), M.proj_rows.data(), (size_t)rows_p * K * sizeof(float));
+  std::memcpy(bias.data(), M.proj_bias.data(), (size_t)rows_p * sizeof(float));
+  const float* wl = M.proj_rows.data() + (size_t)(16 + F * (r - 1)) * K;  // W_p rows of the last frame
+  const float* bl = M.proj_bias.data() + 16 + F * (r - 1);
+  std::vector<double> acc(K);
+  for (int k = 0; k < P; ++k) {
+    std::fill(acc.begin(), acc.end(), 0.0);
+    double bs = 0.0;
+    for (int i = 0; i < F; ++i) {
+      const double w1 = M.pre1_host[(size_t)k * F + i];
+      const float* row = wl + (size_t)i * K;
+      for (int j = 0; j < K; ++j) acc[j] += w1 * row[j];
+      bs += w1 * bl[i];
+    }
+    float* dst = rows.data() + (size_t)(rows_p + k) * K;
+    for (int j = 0; j < K; ++j) dst[j] = (float)acc[j];
+    bias[rows_p + k] = (float)bs;
+  }
+  M.pj_w.upload(swz(rows, rows_p + P, K));
+  M.pj_b.upload(bias);
+  M.pj_r = r;
+}
+
+bool use_persistent(tts_ctx* c) {
+  const char* e = std::getenv("TTS_DECODER");
+  if (e && std::string(e) == "graph") return false;
+  return c->tws.MT <= 2 && persist_supported(c->device);
+}
+
+// the whole decode as one cooperative launch per batch-tile count (decoder_persist.hip)
+void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
+  auto& M = c->taco;
+  auto& W = c->tws;
+  build_pj(c, r);
+  PArgs a{};
+  a.dec_w = M.dec_w.f();
+  a.dec_b = M.dec_bias.f();
+  a.apre_w = M.att_pre.f();
+  a.apre_b = M.att_bias.f();
+  a.attp_w = M.att_p.f();
+  a.pj_w = M.pj_w.f();
+  a.pj_b = M.pj_b.f();
+  a.pre2_w = M.pre2.f();
+  a.WqT = M.WqT.f();
+  a.Wcomb = M.Wcomb.f();
+  a.v = M.v.f();
+  a.bv = M.bv;
+  a.nt_proj = 1 + 5 * r;
+  a.ntj = a.nt_proj + 16;
+  a.r = r;
+  a.penc = W.penc.f();
+  a.enc = W.enc.f();
+  a.ypart = W.ypart.f();
+  a.pb = W.pb.f();
+  a.gatt = W.gatt.f();
+  a.hatt = W.hatt.f();
+  a.catt = W.catt.f();
+  a.hdec0 = W.hdec0.f();
+  a.hdec1 = W.hdec1.f();
+  a.cdec = W.cdec.f();
+  a.ctx = W.ctx.f();
+  a.pq = W.pq.f();
+  a.alpha = W.alpha.f();
+  a.acum = W.acum.f();
+  a.energy = W.energy.f();
+  a.part_s = W.aps.f();
+  a.part_m = W.apm.f();
+  a.part_u = W.apu.f();
+  a.counter = reinterpret_cast<unsigned*>(W.acnt.p);
+  a.nchmax = (W.T_max + persist_attn_tc() - 1) / persist_attn_tc();
+  a.softmax = M.softmax;
+  a.thr = thr;
+  a.bar = reinterpret_cast<unsigned*>(W.pbar.p);
+  // TTS_PTRACE=<file>: phase timestamps of 8 steps from step TTS_PTRACE_T0 (default 100)
+  static DevBuf trace_buf;
+  const char* tr = std::getenv("TTS_PTRACE");
+  if (tr) {
+    trace_buf.ensure((size_t)8 * 18 * 256 * 8);
+    HIP_OK(hipMemsetAsync(trace_buf.p, 0, (size_t)8 * 18 * 256 * 8, s));
+    a.trace = static_cast<unsigned long long*>(trace_buf.p);
+    a.atrace = a.trace + (size_t)8 * 10 * 256;
+    const char* t0 = std::getenv("TTS_PTRACE_T0");
+    a.trace_t0 = t0 ? std::atoi(t0) : 100;
+  }
+  HIP_OK(hipEventRecord(c->ev_dec[0], s));
+  c->dec_nlaunch = 0;
+  for (int mt = W.MT; mt >= 1; --mt) {
+    a.D = make_dev(c, std::min(W.B, 16 * mt));
+    launch_persist_decoder(a, mt, s);
+    if (tr) {  // only the first launch is traced
+      HIP_OK(hipStreamSynchronize(s));
+      std::vector<unsigned long long> h((size_t)8 * 18 * 256);
+      HIP_OK(hipMemcpy(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost));
+      if (FILE* fp = std::fopen(tr, "wb")) {
+        std::fwrite(h.data(), 8, h.size(), fp);
+        std::fclose(fp);
+      }
+      a.trace = nullptr;
+      a.atrace = nullptr;
+      tr = nullptr;
+    }
+    const int i = c->dec_nlaunch++;
+    HIP_OK(hipMemcpyAsync(&c->pinned[8 + i], &reinterpret_cast<DecCtl*>(W.ctl.p)->base, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipEventRecord(c->ev_dec[i + 1], s));
+  }
+}
+
 void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, int T_max, int r,
                 const int32_t* h_max_steps, int S_cap, float thr, float* d_dec, float* d_post, float* d_align,
                 float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream) {
@@ -854,6 +998,11 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   HIP_OK(hipMemsetAsync(W.acnt.p, 0, BMAX * sizeof(unsigned), s));
   bcast_rows_kernel<<<256, 256, 0, s>>>(M.att_bias.f(), 4096, W.gatt.f(), Bp);
   HIP_OK(hipGetLastError());
+  const bool persist = use_persistent(c);
+  c->dec_path = persist ? 1 : 0;
+  if (persist) {
+    run_persistent(c, r, thr, s);
+  } else {
   // step graphs, cached per configuration / buffer generation
   if (W.graph_gen != W.gen || W.gB != B || W.gT != T_max || W.gS != S_cap || W.gr != r || W.gthr != thr) {
     for (auto& ge : W.graphs)
@@ -886,7 +1035,13 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
       else if (pv[1] >= 1 && pv[1] < mt) mt = pv[1];
     }
   }
+  }
   HIP_OK(hipStreamSynchronize(s));
+  if (persist) {
+    unsigned err = 0;
+    HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(W.pbar.p) + 16, 4, hipMemcpyDeviceToHost));
+    TTS_CHECK(err == 0, "persistent decoder: grid barrier timed out (workgroups not co-resident)");
+  }
   std::vector<int> res(3 * BMAX);
   HIP_OK(hipMemcpy(res.data(), W.ctl.i() + 4, 3 * BMAX * 4, hipMemcpyDeviceToHost));
   int maxM = 0;
@@ -1190,8 +1345,9 @@ int tts_ctx_create(int device, tts_ctx** out) {
     HIP_OK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[0], hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[1], hipEventDisableTiming));
-    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), 16, hipHostMallocDefault));
-    std::memset(c->pinned, 0, 16);
+    for (auto& e : c->ev_dec) HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), 64, hipHostMallocDefault));
+    std::memset(c->pinned, 0, 64);
     *out = c.release();
   });
 }
@@ -1212,7 +1368,7 @@ int tts_ctx_destroy(tts_ctx* c) {
     {
       DeviceGuard g(dev);
       hipStream_t s = c->s;
-      hipEvent_t e[4] = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1]};
+      hipEvent_t e[7] = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1], c->ev_dec[0], c->ev_dec[1], c->ev_dec[2]};
       int* pin = c->pinned;
       delete c;
       for (auto ev : e) (void)hipEventDestroy(ev);
@@ -1369,6 +1525,21 @@ int tts_pqmf_synthesis(tts_ctx* c, const float* d_x, int B, int N, int L, const 
     launch_pqmf_synthesis(d_x, (long)N * L, L, d_G, N, taps, c->mws.lens.i(), 0, 1, L, B, d_y, (long)N * L, c->s);
     HIP_OK(hipStreamSynchronize(c->s));
     leave(c, stream);
+  });
+}
+
+int tts_decoder_stats(tts_ctx* c, int* path, int* nlaunch, float* ms, int* steps) {
+  return guarded([&] {
+    TTS_CHECK(c && path && nlaunch && ms && steps, "bad arguments");
+    TTS_CHECK(c->last_B > 0, "run tts_taco_infer first");
+    *path = c->dec_path;
+    *nlaunch = c->dec_path ? c->dec_nlaunch : 0;
+    int prev = 0;
+    for (int i = 0; i < *nlaunch; ++i) {
+      HIP_OK(hipEventElapsedTime(&ms[i], c->ev_dec[i], c->ev_dec[i + 1]));
+      steps[i] = c->pinned[8 + i] - prev;
+      prev = c->pinned[8 + i];
+    }
   });
 }
 

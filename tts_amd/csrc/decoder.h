@@ -102,6 +102,55 @@ struct AttnArgs {
   int softmax;
 };
 
+// persistent decoder (decoder_persist.hip): every decoder tensor the loop touches
+struct PArgs {
+  const float* dec_w;   // [256][160][64][4] decoder_rnn [W_ih | W_hh] gate-interleaved tiles
+  const float* dec_b;   // [4096]
+  const float* apre_w;  // [256][96][64][4] attention_rnn [W_ih,ctx | W_hh]
+  const float* apre_b;  // [4096] b_ih + b_hh
+  const float* attp_w;  // [256][16][64][4] attention_rnn W_ih,prenet
+  const float* pj_w;    // [ntj][96][64][4] stop tile, 5r frame tiles, 16 folded prenet-1 tiles
+  const float* pj_b;    // [ntj * 16]
+  const float* pre2_w;  // [16][16][64][4]
+  const float* WqT;     // [1024][128]
+  const float* Wcomb;   // [64][128]: location_dense . location_conv as one 62-tap filter per dim
+  const float* v;       // (128)
+  float bv;
+  int nt_proj, ntj, r;
+  const float* penc;  // (B, T_max, 128)
+  const float* enc;   // (B, T_max, 512)
+  float* ypart;       // [2][64][ntj*16] projection halves
+  float* pb;          // prenet output, fragment order (Bp, 256)
+  float* gatt;        // [Bp][4096] attention_rnn ctx/h part + biases
+  float* hatt;        // fragment order (Bp, 1024)
+  float* catt;        // [Bp][1024]
+  float* hdec0;       // fragment order (Bp, 1024), double-buffered on t & 1
+  float* hdec1;
+  float* cdec;        // [Bp][1024]
+  float* ctx;         // fragment order (Bp, 512)
+  float* pq;          // [128][Bp][128]
+  float* alpha;       // (B, T_max)
+  float* acum;
+  float* energy;
+  float* part_s;      // (B, nchmax)
+  float* part_m;
+  float* part_u;      // (B, nchmax, 512)
+  unsigned* counter;  // (B)
+  int nchmax;
+  int softmax;
+  float thr;
+  unsigned* bar;  // barrier words (zeroed before each launch): [0] global, [32] go, [64 + 32x] XCD x,
+                  // [16] error
+  unsigned long long* trace;   // optional phase timestamps [8 steps][10][256] (TTS_PTRACE)
+  unsigned long long* atrace;  // optional attention-item timestamps [8 steps][256][8]
+  int trace_t0;
+  DecDev D;
+};
+
+bool persist_supported(int device);
+int persist_attn_tc();  // attention positions per work item (sizes the chunk-partial buffers)
+void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s);
+
 void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s);
 // prenet layer 1 + layer 2 in one launch (16 workgroups) plus the stop workgroup
 void launch_prenet_stop(const SkArgs& a, const DecDev& d, const StopArgs& st, int jstep, hipStream_t s);

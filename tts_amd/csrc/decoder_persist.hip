@@ -1,0 +1,811 @@
+// Persistent Tacotron2 decoder (gfx950): the autoregressive loop as ONE cooperative launch per
+// batch-tile count, 256 workgroups (one per CU) x 8 waves, phases separated by a grid barrier.
+//
+// Why: with the 5-launch graph (decoder.hip) every step re-streams ~72 MB of LSTM / projection
+// weights from MALL/HBM (the decoder_rnn launch alone is ~10 us of a 54 us step). Here the weights
+// stay on chip for the whole decode:
+//   decoder_rnn   [W_ih | W_hh] (41.9 MB)  VGPRs: workgroup g owns gate tile g, 20 k-chunks per wave
+//   attention_rnn ctx/h part   (25.2 MB)   LDS:   96 KB per workgroup (tile g)
+// and a hierarchical grid barrier (per-XCD counters, then 8 arrivals on a global counter, one go
+// word; tools/persist_bench.hip: 1.9 us) replaces each launch boundary (1.7 us + cold start).
+//
+// One decoder step t (TTS/tts/layers/tacotron2.py:354-369 -> decode :259-298), 5 phases:
+//   P1  stop decision for t-1 (workgroup 255; tacotron2.py:357-366)
+//       || prenet layer 2 (workgroups 0-15). Layer 1 was folded into the previous projection:
+//       the prenet reads the LAST frame y[:, 80(r-1):80r] of the projection, and layer 1 has no
+//       bias, so relu(W1 y) = relu(W1 W_p,last [h|ctx] + W1 b_p,last): 16 extra projection tiles
+//   P3  attention_rnn LSTMCell prenet part (K = 256) + cell + partial query projections
+//       (workgroups 0-127, 8 units each) || frames of step t-1 to dec_out (workgroups 128-255)
+//   P4  location-sensitive attention, work item = (utterance, 32 positions); the last arriving
+//       item of an utterance combines (same protocol as decoder.hip K3)
+//   P5  decoder_rnn LSTMCell (tile g, K = 2560, weights in VGPRs)
+//   P6  next step's attention_rnn ctx/h part (tile g, weights in LDS)
+//       || projection + stop tile + folded prenet layer 1, K split in 2 halves (workgroups
+//       0 .. 2*ntj-1); consumers add the two halves and the bias
+//
+// Memory model: cross-workgroup data is written with agent-scope relaxed atomic stores (sc1:
+// write-through past the non-coherent per-XCD L2) and read with agent-scope loads (sc1), every
+// wave drains its stores (vmcnt(0)) before the barrier arrival; no L2 invalidation is needed.
+// Barrier waits give up after 0.2 s (error word set, every workgroup exits): a launch that was
+// not fully co-resident fails loudly instead of hanging.
+#include "common.h"
+#include "decoder.h"
+
+#include <type_traits>
+
+namespace {
+constexpr int PW = 256, PT = 512, NWV = 8;
+constexpr int DEC_NC = 20;   // 160 k-chunks / 8 waves
+constexpr int APRE_NC = 12;  // 96 / 8
+constexpr int ATTP_NC = 4;   // 2 tiles x 16 chunks / 8 waves
+constexpr int PJ_NC = 6;     // 48 / 8
+constexpr int PRE2_NC = 2;   // 16 / 8
+constexpr int PTC = 32;      // attention positions per work item
+constexpr int YROWS = 64;    // rows per projection half (independent of the batch tile: the MT = 1
+                             // launch reads what the MT = 2 launch left)
+constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = 128;
+constexpr unsigned long long BAR_TIMEOUT = 20000000ull;  // s_memrealtime ticks (100 MHz): 0.2 s
+}  // namespace
+
+// ------------------------------------------------------------------ coherent access helpers
+__device__ __forceinline__ float ldc(const float* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ int ldci(const int* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stc(float* p, float v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void stci(int* p, int v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// Opaque copies of lane / wave indices, taken at the start of each phase: without them the
+// compiler hoists every loop-invariant address of every phase out of the step loop and keeps them
+// all live (hundreds of VGPRs / SGPRs, spilled to scratch).
+__device__ __forceinline__ int opaque_v(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+__device__ __forceinline__ int opaque_s(int v) {
+  asm volatile("" : "+s"(v));
+  return v;
+}
+// 16-byte agent-coherent load at byte offset `off` from a wave-uniform base (buffer load, sc1)
+template <int AUX = 16>
+__device__ __forceinline__ f32x4 ldc4(const float* base, int off) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
+}
+#ifdef PLAIN_ACT
+constexpr int ACT_AUX = 0;
+#else
+constexpr int ACT_AUX = 16;
+#endif
+
+
+// LDS-only workgroup barrier: unlike __syncthreads() (whose workgroup-scope fences wait for every
+// outstanding global load, vmcnt(0)), global loads already in flight stay in flight
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
+// Hierarchical grid barrier, split so that loads for the next phase can be issued between the
+// arrival and the wait. arrive: every wave drains its stores (sc1 write-through), then thread 0
+// counts the workgroup in at its XCD's counter; the 32nd arrival of an XCD counts the XCD in at
+// the global counter; the 8th XCD writes the go word.
+__device__ __forceinline__ void gsync_arrive(unsigned* bar, unsigned& gen) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ++gen;
+  if (threadIdx.x == 0) {
+    unsigned* xc = bar + 64 + (blockIdx.x & 7) * 32;
+    const unsigned per = gridDim.x / 8;
+    if (__hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per * gen - 1)
+      if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 8u * gen - 1)
+        __hip_atomic_store(bar + 32, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+// wait for the go word; false = timed out (error word set, the caller exits)
+__device__ __forceinline__ bool gsync_wait(unsigned* bar, unsigned gen, int* flag) {
+  if (threadIdx.x == 0) {
+    int good = 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(bar + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > BAR_TIMEOUT) {
+        __hip_atomic_fetch_or(bar + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        good = 0;
+        break;
+      }
+    }
+    *flag = good;
+  }
+  lds_barrier();
+  return *flag;
+}
+
+// partial sums of one wave's MT accumulators into LDS [wave][m][17]
+template <int MT>
+__device__ __forceinline__ void acc_to_lds(float* part, int w, int lane, const f32x4 (&acc)[MT]) {
+  constexpr int Bp = MT * 16;
+  float* p = part + w * Bp * 17;
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
+}
+template <int KS, int Bp>
+__device__ __forceinline__ float lds_sum(const float* part, int m, int n) {
+  float s = part[m * 17 + n];
+#pragma unroll
+  for (int w = 1; w < KS; ++w) s += part[(w * Bp + m) * 17 + n];
+  return s;
+}
+
+__device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+
+// sum over the 16 lanes of a DPP row (every lane of the row gets the row sum)
+__device__ __forceinline__ float row16_sum(float v) {
+  auto dpp = [](float x, auto ctrl) {
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xf, 0xf, false));
+  };
+  v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm(1,0,3,2)
+  v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm(2,3,0,1)
+  v += dpp(v, std::integral_constant<int, 0x124>{});  // row_ror:4
+  v += dpp(v, std::integral_constant<int, 0x128>{});  // row_ror:8
+  return v;
+}
+// sum over all 64 lanes (uniform result)
+__device__ __forceinline__ float wave64_sum(float v) {
+  v = row16_sum(v);
+  const int b = __float_as_int(v);
+  return __int_as_float(__builtin_amdgcn_readlane(b, 0)) + __int_as_float(__builtin_amdgcn_readlane(b, 16)) +
+         __int_as_float(__builtin_amdgcn_readlane(b, 32)) + __int_as_float(__builtin_amdgcn_readlane(b, 48));
+}
+
+// ------------------------------------------------------------------ attention work item
+// utterance b, positions [PTC ch, PTC ch + PTC): energies (common_layers.py:268-278, 90-110),
+// chunk partials, last arriver normalises and writes alpha, alpha_cum, alignment and context
+// (common_layers.py:347-366). NT = 512 threads: 4 groups over the 128 attention dims, 8 positions
+// per thread.
+// location_dense(location_conv(alpha, alpha_cum)) is linear with no biases, so it is applied as
+// ONE 62-tap filter per attention dim: Wcomb[i*31 + k][a] = sum_c W_dense[a][c] W_conv[c][i][k]
+// (folded in double at load; read from LDS), slid over the alpha window in registers.
+
+// attention item timestamps (P.atrace, optional): [8 steps][256 items][8]
+#define ATRACE(k)                                                                             \
+  if (P.atrace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                         \
+  P.atrace[(((long)(t - P.trace_t0) * PW + b * P.nchmax + ch) * 8) + (k)] = __builtin_amdgcn_s_memrealtime()
+
+template <int MT>
+__device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
+                                           int* is_last) {
+  constexpr int NT = PT, TC = PTC;
+  constexpr int NG = NT / ADIM_;  // 4
+  constexpr int PPG = TC / NG;    // 8 positions per thread
+  constexpr int NPT = NPQ_ / 16;  // 8 query partials per thread (16 groups)
+  constexpr int AW = PPG + LOCK_ - 1;  // alpha window per group (38)
+  constexpr int Bp = MT * 16;
+  const DecDev& D = P.D;
+  const int t0 = ch * TC;
+  const int tid = opaque_v(threadIdx.x);
+  const int a = tid % ADIM_, grp = tid / ADIM_;
+  const int lane = tid & 63, wave = tid >> 6;
+  float* red = sm;                 // [16][ADIM] query-partial group sums
+  float* A0 = red + 16 * ADIM_;    // [TC + LOCK - 1] alpha window
+  float* A1 = A0 + TC + LOCK_;     // alpha_cum window
+  float* esum = A1 + TC + LOCK_;   // [8 waves][PPG] half-sums of the energies
+  float* sv = esum + 8 * PPG;      // [TC] energies
+  float* sw = sv + TC;             // [TC] normalised weights
+  const int T = D.lens[b];
+  const int Tm1 = max(T - 1, 0);
+  // ---- independent loads first (clamped indices); the query partials as 16-byte loads:
+  //      thread = (partial group pg of 8, dims 4*a4 .. 4*a4+3) ----
+  const int a4 = tid & 31, pg = tid >> 5;
+  f32x4 pp[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) pp[i] = ldc4<ACT_AUX>(P.pq, ((((pg * 8 + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
+  float a0, a1;
+  {
+    const int pos = t0 - (LOCK_ - 1) / 2 + min(tid, TC + LOCK_ - 2);
+    const int pc = min(max(pos, 0), Tm1);
+    a0 = ldc(P.alpha + (long)b * D.T_max + pc);
+    a1 = ldc(P.acum + (long)b * D.T_max + pc);
+    if (pos < 0 || pos >= T) a0 = a1 = 0.f;
+  }
+  float pen[PPG];
+#pragma unroll
+  for (int i = 0; i < PPG; ++i) pen[i] = P.penc[((long)b * D.T_max + min(t0 + grp * PPG + i, Tm1)) * ADIM_ + a];
+  const float va = P.v[a];
+  const int dn = ldci(D.done + b);
+  __builtin_amdgcn_sched_barrier(0);
+  ATRACE(0);
+  if (t0 >= T || dn) return;  // workgroup-uniform
+  if (tid < TC + LOCK_ - 1) {
+    A0[tid] = a0;
+    A1[tid] = a1;
+  }
+  {
+    f32x4 s4 = pp[0];
+#pragma unroll
+    for (int i = 1; i < NPT; ++i) s4 += pp[i];
+    *reinterpret_cast<f32x4*>(&red[pg * ADIM_ + 4 * a4]) = s4;
+  }
+  // encoder rows for the partial context, in flight during the energy computation
+  float ev[TC];
+#pragma unroll
+  for (int i = 0; i < TC; ++i) ev[i] = P.enc[((long)b * D.T_max + min(t0 + i, Tm1)) * 512 + tid];
+  __builtin_amdgcn_sched_barrier(0);
+  lds_barrier();
+  ATRACE(1);
+  float pqa = red[a];
+#pragma unroll
+  for (int g = 1; g < 16; ++g) pqa += red[g * ADIM_ + a];
+  // fused location filter for positions grp*PPG + p, p < PPG
+  float l[PPG];
+#pragma unroll
+  for (int p = 0; p < PPG; ++p) l[p] = 0.f;
+#pragma unroll
+  for (int ci = 0; ci < 2; ++ci) {
+    const float* Ai = (ci ? A1 : A0) + grp * PPG;
+    float win[PPG];  // sliding window: one new alpha value per tap
+#pragma unroll
+    for (int p = 0; p < PPG; ++p) win[p] = Ai[p];
+    // taps in groups of 8 (a fully unrolled 31-tap loop hoisted every weight read and ran the
+    // kernel out of VGPRs)
+#pragma unroll 1
+    for (int k0 = 0; k0 < LOCK_; k0 += 8) {
+#pragma unroll
+      for (int kk = 0; kk < 8; ++kk) {
+        const int k = min(k0 + kk, LOCK_ - 1);
+        const float w = k0 + kk < LOCK_ ? wcomb[(ci * LOCK_ + k) * ADIM_ + a] : 0.f;
+#pragma unroll
+        for (int p = 0; p < PPG; ++p) l[p] = fmaf(w, win[p], l[p]);
+#pragma unroll
+        for (int p = 0; p + 1 < PPG; ++p) win[p] = win[p + 1];
+        win[PPG - 1] = Ai[min(k + PPG, AW - 1)];
+      }
+    }
+  }
+  ATRACE(2);
+  // e = v . tanh(pq + loc + penc): per position, a wave sums its 64 dims, LDS joins the two waves
+  float z[PPG];
+#pragma unroll
+  for (int p = 0; p < PPG; ++p) z[p] = tanhf(pqa + l[p] + pen[p]) * va;
+#ifdef NO_DPP
+#pragma unroll
+  for (int off = 32; off > 0; off >>= 1)
+#pragma unroll
+    for (int p = 0; p < PPG; ++p) z[p] += __shfl_xor(z[p], off, 64);
+#else
+#pragma unroll
+  for (int p = 0; p < PPG; ++p) z[p] = wave64_sum(z[p]);
+#endif
+  if (lane < PPG) {
+    float zz = z[0];
+#pragma unroll
+    for (int p = 1; p < PPG; ++p) zz = lane == p ? z[p] : zz;
+    esum[wave * PPG + lane] = zz;
+  }
+  lds_barrier();
+  ATRACE(3);
+  const int nvalid = min(TC, T - t0);
+  const long pidx = (long)b * P.nchmax + ch;
+  if (tid < TC) {  // position tid: group tid / PPG = waves 2g, 2g+1
+    const int gq = tid / PPG, p = tid % PPG;
+    const float e = esum[(2 * gq) * PPG + p] + esum[(2 * gq + 1) * PPG + p] + P.bv;
+    if (tid < nvalid) stc(P.energy + (long)b * D.T_max + t0 + tid, e);
+    sv[tid] = e;
+  }
+  lds_barrier();
+  ATRACE(4);
+  // chunk-local normalisation terms (computed once, shared through LDS)
+  float m_c = -INFINITY;
+  if (P.softmax) {
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+      if (i < nvalid) m_c = fmaxf(m_c, sv[i]);
+  }
+  if (tid < TC) {
+    const float e = sv[tid];
+    const float x = P.softmax ? expf(e - m_c) : 1.f / (1.f + expf(-e));
+    sw[tid] = tid < nvalid ? x : 0.f;
+  }
+  lds_barrier();
+  float S_c = 0.f, u = 0.f;
+#pragma unroll
+  for (int i = 0; i < TC; ++i) {
+    const float sl = sw[i];
+    S_c += sl;
+    u = fmaf(sl, ev[i], u);
+  }
+  stc(P.part_u + pidx * 512 + tid, u);
+  if (tid == 0) {
+    stc(P.part_s + pidx, S_c);
+    stc(P.part_m + pidx, m_c);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  ATRACE(5);
+  const int nch = (T + TC - 1) / TC;
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(&P.counter[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *is_last = (prev == (unsigned)(nch - 1));
+  }
+  lds_barrier();
+  ATRACE(6);
+  if (!*is_last) return;
+  // combine: chunk partials in batches of 8, all loads of a batch in flight (clamped)
+  const long pb0 = (long)b * P.nchmax;
+  constexpr int CB = 8;
+  float m = -INFINITY, S = 0.f, cx = 0.f;
+  for (int cb = 0; cb < nch; cb += CB) {
+    float pm[CB], ps[CB], pu[CB];
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      const long c = pb0 + min(cb + i, nch - 1);
+      pm[i] = ldc(P.part_m + c);
+      ps[i] = ldc(P.part_s + c);
+      pu[i] = ldc(P.part_u + c * 512 + tid);
+    }
+    float wc[CB];
+    if (P.softmax) {
+      float mb = m;
+#pragma unroll
+      for (int i = 0; i < CB; ++i)
+        if (cb + i < nch) mb = fmaxf(mb, pm[i]);
+      const float sc = (m == -INFINITY) ? 0.f : expf(m - mb);
+      S *= sc;
+      cx *= sc;
+      m = mb;
+#pragma unroll
+      for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch) ? expf(pm[i] - m) : 0.f;
+    } else {
+#pragma unroll
+      for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch) ? 1.f : 0.f;
+    }
+#pragma unroll
+    for (int i = 0; i < CB; ++i) {
+      S = fmaf(ps[i], wc[i], S);
+      cx = fmaf(pu[i], wc[i], cx);
+    }
+  }
+  stc(P.ctx + frag_idx(b, tid, 512), cx / S);
+  ATRACE(7);
+  for (int tt = tid; tt < T; tt += NT) {
+    const float e = ldc(P.energy + (long)b * D.T_max + tt);
+    const float al = (P.softmax ? expf(e - m) : 1.f / (1.f + expf(-e))) / S;
+    stc(P.alpha + (long)b * D.T_max + tt, al);
+    stc(P.acum + (long)b * D.T_max + tt, ldc(P.acum + (long)b * D.T_max + tt) + al);
+    if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = al;
+  }
+  if (tid == 0) __hip_atomic_store(&P.counter[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// ------------------------------------------------------------------ the persistent kernel
+// LDS: [att-pre weights 96 x 1 KiB][Wcomb 64 x 128][scratch: GEMM reduction + hs | attention]
+constexpr size_t P_LDS_APRE = 96 * 64 * 16;
+constexpr size_t P_LDS_WC = 64 * 128 * 4;
+constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 8 * 4;  // >= attention scratch (~2.4K floats)
+constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
+
+// phase timestamps of every workgroup for 8 steps (P.trace, optional): [step][10][256]
+#define PTRACE(k)                                                                              \
+  if (P.trace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                          \
+  P.trace[((long)(t - P.trace_t0) * 10 + (k)) * PW + blockIdx.x] = __builtin_amdgcn_s_memrealtime()
+
+template <int MT>
+__global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
+  extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
+  __shared__ int sflag, is_last, dflag[64];
+  constexpr int Bp = MT * 16;
+  const DecDev& D = P.D;
+  f32x4* Wap = smem4;                                              // [96][64]
+  float* wcomb = reinterpret_cast<float*>(smem4) + 96 * 64 * 4;    // [64][128]
+  float* scr = wcomb + 64 * 128;
+  float* red0 = scr;                   // [8][Bp][17]
+  float* hs = red0 + 8 * Bp * 17;      // [Bp][8]
+  const int g = blockIdx.x, tid0 = threadIdx.x, lane0 = tid0 & 63;
+  const int wave0 = __builtin_amdgcn_readfirstlane(tid0 >> 6);
+  const int YP = P.ntj * 16;
+
+  // ---- one-time: resident weights ----
+  int tid = tid0, lane = lane0, wave = wave0;
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(P.apre_w) + (long)g * 96 * 64;
+    for (int i = tid; i < 96 * 64; i += PT) Wap[i] = src[i];
+    for (int i = tid; i < 64 * 128; i += PT) wcomb[i] = P.Wcomb[i];
+  }
+  f32x4 wd[DEC_NC];
+  {
+    const f32x4* src = reinterpret_cast<const f32x4*>(P.dec_w) + ((long)g * 160 + wave * DEC_NC) * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < DEC_NC; ++i) wd[i] = src[(long)i * 64];
+  }
+  // epilogue constants: decoder_rnn biases of this thread's (row, unit) item, attention_rnn
+  // ctx/h-part bias of its column
+  float db[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) db[q] = P.dec_b[g * 16 + q * 4 + (tid & 3)];
+  const float apb = P.apre_b[g * 16 + (tid & 15)];
+  __syncthreads();
+
+  unsigned gen = 0;
+  int t = D.ctl->base;
+  const int pj_jobs = 2 * P.ntj;
+  // per-phase weights, loaded before the barrier that precedes their phase
+  f32x4 w2[PRE2_NC];
+  auto load_w2 = [&]() {
+    const int tl = min(g, 15);
+    const f32x4* src = reinterpret_cast<const f32x4*>(P.pre2_w) + ((long)tl * 16 + wave * PRE2_NC) * 64 + lane;
+#pragma unroll
+    for (int i = 0; i < PRE2_NC; ++i) w2[i] = src[(long)i * 64];
+  };
+  load_w2();
+
+  // frames of step s (< S_cap) from the two projection halves (K5 frame store of decoder.hip):
+  // written when the row was still decoding at step s, i.e. not done or done later than s
+  auto write_frames = [&](int s, int wg0, int nwg) {
+    if (s < 0 || s >= D.S_cap) return;
+    const int FR = 80 * P.r;
+    const int n = D.B * FR;
+    for (int idx = (g - wg0) * PT + tid; idx < n; idx += nwg * PT) {
+      const int m = idx / FR, c = idx - m * FR;
+      if (!ldci(D.done + m) || ldci(D.steps + m) > s) {
+        const float v = ldc(P.ypart + (long)m * YP + 16 + c) + ldc(P.ypart + (long)(YROWS + m) * YP + 16 + c) +
+                        P.pj_b[16 + c];
+        D.dec_out[((long)m * D.S_cap + s) * FR + c] = v;
+      }
+    }
+  };
+
+  for (;; ++t) {
+    PTRACE(0);
+    // ======== P1: stop(t-1) || prenet layer 2 ========
+    tid = opaque_v(tid0);
+    lane = opaque_v(lane0);
+    wave = opaque_s(wave0);
+    if (g < 16) {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if (t > 0) {  // t = 0: prenet input is the zero go-frame, layer 1 has no bias -> 0
+#pragma unroll
+        for (int i = 0; i < PRE2_NC; ++i) {
+          const int kc = wave * PRE2_NC + i;
+          const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pj_b + col);
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const int m = mt * 16 + (lane & 15);
+            f32x4 x = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) acc[mt] = MFMA16(x[q], w2[i][q], acc[mt]);
+          }
+        }
+      }
+      acc_to_lds<MT>(red0, wave, lane, acc);
+      __syncthreads();
+      for (int idx = tid; idx < Bp * 16; idx += PT) {
+        const int m = idx >> 4, n = idx & 15;
+        stc(P.pb + frag_idx(m, g * 16 + n, 256), fmaxf(lds_sum<NWV, Bp>(red0, m, n), 0.f));
+      }
+    } else if (g == PW - 1) {
+      if (tid < D.B) {
+        const int m = tid;
+        int dn = ldci(D.done + m);
+        if (t >= 1 && !dn) {
+          const float logit = ldc(P.ypart + (long)m * YP) + ldc(P.ypart + (long)(YROWS + m) * YP) + P.pj_b[0];
+          const float sg = sigm(logit);
+          if (t - 1 < D.S_cap) D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
+          const bool st = (sg > P.thr) && (t - 1) > 0;
+          if (st || t >= D.max_steps[m]) {
+            stci(D.done + m, 1);
+            stci(D.steps + m, t);
+            stci(D.status + m, st ? 1 : 2);
+            dn = 1;
+          }
+        }
+        dflag[m] = dn;
+      }
+      __syncthreads();
+      if (tid == 0) {
+        int last = -1;
+        for (int k = 0; k < D.B; ++k)
+          if (!dflag[k]) last = k;
+        stci(&D.ctl->all_done, last < 0);
+        stci(&D.ctl->active_tiles, last / 16 + 1);
+      }
+    }
+    PTRACE(1);
+    gsync_arrive(P.bar, gen);
+    // P3 operands that are already final: its epilogue's gate addends (written by P6 of the
+    // previous step), c_att, the query-projection weights
+    float ga[4], ca, wq[8];
+    {
+      const int idx = min(tid, 2 * Bp * 4 - 1);
+      const int gl = idx / (Bp * 4), rem = idx % (Bp * 4);
+      const int m = rem >> 2, u = rem & 3;
+      const int tile = 2 * min(g, 127) + gl;
+#pragma unroll
+      for (int q = 0; q < 4; ++q) ga[q] = ldc(P.gatt + (long)m * 4096 + tile * 16 + q * 4 + u);
+      ca = P.catt[(long)m * 1024 + tile * 4 + u];
+#pragma unroll
+      for (int u2 = 0; u2 < 8; ++u2) wq[u2] = P.WqT[(long)(8 * min(g, 127) + u2) * 128 + (tid & 127)];
+    }
+    // attention_rnn prenet-part weights for P3 (2 tiles per workgroup, 4 k-chunks per wave)
+    f32x4 wa[ATTP_NC];
+    {
+      const int tl = 2 * min(g, 127) + (wave >> 2);
+      const f32x4* src = reinterpret_cast<const f32x4*>(P.attp_w) + ((long)tl * 16 + 4 * (wave & 3)) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < ATTP_NC; ++i) wa[i] = src[(long)i * 64];
+    }
+    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    PTRACE(2);
+    {
+      const int all_done = ldci(&D.ctl->all_done), act = ldci(&D.ctl->active_tiles);
+      if (all_done || act < MT || t > D.S_cap + 1) {
+        write_frames(t - 1, 0, PW);
+        if (g == 0 && tid == 0) D.ctl->base = t;
+        return;
+      }
+    }
+    // ======== P3: attention_rnn (prenet part) + cell + query partials || frames(t-1) ========
+    tid = opaque_v(tid0);
+    lane = opaque_v(lane0);
+    wave = opaque_s(wave0);
+    if (g < 128) {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      f32x4 x[ATTP_NC][MT];
+#pragma unroll
+      for (int i = 0; i < ATTP_NC; ++i)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) x[i][mt] = ldc4(P.pb, ((mt * 16 + 4 * (wave & 3) + i) * 64 + lane) * 16);
+#pragma unroll
+      for (int i = 0; i < ATTP_NC; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[i][mt][q], wa[i][q], acc[mt]);
+      // waves 0-3: tile 2g, waves 4-7: tile 2g+1
+      acc_to_lds<MT>(red0 + (wave >> 2) * 4 * Bp * 17, wave & 3, lane, acc);
+      __syncthreads();
+      if (tid < 2 * Bp * 4) {
+        const int gl = tid / (Bp * 4), rem = tid % (Bp * 4);
+        const int m = rem >> 2, u = rem & 3;
+        const int tile = 2 * g + gl;
+        const float* pg = red0 + gl * 4 * Bp * 17;
+        float pre[4];
+#pragma unroll
+#ifdef NO_PREF
+        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<4, Bp>(pg, m, q * 4 + u) + ldc(P.gatt + (long)m * 4096 + tile * 16 + q * 4 + u);
+        const long ci = (long)m * 1024 + tile * 4 + u;
+        const float c = sigm(pre[1]) * P.catt[ci] + sigm(pre[0]) * tanhf(pre[2]);
+#else
+        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<4, Bp>(pg, m, q * 4 + u) + ga[q];
+        const long ci = (long)m * 1024 + tile * 4 + u;
+        const float c = sigm(pre[1]) * ca + sigm(pre[0]) * tanhf(pre[2]);
+#endif
+        const float h = sigm(pre[3]) * tanhf(c);
+        P.catt[ci] = c;
+        stc(P.hatt + frag_idx(m, tile * 4 + u, 1024), h);
+        hs[m * 8 + gl * 4 + u] = h;
+      }
+      __syncthreads();
+      {  // partial query projection over this workgroup's 8 units
+        const int a = tid & 127;
+        for (int m = tid >> 7; m < Bp; m += PT / 128) {
+          float s = 0.f;
+#pragma unroll
+          for (int u = 0; u < 8; ++u) s = fmaf(wq[u], hs[m * 8 + u], s);
+          stc(P.pq + ((long)g * Bp + m) * 128 + a, s);
+        }
+      }
+    } else {
+      write_frames(t - 1, 128, PW - 128);
+    }
+    PTRACE(3);
+    gsync_arrive(P.bar, gen);
+    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    PTRACE(4);
+    // ======== P4: attention ========
+    {
+      const int nitems = D.B * P.nchmax;
+      for (int it = g; it < nitems; it += PW) {
+        pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last);
+        lds_barrier();
+      }
+    }
+    PTRACE(5);
+    gsync_arrive(P.bar, gen);
+    // P5 epilogue operand (own tile's c_dec), fetched during the barrier
+    const float cd = P.cdec[(long)min(tid >> 2, Bp - 1) * 1024 + g * 4 + (tid & 3)];
+    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    PTRACE(6);
+    // ======== P5: decoder_rnn (tile g, K = [h_att 1024 | ctx 512 | h_dec 1024]) ========
+    tid = opaque_v(tid0);
+    lane = opaque_v(lane0);
+    wave = opaque_s(wave0);
+    float* hd_cur = (t & 1) ? P.hdec1 : P.hdec0;
+    float* hd_nxt = (t & 1) ? P.hdec0 : P.hdec1;
+    {
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      auto ld = [&](int kc, int mt) {
+        // wave-uniform segment select
+        const float* base = kc < 64 ? P.hatt : kc < 96 ? P.ctx : hd_cur;
+        const int kl = kc < 64 ? kc : kc < 96 ? kc - 64 : kc - 96;
+        const int nk = kc < 64 ? 64 : kc < 96 ? 32 : 64;
+        return ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
+      };
+      constexpr int G = 4;
+      f32x4 x[2][G][MT];
+      const int kc0 = wave * DEC_NC;
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) x[0][i][mt] = ld(kc0 + i, mt);
+#pragma unroll
+      for (int i0 = 0; i0 < DEC_NC; i0 += G) {
+        const int cur = (i0 / G) & 1;
+        if (i0 + G < DEC_NC) {
+#pragma unroll
+          for (int i = 0; i < G; ++i)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) x[cur ^ 1][i][mt] = ld(kc0 + i0 + G + i, mt);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < G; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[cur][i][mt][q], wd[i0 + i][q], acc[mt]);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc_to_lds<MT>(red0, wave, lane, acc);
+      __syncthreads();
+      if (tid < Bp * 4) {
+        const int m = tid >> 2, u = tid & 3;
+        float pre[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<NWV, Bp>(red0, m, q * 4 + u) + db[q];
+        const long ci = (long)m * 1024 + g * 4 + u;
+#ifdef NO_PREF
+        const float c = sigm(pre[1]) * P.cdec[ci] + sigm(pre[0]) * tanhf(pre[2]);
+#else
+        const float c = sigm(pre[1]) * cd + sigm(pre[0]) * tanhf(pre[2]);
+#endif
+        const float h = sigm(pre[3]) * tanhf(c);
+        P.cdec[ci] = c;
+        stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
+      }
+    }
+    PTRACE(7);
+    gsync_arrive(P.bar, gen);
+    // projection weights for P6 (half `g & 1` of job tile `g >> 1`, 6 k-chunks per wave)
+    f32x4 wp[PJ_NC];
+    {
+      const int q = min(g >> 1, P.ntj - 1), half = g & 1;
+      const f32x4* src = reinterpret_cast<const f32x4*>(P.pj_w) + ((long)q * 96 + 48 * half + wave * PJ_NC) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < PJ_NC; ++i) wp[i] = src[(long)i * 64];
+    }
+    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    PTRACE(8);
+    // ======== P6: projection halves || attention_rnn ctx/h part (tile g, LDS weights) ========
+    tid = opaque_v(tid0);
+    lane = opaque_v(lane0);
+    wave = opaque_s(wave0);
+    {
+      const bool pj = g < pj_jobs;
+      if (pj) {
+        f32x4 acc2[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int kb = 48 * (g & 1) + wave * PJ_NC;  // K = [h_dec 1024 | ctx 512]
+        f32x4 y[PJ_NC][MT];
+#pragma unroll
+        for (int i = 0; i < PJ_NC; ++i) {
+          const int kc = kb + i;
+          const float* base = kc < 64 ? hd_nxt : P.ctx;
+          const int kl = kc < 64 ? kc : kc - 64;
+          const int nk = kc < 64 ? 64 : 32;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) y[i][mt] = ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < PJ_NC; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
+        acc_to_lds<MT>(red0, wave, lane, acc2);
+        __syncthreads();
+        for (int idx = tid; idx < Bp * 16; idx += PT) {
+          const int m = idx >> 4, n = idx & 15;
+          stc(P.ypart + (long)((g & 1) * YROWS + m) * YP + (g >> 1) * 16 + n, lds_sum<NWV, Bp>(red0, m, n));
+        }
+        __syncthreads();
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      f32x4 acc[MT];
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kc0 = wave * APRE_NC;  // K = [ctx 512 | h_att 1024]
+      auto ld = [&](int kc, int mt) {
+        const float* base = kc < 32 ? P.ctx : P.hatt;
+        const int kl = kc < 32 ? kc : kc - 32;
+        const int nk = kc < 32 ? 32 : 64;
+        return ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
+      };
+      constexpr int G = 4;
+      f32x4 x[2][G][MT];
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) x[0][i][mt] = ld(kc0 + i, mt);
+#pragma unroll
+      for (int i0 = 0; i0 < APRE_NC; i0 += G) {
+        const int cur = (i0 / G) & 1;
+        if (i0 + G < APRE_NC) {
+#pragma unroll
+          for (int i = 0; i < G; ++i)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) x[cur ^ 1][i][mt] = ld(kc0 + i0 + G + i, mt);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < G; ++i) {
+          const f32x4 w = Wap[(kc0 + i0 + i) * 64 + lane];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[cur][i][mt][q], w[q], acc[mt]);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      acc_to_lds<MT>(red0, wave, lane, acc);
+      __syncthreads();
+      for (int idx = tid; idx < Bp * 16; idx += PT) {
+        const int m = idx >> 4, n = idx & 15;
+        stc(P.gatt + (long)m * 4096 + g * 16 + n, lds_sum<NWV, Bp>(red0, m, n) + apb);
+      }
+    }
+    PTRACE(9);
+    gsync_arrive(P.bar, gen);
+    load_w2();
+    if (!gsync_wait(P.bar, gen, &sflag)) return;
+  }
+}
+
+// host side ------------------------------------------------------------------------------
+bool persist_supported(int device) {
+  int cus = 0, coop = 0;
+  if (hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess) return false;
+  if (hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, device) != hipSuccess) return false;
+  return cus == PW && coop;
+}
+
+int persist_attn_tc() { return PTC; }
+
+void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
+  TTS_CHECK(MT == 1 || MT == 2, "persistent decoder: MT must be 1 or 2");
+  TTS_CHECK(a.ntj * 2 <= PW && a.ntj >= 17, "persistent decoder: projection job count");
+  TTS_CHECK(a.nchmax * PTC >= a.D.T_max, "persistent decoder: attention partial buffers too small");
+  TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
+  const void* f = MT == 1 ? (const void*)persist_decoder_kernel<1> : (const void*)persist_decoder_kernel<2>;
+  static bool attr[3] = {false, false, false};
+  if (!attr[MT]) {
+    HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
+    attr[MT] = true;
+  }
+  HIP_OK(hipMemsetAsync(a.bar, 0, 512 * 4, s));
+  PArgs copy = a;
+  void* kargs[] = {&copy};
+  HIP_OK(hipLaunchCooperativeKernel(f, dim3(PW), dim3(PT), kargs, P_LDS, s));
+}
