@@ -6,8 +6,8 @@ import sys
 import numpy as np
 
 raw = np.fromfile(sys.argv[1], dtype=np.uint64).astype(np.int64)
-a = raw[:8 * 10 * 256].reshape(8, 10, 256)
-at = raw[8 * 10 * 256:].reshape(8, 256, 8) if raw.size > 8 * 10 * 256 else None
+a = raw[:8 * 16 * 256].reshape(8, 16, 256)
+at = raw[8 * 16 * 256:].reshape(8, 256, 8) if raw.size > 8 * 16 * 256 else None
 names = ["P1 stop+prenet2", "P3 attLSTM+pq", "P4 attention", "P5 decLSTM", "P6 attpre+proj"]
 rows = []
 for s in range(7):  # the next step's stamp 0 closes the last barrier
@@ -28,6 +28,9 @@ for k in range(5):
     print(f"{names[k]:18s} {med[k,0]:12.2f} {med[k,1]:10.2f} {med[k,2]:8.2f} {med[k,3]:12.2f}")
 step = np.median([(a[s + 1][0].min() - a[s][0].min()) / 100.0 for s in range(7)])
 print(f"step {step:.2f} us")
+sub = [np.median([(a[s][k] - a[s][6]).astype(float) / 100.0 for s in range(7)]) for k in (10, 11, 12, 13, 7)]
+print("P5 inside (median WG, us after release): dec MFMA %.2f, dec epilogue %.2f, att-pre MFMA %.2f, "
+      "att-pre epilogue %.2f, prefetch/arrive %.2f" % tuple(sub))
 
 if at is not None:
     # attention items: stamps 0 start (after loads), 1 query summed, 2 location conv, 3 energies,

@@ -499,7 +499,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.enc, (size_t)B * T_max * 512, g);
   grow<float>(W.penc, (size_t)B * T_max * 128, g);
   grow<float>(W.p1, (size_t)Bp * 256, g);
-  grow<float>(W.pb, (size_t)Bp * 256, g);
+  grow<float>(W.pb, (size_t)2 * 64 * 256, g);  // persistent decoder: two K halves of prenet layer 2
   grow<float>(W.gatt, (size_t)Bp * 4096, g);
   grow<float>(W.hatt, (size_t)Bp * 1024, g);
   grow<float>(W.catt, (size_t)Bp * 1024, g);
@@ -896,10 +896,10 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   static DevBuf trace_buf;
   const char* tr = std::getenv("TTS_PTRACE");
   if (tr) {
-    trace_buf.ensure((size_t)8 * 18 * 256 * 8);
-    HIP_OK(hipMemsetAsync(trace_buf.p, 0, (size_t)8 * 18 * 256 * 8, s));
+    trace_buf.ensure((size_t)8 * 24 * 256 * 8);
+    HIP_OK(hipMemsetAsync(trace_buf.p, 0, (size_t)8 * 24 * 256 * 8, s));
     a.trace = static_cast<unsigned long long*>(trace_buf.p);
-    a.atrace = a.trace + (size_t)8 * 10 * 256;
+    a.atrace = a.trace + (size_t)8 * 16 * 256;
     const char* t0 = std::getenv("TTS_PTRACE_T0");
     a.trace_t0 = t0 ? std::atoi(t0) : 100;
   }
@@ -910,7 +910,7 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     launch_persist_decoder(a, mt, s);
     if (tr) {  // only the first launch is traced
       HIP_OK(hipStreamSynchronize(s));
-      std::vector<unsigned long long> h((size_t)8 * 18 * 256);
+      std::vector<unsigned long long> h((size_t)8 * 24 * 256);
       HIP_OK(hipMemcpy(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost));
       if (FILE* fp = std::fopen(tr, "wb")) {
         std::fwrite(h.data(), 8, h.size(), fp);

@@ -39,7 +39,7 @@ constexpr int DEC_NC = 20;   // 160 k-chunks / 8 waves
 constexpr int APRE_NC = 12;  // 96 / 8
 constexpr int ATTP_NC = 4;   // 2 tiles x 16 chunks / 8 waves
 constexpr int PJ_NC = 6;     // 48 / 8
-constexpr int PRE2_NC = 2;   // 16 / 8
+constexpr int PB_HALF = 64 * 256;  // prenet-2 K halves (fragment order, 64 rows each)
 constexpr int PTC = 32;      // attention positions per work item
 constexpr int YROWS = 64;    // rows per projection half (independent of the batch tile: the MT = 1
                              // launch reads what the MT = 2 launch left)
@@ -179,119 +179,108 @@ template <int MT>
 __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
                                            int* is_last) {
   constexpr int NT = PT, TC = PTC;
-  constexpr int NG = NT / ADIM_;  // 4
-  constexpr int PPG = TC / NG;    // 8 positions per thread
-  constexpr int NPT = NPQ_ / 16;  // 8 query partials per thread (16 groups)
-  constexpr int AW = PPG + LOCK_ - 1;  // alpha window per group (38)
+  constexpr int NPT = NPQ_ / 16;  // 8 query partials per thread (16 groups of 8)
   constexpr int Bp = MT * 16;
+  static_assert(TC == 32 && NT == 512, "attention item geometry: 2 position tiles x 8 dim tiles");
   const DecDev& D = P.D;
   const int t0 = ch * TC;
   const int tid = opaque_v(threadIdx.x);
-  const int a = tid % ADIM_, grp = tid / ADIM_;
-  const int lane = tid & 63, wave = tid >> 6;
-  float* red = sm;                 // [16][ADIM] query-partial group sums
-  float* A0 = red + 16 * ADIM_;    // [TC + LOCK - 1] alpha window
-  float* A1 = A0 + TC + LOCK_;     // alpha_cum window
-  float* esum = A1 + TC + LOCK_;   // [8 waves][PPG] half-sums of the energies
-  float* sv = esum + 8 * PPG;      // [TC] energies
-  float* sw = sv + TC;             // [TC] normalised weights
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // attention dims 16 wave .. 16 wave + 15
+  const int a = 16 * wave + (lane & 15);                       // this lane's dim in the MFMA output
+  float* red = sm;              // [16][ADIM] query-partial group sums
+  float* Aw = red + 16 * ADIM_; // [2][64]: alpha / alpha_cum windows, alpha[t0 - 15 + q]
+  float* esum = Aw + 128;       // [8 waves][TC] partial energies
+  float* sv = esum + 8 * TC;    // [TC] energies
+  float* sw = sv + TC;          // [TC] normalised weights
   const int T = D.lens[b];
   const int Tm1 = max(T - 1, 0);
-  // ---- independent loads first (clamped indices); the query partials as 16-byte loads:
-  //      thread = (partial group pg of 8, dims 4*a4 .. 4*a4+3) ----
-  const int a4 = tid & 31, pg = tid >> 5;
+  // ---- independent loads first (clamped indices), in the order they are consumed: vmcnt is an
+  //      in-order counter, so waiting for an early load does not wait for the later ones ----
+  const int dn = ldci(D.done + b);
+  __builtin_amdgcn_sched_barrier(0);
+  const int a4 = tid & 31, pg = tid >> 5;  // query partials: 16-byte loads, dims 4 a4 .. 4 a4 + 3
   f32x4 pp[NPT];
 #pragma unroll
-  for (int i = 0; i < NPT; ++i) pp[i] = ldc4<ACT_AUX>(P.pq, ((((pg * 8 + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
-  float a0, a1;
+  for (int i = 0; i < NPT; ++i) pp[i] = ldc4(P.pq, ((((pg * 8 + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
+  float aw;
   {
-    const int pos = t0 - (LOCK_ - 1) / 2 + min(tid, TC + LOCK_ - 2);
+    const int q = tid & 63, ci = (tid >> 6) & 1;  // threads 0-127 fill the two windows
+    const int pos = t0 - (LOCK_ - 1) / 2 + q;
     const int pc = min(max(pos, 0), Tm1);
-    a0 = ldc(P.alpha + (long)b * D.T_max + pc);
-    a1 = ldc(P.acum + (long)b * D.T_max + pc);
-    if (pos < 0 || pos >= T) a0 = a1 = 0.f;
+    aw = ldc((ci ? P.acum : P.alpha) + (long)b * D.T_max + pc);
+    if (pos < 0 || pos >= T) aw = 0.f;
   }
-  float pen[PPG];
+  float pen[8];  // (position tile mt, row r) -> position 16 mt + 4 (lane >> 4) + r
 #pragma unroll
-  for (int i = 0; i < PPG; ++i) pen[i] = P.penc[((long)b * D.T_max + min(t0 + grp * PPG + i, Tm1)) * ADIM_ + a];
+  for (int i = 0; i < 8; ++i) {
+    const int pos = 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3);
+    pen[i] = P.penc[((long)b * D.T_max + min(t0 + pos, Tm1)) * ADIM_ + a];
+  }
   const float va = P.v[a];
-  const int dn = ldci(D.done + b);
+  __builtin_amdgcn_sched_barrier(0);
   __builtin_amdgcn_sched_barrier(0);
   ATRACE(0);
   if (t0 >= T || dn) return;  // workgroup-uniform
-  if (tid < TC + LOCK_ - 1) {
-    A0[tid] = a0;
-    A1[tid] = a1;
-  }
+  if (tid < 128) Aw[tid] = aw;
   {
     f32x4 s4 = pp[0];
 #pragma unroll
     for (int i = 1; i < NPT; ++i) s4 += pp[i];
     *reinterpret_cast<f32x4*>(&red[pg * ADIM_ + 4 * a4]) = s4;
   }
-  // encoder rows for the partial context, in flight during the energy computation
-  float ev[TC];
-#pragma unroll
-  for (int i = 0; i < TC; ++i) ev[i] = P.enc[((long)b * D.T_max + min(t0 + i, Tm1)) * 512 + tid];
-  __builtin_amdgcn_sched_barrier(0);
   lds_barrier();
   ATRACE(1);
+  // encoder rows for the partial context (row offsets in SGPRs, one buffer load each), issued
+  // once the first batch of loads has drained; consumed after the energies
+  float ev[TC];
+  {
+    const __amdgpu_buffer_rsrc_t er =
+        __builtin_amdgcn_make_buffer_rsrc((void*)(P.enc + (long)b * D.T_max * 512), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int i = 0; i < TC; ++i)
+      ev[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
+          er, tid * 4, __builtin_amdgcn_readfirstlane(min(t0 + i, Tm1) * 2048), 0));
+  }
   float pqa = red[a];
 #pragma unroll
   for (int g = 1; g < 16; ++g) pqa += red[g * ADIM_ + a];
-  // fused location filter for positions grp*PPG + p, p < PPG
-  float l[PPG];
+  // location_dense(location_conv(.)) on MFMA: E[pos][dim] = sum_j X[pos][j] Wcomb[j][dim],
+  // X[pos][ci*31 + k] = window_ci[pos + k]; K = 62 taps padded to 64 (Wcomb rows 62, 63 are 0)
+  f32x4 le[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
 #pragma unroll
-  for (int p = 0; p < PPG; ++p) l[p] = 0.f;
+  for (int st = 0; st < 16; ++st) {
+    const int j = 4 * st + (lane >> 4);
+    const int ci = j >= LOCK_ ? 1 : 0;
+    const int k = j - LOCK_ * ci;
+    const bool valid = j < 2 * LOCK_;
+    const float w = wcomb[j * ADIM_ + a];
 #pragma unroll
-  for (int ci = 0; ci < 2; ++ci) {
-    const float* Ai = (ci ? A1 : A0) + grp * PPG;
-    float win[PPG];  // sliding window: one new alpha value per tap
-#pragma unroll
-    for (int p = 0; p < PPG; ++p) win[p] = Ai[p];
-    // taps in groups of 8 (a fully unrolled 31-tap loop hoisted every weight read and ran the
-    // kernel out of VGPRs)
-#pragma unroll 1
-    for (int k0 = 0; k0 < LOCK_; k0 += 8) {
-#pragma unroll
-      for (int kk = 0; kk < 8; ++kk) {
-        const int k = min(k0 + kk, LOCK_ - 1);
-        const float w = k0 + kk < LOCK_ ? wcomb[(ci * LOCK_ + k) * ADIM_ + a] : 0.f;
-#pragma unroll
-        for (int p = 0; p < PPG; ++p) l[p] = fmaf(w, win[p], l[p]);
-#pragma unroll
-        for (int p = 0; p + 1 < PPG; ++p) win[p] = win[p + 1];
-        win[PPG - 1] = Ai[min(k + PPG, AW - 1)];
-      }
+    for (int mt = 0; mt < 2; ++mt) {
+      const float x = valid ? Aw[ci * 64 + 16 * mt + (lane & 15) + k] : 0.f;
+      le[mt] = MFMA16(x, w, le[mt]);
     }
   }
   ATRACE(2);
-  // e = v . tanh(pq + loc + penc): per position, a wave sums its 64 dims, LDS joins the two waves
-  float z[PPG];
+  // e = v . tanh(pq + loc + penc): the 16 dims of a DPP row summed in registers, the 8 waves
+  // (dim tiles) through LDS
+  {
+    float z[8];
 #pragma unroll
-  for (int p = 0; p < PPG; ++p) z[p] = tanhf(pqa + l[p] + pen[p]) * va;
-#ifdef NO_DPP
+    for (int i = 0; i < 8; ++i) z[i] = row16_sum(tanhf(pqa + le[i >> 2][i & 3] + pen[i]) * va);
+    if ((lane & 15) == 0) {
 #pragma unroll
-  for (int off = 32; off > 0; off >>= 1)
-#pragma unroll
-    for (int p = 0; p < PPG; ++p) z[p] += __shfl_xor(z[p], off, 64);
-#else
-#pragma unroll
-  for (int p = 0; p < PPG; ++p) z[p] = wave64_sum(z[p]);
-#endif
-  if (lane < PPG) {
-    float zz = z[0];
-#pragma unroll
-    for (int p = 1; p < PPG; ++p) zz = lane == p ? z[p] : zz;
-    esum[wave * PPG + lane] = zz;
+      for (int i = 0; i < 8; ++i) esum[wave * TC + 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3)] = z[i];
+    }
   }
   lds_barrier();
   ATRACE(3);
   const int nvalid = min(TC, T - t0);
   const long pidx = (long)b * P.nchmax + ch;
-  if (tid < TC) {  // position tid: group tid / PPG = waves 2g, 2g+1
-    const int gq = tid / PPG, p = tid % PPG;
-    const float e = esum[(2 * gq) * PPG + p] + esum[(2 * gq + 1) * PPG + p] + P.bv;
+  if (tid < TC) {
+    float e = P.bv;
+#pragma unroll
+    for (int w = 0; w < 8; ++w) e += esum[w * TC + tid];
     if (tid < nvalid) stc(P.energy + (long)b * D.T_max + t0 + tid, e);
     sv[tid] = e;
   }
@@ -387,10 +376,11 @@ constexpr size_t P_LDS_WC = 64 * 128 * 4;
 constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 8 * 4;  // >= attention scratch (~2.4K floats)
 constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
 
-// phase timestamps of every workgroup for 8 steps (P.trace, optional): [step][10][256]
+// phase timestamps of every workgroup for 8 steps (P.trace, optional): [step][16][256]
+// (0-9 phase boundaries, 10-15 points inside P5)
 #define PTRACE(k)                                                                              \
   if (P.trace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                          \
-  P.trace[((long)(t - P.trace_t0) * 10 + (k)) * PW + blockIdx.x] = __builtin_amdgcn_s_memrealtime()
+  P.trace[((long)(t - P.trace_t0) * 16 + (k)) * PW + blockIdx.x] = __builtin_amdgcn_s_memrealtime()
 
 template <int MT>
 __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
@@ -432,14 +422,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   int t = D.ctl->base;
   const int pj_jobs = 2 * P.ntj;
   // per-phase weights, loaded before the barrier that precedes their phase
-  f32x4 w2[PRE2_NC];
-  auto load_w2 = [&]() {
-    const int tl = min(g, 15);
-    const f32x4* src = reinterpret_cast<const f32x4*>(P.pre2_w) + ((long)tl * 16 + wave * PRE2_NC) * 64 + lane;
-#pragma unroll
-    for (int i = 0; i < PRE2_NC; ++i) w2[i] = src[(long)i * 64];
-  };
-  load_w2();
+  // prenet layer-2 weight chunk of this wave (workgroups 0-31: tile g & 15, k-chunk 8 (g >> 4) + wave)
+  const f32x4 w2 = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + 8 * ((g >> 4) & 1) + wave) * 64 + lane];
 
   // frames of step s (< S_cap) from the two projection halves (K5 frame store of decoder.hip):
   // written when the row was still decoding at step s, i.e. not done or done later than s
@@ -459,38 +443,37 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 
   for (;; ++t) {
     PTRACE(0);
-    // ======== P1: stop(t-1) || prenet layer 2 ========
+    // ======== P1: prenet layer 2 halves (workgroups 0-31) || stop(t-1) (workgroup 255) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (g < 16) {
+    if (g < 32) {  // prenet layer 2, tile g & 15, K half g >> 4 (one k-chunk per wave)
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (t > 0) {  // t = 0: prenet input is the zero go-frame, layer 1 has no bias -> 0
+        const int kc = 8 * (g >> 4) + wave;
+        const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
+        const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pj_b + col);
 #pragma unroll
-        for (int i = 0; i < PRE2_NC; ++i) {
-          const int kc = wave * PRE2_NC + i;
-          const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pj_b + col);
+        for (int mt = 0; mt < MT; ++mt) {
+          const int m = mt * 16 + (lane & 15);
+          f32x4 x = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const int m = mt * 16 + (lane & 15);
-            f32x4 x = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
+          for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
 #pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
-#pragma unroll
-            for (int q = 0; q < 4; ++q) acc[mt] = MFMA16(x[q], w2[i][q], acc[mt]);
-          }
+          for (int q = 0; q < 4; ++q) acc[mt] = MFMA16(x[q], w2[q], acc[mt]);
         }
       }
       acc_to_lds<MT>(red0, wave, lane, acc);
-      __syncthreads();
+      lds_barrier();
       for (int idx = tid; idx < Bp * 16; idx += PT) {
         const int m = idx >> 4, n = idx & 15;
-        stc(P.pb + frag_idx(m, g * 16 + n, 256), fmaxf(lds_sum<NWV, Bp>(red0, m, n), 0.f));
+        stc(P.pb + (g >> 4) * PB_HALF + frag_idx(m, (g & 15) * 16 + n, 256), lds_sum<NWV, Bp>(red0, m, n));
       }
-    } else if (g == PW - 1) {
+      lds_barrier();
+    }
+    if (g == PW - 1) {
       if (tid < D.B) {
         const int m = tid;
         int dn = ldci(D.done + m);
@@ -508,7 +491,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         }
         dflag[m] = dn;
       }
-      __syncthreads();
+      lds_barrier();
       if (tid == 0) {
         int last = -1;
         for (int k = 0; k < D.B; ++k)
@@ -519,7 +502,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     }
     PTRACE(1);
     gsync_arrive(P.bar, gen);
-    // P3 operands that are already final: its epilogue's gate addends (written by P6 of the
+    // P3 operands that are already final: its epilogue's gate addends (written by P5 of the
     // previous step), c_att, the query-projection weights
     float ga[4], ca, wq[8];
     {
@@ -563,7 +546,13 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
       for (int i = 0; i < ATTP_NC; ++i)
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) x[i][mt] = ldc4(P.pb, ((mt * 16 + 4 * (wave & 3) + i) * 64 + lane) * 16);
+        for (int mt = 0; mt < MT; ++mt) {
+          const int off = ((mt * 16 + 4 * (wave & 3) + i) * 64 + lane) * 16;
+          x[i][mt] = ldc4(P.pb, off) + ldc4(P.pb, off + PB_HALF * 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[i][mt][q] = fmaxf(x[i][mt][q], 0.f);
+        }
+
 #pragma unroll
       for (int i = 0; i < ATTP_NC; ++i)
 #pragma unroll
@@ -572,7 +561,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[i][mt][q], wa[i][q], acc[mt]);
       // waves 0-3: tile 2g, waves 4-7: tile 2g+1
       acc_to_lds<MT>(red0 + (wave >> 2) * 4 * Bp * 17, wave & 3, lane, acc);
-      __syncthreads();
+      lds_barrier();
       if (tid < 2 * Bp * 4) {
         const int gl = tid / (Bp * 4), rem = tid % (Bp * 4);
         const int m = rem >> 2, u = rem & 3;
@@ -580,21 +569,15 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         const float* pg = red0 + gl * 4 * Bp * 17;
         float pre[4];
 #pragma unroll
-#ifdef NO_PREF
-        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<4, Bp>(pg, m, q * 4 + u) + ldc(P.gatt + (long)m * 4096 + tile * 16 + q * 4 + u);
-        const long ci = (long)m * 1024 + tile * 4 + u;
-        const float c = sigm(pre[1]) * P.catt[ci] + sigm(pre[0]) * tanhf(pre[2]);
-#else
         for (int q = 0; q < 4; ++q) pre[q] = lds_sum<4, Bp>(pg, m, q * 4 + u) + ga[q];
         const long ci = (long)m * 1024 + tile * 4 + u;
         const float c = sigm(pre[1]) * ca + sigm(pre[0]) * tanhf(pre[2]);
-#endif
         const float h = sigm(pre[3]) * tanhf(c);
         P.catt[ci] = c;
         stc(P.hatt + frag_idx(m, tile * 4 + u, 1024), h);
         hs[m * 8 + gl * 4 + u] = h;
       }
-      __syncthreads();
+      lds_barrier();
       {  // partial query projection over this workgroup's 8 units
         const int a = tid & 127;
         for (int m = tid >> 7; m < Bp; m += PT / 128) {
@@ -625,7 +608,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     const float cd = P.cdec[(long)min(tid >> 2, Bp - 1) * 1024 + g * 4 + (tid & 3)];
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(6);
-    // ======== P5: decoder_rnn (tile g, K = [h_att 1024 | ctx 512 | h_dec 1024]) ========
+    // ======== P5: decoder_rnn (tile g, K = [h_att 1024 | ctx 512 | h_dec 1024], VGPR weights)
+    //            + next step's attention_rnn ctx/h part (tile g, LDS weights) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
@@ -667,72 +651,24 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
             for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[cur][i][mt][q], wd[i0 + i][q], acc[mt]);
         __builtin_amdgcn_sched_barrier(0);
       }
+      PTRACE(10);
       acc_to_lds<MT>(red0, wave, lane, acc);
-      __syncthreads();
+      lds_barrier();
       if (tid < Bp * 4) {
         const int m = tid >> 2, u = tid & 3;
         float pre[4];
 #pragma unroll
         for (int q = 0; q < 4; ++q) pre[q] = lds_sum<NWV, Bp>(red0, m, q * 4 + u) + db[q];
         const long ci = (long)m * 1024 + g * 4 + u;
-#ifdef NO_PREF
-        const float c = sigm(pre[1]) * P.cdec[ci] + sigm(pre[0]) * tanhf(pre[2]);
-#else
         const float c = sigm(pre[1]) * cd + sigm(pre[0]) * tanhf(pre[2]);
-#endif
         const float h = sigm(pre[3]) * tanhf(c);
         P.cdec[ci] = c;
         stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
       }
     }
-    PTRACE(7);
-    gsync_arrive(P.bar, gen);
-    // projection weights for P6 (half `g & 1` of job tile `g >> 1`, 6 k-chunks per wave)
-    f32x4 wp[PJ_NC];
-    {
-      const int q = min(g >> 1, P.ntj - 1), half = g & 1;
-      const f32x4* src = reinterpret_cast<const f32x4*>(P.pj_w) + ((long)q * 96 + 48 * half + wave * PJ_NC) * 64 + lane;
-#pragma unroll
-      for (int i = 0; i < PJ_NC; ++i) wp[i] = src[(long)i * 64];
-    }
-    if (!gsync_wait(P.bar, gen, &sflag)) return;
-    PTRACE(8);
-    // ======== P6: projection halves || attention_rnn ctx/h part (tile g, LDS weights) ========
-    tid = opaque_v(tid0);
-    lane = opaque_v(lane0);
-    wave = opaque_s(wave0);
-    {
-      const bool pj = g < pj_jobs;
-      if (pj) {
-        f32x4 acc2[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int kb = 48 * (g & 1) + wave * PJ_NC;  // K = [h_dec 1024 | ctx 512]
-        f32x4 y[PJ_NC][MT];
-#pragma unroll
-        for (int i = 0; i < PJ_NC; ++i) {
-          const int kc = kb + i;
-          const float* base = kc < 64 ? hd_nxt : P.ctx;
-          const int kl = kc < 64 ? kc : kc - 64;
-          const int nk = kc < 64 ? 64 : 32;
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) y[i][mt] = ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < PJ_NC; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
-        acc_to_lds<MT>(red0, wave, lane, acc2);
-        __syncthreads();
-        for (int idx = tid; idx < Bp * 16; idx += PT) {
-          const int m = idx >> 4, n = idx & 15;
-          stc(P.ypart + (long)((g & 1) * YROWS + m) * YP + (g >> 1) * 16 + n, lds_sum<NWV, Bp>(red0, m, n));
-        }
-        __syncthreads();
-      }
-      __builtin_amdgcn_sched_barrier(0);
+    PTRACE(11);
+    {  // next step's attention_rnn ctx/h part of tile g (+ biases): ctx from P4, h_att from P3
+      lds_barrier();  // red0 reuse (the h_dec stores keep draining)
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -769,16 +705,65 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         }
         __builtin_amdgcn_sched_barrier(0);
       }
+      PTRACE(12);
       acc_to_lds<MT>(red0, wave, lane, acc);
-      __syncthreads();
+      lds_barrier();
       for (int idx = tid; idx < Bp * 16; idx += PT) {
         const int m = idx >> 4, n = idx & 15;
         stc(P.gatt + (long)m * 4096 + g * 16 + n, lds_sum<NWV, Bp>(red0, m, n) + apb);
       }
     }
+    PTRACE(13);
+    PTRACE(7);
+    gsync_arrive(P.bar, gen);
+    // projection weights for P6 (half `g & 1` of job tile `g >> 1`, 6 k-chunks per wave)
+    f32x4 wp[PJ_NC];
+    {
+      const int q = min(g >> 1, P.ntj - 1), half = g & 1;
+      const f32x4* src = reinterpret_cast<const f32x4*>(P.pj_w) + ((long)q * 96 + 48 * half + wave * PJ_NC) * 64 + lane;
+#pragma unroll
+      for (int i = 0; i < PJ_NC; ++i) wp[i] = src[(long)i * 64];
+    }
+    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    PTRACE(8);
+    // ======== P6: projection halves (workgroups 0 .. 2*ntj-1) ========
+    tid = opaque_v(tid0);
+    lane = opaque_v(lane0);
+    wave = opaque_s(wave0);
+    {
+      const bool pj = g < pj_jobs;
+      if (pj) {
+        f32x4 acc2[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        const int kb = 48 * (g & 1) + wave * PJ_NC;  // K = [h_dec 1024 | ctx 512]
+        f32x4 y[PJ_NC][MT];
+#pragma unroll
+        for (int i = 0; i < PJ_NC; ++i) {
+          const int kc = kb + i;
+          const float* base = kc < 64 ? hd_nxt : P.ctx;
+          const int kl = kc < 64 ? kc : kc - 64;
+          const int nk = kc < 64 ? 64 : 32;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) y[i][mt] = ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < PJ_NC; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
+        acc_to_lds<MT>(red0, wave, lane, acc2);
+        lds_barrier();
+        for (int idx = tid; idx < Bp * 16; idx += PT) {
+          const int m = idx >> 4, n = idx & 15;
+          stc(P.ypart + (long)((g & 1) * YROWS + m) * YP + (g >> 1) * 16 + n, lds_sum<NWV, Bp>(red0, m, n));
+        }
+        lds_barrier();
+      }
+    }
     PTRACE(9);
     gsync_arrive(P.bar, gen);
-    load_w2();
     if (!gsync_wait(P.bar, gen, &sflag)) return;
   }
 }
