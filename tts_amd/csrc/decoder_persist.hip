@@ -36,10 +36,10 @@
 namespace {
 constexpr int PW = 256, PT = 512, NWV = 8;
 constexpr int DEC_NC = 20;   // 160 k-chunks / 8 waves
-constexpr int APRE_NC = 12;  // 96 / 8
 constexpr int ATTP_NC = 4;   // 2 tiles x 16 chunks / 8 waves
 constexpr int PJ_NC = 6;     // 48 / 8
 constexpr int PB_HALF = 64 * 256;  // prenet-2 K halves (fragment order, 64 rows each)
+constexpr int PJ_WG0 = 128;        // first projection workgroup (P6; idle in P3 apart from frames)
 constexpr int PTC = 32;      // attention positions per work item
 constexpr int YROWS = 64;    // rows per projection half (independent of the batch tile: the MT = 1
                              // launch reads what the MT = 2 launch left)
@@ -175,9 +175,9 @@ __device__ __forceinline__ float wave64_sum(float v) {
   if (P.atrace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                         \
   P.atrace[(((long)(t - P.trace_t0) * PW + b * P.nchmax + ch) * 8) + (k)] = __builtin_amdgcn_s_memrealtime()
 
-template <int MT>
+template <int MT, class GAP>
 __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
-                                           int* is_last) {
+                                           int* is_last, GAP&& gap) {
   constexpr int NT = PT, TC = PTC;
   constexpr int NPT = NPQ_ / 16;  // 8 query partials per thread (16 groups of 8)
   constexpr int Bp = MT * 16;
@@ -219,6 +219,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   }
   const float va = P.v[a];
   __builtin_amdgcn_sched_barrier(0);
+  gap();  // independent MFMA work while the loads are in flight
   __builtin_amdgcn_sched_barrier(0);
   ATRACE(0);
   if (t0 >= T || dn) return;  // workgroup-uniform
@@ -369,6 +370,41 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   if (tid == 0) __hip_atomic_store(&P.counter[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+
+// acc[MT] += act[:, chunks kc0 .. kc0+NC) . W^T for one fragment-order activation with nk 16-column
+// chunks; wf(i) gives the weight fragment of local chunk i (registers or LDS). Activation loads
+// run G chunks ahead (two register stages).
+template <int MT, int NC, int G, class WF>
+__device__ __forceinline__ void gemm_seg(f32x4 (&acc)[MT], const float* base, int nk, int kc0, int lane, WF wf) {
+  static_assert(NC % G == 0, "chunk groups");
+  auto ld = [&](int kc, int mt) { return ldc4<ACT_AUX>(base, ((mt * nk + kc) * 64 + lane) * 16); };
+  f32x4 x[2][G][MT];
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) x[0][i][mt] = ld(kc0 + i, mt);
+#pragma unroll
+  for (int i0 = 0; i0 < NC; i0 += G) {
+    const int cur = (i0 / G) & 1;
+    if (i0 + G < NC) {
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) x[cur ^ 1][i][mt] = ld(kc0 + i0 + G + i, mt);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const f32x4 w = wf(i0 + i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[cur][i][mt][q], w[q], acc[mt]);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // ------------------------------------------------------------------ the persistent kernel
 // LDS: [att-pre weights 96 x 1 KiB][Wcomb 64 x 128][scratch: GEMM reduction + hs | attention]
 constexpr size_t P_LDS_APRE = 96 * 64 * 16;
@@ -404,11 +440,18 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     for (int i = tid; i < 96 * 64; i += PT) Wap[i] = src[i];
     for (int i = tid; i < 64 * 128; i += PT) wcomb[i] = P.Wcomb[i];
   }
+  // decoder_rnn weights of this wave: K = [h_att 64 chunks | ctx 32 | h_dec 64]; wave w keeps
+  // h_att chunks 8w..8w+7 (wd[0..7]), ctx chunks 4w..4w+3 (wd[8..11]), h_dec chunks 8w..8w+7
+  // (wd[12..19]), so that each part can run in the phase where its input becomes final
   f32x4 wd[DEC_NC];
   {
-    const f32x4* src = reinterpret_cast<const f32x4*>(P.dec_w) + ((long)g * 160 + wave * DEC_NC) * 64 + lane;
+    const f32x4* src = reinterpret_cast<const f32x4*>(P.dec_w) + (long)g * 160 * 64 + lane;
 #pragma unroll
-    for (int i = 0; i < DEC_NC; ++i) wd[i] = src[(long)i * 64];
+    for (int i = 0; i < 8; ++i) wd[i] = src[(long)(8 * wave + i) * 64];
+#pragma unroll
+    for (int i = 0; i < 4; ++i) wd[8 + i] = src[(long)(64 + 4 * wave + i) * 64];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) wd[12 + i] = src[(long)(96 + 8 * wave + i) * 64];
   }
   // epilogue constants: decoder_rnn biases of this thread's (row, unit) item, attention_rnn
   // ctx/h-part bias of its column
@@ -419,11 +462,22 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   __syncthreads();
 
   unsigned gen = 0;
-  int t = D.ctl->base;
+  const int t_first = D.ctl->base;
+  int t = t_first;
   const int pj_jobs = 2 * P.ntj;
-  // per-phase weights, loaded before the barrier that precedes their phase
+  const int pj = g - PJ_WG0;  // projection job of this workgroup (P6), if 0 <= pj < pj_jobs
+  const bool is_pj = pj >= 0 && pj < pj_jobs;
   // prenet layer-2 weight chunk of this wave (workgroups 0-31: tile g & 15, k-chunk 8 (g >> 4) + wave)
   const f32x4 w2 = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + 8 * ((g >> 4) & 1) + wave) * 64 + lane];
+  // partial sums of this workgroup's decoder_rnn tile (accd) and attention_rnn ctx/h tile (acca),
+  // accumulated across phases: h_dec part in P6 of the previous step (P3 for projection
+  // workgroups, P1 on a launch's first step), h_att parts in P4, ctx parts in P5
+  f32x4 accd[MT], acca[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) accd[mt] = acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto dec_hdec_part = [&](const float* hd) {
+    gemm_seg<MT, 8, 4>(accd, hd, 64, 8 * wave, lane, [&](int i) { return wd[12 + i]; });
+  };
 
   // frames of step s (< S_cap) from the two projection halves (K5 frame store of decoder.hip):
   // written when the row was still decoding at step s, i.e. not done or done later than s
@@ -443,10 +497,13 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 
   for (;; ++t) {
     PTRACE(0);
+    float* hd_cur = (t & 1) ? P.hdec1 : P.hdec0;
+    float* hd_nxt = (t & 1) ? P.hdec0 : P.hdec1;
     // ======== P1: prenet layer 2 halves (workgroups 0-31) || stop(t-1) (workgroup 255) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
+    if (t == t_first) dec_hdec_part(hd_cur);
     if (g < 32) {  // prenet layer 2, tile g & 15, K half g >> 4 (one k-chunk per wave)
       f32x4 acc[MT];
 #pragma unroll
@@ -534,7 +591,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         return;
       }
     }
-    // ======== P3: attention_rnn (prenet part) + cell + query partials || frames(t-1) ========
+    // ======== P3: attention_rnn (prenet part) + cell + query partials (workgroups 0-127)
+    //            || frames(t-1) + the h_dec part for projection workgroups (128-255) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
@@ -552,7 +610,6 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
           for (int q = 0; q < 4; ++q) x[i][mt][q] = fmaxf(x[i][mt][q], 0.f);
         }
-
 #pragma unroll
       for (int i = 0; i < ATTP_NC; ++i)
 #pragma unroll
@@ -588,17 +645,29 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         }
       }
     } else {
+      if (is_pj && t != t_first) dec_hdec_part(hd_cur);
       write_frames(t - 1, 128, PW - 128);
     }
     PTRACE(3);
     gsync_arrive(P.bar, gen);
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(4);
-    // ======== P4: attention ========
+    // ======== P4: attention || the h_att parts of decoder_rnn and attention_rnn ========
+    tid = opaque_v(tid0);
+    lane = opaque_v(lane0);
+    wave = opaque_s(wave0);
     {
+      // run while the attention loads are in flight (or alone when this workgroup has no item)
+      auto hatt_parts = [&]() {
+        gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
+        gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane,
+                           [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
+      };
       const int nitems = D.B * P.nchmax;
+      if (g >= nitems) hatt_parts();
       for (int it = g; it < nitems; it += PW) {
-        pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last);
+        if (it == g) pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, hatt_parts);
+        else pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, [] {});
         lds_barrier();
       }
     }
@@ -608,51 +677,17 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     const float cd = P.cdec[(long)min(tid >> 2, Bp - 1) * 1024 + g * 4 + (tid & 3)];
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(6);
-    // ======== P5: decoder_rnn (tile g, K = [h_att 1024 | ctx 512 | h_dec 1024], VGPR weights)
-    //            + next step's attention_rnn ctx/h part (tile g, LDS weights) ========
+    // ======== P5: ctx parts, then the decoder_rnn cell (tile g) and the next step's
+    //            attention_rnn ctx/h part (tile g, + biases) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    float* hd_cur = (t & 1) ? P.hdec1 : P.hdec0;
-    float* hd_nxt = (t & 1) ? P.hdec0 : P.hdec1;
     {
-      f32x4 acc[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      auto ld = [&](int kc, int mt) {
-        // wave-uniform segment select
-        const float* base = kc < 64 ? P.hatt : kc < 96 ? P.ctx : hd_cur;
-        const int kl = kc < 64 ? kc : kc < 96 ? kc - 64 : kc - 96;
-        const int nk = kc < 64 ? 64 : kc < 96 ? 32 : 64;
-        return ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
-      };
-      constexpr int G = 4;
-      f32x4 x[2][G][MT];
-      const int kc0 = wave * DEC_NC;
-#pragma unroll
-      for (int i = 0; i < G; ++i)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) x[0][i][mt] = ld(kc0 + i, mt);
-#pragma unroll
-      for (int i0 = 0; i0 < DEC_NC; i0 += G) {
-        const int cur = (i0 / G) & 1;
-        if (i0 + G < DEC_NC) {
-#pragma unroll
-          for (int i = 0; i < G; ++i)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) x[cur ^ 1][i][mt] = ld(kc0 + i0 + G + i, mt);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < G; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[cur][i][mt][q], wd[i0 + i][q], acc[mt]);
-        __builtin_amdgcn_sched_barrier(0);
-      }
+      gemm_seg<MT, 4, 4>(accd, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; });
+      gemm_seg<MT, 4, 4>(acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return Wap[(4 * wave + i) * 64 + lane]; });
       PTRACE(10);
-      acc_to_lds<MT>(red0, wave, lane, acc);
+      float* red1 = red0;  // two reductions back to back: [2][8][Bp][17] would not fit; reuse
+      acc_to_lds<MT>(red0, wave, lane, accd);
       lds_barrier();
       if (tid < Bp * 4) {
         const int m = tid >> 2, u = tid & 3;
@@ -665,102 +700,65 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         P.cdec[ci] = c;
         stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
       }
-    }
-    PTRACE(11);
-    {  // next step's attention_rnn ctx/h part of tile g (+ biases): ctx from P4, h_att from P3
-      lds_barrier();  // red0 reuse (the h_dec stores keep draining)
-      f32x4 acc[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      const int kc0 = wave * APRE_NC;  // K = [ctx 512 | h_att 1024]
-      auto ld = [&](int kc, int mt) {
-        const float* base = kc < 32 ? P.ctx : P.hatt;
-        const int kl = kc < 32 ? kc : kc - 32;
-        const int nk = kc < 32 ? 32 : 64;
-        return ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
-      };
-      constexpr int G = 4;
-      f32x4 x[2][G][MT];
-#pragma unroll
-      for (int i = 0; i < G; ++i)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) x[0][i][mt] = ld(kc0 + i, mt);
-#pragma unroll
-      for (int i0 = 0; i0 < APRE_NC; i0 += G) {
-        const int cur = (i0 / G) & 1;
-        if (i0 + G < APRE_NC) {
-#pragma unroll
-          for (int i = 0; i < G; ++i)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) x[cur ^ 1][i][mt] = ld(kc0 + i0 + G + i, mt);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int i = 0; i < G; ++i) {
-          const f32x4 w = Wap[(kc0 + i0 + i) * 64 + lane];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[cur][i][mt][q], w[q], acc[mt]);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-      }
-      PTRACE(12);
-      acc_to_lds<MT>(red0, wave, lane, acc);
+      PTRACE(11);
       lds_barrier();
+      acc_to_lds<MT>(red1, wave, lane, acca);
+      lds_barrier();
+      PTRACE(12);
       for (int idx = tid; idx < Bp * 16; idx += PT) {
         const int m = idx >> 4, n = idx & 15;
-        stc(P.gatt + (long)m * 4096 + g * 16 + n, lds_sum<NWV, Bp>(red0, m, n) + apb);
+        stc(P.gatt + (long)m * 4096 + g * 16 + n, lds_sum<NWV, Bp>(red1, m, n) + apb);
       }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) accd[mt] = acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     PTRACE(13);
     PTRACE(7);
     gsync_arrive(P.bar, gen);
-    // projection weights for P6 (half `g & 1` of job tile `g >> 1`, 6 k-chunks per wave)
+    // projection weights for P6 (half pj & 1 of job tile pj >> 1, 6 k-chunks per wave)
     f32x4 wp[PJ_NC];
     {
-      const int q = min(g >> 1, P.ntj - 1), half = g & 1;
+      const int q = min(max(pj, 0) >> 1, P.ntj - 1), half = pj & 1;
       const f32x4* src = reinterpret_cast<const f32x4*>(P.pj_w) + ((long)q * 96 + 48 * half + wave * PJ_NC) * 64 + lane;
 #pragma unroll
       for (int i = 0; i < PJ_NC; ++i) wp[i] = src[(long)i * 64];
     }
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(8);
-    // ======== P6: projection halves (workgroups 0 .. 2*ntj-1) ========
+    // ======== P6: projection halves (workgroups PJ_WG0 ..) || the next step's h_dec part ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    {
-      const bool pj = g < pj_jobs;
-      if (pj) {
-        f32x4 acc2[MT];
+    if (is_pj) {
+      f32x4 acc2[MT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-        const int kb = 48 * (g & 1) + wave * PJ_NC;  // K = [h_dec 1024 | ctx 512]
-        f32x4 y[PJ_NC][MT];
+      for (int mt = 0; mt < MT; ++mt) acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      const int kb = 48 * (pj & 1) + wave * PJ_NC;  // K = [h_dec 1024 | ctx 512]
+      f32x4 y[PJ_NC][MT];
 #pragma unroll
-        for (int i = 0; i < PJ_NC; ++i) {
-          const int kc = kb + i;
-          const float* base = kc < 64 ? hd_nxt : P.ctx;
-          const int kl = kc < 64 ? kc : kc - 64;
-          const int nk = kc < 64 ? 64 : 32;
+      for (int i = 0; i < PJ_NC; ++i) {
+        const int kc = kb + i;
+        const float* base = kc < 64 ? hd_nxt : P.ctx;
+        const int kl = kc < 64 ? kc : kc - 64;
+        const int nk = kc < 64 ? 64 : 32;
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) y[i][mt] = ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
-        }
-#pragma unroll
-        for (int i = 0; i < PJ_NC; ++i)
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
-        acc_to_lds<MT>(red0, wave, lane, acc2);
-        lds_barrier();
-        for (int idx = tid; idx < Bp * 16; idx += PT) {
-          const int m = idx >> 4, n = idx & 15;
-          stc(P.ypart + (long)((g & 1) * YROWS + m) * YP + (g >> 1) * 16 + n, lds_sum<NWV, Bp>(red0, m, n));
-        }
-        lds_barrier();
+        for (int mt = 0; mt < MT; ++mt) y[i][mt] = ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
       }
+#pragma unroll
+      for (int i = 0; i < PJ_NC; ++i)
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
+      acc_to_lds<MT>(red0, wave, lane, acc2);
+      lds_barrier();
+      for (int idx = tid; idx < Bp * 16; idx += PT) {
+        const int m = idx >> 4, n = idx & 15;
+        stc(P.ypart + (long)((pj & 1) * YROWS + m) * YP + (pj >> 1) * 16 + n, lds_sum<NWV, Bp>(red0, m, n));
+      }
+      lds_barrier();
+    } else {
+      dec_hdec_part(hd_nxt);  // h_dec of step t+1
     }
     PTRACE(9);
     gsync_arrive(P.bar, gen);
@@ -780,7 +778,7 @@ int persist_attn_tc() { return PTC; }
 
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
   TTS_CHECK(MT == 1 || MT == 2, "persistent decoder: MT must be 1 or 2");
-  TTS_CHECK(a.ntj * 2 <= PW && a.ntj >= 17, "persistent decoder: projection job count");
+  TTS_CHECK(PJ_WG0 + a.ntj * 2 <= PW && a.ntj >= 17, "persistent decoder: projection job count");
   TTS_CHECK(a.nchmax * PTC >= a.D.T_max, "persistent decoder: attention partial buffers too small");
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
   const void* f = MT == 1 ? (const void*)persist_decoder_kernel<1> : (const void*)persist_decoder_kernel<2>;
