@@ -6,7 +6,7 @@ mkdir -p gpurun_out
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
 step() { local name=$1; shift; echo "== $name"; "$@"; local rc=$?; echo "== $name rc=$rc"; return $rc; }
-step tests timeout -k 10 400 python -m pytest tests -x -q -m gpu > gpurun_out/gpu_tests.log 2>&1 &&
+step tests timeout -k 10 400 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
 step smoke timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 step bench timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 &&
 step prof timeout -k 10 400 rocprofv3 --kernel-trace --stats -d gpurun_out/prof -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline > gpurun_out/prof.log 2>&1

@@ -32,6 +32,11 @@ sub = [np.median([(a[s][k] - a[s][6]).astype(float) / 100.0 for s in range(7)]) 
 print("P5 inside (median WG, us after release): dec MFMA %.2f, dec epilogue %.2f, att-pre MFMA %.2f, "
       "att-pre epilogue %.2f, prefetch/arrive %.2f" % tuple(sub))
 
+g14 = [np.median([(a[s][14] - a[s][4]).astype(float) / 100.0 for s in range(7) if a[s][14].min() > 0])
+       for _ in (0,)] if a[:, 14].min() > 0 else None
+if g14 is not None:
+    print("P4 GEMM waves done (median WG, us after release): %.2f" % g14[0])
+
 if at is not None:
     # attention items: stamps 0 start (after loads), 1 query summed, 2 location conv, 3 energies,
     # 4 energy reduction, 5 partials published, 6 ticket, 7 combine done (last arriver only)

@@ -5,6 +5,7 @@ The library is built in-tree (``tts_amd/libttship.so``, see ``tts_amd/csrc/Makef
 missing, every entry point raises ``RuntimeError``.
 """
 
+import atexit
 import ctypes
 import os
 import threading
@@ -193,3 +194,17 @@ def get_engine(device) -> Engine:
         with _lock:
             _engines[idx] = eng
     return eng
+
+
+@atexit.register
+def _close_engines():
+    """Destroy every context (graphs, streams, device buffers) before interpreter teardown, so the
+    HIP runtime and any attached tool (rocprofv3) never see leaked objects after finalisation."""
+    with _lock:
+        engines = list(_engines.values())
+        _engines.clear()
+    for eng in engines:
+        try:
+            eng.close()
+        except Exception:
+            pass

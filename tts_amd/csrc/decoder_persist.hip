@@ -41,6 +41,7 @@ constexpr int PJ_NC = 6;     // 48 / 8
 constexpr int PB_HALF = 64 * 256;  // prenet-2 K halves (fragment order, 64 rows each)
 constexpr int PJ_WG0 = 128;        // first projection workgroup (P6; idle in P3 apart from frames)
 constexpr int PTC = 32;      // attention positions per work item
+constexpr int IW0 = 32;      // workgroup of attention item 0 (items wrap round the grid from there)
 constexpr int YROWS = 64;    // rows per projection half (independent of the batch tile: the MT = 1
                              // launch reads what the MT = 2 launch left)
 constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = 128;
@@ -77,11 +78,7 @@ __device__ __forceinline__ f32x4 ldc4(const float* base, int off) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
 }
-#ifdef PLAIN_ACT
-constexpr int ACT_AUX = 0;
-#else
-constexpr int ACT_AUX = 16;
-#endif
+constexpr int ACT_AUX = 16;  // sc1; measured: plain / sc0 / sc0|sc1 loads are no faster
 
 
 // LDS-only workgroup barrier: unlike __syncthreads() (whose workgroup-scope fences wait for every
@@ -175,34 +172,20 @@ __device__ __forceinline__ float wave64_sum(float v) {
   if (P.atrace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                         \
   P.atrace[(((long)(t - P.trace_t0) * PW + b * P.nchmax + ch) * 8) + (k)] = __builtin_amdgcn_s_memrealtime()
 
-template <int MT, class GAP>
-__device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
-                                           int* is_last, GAP&& gap) {
-  constexpr int NT = PT, TC = PTC;
-  constexpr int NPT = NPQ_ / 16;  // 8 query partials per thread (16 groups of 8)
-  constexpr int Bp = MT * 16;
-  static_assert(TC == 32 && NT == 512, "attention item geometry: 2 position tiles x 8 dim tiles");
+// Location features of item (b, ch) for this step, computed one phase early (P1, from the alpha /
+// alpha_cum the previous step's combine wrote): L[i] = location term + processed input at position
+// t0 + 16 (i >> 2) + 4 (lane >> 4) + (i & 3), attention dim 16 wave + (lane & 15). Sums
+// loc + penc before the query is added: (pq + (loc + penc)) instead of the reference's
+// ((pq + loc) + penc), a one-ulp reassociation inside the tanh argument.
+__device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* Aw, const float* wcomb, float (&L)[8]) {
   const DecDev& D = P.D;
-  const int t0 = ch * TC;
+  const int t0 = ch * PTC;
   const int tid = opaque_v(threadIdx.x);
   const int lane = tid & 63;
-  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // attention dims 16 wave .. 16 wave + 15
-  const int a = 16 * wave + (lane & 15);                       // this lane's dim in the MFMA output
-  float* red = sm;              // [16][ADIM] query-partial group sums
-  float* Aw = red + 16 * ADIM_; // [2][64]: alpha / alpha_cum windows, alpha[t0 - 15 + q]
-  float* esum = Aw + 128;       // [8 waves][TC] partial energies
-  float* sv = esum + 8 * TC;    // [TC] energies
-  float* sw = sv + TC;          // [TC] normalised weights
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int a = 16 * wave + (lane & 15);
   const int T = D.lens[b];
   const int Tm1 = max(T - 1, 0);
-  // ---- independent loads first (clamped indices), in the order they are consumed: vmcnt is an
-  //      in-order counter, so waiting for an early load does not wait for the later ones ----
-  const int dn = ldci(D.done + b);
-  __builtin_amdgcn_sched_barrier(0);
-  const int a4 = tid & 31, pg = tid >> 5;  // query partials: 16-byte loads, dims 4 a4 .. 4 a4 + 3
-  f32x4 pp[NPT];
-#pragma unroll
-  for (int i = 0; i < NPT; ++i) pp[i] = ldc4(P.pq, ((((pg * 8 + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
   float aw;
   {
     const int q = tid & 63, ci = (tid >> 6) & 1;  // threads 0-127 fill the two windows
@@ -217,13 +200,62 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     const int pos = 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3);
     pen[i] = P.penc[((long)b * D.T_max + min(t0 + pos, Tm1)) * ADIM_ + a];
   }
-  const float va = P.v[a];
+  if (tid < 128) Aw[tid] = aw;
+  lds_barrier();
+  // location_dense(location_conv(.)) on MFMA: E[pos][dim] = sum_j X[pos][j] Wcomb[j][dim],
+  // X[pos][ci*31 + k] = window_ci[pos + k]; K = 62 taps padded to 64 (Wcomb rows 62, 63 are 0)
+  f32x4 le[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
+#pragma unroll
+  for (int st = 0; st < 16; ++st) {
+    const int j = 4 * st + (lane >> 4);
+    const int ci = j >= LOCK_ ? 1 : 0;
+    const int k = j - LOCK_ * ci;
+    const bool valid = j < 2 * LOCK_;
+    const float w = wcomb[j * ADIM_ + a];
+#pragma unroll
+    for (int mt = 0; mt < 2; ++mt) {
+      const float x = valid ? Aw[ci * 64 + 16 * mt + (lane & 15) + k] : 0.f;
+      le[mt] = MFMA16(x, w, le[mt]);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 8; ++i) L[i] = le[i >> 2][i & 3] + pen[i];
+  lds_barrier();  // window reads done before the scratch is reused
+}
+
+template <int MT>
+__device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
+                                           int* is_last, float (&L)[8], bool haveL) {
+  constexpr int NT = PT, TC = PTC;
+  constexpr int NPT = NPQ_ / 16;  // 8 query partials per thread (16 groups of 8)
+  constexpr int Bp = MT * 16;
+  static_assert(TC == 32 && NT == 512, "attention item geometry: 2 position tiles x 8 dim tiles");
+  const DecDev& D = P.D;
+  const int t0 = ch * TC;
+  float* red = sm;              // [16][ADIM] query-partial group sums
+  float* Aw = red + 16 * ADIM_; // [2][64]: alpha / alpha_cum windows, alpha[t0 - 15 + q]
+  float* esum = Aw + 128;       // [8 waves][TC] partial energies
+  float* sv = esum + 8 * TC;    // [TC] energies
+  float* sw = sv + TC;          // [TC] normalised weights
+  if (!haveL) attn_loc(P, b, ch, Aw, wcomb, L);  // items beyond a workgroup's first
+  const int tid = opaque_v(threadIdx.x);
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // attention dims 16 wave .. 16 wave + 15
+  const int a = 16 * wave + (lane & 15);                       // this lane's dim in the MFMA output
+  const int T = D.lens[b];
+  const int Tm1 = max(T - 1, 0);
+  // ---- independent loads first (clamped indices), in the order they are consumed: vmcnt is an
+  //      in-order counter, so waiting for an early load does not wait for the later ones ----
+  const int dn = ldci(D.done + b);
   __builtin_amdgcn_sched_barrier(0);
-  gap();  // independent MFMA work while the loads are in flight
+  const int a4 = tid & 31, pg = tid >> 5;  // query partials: 16-byte loads, dims 4 a4 .. 4 a4 + 3
+  f32x4 pp[NPT];
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) pp[i] = ldc4(P.pq, ((((pg * 8 + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
+  const float va = P.v[a];
   __builtin_amdgcn_sched_barrier(0);
   ATRACE(0);
   if (t0 >= T || dn) return;  // workgroup-uniform
-  if (tid < 128) Aw[tid] = aw;
   {
     f32x4 s4 = pp[0];
 #pragma unroll
@@ -246,29 +278,13 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   float pqa = red[a];
 #pragma unroll
   for (int g = 1; g < 16; ++g) pqa += red[g * ADIM_ + a];
-  // location_dense(location_conv(.)) on MFMA: E[pos][dim] = sum_j X[pos][j] Wcomb[j][dim],
-  // X[pos][ci*31 + k] = window_ci[pos + k]; K = 62 taps padded to 64 (Wcomb rows 62, 63 are 0)
-  f32x4 le[2] = {f32x4{0.f, 0.f, 0.f, 0.f}, f32x4{0.f, 0.f, 0.f, 0.f}};
-#pragma unroll
-  for (int st = 0; st < 16; ++st) {
-    const int j = 4 * st + (lane >> 4);
-    const int ci = j >= LOCK_ ? 1 : 0;
-    const int k = j - LOCK_ * ci;
-    const bool valid = j < 2 * LOCK_;
-    const float w = wcomb[j * ADIM_ + a];
-#pragma unroll
-    for (int mt = 0; mt < 2; ++mt) {
-      const float x = valid ? Aw[ci * 64 + 16 * mt + (lane & 15) + k] : 0.f;
-      le[mt] = MFMA16(x, w, le[mt]);
-    }
-  }
   ATRACE(2);
   // e = v . tanh(pq + loc + penc): the 16 dims of a DPP row summed in registers, the 8 waves
   // (dim tiles) through LDS
   {
     float z[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) z[i] = row16_sum(tanhf(pqa + le[i >> 2][i & 3] + pen[i]) * va);
+    for (int i = 0; i < 8; ++i) z[i] = row16_sum(tanhf(pqa + L[i]) * va);
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) esum[wave * TC + 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3)] = z[i];
@@ -405,6 +421,43 @@ __device__ __forceinline__ void gemm_seg(f32x4 (&acc)[MT], const float* base, in
   }
 }
 
+// gemm_seg for two accumulator sets over the SAME activation chunks (one load per chunk feeds both)
+template <int MT, int NC, int G, class WF1, class WF2>
+__device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* base, int nk, int kc0,
+                                          int lane, WF1 wf1, WF2 wf2) {
+  static_assert(NC % G == 0, "chunk groups");
+  auto ld = [&](int kc, int mt) { return ldc4<ACT_AUX>(base, ((mt * nk + kc) * 64 + lane) * 16); };
+  f32x4 x[2][G][MT];
+#pragma unroll
+  for (int i = 0; i < G; ++i)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) x[0][i][mt] = ld(kc0 + i, mt);
+#pragma unroll
+  for (int i0 = 0; i0 < NC; i0 += G) {
+    const int cur = (i0 / G) & 1;
+    if (i0 + G < NC) {
+#pragma unroll
+      for (int i = 0; i < G; ++i)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) x[cur ^ 1][i][mt] = ld(kc0 + i0 + G + i, mt);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int i = 0; i < G; ++i) {
+      const f32x4 w1 = wf1(i0 + i);
+      const f32x4 w2 = wf2(i0 + i);
+#pragma unroll
+      for (int q = 0; q < 4; ++q)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          acc1[mt] = MFMA16(x[cur][i][mt][q], w1[q], acc1[mt]);
+          acc2[mt] = MFMA16(x[cur][i][mt][q], w2[q], acc2[mt]);
+        }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+  }
+}
+
 // ------------------------------------------------------------------ the persistent kernel
 // LDS: [att-pre weights 96 x 1 KiB][Wcomb 64 x 128][scratch: GEMM reduction + hs | attention]
 constexpr size_t P_LDS_APRE = 96 * 64 * 16;
@@ -462,6 +515,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   __syncthreads();
 
   unsigned gen = 0;
+  float Lr[8];  // location features of the first attention item (attn_loc in P1, used in P4)
   const int t_first = D.ctl->base;
   int t = t_first;
   const int pj_jobs = 2 * P.ntj;
@@ -530,6 +584,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
       lds_barrier();
     }
+    // location features of this workgroup's first attention item for step t (alpha of t-1 is
+    // final); items sit on workgroups IW0.. so that they miss the prenet workgroups
+    const int it0 = (g - IW0 + PW) % PW;
+    if (it0 < D.B * P.nchmax) attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
     if (g == PW - 1) {
       if (tid < D.B) {
         const int m = tid;
@@ -657,19 +715,16 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
     {
-      // run while the attention loads are in flight (or alone when this workgroup has no item)
-      auto hatt_parts = [&]() {
-        gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
-        gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane,
-                           [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
-      };
+      // The h_att parts run AFTER this workgroup's attention item: fp32 MFMA occupies the SIMD
+      // (no co-issue with the attention's VALU work on the other wave), so under the item they
+      // only lengthen the attention chain; after it they overlap the other items' tails.
       const int nitems = D.B * P.nchmax;
-      if (g >= nitems) hatt_parts();
-      for (int it = g; it < nitems; it += PW) {
-        if (it == g) pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, hatt_parts);
-        else pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, [] {});
+      for (int it = (g - IW0 + PW) % PW; it < nitems; it += PW) {
+        pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW);
         lds_barrier();
       }
+      gemm_seg2<MT, 8, 2>(accd, acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; },
+                          [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
     }
     PTRACE(5);
     gsync_arrive(P.bar, gen);
