@@ -28,9 +28,12 @@ for k in range(5):
     print(f"{names[k]:18s} {med[k,0]:12.2f} {med[k,1]:10.2f} {med[k,2]:8.2f} {med[k,3]:12.2f}")
 step = np.median([(a[s + 1][0].min() - a[s][0].min()) / 100.0 for s in range(7)])
 print(f"step {step:.2f} us")
-sub = [np.median([(a[s][k] - a[s][6]).astype(float) / 100.0 for s in range(7)]) for k in (10, 11, 12, 13, 7)]
-print("P5 inside (median WG, us after release): dec MFMA %.2f, dec epilogue %.2f, att-pre MFMA %.2f, "
-      "att-pre epilogue %.2f, prefetch/arrive %.2f" % tuple(sub))
+NATT = 64
+sub = [np.median([(a[s][k][:NATT] - a[s][2][:NATT]).astype(float) / 100.0 for s in range(7)]) for k in (10, 11, 12, 3)]
+print("P3 inside attention_rnn workgroups (median, us after release): MFMA %.2f, cell %.2f, query partials %.2f, "
+      "done %.2f" % tuple(sub))
+sub = [np.median([(a[s][k][NATT:] - a[s][2][NATT:]).astype(float) / 100.0 for s in range(7)]) for k in (3,)]
+print("P3 item workgroups (h_dec part + frames) done %.2f" % tuple(sub))
 
 g14 = [np.median([(a[s][14] - a[s][4]).astype(float) / 100.0 for s in range(7) if a[s][14].min() > 0])
        for _ in (0,)] if a[:, 14].min() > 0 else None

@@ -36,15 +36,17 @@
 namespace {
 constexpr int PW = 256, PT = 512, NWV = 8;
 constexpr int DEC_NC = 20;   // 160 k-chunks / 8 waves
-constexpr int ATTP_NC = 4;   // 2 tiles x 16 chunks / 8 waves
+constexpr int ATTP_NC = 8;   // 4 tiles x 16 chunks / 8 waves
 constexpr int PJ_NC = 6;     // 48 / 8
 constexpr int PB_HALF = 64 * 256;  // prenet-2 K halves (fragment order, 64 rows each)
-constexpr int PJ_WG0 = 128;        // first projection workgroup (P6; idle in P3 apart from frames)
+constexpr int NATT = 64;           // attention_rnn workgroups (P3): 4 gate tiles = 16 units each
+constexpr int PJ_WG0 = 0;          // first projection workgroup (P6); jobs sit on the attention_rnn
+                                   // workgroups, which have no attention item
 constexpr int PTC = 32;      // attention positions per work item
-constexpr int IW0 = 32;      // workgroup of attention item 0 (items wrap round the grid from there)
+constexpr int IW0 = NATT;    // attention items live on workgroups IW0 .. PW-1 (round-robin)
 constexpr int YROWS = 64;    // rows per projection half (independent of the batch tile: the MT = 1
                              // launch reads what the MT = 2 launch left)
-constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = 128;
+constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = NATT;  // NPQ_: query-projection partials
 constexpr unsigned long long BAR_TIMEOUT = 20000000ull;  // s_memrealtime ticks (100 MHz): 0.2 s
 }  // namespace
 
@@ -227,7 +229,7 @@ template <int MT>
 __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
                                            int* is_last, float (&L)[8], bool haveL) {
   constexpr int NT = PT, TC = PTC;
-  constexpr int NPT = NPQ_ / 16;  // 8 query partials per thread (16 groups of 8)
+  constexpr int NPT = NPQ_ / 16;  // query partials per thread (16 groups)
   constexpr int Bp = MT * 16;
   static_assert(TC == 32 && NT == 512, "attention item geometry: 2 position tiles x 8 dim tiles");
   const DecDev& D = P.D;
@@ -251,7 +253,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   const int a4 = tid & 31, pg = tid >> 5;  // query partials: 16-byte loads, dims 4 a4 .. 4 a4 + 3
   f32x4 pp[NPT];
 #pragma unroll
-  for (int i = 0; i < NPT; ++i) pp[i] = ldc4(P.pq, ((((pg * 8 + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
+  for (int i = 0; i < NPT; ++i) pp[i] = ldc4(P.pq, ((((pg * NPT + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
   const float va = P.v[a];
   __builtin_amdgcn_sched_barrier(0);
   ATRACE(0);
@@ -462,7 +464,7 @@ __device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], 
 // LDS: [att-pre weights 96 x 1 KiB][Wcomb 64 x 128][scratch: GEMM reduction + hs | attention]
 constexpr size_t P_LDS_APRE = 96 * 64 * 16;
 constexpr size_t P_LDS_WC = 64 * 128 * 4;
-constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 8 * 4;  // >= attention scratch (~2.4K floats)
+constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 16 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
 constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
 
 // phase timestamps of every workgroup for 8 steps (P.trace, optional): [step][16][256]
@@ -481,7 +483,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   float* wcomb = reinterpret_cast<float*>(smem4) + 96 * 64 * 4;    // [64][128]
   float* scr = wcomb + 64 * 128;
   float* red0 = scr;                   // [8][Bp][17]
-  float* hs = red0 + 8 * Bp * 17;      // [Bp][8]
+  float* hs = red0 + 8 * Bp * 17;      // [Bp][16]
   const int g = blockIdx.x, tid0 = threadIdx.x, lane0 = tid0 & 63;
   const int wave0 = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   const int YP = P.ntj * 16;
@@ -491,7 +493,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   {
     const f32x4* src = reinterpret_cast<const f32x4*>(P.apre_w) + (long)g * 96 * 64;
     for (int i = tid; i < 96 * 64; i += PT) Wap[i] = src[i];
-    for (int i = tid; i < 64 * 128; i += PT) wcomb[i] = P.Wcomb[i];
+    if (g >= IW0)  // attention_rnn workgroups use this area as P3 staging instead
+      for (int i = tid; i < 64 * 128; i += PT) wcomb[i] = P.Wcomb[i];
   }
   // decoder_rnn weights of this wave: K = [h_att 64 chunks | ctx 32 | h_dec 64]; wave w keeps
   // h_att chunks 8w..8w+7 (wd[0..7]), ctx chunks 4w..4w+3 (wd[8..11]), h_dec chunks 8w..8w+7
@@ -524,13 +527,27 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   // prenet layer-2 weight chunk of this wave (workgroups 0-31: tile g & 15, k-chunk 8 (g >> 4) + wave)
   const f32x4 w2 = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + 8 * ((g >> 4) & 1) + wave) * 64 + lane];
   // partial sums of this workgroup's decoder_rnn tile (accd) and attention_rnn ctx/h tile (acca),
-  // accumulated across phases: h_dec part in P6 of the previous step (P3 for projection
-  // workgroups, P1 on a launch's first step), h_att parts in P4, ctx parts in P5
+  // accumulated across phases. Attention-item workgroups (g >= IW0): accd h_dec part in P3, h_att
+  // part in P4 after the item, ctx part in P5; acca ctx part in P5, h_att part + epilogue in P6.
+  // attention_rnn workgroups (g < IW0, no item): accd h_dec and both h_att parts in P4, ctx parts
+  // and both epilogues in P5.
   f32x4 accd[MT], acca[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) accd[mt] = acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto dec_hdec_part = [&](const float* hd) {
     gemm_seg<MT, 8, 4>(accd, hd, 64, 8 * wave, lane, [&](int i) { return wd[12 + i]; });
+  };
+  // attention_rnn ctx/h tile g complete: reduce over the waves, add the biases, publish the next
+  // step's gate addends, reset the accumulator
+  auto att_epilogue = [&](float* red) {
+    acc_to_lds<MT>(red, wave, lane, acca);
+    lds_barrier();
+    for (int idx = tid; idx < Bp * 16; idx += PT) {
+      const int m = idx >> 4, n = idx & 15;
+      stc(P.gatt + (long)m * 4096 + g * 16 + n, lds_sum<NWV, Bp>(red, m, n) + apb);
+    }
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   };
 
   // frames of step s (< S_cap) from the two projection halves (K5 frame store of decoder.hip):
@@ -557,7 +574,6 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (t == t_first) dec_hdec_part(hd_cur);
     if (g < 32) {  // prenet layer 2, tile g & 15, K half g >> 4 (one k-chunk per wave)
       f32x4 acc[MT];
 #pragma unroll
@@ -586,9 +602,9 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     }
     // location features of this workgroup's first attention item for step t (alpha of t-1 is
     // final); items sit on workgroups IW0.. so that they miss the prenet workgroups
-    const int it0 = (g - IW0 + PW) % PW;
-    if (it0 < D.B * P.nchmax) attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
-    if (g == PW - 1) {
+    const int it0 = g - IW0;
+    if (it0 >= 0 && it0 < D.B * P.nchmax) attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
+    if (g == IW0 - 1) {  // stop decision: an attention_rnn workgroup that is not a prenet one
       if (tid < D.B) {
         const int m = tid;
         int dn = ldci(D.done + m);
@@ -619,23 +635,24 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     gsync_arrive(P.bar, gen);
     // P3 operands that are already final: its epilogue's gate addends (written by P5 of the
     // previous step), c_att, the query-projection weights
-    float ga[4], ca, wq[8];
+    float ga[4], ca, wq[16];
     {
-      const int idx = min(tid, 2 * Bp * 4 - 1);
+      const int idx = min(tid, 4 * Bp * 4 - 1);
       const int gl = idx / (Bp * 4), rem = idx % (Bp * 4);
       const int m = rem >> 2, u = rem & 3;
-      const int tile = 2 * min(g, 127) + gl;
+      const int tile = 4 * min(g, NATT - 1) + gl;
 #pragma unroll
       for (int q = 0; q < 4; ++q) ga[q] = ldc(P.gatt + (long)m * 4096 + tile * 16 + q * 4 + u);
       ca = P.catt[(long)m * 1024 + tile * 4 + u];
 #pragma unroll
-      for (int u2 = 0; u2 < 8; ++u2) wq[u2] = P.WqT[(long)(8 * min(g, 127) + u2) * 128 + (tid & 127)];
+      for (int u2 = 0; u2 < 16; ++u2) wq[u2] = P.WqT[(long)(16 * min(g, NATT - 1) + u2) * 128 + (tid & 127)];
     }
-    // attention_rnn prenet-part weights for P3 (2 tiles per workgroup, 4 k-chunks per wave)
+    // attention_rnn prenet-part weights for P3: 4 tiles per workgroup, waves 2j, 2j+1 = tile j
+    // K halves (8 k-chunks each)
     f32x4 wa[ATTP_NC];
     {
-      const int tl = 2 * min(g, 127) + (wave >> 2);
-      const f32x4* src = reinterpret_cast<const f32x4*>(P.attp_w) + ((long)tl * 16 + 4 * (wave & 3)) * 64 + lane;
+      const int tl = 4 * min(g, NATT - 1) + (wave >> 1);
+      const f32x4* src = reinterpret_cast<const f32x4*>(P.attp_w) + ((long)tl * 16 + 8 * (wave & 1)) * 64 + lane;
 #pragma unroll
       for (int i = 0; i < ATTP_NC; ++i) wa[i] = src[(long)i * 64];
     }
@@ -649,62 +666,73 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         return;
       }
     }
-    // ======== P3: attention_rnn (prenet part) + cell + query partials (workgroups 0-127)
-    //            || frames(t-1) + the h_dec part for projection workgroups (128-255) ========
+    // ======== P3: attention_rnn (prenet part) + cell + query partials (workgroups 0 .. NATT-1)
+    //            || frames(t-1) + the decoder_rnn h_dec part (item workgroups) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (g < 128) {
+    if (g < NATT) {
+      // relu(prenet output) staged once per workgroup in LDS (the Wcomb area: attention_rnn
+      // workgroups have no attention item); wave w loads k-chunks 2w, 2w+1
+      f32x4* xs = reinterpret_cast<f32x4*>(wcomb);  // [MT * 16 chunks][64 lanes]
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const int c = mt * 16 + 2 * wave + i;
+          f32x4 x = ldc4(P.pb, (c * 64 + lane) * 16) + ldc4(P.pb, (c * 64 + lane) * 16 + PB_HALF * 4);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
+          xs[c * 64 + lane] = x;
+        }
+      lds_barrier();
+      // waves 2j, 2j+1: tile 4g + j, K halves (8 chunks each)
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      f32x4 x[ATTP_NC][MT];
 #pragma unroll
-      for (int i = 0; i < ATTP_NC; ++i)
+      for (int i = 0; i < ATTP_NC; ++i) {
+        f32x4 x[MT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int off = ((mt * 16 + 4 * (wave & 3) + i) * 64 + lane) * 16;
-          x[i][mt] = ldc4(P.pb, off) + ldc4(P.pb, off + PB_HALF * 4);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[i][mt][q] = fmaxf(x[i][mt][q], 0.f);
-        }
-#pragma unroll
-      for (int i = 0; i < ATTP_NC; ++i)
+        for (int mt = 0; mt < MT; ++mt) x[mt] = xs[(mt * 16 + 8 * (wave & 1) + i) * 64 + lane];
 #pragma unroll
         for (int q = 0; q < 4; ++q)
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[i][mt][q], wa[i][q], acc[mt]);
-      // waves 0-3: tile 2g, waves 4-7: tile 2g+1
-      acc_to_lds<MT>(red0 + (wave >> 2) * 4 * Bp * 17, wave & 3, lane, acc);
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[mt][q], wa[i][q], acc[mt]);
+      }
+      PTRACE(10);
+      acc_to_lds<MT>(red0 + (wave >> 1) * 2 * Bp * 17, wave & 1, lane, acc);
       lds_barrier();
-      if (tid < 2 * Bp * 4) {
+      if (tid < 4 * Bp * 4) {
         const int gl = tid / (Bp * 4), rem = tid % (Bp * 4);
         const int m = rem >> 2, u = rem & 3;
-        const int tile = 2 * g + gl;
-        const float* pg = red0 + gl * 4 * Bp * 17;
+        const int tile = 4 * g + gl;
+        const float* pg = red0 + gl * 2 * Bp * 17;
         float pre[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<4, Bp>(pg, m, q * 4 + u) + ga[q];
+        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<2, Bp>(pg, m, q * 4 + u) + ga[q];
         const long ci = (long)m * 1024 + tile * 4 + u;
         const float c = sigm(pre[1]) * ca + sigm(pre[0]) * tanhf(pre[2]);
         const float h = sigm(pre[3]) * tanhf(c);
         P.catt[ci] = c;
         stc(P.hatt + frag_idx(m, tile * 4 + u, 1024), h);
-        hs[m * 8 + gl * 4 + u] = h;
+        hs[m * 16 + gl * 4 + u] = h;
       }
       lds_barrier();
-      {  // partial query projection over this workgroup's 8 units
+      PTRACE(11);
+      {  // partial query projection over this workgroup's 16 units
         const int a = tid & 127;
         for (int m = tid >> 7; m < Bp; m += PT / 128) {
           float s = 0.f;
 #pragma unroll
-          for (int u = 0; u < 8; ++u) s = fmaf(wq[u], hs[m * 8 + u], s);
+          for (int u = 0; u < 16; ++u) s = fmaf(wq[u], hs[m * 16 + u], s);
           stc(P.pq + ((long)g * Bp + m) * 128 + a, s);
         }
       }
+      PTRACE(12);
     } else {
-      if (is_pj && t != t_first) dec_hdec_part(hd_cur);
-      write_frames(t - 1, 128, PW - 128);
+      dec_hdec_part(hd_cur);
+      write_frames(t - 1, NATT, PW - NATT);
     }
     PTRACE(3);
     gsync_arrive(P.bar, gen);
@@ -718,13 +746,18 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       // The h_att parts run AFTER this workgroup's attention item: fp32 MFMA occupies the SIMD
       // (no co-issue with the attention's VALU work on the other wave), so under the item they
       // only lengthen the attention chain; after it they overlap the other items' tails.
-      const int nitems = D.B * P.nchmax;
-      for (int it = (g - IW0 + PW) % PW; it < nitems; it += PW) {
-        pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW);
-        lds_barrier();
+      if (g >= IW0) {  // items, then the decoder_rnn h_att part (attention_rnn's waits for P6)
+        const int nitems = D.B * P.nchmax;
+        for (int it = g - IW0; it < nitems; it += PW - IW0) {
+          pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
+          lds_barrier();
+        }
+        gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
+      } else {  // no item: both h_att parts and the decoder_rnn h_dec part
+        gemm_seg2<MT, 8, 2>(accd, acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; },
+                            [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
+        dec_hdec_part(hd_cur);
       }
-      gemm_seg2<MT, 8, 2>(accd, acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; },
-                          [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
     }
     PTRACE(5);
     gsync_arrive(P.bar, gen);
@@ -740,7 +773,6 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     {
       gemm_seg<MT, 4, 4>(accd, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; });
       gemm_seg<MT, 4, 4>(acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return Wap[(4 * wave + i) * 64 + lane]; });
-      PTRACE(10);
       float* red1 = red0;  // two reductions back to back: [2][8][Bp][17] would not fit; reuse
       acc_to_lds<MT>(red0, wave, lane, accd);
       lds_barrier();
@@ -755,19 +787,11 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         P.cdec[ci] = c;
         stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
       }
-      PTRACE(11);
       lds_barrier();
-      acc_to_lds<MT>(red1, wave, lane, acca);
-      lds_barrier();
-      PTRACE(12);
-      for (int idx = tid; idx < Bp * 16; idx += PT) {
-        const int m = idx >> 4, n = idx & 15;
-        stc(P.gatt + (long)m * 4096 + g * 16 + n, lds_sum<NWV, Bp>(red1, m, n) + apb);
-      }
+      if (g < IW0) att_epilogue(red1);
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) accd[mt] = acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      for (int mt = 0; mt < MT; ++mt) accd[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
-    PTRACE(13);
     PTRACE(7);
     gsync_arrive(P.bar, gen);
     // projection weights for P6 (half pj & 1 of job tile pj >> 1, 6 k-chunks per wave)
@@ -780,7 +804,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     }
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(8);
-    // ======== P6: projection halves (workgroups PJ_WG0 ..) || the next step's h_dec part ========
+    // ======== P6: projection halves (workgroups PJ_WG0 ..) || attention_rnn h_att part (items) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
@@ -812,8 +836,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         stc(P.ypart + (long)((pj & 1) * YROWS + m) * YP + (pj >> 1) * 16 + n, lds_sum<NWV, Bp>(red0, m, n));
       }
       lds_barrier();
-    } else {
-      dec_hdec_part(hd_nxt);  // h_dec of step t+1
+    }
+    if (g >= IW0) {  // item workgroups: attention_rnn h_att part (h_att of step t is still in place)
+      gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
+      att_epilogue(red0);
     }
     PTRACE(9);
     gsync_arrive(P.bar, gen);
@@ -834,6 +860,7 @@ int persist_attn_tc() { return PTC; }
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
   TTS_CHECK(MT == 1 || MT == 2, "persistent decoder: MT must be 1 or 2");
   TTS_CHECK(PJ_WG0 + a.ntj * 2 <= PW && a.ntj >= 17, "persistent decoder: projection job count");
+  TTS_CHECK(a.D.B <= 64 && NATT * 4 * 4 == 1024, "persistent decoder: attention_rnn layout");
   TTS_CHECK(a.nchmax * PTC >= a.D.T_max, "persistent decoder: attention partial buffers too small");
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
   const void* f = MT == 1 ? (const void*)persist_decoder_kernel<1> : (const void*)persist_decoder_kernel<2>;
