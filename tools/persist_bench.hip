@@ -81,6 +81,39 @@ __global__ __launch_bounds__(256) void bar_hier_kernel(unsigned* ctr, int iters)
   }
 }
 
+// (F) per-XCD counters, the last arriver of an XCD writes its XCD's slot of one 8-slot line; every
+// workgroup polls that line (lanes 0-7) until all slots hold the generation (no second atomic)
+__global__ __launch_bounds__(256) void bar_hier8_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  const int xcd = blockIdx.x & 7;
+  const unsigned per = gridDim.x / 8;
+  unsigned* xc = ctr + 64 + xcd * 32;
+  unsigned* line = ctr + 32;
+  for (int i = 0; i < iters; ++i) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const unsigned old = __hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == per * (i + 1) - 1) __hip_atomic_store(line + xcd, (unsigned)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    if (threadIdx.x < 64) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      int good = 1;
+      const int l = threadIdx.x & 7;
+      while (true) {
+        unsigned v = __hip_atomic_load(line + l, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_ballot_w64(v < (unsigned)(i + 1)) == 0) break;
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      }
+      if (threadIdx.x == 0) ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
 // (C) flag array, no atomics: each workgroup stores its generation to its own slot; wave 0 polls
 // all slots (4 per lane) until the minimum reaches the generation
 __global__ __launch_bounds__(256) void bar_flags_kernel(unsigned* flags, int iters) {
@@ -253,9 +286,10 @@ int main() {
   }
   unsigned* big;
   HIP_OK(hipMalloc(&big, 4096 * 4));
-  for (int v = 0; v < 3; ++v) {
-    const void* f = v == 0 ? (const void*)bar_hier_kernel : v == 1 ? (const void*)bar_flags_kernel : (const void*)bar_go_kernel;
-    const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : "counter + go flag";
+  for (int v = 0; v < 4; ++v) {
+    const void* f = v == 0 ? (const void*)bar_hier_kernel : v == 1 ? (const void*)bar_flags_kernel
+                  : v == 2 ? (const void*)bar_go_kernel : (const void*)bar_hier8_kernel;
+    const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : v == 2 ? "counter + go flag" : "xcd ctr + 8-slot line";
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
     for (int nwg : {256, 128}) {
       const int iters = 2000;
