@@ -17,6 +17,8 @@
 
 void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int num_rows, int D,
                          const int* lens, int B, float* out, hipStream_t s);
+bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
+                           unsigned* bar, float* out, hipStream_t s);
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
                    float* out,
                        hipStream_t s);
@@ -207,6 +209,7 @@ struct TacoWS {
   DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
   DevBuf ids, post, map;       // rows in decode order (longest first), output scatter map
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
+  bool enc_persist = false;    // the last encoder ran the persistent BiLSTM (lc = its barrier words)
   // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
   // longest-first rows finish); all share one configuration key
   hipGraphExec_t graphs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -734,7 +737,23 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
   cc.epi = 0;
   run_conv(M.lstm_in, cc, s);
   HIP_OK(hipMemsetAsync(enc_out, 0, (size_t)B * T_max * 512 * 4, s));
-  launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
+  // one cooperative launch for the whole recurrence (W.lc then holds its grid-barrier words);
+  // per-step launches when cooperative launch is unavailable or TTS_ENCODER=steps
+  const char* e = std::getenv("TTS_ENCODER");
+  W.enc_persist = !(e && std::string(e) == "steps") &&
+                  launch_bilstm_persist(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(),
+                                        reinterpret_cast<unsigned*>(W.lc.p), enc_out, s);
+  if (!W.enc_persist) launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
+}
+
+// after a stream synchronisation: a persistent BiLSTM whose grid barrier timed out set its error word
+void check_encoder_barrier(tts_ctx* c) {
+  if (!c->tws.enc_persist) return;
+  unsigned err = 0;
+  unsigned err2 = 0;
+  HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(c->tws.lc.p) + 16, 4, hipMemcpyDeviceToHost));
+  HIP_OK(hipMemcpy(&err2, reinterpret_cast<unsigned*>(c->tws.lc.p) + 512 + 16, 4, hipMemcpyDeviceToHost));
+  TTS_CHECK(err == 0 && err2 == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident)");
 }
 
 void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int B, int Mmax_alloc, int max_q,
@@ -1037,6 +1056,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   }
   }
   HIP_OK(hipStreamSynchronize(s));
+  check_encoder_barrier(c);
   if (persist) {
     unsigned err = 0;
     HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(W.pbar.p) + 16, 4, hipMemcpyDeviceToHost));
@@ -1421,6 +1441,7 @@ int tts_taco_encoder(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, in
     HIP_OK(hipMemcpyAsync(c->tws.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, c->s));
     run_encoder(c, d_ids, B, T_max, d_out, c->s);
     HIP_OK(hipStreamSynchronize(c->s));
+    check_encoder_barrier(c);
     leave(c, stream);
   });
 }

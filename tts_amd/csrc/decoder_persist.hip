@@ -30,6 +30,7 @@
 // not fully co-resident fails loudly instead of hanging.
 #include "common.h"
 #include "decoder.h"
+#include "gsync.h"
 
 #include <type_traits>
 
@@ -47,22 +48,8 @@ constexpr int IW0 = NATT;    // attention items live on workgroups IW0 .. PW-1 (
 constexpr int YROWS = 64;    // rows per projection half (independent of the batch tile: the MT = 1
                              // launch reads what the MT = 2 launch left)
 constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = NATT;  // NPQ_: query-projection partials
-constexpr unsigned long long BAR_TIMEOUT = 20000000ull;  // s_memrealtime ticks (100 MHz): 0.2 s
 }  // namespace
 
-// ------------------------------------------------------------------ coherent access helpers
-__device__ __forceinline__ float ldc(const float* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ int ldci(const int* p) {
-  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void stc(float* p, float v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-__device__ __forceinline__ void stci(int* p, int v) {
-  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
 // Opaque copies of lane / wave indices, taken at the start of each phase: without them the
 // compiler hoists every loop-invariant address of every phase out of the step loop and keeps them
 // all live (hundreds of VGPRs / SGPRs, spilled to scratch).
@@ -74,52 +61,7 @@ __device__ __forceinline__ int opaque_s(int v) {
   asm volatile("" : "+s"(v));
   return v;
 }
-// 16-byte agent-coherent load at byte offset `off` from a wave-uniform base (buffer load, sc1)
-template <int AUX = 16>
-__device__ __forceinline__ f32x4 ldc4(const float* base, int off) {
-  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
-  return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
-}
 constexpr int ACT_AUX = 16;  // sc1; measured: plain / sc0 / sc0|sc1 loads are no faster
-
-
-// LDS-only workgroup barrier: unlike __syncthreads() (whose workgroup-scope fences wait for every
-// outstanding global load, vmcnt(0)), global loads already in flight stay in flight
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
-
-// Hierarchical grid barrier, split so that loads for the next phase can be issued between the
-// arrival and the wait. arrive: every wave drains its stores (sc1 write-through), then thread 0
-// counts the workgroup in at its XCD's counter; the 32nd arrival of an XCD counts the XCD in at
-// the global counter; the 8th XCD writes the go word.
-__device__ __forceinline__ void gsync_arrive(unsigned* bar, unsigned& gen) {
-  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-  __syncthreads();
-  ++gen;
-  if (threadIdx.x == 0) {
-    unsigned* xc = bar + 64 + (blockIdx.x & 7) * 32;
-    const unsigned per = gridDim.x / 8;
-    if (__hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per * gen - 1)
-      if (__hip_atomic_fetch_add(bar, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 8u * gen - 1)
-        __hip_atomic_store(bar + 32, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-  }
-}
-// wait for the go word; false = timed out (error word set, the caller exits)
-__device__ __forceinline__ bool gsync_wait(unsigned* bar, unsigned gen, int* flag) {
-  if (threadIdx.x == 0) {
-    int good = 1;
-    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-    while (__hip_atomic_load(bar + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > BAR_TIMEOUT) {
-        __hip_atomic_fetch_or(bar + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        good = 0;
-        break;
-      }
-    }
-    *flag = good;
-  }
-  lds_barrier();
-  return *flag;
-}
 
 // partial sums of one wave's MT accumulators into LDS [wave][m][17]
 template <int MT>

@@ -7,6 +7,7 @@
 //    in the padding (a padded reverse pass differs by 0.29 L-inf).
 #include "common.h"
 #include "decoder.h"  // frag_idx
+#include "gsync.h"
 
 __global__ __launch_bounds__(256) void embed_gather_kernel(const int64_t* __restrict__ ids, int T_max,
                                                            const float* __restrict__ table, int num_rows,
@@ -100,6 +101,104 @@ __global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restric
   c[ci] = cn;
   h_out[(long)dir * Bp * H + frag_idx(m, tl * 4 + u, H)] = hn;
   out[((long)m * T_max + t) * 512 + dir * 256 + tl * 4 + u] = hn;
+}
+
+// The whole recurrence as ONE cooperative launch of the same 128 workgroups: W_hh fragments stay
+// in VGPRs, the cell state in a register of the thread that owns (row, unit), and a hierarchical
+// grid barrier (gsync.h) replaces the launch boundary between steps (per-step launches were
+// host-enqueue bound at ~8 us per step).
+template <int MT>
+__global__ __launch_bounds__(256) void bilstm_persist_kernel(const float* __restrict__ Whh,
+                                                             const float* __restrict__ Gin, const int* lens,
+                                                             int T_max, int B, float* hbuf, float* __restrict__ out,
+                                                             unsigned* bar) {
+  constexpr int Bp = MT * 16;
+  constexpr int H = 256, NKC = H / 16, KPW = NKC / 4;  // 4 k-chunks per wave
+  __shared__ float part[4 * Bp * 17];
+  __shared__ int sflag;
+  const int dir = blockIdx.x >> 6, tl = blockIdx.x & 63;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  f32x4 w[KPW];
+  {
+    const f32x4* Wv = reinterpret_cast<const f32x4*>(Whh) + ((long)(dir * 64 + tl) * NKC + wave * KPW) * 64 + lane;
+#pragma unroll
+    for (int k = 0; k < KPW; ++k) w[k] = Wv[(long)k * 64];
+  }
+  const int m = min(tid >> 2, Bp - 1), u = tid & 3;
+  const bool row = (tid >> 2) < Bp && m < B;
+  const int Tm = lens[min(m, B - 1)];
+  const float* gbase = Gin + (long)min(m, B - 1) * T_max * 2048 + dir * 1024 + tl * 16 + u;
+  float cst = 0.f;
+  unsigned gen = 0;
+  // input-projection gates of a step do not depend on h: loaded one step ahead, under the barrier
+  auto tpos = [&](int step) { return min(max(dir ? Tm - 1 - step : step, 0), T_max - 1); };
+  float gin[4];
+#pragma unroll
+  for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(0) * 2048 + q * 4];
+  for (int step = 0; step < T_max; ++step) {
+    const float* hi = hbuf + (size_t)(step & 1) * 2 * Bp * H + (long)dir * Bp * H;
+    float* ho = hbuf + (size_t)((step + 1) & 1) * 2 * Bp * H + (long)dir * Bp * H;
+    const int t = tpos(step);
+    f32x4 x[KPW][MT];
+#pragma unroll
+    for (int k = 0; k < KPW; ++k)
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt) x[k][mt] = ldc4(hi, ((mt * 16 + wave * KPW + k) * 64 + lane) * 16);
+    f32x4 acc[MT];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int k = 0; k < KPW; ++k)
+#pragma unroll
+      for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[k][mt][s4], w[k][s4], acc[mt]);
+    float* p = part + wave * Bp * 17;
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
+    lds_barrier();
+    if (row && step < Tm) {
+      float pre[4];
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const int n = q * 4 + u;
+        pre[q] = part[m * 17 + n] + part[(Bp + m) * 17 + n] + part[(2 * Bp + m) * 17 + n] +
+                 part[(3 * Bp + m) * 17 + n] + gin[q];
+      }
+      const float ig = 1.f / (1.f + expf(-pre[0]));
+      const float fg = 1.f / (1.f + expf(-pre[1]));
+      const float gg = tanhf(pre[2]);
+      const float og = 1.f / (1.f + expf(-pre[3]));
+      cst = fg * cst + ig * gg;
+      const float hn = og * tanhf(cst);
+      stc(ho + frag_idx(m, tl * 4 + u, H), hn);
+      out[((long)m * T_max + t) * 512 + dir * 256 + tl * 4 + u] = hn;
+    }
+    if (step + 1 < T_max) {  // the two directions are independent: one 64-workgroup barrier each
+      gsync_arrive(bar + dir * 512, gen, 64);
+#pragma unroll
+      for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(step + 1) * 2048 + q * 4];
+      if (!gsync_wait(bar + dir * 512, gen, &sflag)) return;
+    }
+  }
+}
+
+bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
+                           unsigned* bar, float* out, hipStream_t s) {
+  int dev = 0, coop = 0;
+  HIP_OK(hipGetDevice(&dev));
+  HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
+  if (!coop) return false;
+  const int MT = (B + 15) / 16, Bp = MT * 16;
+  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * 2 * Bp * 256 * 4, s));
+  HIP_OK(hipMemsetAsync(bar, 0, 1024 * 4, s));
+  void* args[] = {(void*)&Whh, (void*)&Gin, (void*)&lens, (void*)&T_max, (void*)&B, (void*)&hbuf, (void*)&out, (void*)&bar};
+  const void* f = MT == 1 ? (const void*)bilstm_persist_kernel<1> : MT == 2 ? (const void*)bilstm_persist_kernel<2>
+                : MT == 3 ? (const void*)bilstm_persist_kernel<3> : (const void*)bilstm_persist_kernel<4>;
+  HIP_OK(hipLaunchCooperativeKernel(f, dim3(128), dim3(256), args, 0, s));
+  return true;
 }
 
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
