@@ -206,9 +206,14 @@ class TacoOracle:
             o = self.conv_bn_block(f"postnet.convolutions.{i}", o, "tanh" if i < 4 else None)
         return (x + o).T.astype(F32)
 
-    def inference(self, ids, r, max_steps=1000, stop_threshold=0.5):
-        """Tacotron2.inference (models/tacotron2.py:142-163) for one utterance."""
+    def inference(self, ids, r, max_steps=1000, stop_threshold=0.5, speaker=None):
+        """Tacotron2.inference (models/tacotron2.py:142-163) for one utterance. ``speaker``: the
+        speaker vector (learned-embedding row or external embedding) concatenated to every
+        encoder output (models/tacotron2.py:152-155, tacotron_abstract.py:213-217)."""
         enc = self.encoder(np.asarray(ids))
+        if speaker is not None:
+            spk = np.asarray(speaker, F32).reshape(1, -1)
+            enc = np.concatenate([enc, np.repeat(spk, enc.shape[0], axis=0)], axis=1).astype(F32)
         dec, stop, align = self.decoder_inference(enc, r, max_steps, stop_threshold)
         post = self.postnet(dec)
         return dec, post, align, stop

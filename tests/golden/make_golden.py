@@ -44,10 +44,10 @@ STOP_GAIN = {"linear_sigmoid": 100.0, "attn_v": 4.0, "linear_tanh": 3.0}
 
 def build_taco(cfg: TacotronConfig, seed: int, stop_bias: float, dtype=torch.float32):
     torch.set_default_dtype(dtype)
-    m = Tacotron2(num_chars=cfg.num_chars, num_speakers=0, r=cfg.r, attn_norm=cfg.attn_norm,
+    m = Tacotron2(num_chars=cfg.num_chars, num_speakers=cfg.num_speakers, r=cfg.r, attn_norm=cfg.attn_norm,
                   prenet_dropout=False, location_attn=cfg.location_attn,
                   double_decoder_consistency=cfg.double_decoder_consistency, ddc_r=cfg.ddc_r,
-                  separate_stopnet=True)
+                  separate_stopnet=True, speaker_embedding_dim=cfg.speaker_embedding_dim)
     sd = synth_state_dict(tacotron2_spec(cfg), seed, STOP_GAIN)
     sd["decoder.stopnet.1.linear_layer.bias"] = np.array([stop_bias], np.float32)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
@@ -58,7 +58,7 @@ def build_taco(cfg: TacotronConfig, seed: int, stop_bias: float, dtype=torch.flo
     return m
 
 
-def run_taco(m, ids, r, max_steps, dtype=torch.float32):
+def run_taco(m, ids, r, max_steps, dtype=torch.float32, spk=None):
     m.decoder.set_r(r)
     m.decoder.max_decoder_steps = max_steps
     logits = []
@@ -68,7 +68,12 @@ def run_taco(m, ids, r, max_steps, dtype=torch.float32):
         x = torch.from_numpy(ids[None].astype(np.int64))
         emb = m.embedding(x).transpose(1, 2)
         enc_out = m.encoder.inference(emb)
-        dec, post, align, stop = m.inference(x)
+        kw = {}
+        if spk is not None and np.ndim(spk) == 0:     # learned embedding: speaker id
+            kw["speaker_ids"] = torch.tensor([int(spk)])
+        elif spk is not None:                          # external per-sample embedding (1, E)
+            kw["speaker_embeddings"] = torch.from_numpy(np.asarray(spk)[None]).to(dtype)
+        dec, post, align, stop = m.inference(x, **kw)
     h.remove()
     torch.set_default_dtype(torch.float32)
     lg = torch.cat(logits, 0).reshape(-1).double().numpy()
@@ -102,9 +107,11 @@ def choose_stop_bias(raw_logits_list, max_steps, min_stopping, min_stop_step=4):
     return best
 
 
-def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_seed):
+def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_seed, speakers=None):
+    """speakers: per utterance a speaker id (learned table) or an embedding vector (external)."""
     rs = np.random.RandomState(id_seed)
     utts = [rs.randint(1, cfg.num_chars, size=T).astype(np.int64) for T in utt_lens]
+    spks = speakers if speakers is not None else [None] * len(utts)
     # pass 1: never stop; record bias-free logits at the largest r (same decoder state
     # trajectory for any stop bias, since the stopnet output is never fed back)
     out = {"seed": seed, "cfg": json.dumps(cfg.__dict__), "r_list": np.array(r_list),
@@ -112,22 +119,25 @@ def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_see
     for r in r_list:
         m = build_taco(cfg, seed, -1e4)
         raw = []
-        for ids in utts:
-            lg = run_taco(m, ids, r, max_steps[r])[4]
+        for ids, sp in zip(utts, spks):
+            lg = run_taco(m, ids, r, max_steps[r], spk=sp)[4]
             raw.append(lg + 1e4)
         b, margin = choose_stop_bias(raw, max_steps[r], min_stopping)
         print(f"[{name}] r={r} stop bias {b:.6f} min margin {margin:.3e}")
         m32 = build_taco(cfg, seed, b)
         m64 = build_taco(cfg, seed, b, torch.float64)
         for i, ids in enumerate(utts):
-            dec, post, align, stop, lg, enc = run_taco(m32, ids, r, max_steps[r])
-            dec64, post64, _, _, _, _ = run_taco(m64, ids, r, max_steps[r], torch.float64)
+            sp = spks[i]
+            dec, post, align, stop, lg, enc = run_taco(m32, ids, r, max_steps[r], spk=sp)
+            dec64, post64, _, _, _, _ = run_taco(m64, ids, r, max_steps[r], torch.float64, spk=sp)
             n = min(len(dec), len(dec64))
             drift = float(np.max(np.abs(post[:n] - post64[:n]))) if len(dec) == len(dec64) else float("nan")
             am = np.sort(align, axis=1)
             top2 = am[:, -1] - am[:, -2] if align.shape[1] > 1 else np.full(len(align), np.inf)
             k = f"r{r}_u{i}"
             out[f"{k}_ids"] = ids
+            if sp is not None:
+                out[f"{k}_spk"] = np.asarray(sp, np.float32 if np.ndim(sp) else np.int64)
             out[f"{k}_dec"] = dec.astype(np.float32)
             out[f"{k}_post"] = post.astype(np.float32)
             out[f"{k}_align"] = align.astype(np.float32)
@@ -221,6 +231,17 @@ if __name__ == "__main__":
         taco_case("taco_sigmoid", TacotronConfig(attn_norm="sigmoid"), seed=1,
                   utt_lens=[12, 37, 80], r_list=[2, 1], max_steps={2: 70, 1: 110},
                   min_stopping=2, id_seed=7)
+    if "taco_multispk" in which:  # learned speaker table (4 speakers x 512)
+        taco_case("taco_multispk", TacotronConfig(attn_norm="sigmoid", num_speakers=4), seed=11,
+                  utt_lens=[21, 44, 15], r_list=[2], max_steps={2: 60}, min_stopping=1, id_seed=9,
+                  speakers=[2, 0, 3])
+    if "taco_extspk" in which:  # external per-sample speaker embeddings (GE2E-style, 256-d)
+        rs = np.random.RandomState(12)
+        embs = [(rs.randn(256) / 16.0).astype(np.float32) for _ in range(2)]
+        embs = [e / np.linalg.norm(e) for e in embs]
+        taco_case("taco_extspk", TacotronConfig(attn_norm="sigmoid", num_speakers=2, speaker_embedding_dim=256),
+                  seed=9, utt_lens=[30, 18], r_list=[2], max_steps={2: 60}, min_stopping=1, id_seed=10,
+                  speakers=embs)
     if "taco_softmax" in which:
         taco_case("taco_softmax", TacotronConfig(attn_norm="softmax"), seed=2,
                   utt_lens=[25, 9], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=8)

@@ -79,9 +79,32 @@ def test_tacotron2_oracle_softmax_matches_reference():
         assert np.abs(align - fx[k + "_align"]).max() <= 1e-6
 
 
+def speaker_vector(fx, sd, k):
+    """The speaker vector of fixture utterance k: a row of the learned table (speaker id) or the
+    stored external embedding (models/tacotron2.py:152-155)."""
+    sp = fx[k + "_spk"]
+    return sd["speaker_embedding.weight"][int(sp)] if sp.ndim == 0 else sp
+
+
+@pytest.mark.parametrize("name,n", [("taco_multispk", 3), ("taco_extspk", 2)])
+def test_tacotron2_oracle_multispeaker_matches_reference(name, n):
+    fx = load_fixture(name)
+    cfg, sd = taco_state_dict(fx, r=2)
+    assert cfg.num_speakers > 1
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for u in range(n):
+        k = f"r2_u{u}"
+        dec, post, align, stop = orc.inference(fx[k + "_ids"], 2, int(fx["r2_max_steps"]),
+                                               speaker=speaker_vector(fx, sd, k))
+        assert len(stop) == len(fx[k + "_stop"])
+        assert np.abs(post - fx[k + "_post"]).max() <= 1e-5
+        assert np.abs(align - fx[k + "_align"]).max() <= 1e-6
+        assert np.abs(stop - fx[k + "_stop"]).max() <= 1e-5
+
+
 def test_fixture_fp64_drift_is_small():
     """Every Tacotron2 fixture records its fp32-vs-fp64 drift; the 1e-4 tolerance needs it tiny."""
-    for name in ("taco_sigmoid", "taco_softmax"):
+    for name in ("taco_sigmoid", "taco_softmax", "taco_multispk", "taco_extspk"):
         fx = load_fixture(name)
         drifts = [float(fx[k]) for k in fx.files if k.endswith("_drift64")]
         assert drifts and max(drifts) < 1e-6

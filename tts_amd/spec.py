@@ -15,7 +15,7 @@ generator (``tts_amd.weights``) to pick a scale, and by the packers to know what
 """
 
 from dataclasses import dataclass, field
-from typing import List, Tuple
+from typing import List, Optional, Tuple
 
 Spec = List[Tuple[str, Tuple[int, ...], str]]
 
@@ -42,6 +42,22 @@ class TacotronConfig:
     attn_dim: int = 128
     loc_filters: int = 32
     loc_kernel: int = 31
+    # multi-speaker (models/tacotron2.py:50-58): num_speakers > 1 concatenates a speaker vector to
+    # every encoder output; a learned nn.Embedding(num_speakers, 512) unless speaker_embedding_dim
+    # is given (external per-sample embeddings, tacotron_abstract.py:76-81)
+    num_speakers: int = 0
+    speaker_embedding_dim: Optional[int] = None
+
+    @property
+    def spk_dim(self) -> int:
+        if self.num_speakers <= 1:
+            return 0
+        return 512 if self.speaker_embedding_dim is None else int(self.speaker_embedding_dim)
+
+    @property
+    def decoder_in(self) -> int:
+        """decoder_in_features (models/tacotron2.py:57-58)."""
+        return self.encoder_dim + self.spk_dim
 
 
 @dataclass
@@ -74,7 +90,7 @@ def _conv_bn(prefix: str, cin: int, cout: int, k: int) -> Spec:
 
 
 def _decoder(prefix: str, c: TacotronConfig, r: int) -> Spec:
-    E, Q, D, P, A = c.encoder_dim, c.query_dim, c.decoder_rnn_dim, c.prenet_dim, c.attn_dim
+    E, Q, D, P, A = c.decoder_in, c.query_dim, c.decoder_rnn_dim, c.prenet_dim, c.attn_dim
     F = c.frame_channels
     s: Spec = [
         (f"{prefix}.prenet.linear_layers.0.linear_layer.weight", (P, F), "linear_relu"),
@@ -109,9 +125,12 @@ def _decoder(prefix: str, c: TacotronConfig, r: int) -> Spec:
 
 
 def tacotron2_spec(c: TacotronConfig) -> Spec:
-    """Ordered state_dict spec of ``Tacotron2`` (single speaker, no GST)."""
+    """Ordered state_dict spec of ``Tacotron2`` (no GST)."""
     E = c.encoder_dim
-    s: Spec = [("embedding.weight", (c.num_chars, E), "embedding")]
+    s: Spec = []
+    if c.num_speakers > 1 and c.speaker_embedding_dim is None:
+        s.append(("speaker_embedding.weight", (c.num_speakers, 512), "speaker_emb"))
+    s.append(("embedding.weight", (c.num_chars, E), "embedding"))
     for i in range(3):
         s += _conv_bn(f"encoder.convolutions.{i}", E, E, 5)
     H = E // 2

@@ -70,6 +70,8 @@ def synth_tensor(name: str, shape: Tuple[int, ...], kind: str, seed: int,
     elif kind in ("lstm", "lstm_enc"):
         H = shape[0] // 4
         x = u / math.sqrt(H)
+    elif kind == "speaker_emb":  # normal_(0, 0.3) in the reference: same std, uniform
+        x = u * (0.3 * math.sqrt(3.0))
     elif kind == "bias":
         x = 0.05 * u
     elif kind == "stop_bias":
