@@ -8,6 +8,7 @@
  *   tts_taco_set_tensor/finalize  <- Tacotron2.load_state_dict(cp['model'])
  *                                    (TTS/server/synthesizer.py:68-79, TTS/tts/utils/io.py:9-24)
  *   tts_taco_infer                <- Tacotron2.inference(text)  (TTS/tts/models/tacotron2.py:142-163)
+ *   tts_taco_infer_spk            <- Tacotron2.inference(text, speaker_ids | speaker_embeddings)
  *                                    with decoder.set_r / max_decoder_steps (layers/tacotron2.py:209,156)
  *   tts_taco_encoder              <- embedding + Encoder.inference (models/tacotron2.py:144-145,
  *                                    layers/tacotron2.py:112-119)
@@ -59,6 +60,19 @@ int tts_taco_finalize(tts_ctx* ctx, int num_chars, int r_init, int attn_norm);
 int tts_taco_infer(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
                    const int32_t* h_max_steps, int S_cap, float stop_threshold, float* d_dec, float* d_post,
                    float* d_align, float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream);
+
+/* Multi-speaker Tacotron2.inference(text, speaker_ids=..., speaker_embeddings=...)
+   (TTS/tts/models/tacotron2.py:142-156; speaker vector concatenated to the encoder outputs,
+   tacotron_abstract.py:213-217). Exactly one of d_spk_ids (int64 (B), rows of the learned
+   speaker_embedding table) or d_spk_emb (float (B, spk_dim), external per-sample embeddings) is
+   non-null. At most 32 utterances per call. Other arguments as tts_taco_infer. */
+int tts_taco_infer_spk(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                       const int32_t* h_max_steps, int S_cap, float stop_threshold, const int64_t* d_spk_ids,
+                       const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
+                       int32_t* h_steps, int32_t* h_status, void* stream);
+
+/* speaker dimension of the finalized model (0 = single speaker) and its learned table size */
+int tts_taco_speaker_dim(tts_ctx* ctx, int* spk_dim, int* num_speakers);
 
 /* encoder outputs (B, T_max, 512), zero for t >= h_lens[b] */
 int tts_taco_encoder(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max,

@@ -167,6 +167,42 @@ def test_tacotron2_batched_matches_reference(taco_sig, r):
                 m.last_steps, range(3))
 
 
+@pytest.mark.parametrize("name,n", [("taco_multispk", 3), ("taco_extspk", 2)])
+def test_tacotron2_multispeaker_matches_reference(name, n):
+    """Multi-speaker Tacotron2 (models/tacotron2.py:50-58,152-155), every utterance of the fixture
+    in ONE batched call with its own speaker: learned table ids, or external 256-d embeddings."""
+    _dev()
+    fx = load_fixture(name)
+    r = 2
+    cfg, sd = taco_state_dict(fx, r=r)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(r)
+    m.decoder.max_decoder_steps = int(fx[f"r{r}_max_steps"])
+    ids = [fx[f"r{r}_u{i}_ids"] for i in range(n)]
+    spk = [fx[f"r{r}_u{i}_spk"] for i in range(n)]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((n, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    kw = ({"speaker_embeddings": torch.from_numpy(np.stack(spk)).cuda()} if spk[0].ndim
+          else {"speaker_ids": torch.tensor([int(x) for x in spk])})
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=[len(x) for x in ids], **kw)
+    _check_taco(fx, r, dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy(), stop.cpu().numpy(),
+                m.last_steps, range(n))
+
+
+def test_tacotron2_multispeaker_requires_speaker():
+    _dev()
+    fx = load_fixture("taco_multispk")
+    cfg, sd = taco_state_dict(fx, r=2)
+    m = build_taco(cfg, sd)
+    ids = torch.from_numpy(fx["r2_u0_ids"][None]).cuda()
+    with pytest.raises(ValueError):
+        m.inference(ids)
+    with pytest.raises(IndexError):
+        m.inference(ids, speaker_ids=torch.tensor([4]))
+
+
 @pytest.mark.parametrize("u", [0, 1, 2])
 def test_tacotron2_single_utterance_matches_reference(taco_sig, u):
     fx = taco_sig

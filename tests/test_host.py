@@ -62,7 +62,22 @@ def test_synthetic_weights_are_version_stable():
     assert sd["decoder.decoder_rnn.weight_hh"].dtype == np.float32
 
 
-@pytest.mark.parametrize("kw", [dict(num_speakers=4), dict(gst=True), dict(attn_win=True), dict(forward_attn=True),
+def test_multispeaker_state_dict_keys_and_shapes():
+    """models/tacotron2.py:50-58: a learned (num_speakers, 512) table, decoder_in_features 1024;
+    per-sample embeddings (tacotron_abstract.py:76-81): no table, 512 + speaker_embedding_dim."""
+    m = Tacotron2(num_chars=129, num_speakers=4, double_decoder_consistency=True, ddc_r=7)
+    sd = m.state_dict()
+    assert tuple(sd["speaker_embedding.weight"].shape) == (4, 512)
+    assert tuple(sd["decoder.attention.inputs_layer.linear_layer.weight"].shape) == (128, 1024)
+    assert tuple(sd["decoder.linear_projection.linear_layer.weight"].shape) == (560, 2048)
+    assert tuple(sd["coarse_decoder.decoder_rnn.weight_ih"].shape) == (4096, 2048)
+    m2 = Tacotron2(num_chars=129, num_speakers=2, speaker_embedding_dim=256)
+    sd2 = m2.state_dict()
+    assert "speaker_embedding.weight" not in sd2
+    assert tuple(sd2["decoder.attention_rnn.weight_ih"].shape) == (4096, 256 + 768)
+
+
+@pytest.mark.parametrize("kw", [dict(gst=True), dict(attn_win=True), dict(forward_attn=True),
                                 dict(prenet_type="bn"), dict(attn_type="graves"), dict(location_attn=False)])
 def test_unsupported_tacotron_variants_raise(kw):
     with pytest.raises(NotImplementedError):

@@ -35,6 +35,10 @@ SIGNATURES = [
     ("tts_taco_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_taco_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p,
                                       ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _c_int_p, _c_int_p, _vp]),
+    ("tts_taco_infer_spk", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p,
+                                          ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_int_p,
+                                          _c_int_p, _vp]),
+    ("tts_taco_speaker_dim", ctypes.c_int, [_vp, _c_i_p, _c_i_p]),
     ("tts_taco_encoder", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_taco_postnet", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_melgan_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
@@ -124,17 +128,31 @@ class Engine:
                                             num_res_blocks, 1 if use_pqmf else 0))
 
     # -- compute (device tensors) ----------------------------------------------------
-    def taco_infer(self, ids, lens, r, max_steps, S_cap, stop_threshold, dec, post, align, stop):
+    def taco_infer(self, ids, lens, r, max_steps, S_cap, stop_threshold, dec, post, align, stop,
+                   speaker_ids=None, speaker_embeddings=None):
         B, T = ids.shape
         lens_a, lens_p = _i32(lens)
         ms_a, ms_p = _i32(max_steps)
         steps = np.zeros(B, np.int32)
         status = np.zeros(B, np.int32)
-        _check(self.lib.tts_taco_infer(self.h, _ptr(ids), lens_p, B, T, r, ms_p, S_cap, float(stop_threshold),
-                                       _ptr(dec), _ptr(post), _ptr(align), _ptr(stop),
-                                       steps.ctypes.data_as(_c_int_p), status.ctypes.data_as(_c_int_p),
-                                       _stream(ids.device)))
+        if speaker_ids is None and speaker_embeddings is None:
+            _check(self.lib.tts_taco_infer(self.h, _ptr(ids), lens_p, B, T, r, ms_p, S_cap, float(stop_threshold),
+                                           _ptr(dec), _ptr(post), _ptr(align), _ptr(stop),
+                                           steps.ctypes.data_as(_c_int_p), status.ctypes.data_as(_c_int_p),
+                                           _stream(ids.device)))
+        else:
+            sid = None if speaker_ids is None else _ptr(speaker_ids)
+            semb = None if speaker_embeddings is None else _ptr(speaker_embeddings)
+            _check(self.lib.tts_taco_infer_spk(self.h, _ptr(ids), lens_p, B, T, r, ms_p, S_cap,
+                                               float(stop_threshold), sid, semb, _ptr(dec), _ptr(post),
+                                               _ptr(align), _ptr(stop), steps.ctypes.data_as(_c_int_p),
+                                               status.ctypes.data_as(_c_int_p), _stream(ids.device)))
         return steps, status
+
+    def taco_speaker_dim(self):
+        d, n = ctypes.c_int(0), ctypes.c_int(0)
+        _check(self.lib.tts_taco_speaker_dim(self.h, ctypes.byref(d), ctypes.byref(n)))
+        return d.value, n.value
 
     def taco_encoder(self, ids, lens, out):
         B, T = ids.shape

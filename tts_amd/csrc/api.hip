@@ -197,6 +197,14 @@ struct TacoModel {
   std::vector<float> proj_rows, proj_bias, pre1_host;
   DevBuf pj_w, pj_b;
   int pj_r = -1;
+  // multi-speaker (models/tacotron2.py:50-58, 152-155): the speaker vector s is constant over the
+  // encoder positions and the attention weights of a step sum to 1, so every ctx-fed GEMM splits
+  // into its 512 encoder columns plus W_s s, a per-utterance bias. Host copies of the speaker
+  // columns (rows in the kernels' order), spk_dim x ... each; spk_wT = [spk_dim][NSPK] for pj_r.
+  int spk_dim = 0, num_spk = 0;
+  DevBuf spk_table;  // speaker_embedding.weight (num_spk, 512) when learned
+  std::vector<float> spk_att_h, spk_dec_h, spk_penc_h, proj_spk;
+  DevBuf spk_wT;
 };
 
 struct TacoWS {
@@ -209,6 +217,7 @@ struct TacoWS {
   DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
   DevBuf ids, post, map;       // rows in decode order (longest first), output scatter map
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
+  DevBuf spk, spkid, spkb;     // speaker vectors (decode order), per-row biases [Bp][NSPK]
   bool enc_persist = false;    // the last encoder ran the persistent BiLSTM (lc = its barrier words)
   // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
   // longest-first rows finish); all share one configuration key
@@ -351,6 +360,23 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
   M.softmax = attn_norm;
   const int E = 512, H = 256, Q = 1024, D = 1024, P = 256, A = 128, F = 80;
   M.emb.upload(need(h, "embedding.weight", {num_chars, E}).d);
+  // decoder_in_features = 512 + speaker dim (models/tacotron2.py:57-58), read off inputs_layer
+  {
+    auto it = h.find("decoder.attention.inputs_layer.linear_layer.weight");
+    TTS_CHECK(it != h.end() && it->second.shape.size() == 2 && it->second.shape[1] >= E,
+              "missing tensor: decoder.attention.inputs_layer.linear_layer.weight");
+    M.spk_dim = (int)it->second.shape[1] - E;
+    TTS_CHECK(M.spk_dim <= 1024, "speaker embedding dim must be <= 1024");
+    auto st = h.find("speaker_embedding.weight");
+    M.num_spk = 0;
+    if (st != h.end()) {
+      TTS_CHECK(st->second.shape.size() == 2 && st->second.shape[1] == M.spk_dim,
+                "speaker_embedding.weight must be (num_speakers, decoder_in_features - 512)");
+      M.num_spk = (int)st->second.shape[0];
+      M.spk_table.upload(st->second.d);
+    }
+  }
+  const int S = M.spk_dim, ES = E + S;
   int pl2[8] = {2}, pl0[8] = {0};
   for (int i = 0; i < 3; ++i) {
     std::vector<float> Wm, b;
@@ -381,19 +407,22 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     M.whhT.upload(whh_all);
   }
   {  // processed_inputs = inputs_layer(enc)  (common_layers.py:262-263), K=1 conv, no bias
-    const auto& win = need(h, "decoder.attention.inputs_layer.linear_layer.weight", {A, E}).d;
+    const auto& win_all = need(h, "decoder.attention.inputs_layer.linear_layer.weight", {A, ES}).d;
+    const auto win = slice_cols(win_all, A, ES, 0, E);
     pack_conv(M.penc, win, std::vector<float>(A, 0.f), E, A, 1, 1, 1, pl0);
+    M.spk_penc_h = slice_cols(win_all, A, ES, E, ES);
   }
   M.pre1_host = need(h, "decoder.prenet.linear_layers.0.linear_layer.weight", {P, F}).d;
   M.pre1.upload(swz(M.pre1_host, P, F));
   M.pre2.upload(swz(need(h, "decoder.prenet.linear_layers.1.linear_layer.weight", {P, P}).d, P, P));
   {
-    const auto& wih = need(h, "decoder.attention_rnn.weight_ih", {4 * Q, P + E}).d;
+    const auto& wih = need(h, "decoder.attention_rnn.weight_ih", {4 * Q, P + ES}).d;
     const auto& whh = need(h, "decoder.attention_rnn.weight_hh", {4 * Q, Q}).d;
     const auto& bih = need(h, "decoder.attention_rnn.bias_ih", {4 * Q}).d;
     const auto& bhh = need(h, "decoder.attention_rnn.bias_hh", {4 * Q}).d;
-    auto wp = slice_cols(wih, 4 * Q, P + E, 0, P);
-    auto wc = slice_cols(wih, 4 * Q, P + E, P, P + E);
+    auto wp = slice_cols(wih, 4 * Q, P + ES, 0, P);
+    auto wc = slice_cols(wih, 4 * Q, P + ES, P, P + E);
+    M.spk_att_h = S ? lstm_tile_rows(slice_cols(wih, 4 * Q, P + ES, P + E, P + ES), Q, S) : std::vector<float>();
     M.att_p.upload(swz(lstm_tile_rows(wp, Q, P), 4 * Q, P));
     auto pre = hcat({{wc.data(), E}, {whh.data(), Q}}, 4 * Q);
     M.att_pre.upload(swz(lstm_tile_rows(pre, Q, E + Q), 4 * Q, E + Q));
@@ -429,10 +458,12 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     M.bv = need(h, "decoder.attention.v.linear_layer.bias", {1}).d[0];
   }
   {
-    const auto& wih = need(h, "decoder.decoder_rnn.weight_ih", {4 * D, Q + E}).d;
+    const auto& wih_all = need(h, "decoder.decoder_rnn.weight_ih", {4 * D, Q + ES}).d;
     const auto& whh = need(h, "decoder.decoder_rnn.weight_hh", {4 * D, D}).d;
     const auto& bih = need(h, "decoder.decoder_rnn.bias_ih", {4 * D}).d;
     const auto& bhh = need(h, "decoder.decoder_rnn.bias_hh", {4 * D}).d;
+    const auto wih = slice_cols(wih_all, 4 * D, Q + ES, 0, Q + E);
+    M.spk_dec_h = S ? lstm_tile_rows(slice_cols(wih_all, 4 * D, Q + ES, Q + E, Q + ES), D, S) : std::vector<float>();
     auto w = hcat({{wih.data(), Q + E}, {whh.data(), D}}, 4 * D);
     M.dec_w.upload(swz(lstm_tile_rows(w, D, Q + E + D), 4 * D, Q + E + D));
     std::vector<float> bsum(4 * D);
@@ -441,9 +472,22 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
   }
   {
     const int NP = F * r_init;
-    const auto& wp = need(h, "decoder.linear_projection.linear_layer.weight", {NP, D + E}).d;
+    const auto& wp_all = need(h, "decoder.linear_projection.linear_layer.weight", {NP, D + ES}).d;
     const auto& bp = need(h, "decoder.linear_projection.linear_layer.bias", {NP}).d;
     const auto& ws = need(h, "decoder.stopnet.1.linear_layer.weight", {1, D + NP}).d;
+    const auto wp = slice_cols(wp_all, NP, D + ES, 0, D + E);
+    // speaker columns of [stop tile | W_p] (stop row = sum_o w_y,o W_p,s[o]), same row order
+    M.proj_spk.assign((size_t)(16 + NP) * S, 0.f);
+    for (int o = 0; o < NP && S; ++o)
+      for (int k = 0; k < S; ++k) {
+        const float v = wp_all[(size_t)o * (D + ES) + D + E + k];
+        M.proj_spk[(size_t)(16 + o) * S + k] = v;
+      }
+    for (int k = 0; k < S; ++k) {
+      double acc = 0.0;
+      for (int o = 0; o < NP; ++o) acc += (double)ws[D + o] * wp_all[(size_t)o * (D + ES) + D + E + k];
+      M.proj_spk[k] = (float)acc;
+    }
 
     // stopnet folded through the projection (tacotron2.py:286-295, the stopnet sees all r_init
     // frames): stop = [w_h + W_p,h^T w_y | W_p,ctx^T w_y] . [h | ctx] + (b_s + w_y . b_p)
@@ -532,6 +576,8 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<int>(W.map, BMAX, g);
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
   grow<unsigned>(W.pbar, 512, g);
+  grow<float>(W.spk, (size_t)64 * 1024, g);
+  grow<int64_t>(W.spkid, 64, g);
   W.B = B;
   W.T_max = T_max;
   W.S_cap = S_cap;
@@ -706,6 +752,35 @@ __global__ void bcast_rows_kernel(const float* src, int n, float* dst, int rows)
     dst[i] = src[i % n];
 }
 
+// Per-row biases of the persistent decoder, one column per thread:
+//   out[m][n] = base[n] + sum_e spk[m][e] WT[e][n]   (m < B; rows B..Bp-1 get base[n])
+// base = 0 on the attention_rnn / decoder_rnn / processed-inputs columns, the projection bias on
+// the projection columns [pj0, N). With no speaker (Es = 0) only the projection columns are built.
+constexpr int SPK_BMAX = 32;
+__global__ __launch_bounds__(256) void spk_bias_kernel(const float* __restrict__ spk, int B, int Es,
+                                                       const float* __restrict__ WT, int N,
+                                                       const float* __restrict__ pjb, int pj0, int Bp,
+                                                       float* __restrict__ out) {
+  extern __shared__ float sv[];  // [B][Es]
+  for (int i = threadIdx.x; i < B * Es; i += blockDim.x) sv[i] = spk[i];
+  __syncthreads();
+  const int n = blockIdx.x * blockDim.x + threadIdx.x;
+  if (n >= N) return;
+  float acc[SPK_BMAX];
+#pragma unroll
+  for (int m = 0; m < SPK_BMAX; ++m) acc[m] = 0.f;
+  for (int e = 0; e < Es; ++e) {
+    const float w = WT[(long)e * N + n];
+#pragma unroll
+    for (int m = 0; m < SPK_BMAX; ++m)
+      if (m < B) acc[m] = fmaf(sv[m * Es + e], w, acc[m]);
+  }
+  const float base = n >= pj0 ? pjb[n - pj0] : 0.f;
+#pragma unroll
+  for (int m = 0; m < SPK_BMAX; ++m)
+    if (m < Bp) out[(long)m * N + n] = base + (m < B ? acc[m] : 0.f);
+}
+
 void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_out, hipStream_t s) {
   auto& M = c->taco;
   auto& W = c->tws;
@@ -858,6 +933,27 @@ void build_pj(tts_ctx* c, int r) {
   }
   M.pj_w.upload(swz(rows, rows_p + P, K));
   M.pj_b.upload(bias);
+  if (M.spk_dim) {
+    // speaker columns, transposed [Es][att 4096 | dec 4096 | penc 128 | pj rows_p + P]
+    const int S = M.spk_dim, N = 4096 + 4096 + 128 + rows_p + P;
+    std::vector<float> wt((size_t)S * N);
+    auto put = [&](const std::vector<float>& rm, int n0, int nrows) {
+      for (int i = 0; i < nrows; ++i)
+        for (int e = 0; e < S; ++e) wt[(size_t)e * N + n0 + i] = rm[(size_t)i * S + e];
+    };
+    put(M.spk_att_h, 0, 4096);
+    put(M.spk_dec_h, 4096, 4096);
+    put(M.spk_penc_h, 8192, 128);
+    put(M.proj_spk, 8320, rows_p);
+    const float* sl = M.proj_spk.data() + (size_t)(16 + F * (r - 1)) * S;  // last frame's rows
+    for (int k = 0; k < P; ++k)
+      for (int e = 0; e < S; ++e) {
+        double acc = 0.0;
+        for (int i = 0; i < F; ++i) acc += (double)M.pre1_host[(size_t)k * F + i] * sl[(size_t)i * S + e];
+        wt[(size_t)e * N + 8320 + rows_p + k] = (float)acc;
+      }
+    M.spk_wT.upload(wt);
+  }
   M.pj_r = r;
 }
 
@@ -880,6 +976,23 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.attp_w = M.att_p.f();
   a.pj_w = M.pj_w.f();
   a.pj_b = M.pj_b.f();
+  {  // per-row biases: projection (always), speaker columns when the model has them
+    const int YP = (1 + 5 * r + 16) * 16;
+    const int N = M.spk_dim ? 8320 + YP : YP;
+    const int pj0 = M.spk_dim ? 8320 : 0;
+    const int Bp = W.MT * 16;
+    grow<float>(W.spkb, (size_t)64 * (8320 + 112 * 16), W.gen);
+    TTS_CHECK(W.B <= SPK_BMAX || !M.spk_dim, "multi-speaker decoding: at most 32 utterances per call");
+    const int Bs = M.spk_dim ? W.B : 0;
+    spk_bias_kernel<<<(N + 255) / 256, 256, (size_t)Bs * M.spk_dim * 4, s>>>(
+        W.spk.f(), Bs, M.spk_dim, M.spk_dim ? M.spk_wT.f() : nullptr, N, M.pj_b.f(), pj0, Bp, W.spkb.f());
+    HIP_OK(hipGetLastError());
+    a.spk_ld = N;
+    a.pjb_rows = W.spkb.f() + pj0;
+    a.spk_att = M.spk_dim ? W.spkb.f() : nullptr;
+    a.spk_dec = M.spk_dim ? W.spkb.f() + 4096 : nullptr;
+    a.spk_penc = M.spk_dim ? W.spkb.f() + 8192 : nullptr;
+  }
   a.pre2_w = M.pre2.f();
   a.WqT = M.WqT.f();
   a.Wcomb = M.Wcomb.f();
@@ -947,7 +1060,8 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
 
 void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, int T_max, int r,
                 const int32_t* h_max_steps, int S_cap, float thr, float* d_dec, float* d_post, float* d_align,
-                float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream) {
+                float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream,
+                const int64_t* d_spk_ids = nullptr, const float* d_spk_emb = nullptr) {
   auto& M = c->taco;
   TTS_CHECK(M.ready, "tacotron2 weights not finalized");
   TTS_CHECK(B >= 1 && B <= BMAX, "B must be in [1, 64]");
@@ -986,6 +1100,20 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   for (int i = 0; i < B; ++i) lens[i] = h_lens[perm[i]];
   HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
   W.thr = thr;
+  // speaker vectors in decode order: external embeddings, or rows of the learned table
+  if (M.spk_dim) {
+    TTS_CHECK(d_spk_ids || d_spk_emb, "multi-speaker model: speaker ids or speaker embeddings are required");
+    TTS_CHECK(use_persistent(c), "multi-speaker decoding runs on the persistent decoder only (<= 32 utterances "
+                                 "per call on a 256-CU device)");
+    if (d_spk_emb) {
+      gather_rows<float>(d_spk_emb, W.spk.f(), d_map, M.spk_dim, B, s);
+    } else {
+      TTS_CHECK(M.num_spk > 0, "model has no speaker_embedding table: pass speaker embeddings");
+      gather_rows<int64_t>(d_spk_ids, reinterpret_cast<int64_t*>(W.spkid.p), d_map, 1, B, s);
+      launch_embed_gather(reinterpret_cast<const int64_t*>(W.spkid.p), 1, M.spk_table.f(), M.num_spk, M.spk_dim,
+                          W.lens.i(), B, W.spk.f(), s);
+    }
+  }
   // encoder + processed inputs
   run_encoder(c, reinterpret_cast<const int64_t*>(W.ids.p), B, T_max, W.enc.f(), s);
   {
@@ -1405,12 +1533,19 @@ int tts_taco_set_tensor(tts_ctx* c, const char* name, const float* h, const int6
   });
 }
 
+// finalize consumes the tensors staged by *_set_tensor, so the next model starts from an empty map
+struct HostMapConsumer {
+  HostMap& m;
+  ~HostMapConsumer() { m.clear(); }
+};
+
 int tts_taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
   return guarded([&] {
     TTS_CHECK(c, "null ctx");
     TTS_CHECK(attn_norm == 0 || attn_norm == 1, "attn_norm must be 0 (sigmoid) or 1 (softmax)");
     TTS_CHECK(r_init >= 1 && r_init <= 16, "r_init out of range");
     DeviceGuard g(c->device);
+    HostMapConsumer consume{c->taco_host};  // staged tensors are consumed, even on failure
     taco_finalize(c, num_chars, r_init, attn_norm);
   });
 }
@@ -1424,6 +1559,28 @@ int tts_taco_infer(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int 
     DeviceGuard g(c->device);
     taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
                h_status, stream);
+  });
+}
+
+int tts_taco_infer_spk(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                       const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
+                       const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
+                       int32_t* h_steps, int32_t* h_status, void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && h_steps && h_status,
+              "null argument");
+    DeviceGuard g(c->device);
+    taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+               h_status, stream, d_spk_ids, d_spk_emb);
+  });
+}
+
+int tts_taco_speaker_dim(tts_ctx* c, int* spk_dim, int* num_speakers) {
+  return guarded([&] {
+    TTS_CHECK(c && spk_dim && num_speakers, "null argument");
+    TTS_CHECK(c->taco.ready, "tacotron2 weights not finalized");
+    *spk_dim = c->taco.spk_dim;
+    *num_speakers = c->taco.num_spk;
   });
 }
 
@@ -1486,6 +1643,7 @@ int tts_melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32
   return guarded([&] {
     TTS_CHECK(c && ups && n_up >= 1 && n_up <= 6, "bad arguments");
     DeviceGuard g(c->device);
+    HostMapConsumer consume{c->mg_host};
     melgan_finalize(c, in_ch, out_ch, base, ups, n_up, nres, use_pqmf);
   });
 }

@@ -111,6 +111,14 @@ struct PArgs {
   const float* attp_w;  // [256][16][64][4] attention_rnn W_ih,prenet
   const float* pj_w;    // [ntj][96][64][4] stop tile, 5r frame tiles, 16 folded prenet-1 tiles
   const float* pj_b;    // [ntj * 16]
+  // per-row biases (api.hip spk_bias_kernel), row stride spk_ld: projection bias per row (always),
+  // speaker parts W_s s of the attention_rnn / decoder_rnn gates and processed inputs (null
+  // without speakers)
+  const float* pjb_rows;
+  const float* spk_att;
+  const float* spk_dec;
+  const float* spk_penc;
+  int spk_ld;
   const float* pre2_w;  // [16][16][64][4]
   const float* WqT;     // [1024][128]
   const float* Wcomb;   // [64][128]: location_dense . location_conv as one 62-tap filter per dim

@@ -144,6 +144,11 @@ __device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* A
     const int pos = 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3);
     pen[i] = P.penc[((long)b * D.T_max + min(t0 + pos, Tm1)) * ADIM_ + a];
   }
+  if (P.spk_penc) {  // processed inputs of the speaker columns: W_in,s s, constant over positions
+    const float ps = P.spk_penc[(long)b * P.spk_ld + a];
+#pragma unroll
+    for (int i = 0; i < 8; ++i) pen[i] += ps;
+  }
   if (tid < 128) Aw[tid] = aw;
   lds_barrier();
   // location_dense(location_conv(.)) on MFMA: E[pos][dim] = sum_j X[pos][j] Wcomb[j][dim],
@@ -455,7 +460,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   // ctx/h-part bias of its column
   float db[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) db[q] = P.dec_b[g * 16 + q * 4 + (tid & 3)];
+  for (int q = 0; q < 4; ++q) {  // + the row's speaker part (W_dec,s s, api.hip spk_bias_kernel)
+    db[q] = P.dec_b[g * 16 + q * 4 + (tid & 3)];
+    if (P.spk_dec) db[q] += P.spk_dec[(long)min(tid >> 2, Bp - 1) * P.spk_ld + g * 16 + q * 4 + (tid & 3)];
+  }
   const float apb = P.apre_b[g * 16 + (tid & 15)];
   __syncthreads();
 
@@ -486,7 +494,9 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     lds_barrier();
     for (int idx = tid; idx < Bp * 16; idx += PT) {
       const int m = idx >> 4, n = idx & 15;
-      stc(P.gatt + (long)m * 4096 + g * 16 + n, lds_sum<NWV, Bp>(red, m, n) + apb);
+      float v = lds_sum<NWV, Bp>(red, m, n) + apb;
+      if (P.spk_att) v += P.spk_att[(long)m * P.spk_ld + g * 16 + n];  // speaker part of the new ctx
+      stc(P.gatt + (long)m * 4096 + g * 16 + n, v);
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -502,7 +512,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       const int m = idx / FR, c = idx - m * FR;
       if (!ldci(D.done + m) || ldci(D.steps + m) > s) {
         const float v = ldc(P.ypart + (long)m * YP + 16 + c) + ldc(P.ypart + (long)(YROWS + m) * YP + 16 + c) +
-                        P.pj_b[16 + c];
+                        P.pjb_rows[(long)m * P.spk_ld + 16 + c];
         D.dec_out[((long)m * D.S_cap + s) * FR + c] = v;
       }
     }
@@ -523,10 +533,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       if (t > 0) {  // t = 0: prenet input is the zero go-frame, layer 1 has no bias -> 0
         const int kc = 8 * (g >> 4) + wave;
         const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pj_b + col);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int m = mt * 16 + (lane & 15);
+          const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pjb_rows + (long)m * P.spk_ld + col);
           f32x4 x = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
 #pragma unroll
           for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
@@ -551,7 +561,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         const int m = tid;
         int dn = ldci(D.done + m);
         if (t >= 1 && !dn) {
-          const float logit = ldc(P.ypart + (long)m * YP) + ldc(P.ypart + (long)(YROWS + m) * YP) + P.pj_b[0];
+          const float logit = ldc(P.ypart + (long)m * YP) + ldc(P.ypart + (long)(YROWS + m) * YP) +
+                              P.pjb_rows[(long)m * P.spk_ld];
           const float sg = sigm(logit);
           if (t - 1 < D.S_cap) D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
           const bool st = (sg > P.thr) && (t - 1) > 0;

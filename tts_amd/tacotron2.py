@@ -25,6 +25,7 @@ from .params import Container, host_tensors, new_token, populate
 from .spec import TacotronConfig, tacotron2_spec
 
 BATCH_LIMIT = 64
+SPEAKER_BATCH_LIMIT = 32  # multi-speaker decoding runs on the persistent decoder (<= 32 rows)
 
 
 class Decoder(Container):
@@ -52,8 +53,6 @@ class Tacotron2(nn.Module):
                  gst_num_heads=4, gst_style_tokens=10, gst_use_speaker_embedding=False):
         super().__init__()
         unsupported = []
-        if num_speakers > 1:
-            unsupported.append("multi-speaker embeddings")
         if gst:
             unsupported.append("GST")
         if attn_type != "original":
@@ -68,7 +67,7 @@ class Tacotron2(nn.Module):
             unsupported.append(f"prenet_type={prenet_type}")
         if bidirectional_decoder:
             unsupported.append("bidirectional_decoder")
-        if encoder_in_features != 512 or decoder_in_features != 512:
+        if encoder_in_features != 512 or decoder_in_features != 512:  # before the speaker columns
             unsupported.append("non-default encoder/decoder feature sizes")
         if decoder_output_dim != 80 or postnet_output_dim != 80:
             unsupported.append("frame channels != 80")
@@ -84,7 +83,12 @@ class Tacotron2(nn.Module):
         self.double_decoder_consistency = double_decoder_consistency
         self.cfg = TacotronConfig(num_chars=num_chars, r=r, attn_norm=attn_norm,
                                   double_decoder_consistency=double_decoder_consistency,
-                                  ddc_r=ddc_r if ddc_r is not None else r)
+                                  ddc_r=ddc_r if ddc_r is not None else r,
+                                  num_speakers=num_speakers, speaker_embedding_dim=speaker_embedding_dim)
+        # models/tacotron2.py:50-58 / tacotron_abstract.py:76-81: a learned table unless the caller
+        # gives per-sample embeddings of speaker_embedding_dim
+        self.embeddings_per_sample = speaker_embedding_dim is not None
+        self.speaker_embedding_dim = self.cfg.spk_dim
         self.decoder = Decoder(r, decoder_output_dim)
         populate(self, tacotron2_spec(self.cfg))
         self._version = 0
@@ -92,6 +96,33 @@ class Tacotron2(nn.Module):
         self.last_steps = None
         self.last_mel_lengths = None
         self.last_status = None
+
+    def _speaker_args(self, speaker_ids, speaker_embeddings, B, dev):
+        """Speaker conditioning as the reference takes it (models/tacotron2.py:152-155): ids into
+        the learned table, or per-sample embeddings (B, speaker_embedding_dim) / (B, 1, dim)."""
+        if self.num_speakers <= 1:
+            if speaker_ids is not None or speaker_embeddings is not None:
+                raise ValueError("single-speaker model: speaker_ids / speaker_embeddings must be None")
+            return None, None
+        if self.embeddings_per_sample:
+            if speaker_embeddings is None:
+                raise ValueError("this model takes per-sample speaker_embeddings")
+            e = torch.as_tensor(speaker_embeddings).to(dev, torch.float32).reshape(-1, self.speaker_embedding_dim)
+            if e.shape[0] == 1 and B > 1:
+                e = e.expand(B, -1)
+            if e.shape[0] != B:
+                raise ValueError("speaker_embeddings must have one row per utterance")
+            return None, e.contiguous()
+        if speaker_ids is None:
+            raise ValueError("multi-speaker model: speaker_ids are required")
+        ids = torch.as_tensor(speaker_ids).reshape(-1).to(torch.int64)
+        if ids.numel() == 1 and B > 1:
+            ids = ids.expand(B)
+        if ids.numel() != B:
+            raise ValueError("speaker_ids must have one entry per utterance")
+        if int(ids.min()) < 0 or int(ids.max()) >= self.num_speakers:
+            raise IndexError("speaker id out of range")  # nn.Embedding raises too
+        return ids.to(dev).contiguous(), None
 
     # any change of parameters or placement invalidates the packed device copy
     def load_state_dict(self, state_dict, strict=True, **kw):
@@ -121,8 +152,8 @@ class Tacotron2(nn.Module):
     @torch.no_grad()
     def inference(self, text, speaker_ids=None, style_mel=None, speaker_embeddings=None,
                   text_lengths: Optional[Sequence[int]] = None, max_decoder_steps=None):
-        if speaker_ids is not None or speaker_embeddings is not None or style_mel is not None:
-            raise NotImplementedError("speaker / style conditioning is not implemented (SURVEY.md §8f)")
+        if style_mel is not None:
+            raise NotImplementedError("GST style conditioning is not implemented (SURVEY.md §8f)")
         dev = self.embedding.weight.device
         eng = get_engine(dev)
         self._sync(eng)
@@ -140,9 +171,11 @@ class Tacotron2(nn.Module):
         r = int(self.decoder.r)
         if not 1 <= r <= self.decoder.r_init:
             raise ValueError(f"r={r} must be in [1, r_init={self.decoder.r_init}]")
+        spk_ids, spk_emb = self._speaker_args(speaker_ids, speaker_embeddings, B, dev)
+        limit = BATCH_LIMIT if self.num_speakers <= 1 else SPEAKER_BATCH_LIMIT
         outs = []
-        for b0 in range(0, B, BATCH_LIMIT):
-            b1 = min(B, b0 + BATCH_LIMIT)
+        for b0 in range(0, B, limit):
+            b1 = min(B, b0 + limit)
             sub = text[b0:b1]
             Tn = int(lens[b0:b1].max())
             sub = sub[:, :Tn].contiguous()
@@ -152,8 +185,10 @@ class Tacotron2(nn.Module):
             post = torch.empty_like(dec)
             align = torch.empty(nb, S_cap, Tn, device=dev, dtype=torch.float32)
             stop = torch.empty(nb, S_cap, device=dev, dtype=torch.float32)
-            steps, status = eng.taco_infer(sub, lens[b0:b1], r, ms[b0:b1], S_cap, self.decoder.stop_threshold,
-                                           dec, post, align, stop)
+            steps, status = eng.taco_infer(
+                sub, lens[b0:b1], r, ms[b0:b1], S_cap, self.decoder.stop_threshold, dec, post, align, stop,
+                speaker_ids=None if spk_ids is None else spk_ids[b0:b1].contiguous(),
+                speaker_embeddings=None if spk_emb is None else spk_emb[b0:b1].contiguous())
             outs.append((dec, post, align, stop, steps, status, Tn))
         steps = np.concatenate([o[4] for o in outs])
         status = np.concatenate([o[5] for o in outs])
