@@ -103,6 +103,18 @@ int tts_melgan_generator(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens
 int tts_pqmf_synthesis(tts_ctx* ctx, const float* d_x, int B, int N, int L, const float* d_G, int taps,
                        float* d_y, void* stream);
 
+/* ---- GE2E speaker encoder (TTS/speaker_encoder/model.py) ----
+   tts_ge2e_set_tensor/finalize <- SpeakerEncoder(input_dim, proj_dim, lstm_dim, num_lstm_layers,
+                                   use_lstm_with_projection).load_state_dict  (model.py:31-47)
+   tts_ge2e_infer               <- SpeakerEncoder.inference(x) (model.py:62-68) on B sequences of
+                                   per-sequence length h_lens[b]: d_x (B, T_max, input_dim) fp32,
+                                   d_out (B, proj_dim) L2-normalised embeddings. lstm_dim must be 768. */
+int tts_ge2e_set_tensor(tts_ctx* ctx, const char* name, const float* host, const int64_t* shape, int ndim);
+int tts_ge2e_finalize(tts_ctx* ctx, int input_dim, int proj_dim, int lstm_dim, int num_lstm_layers,
+                      int use_lstm_with_projection);
+int tts_ge2e_infer(tts_ctx* ctx, const float* d_x, const int32_t* h_lens, int B, int T_max, float* d_out,
+                   void* stream);
+
 /* Measurement hook for bench.py: average device time (ms) of `iters` launches of one kernel of the
    last tts_taco_infer configuration, timed with hipEvents on the context's stream.
    which: 0 = decoder LSTM GEMM step kernel (K4), 1 = full decoder step (all 7 kernels). */

@@ -203,6 +203,30 @@ def pqmf_case(name):
     print(f"[{name}] synth {y.shape}; known answer {ka.shape}")
 
 
+def ge2e_case(name):
+    """GE2E speaker encoder (TTS/speaker_encoder/model.py): with and without projection."""
+    from TTS.speaker_encoder.model import SpeakerEncoder
+    from tts_amd.spec import Ge2eConfig, ge2e_spec
+    out = {}
+    rs = np.random.RandomState(21)
+    x = rs.normal(0, 1, size=(1, 230, 40)).astype(np.float32)
+    x2 = rs.normal(0, 1, size=(1, 37, 40)).astype(np.float32)
+    out["x"], out["x2"] = x, x2
+    for tag, proj, seed in (("proj", True, 6), ("noproj", False, 7)):
+        cfg = Ge2eConfig(use_lstm_with_projection=proj)
+        m = SpeakerEncoder(cfg.input_dim, cfg.proj_dim, cfg.lstm_dim, cfg.num_lstm_layers, proj)
+        sd = synth_state_dict(ge2e_spec(cfg), seed)
+        m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+        m.eval()
+        with torch.no_grad():
+            out[f"{tag}_seed"] = np.int64(seed)
+            out[f"{tag}_emb"] = m.inference(torch.from_numpy(x)).numpy()
+            out[f"{tag}_emb2"] = m.inference(torch.from_numpy(x2)).numpy()
+            out[f"{tag}_cemb"] = m.compute_embedding(torch.from_numpy(x), num_frames=160, overlap=0.5).numpy()
+        print(f"[{name}] {tag}: |emb| {np.linalg.norm(out[f'{tag}_emb']):.4f} cemb[:3] {out[f'{tag}_cemb'][0, :3]}")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
 def lj_profile():
     import scipy.io.wavfile as wavfile
     d = os.path.join(REF, "tests/data/ljspeech")
@@ -242,6 +266,8 @@ if __name__ == "__main__":
         taco_case("taco_extspk", TacotronConfig(attn_norm="sigmoid", num_speakers=2, speaker_embedding_dim=256),
                   seed=9, utt_lens=[30, 18], r_list=[2], max_steps={2: 60}, min_stopping=1, id_seed=10,
                   speakers=embs)
+    if "ge2e" in which:
+        ge2e_case("ge2e")
     if "taco_softmax" in which:
         taco_case("taco_softmax", TacotronConfig(attn_norm="softmax"), seed=2,
                   utt_lens=[25, 9], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=8)

@@ -422,3 +422,28 @@ def test_synthesizer_griffin_lim_fallback(tmp_path):
     wavs = synth.synthesize_batch(["Griffin and Lim.", "Phase from noise."])
     for w in wavs:
         assert np.isfinite(w).all() and abs(len(w) - 20 * 256) <= 256
+
+
+# --------------------------------------------------------------------- GE2E speaker encoder
+@pytest.mark.parametrize("tag,proj", [("proj", True), ("noproj", False)])
+def test_ge2e_speaker_encoder_matches_reference(tag, proj):
+    """SpeakerEncoder.inference / compute_embedding (TTS/speaker_encoder/model.py:62-88) on the
+    persistent 768-unit LSTM: both fixture sequences in ONE batched call with their own lengths."""
+    from tts_amd import SpeakerEncoder
+    from tts_amd.spec import Ge2eConfig, ge2e_spec
+    from tts_amd.weights import synth_state_dict
+    _dev()
+    fx = load_fixture("ge2e")
+    m = SpeakerEncoder(40, 256, 768, 3, proj)
+    sd = synth_state_dict(ge2e_spec(Ge2eConfig(use_lstm_with_projection=proj)), int(fx[f"{tag}_seed"]))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    x, x2 = fx["x"][0], fx["x2"][0]
+    batch = np.zeros((2, x.shape[0], 40), np.float32)
+    batch[0] = x
+    batch[1, :len(x2)] = x2
+    emb = m.inference(torch.from_numpy(batch).cuda(), lengths=[len(x), len(x2)]).cpu().numpy()
+    assert np.abs(emb[0] - fx[f"{tag}_emb"][0]).max() <= 1e-5
+    assert np.abs(emb[1] - fx[f"{tag}_emb2"][0]).max() <= 1e-5
+    cemb = m.compute_embedding(torch.from_numpy(fx["x"]).cuda()).cpu().numpy()
+    assert np.abs(cemb - fx[f"{tag}_cemb"]).max() <= 1e-5

@@ -108,3 +108,18 @@ def test_fixture_fp64_drift_is_small():
         fx = load_fixture(name)
         drifts = [float(fx[k]) for k in fx.files if k.endswith("_drift64")]
         assert drifts and max(drifts) < 1e-6
+
+
+@pytest.mark.parametrize("tag,proj", [("proj", True), ("noproj", False)])
+def test_ge2e_oracle_matches_reference(tag, proj):
+    """GE2E SpeakerEncoder (TTS/speaker_encoder/model.py): inference on two lengths and
+    compute_embedding (windows of 160, 50 % overlap) against the reference run."""
+    from oracle.ge2e_np import Ge2eOracle
+    from tts_amd.spec import Ge2eConfig, ge2e_spec
+    from tts_amd.weights import synth_state_dict
+    fx = load_fixture("ge2e")
+    sd = synth_state_dict(ge2e_spec(Ge2eConfig(use_lstm_with_projection=proj)), int(fx[f"{tag}_seed"]))
+    orc = Ge2eOracle(sd, 3, proj)
+    assert np.abs(orc.inference(fx["x"][0]) - fx[f"{tag}_emb"][0]).max() <= 2e-6
+    assert np.abs(orc.inference(fx["x2"][0]) - fx[f"{tag}_emb2"][0]).max() <= 2e-6
+    assert np.abs(orc.compute_embedding(fx["x"][0]) - fx[f"{tag}_cemb"][0]).max() <= 2e-6

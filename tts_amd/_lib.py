@@ -49,6 +49,10 @@ SIGNATURES = [
                                             _vp]),
     ("tts_pqmf_synthesis", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int,
                                           _vp, _vp]),
+    ("tts_ge2e_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
+    ("tts_ge2e_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                         ctypes.c_int]),
+    ("tts_ge2e_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_time_decoder_kernel", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_f_p]),
     ("tts_decoder_stats", ctypes.c_int, [_vp, _c_i_p, _c_i_p, _c_f_p, _c_i_p]),
 ]
@@ -102,6 +106,7 @@ class Engine:
         self.h = h
         self.taco_key = None
         self.melgan_key = None
+        self.ge2e_key = None
 
     def close(self):
         if self.h:
@@ -163,6 +168,16 @@ class Engine:
         B, M, _ = dec.shape
         lens_a, lens_p = _i32(lens)
         _check(self.lib.tts_taco_postnet(self.h, _ptr(dec), lens_p, B, M, _ptr(out), _stream(dec.device)))
+
+    def load_ge2e(self, tensors: Dict[str, np.ndarray], input_dim, proj_dim, lstm_dim, num_layers, with_proj):
+        for k, v in tensors.items():
+            self._set(self.lib.tts_ge2e_set_tensor, k, v)
+        _check(self.lib.tts_ge2e_finalize(self.h, input_dim, proj_dim, lstm_dim, num_layers, 1 if with_proj else 0))
+
+    def ge2e_infer(self, x, lens, out):
+        B, T, _ = x.shape
+        lens_a, lens_p = _i32(lens)
+        _check(self.lib.tts_ge2e_infer(self.h, _ptr(x), lens_p, B, T, _ptr(out), _stream(x.device)))
 
     def melgan_infer(self, mel, lens, pad, wav):
         B, _, M = mel.shape

@@ -19,6 +19,8 @@ void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int 
                          const int* lens, int B, float* out, hipStream_t s);
 bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
                            unsigned* bar, float* out, hipStream_t s);
+bool launch_lstm768_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
+                            unsigned* bar, float* out, hipStream_t s);
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
                    float* out,
                        hipStream_t s);
@@ -253,6 +255,22 @@ struct MelganWS {
 
 }  // namespace
 
+// GE2E speaker encoder (TTS/speaker_encoder/model.py:5-80): 3 x [LSTM(in -> 768), Linear(768 -> 256,
+// no bias)] (use_lstm_with_projection) or one 3-layer LSTM + Linear(bias) + ReLU on the last hidden
+// state; the embedding is the L2-normalised output at each sequence's last frame.
+struct Ge2eModel {
+  bool ready = false;
+  int in_dim = 40, in_pad = 48, proj = 256, H = 768, nl = 3, with_proj = 1;
+  ConvLayer gin[4];      // input projections (K = 1, Cout = 4H gate-interleaved tiles, b_ih + b_hh)
+  DevBuf whh[4];         // W_hh, swizzled tiles
+  ConvLayer proj_l[4];   // with_proj: Linear(768 -> proj) per layer as a K = 1 conv
+  DevBuf lin_w, lin_b;   // without projection: final Linear (proj x H) + bias
+};
+
+struct Ge2eWS {
+  DevBuf x, lens, g, o, p, bar, hbuf;
+};
+
 struct tts_ctx {
   int device = 0;
   hipStream_t s = nullptr;
@@ -266,6 +284,9 @@ struct tts_ctx {
   TacoWS tws;
   MelganModel mg;
   MelganWS mws;
+  HostMap ge2e_host;
+  Ge2eModel ge2e;
+  Ge2eWS gws;
   // last decode configuration (for tts_time_decoder_kernel)
   int last_B = 0, last_T = 0, last_S = 0, last_r = 0;
 };
@@ -1459,6 +1480,157 @@ int guarded(F&& f) {
   }
 }
 
+// (B, T, D) -> (B, T, Dp) with zero channels D..Dp-1 (the conv staging reads 16-channel chunks)
+__global__ void pad_channels_kernel(const float* __restrict__ x, int D, int Dp, long n_rows, float* __restrict__ y) {
+  for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_rows * Dp; i += (long)gridDim.x * blockDim.x) {
+    const long r = i / Dp;
+    const int c = (int)(i - r * Dp);
+    y[i] = c < D ? x[r * D + c] : 0.f;
+  }
+}
+
+// one workgroup per sequence: v = last frame (with_proj) or relu(W h_last + b), then
+// F.normalize(v, p=2, dim=1) = v / max(||v||, 1e-12)  (model.py:58-63)
+__global__ __launch_bounds__(256) void ge2e_final_kernel(const float* __restrict__ src, long sb, int width,
+                                                         const int* lens, int T_max, const float* __restrict__ W,
+                                                         const float* __restrict__ bias, int P,
+                                                         float* __restrict__ out) {
+  __shared__ float v[1024], red[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* last = src + b * sb + (long)(lens[b] - 1) * width;
+  for (int i = tid; i < P; i += blockDim.x) {
+    float x;
+    if (W) {
+      float acc = bias[i];
+      for (int k = 0; k < width; ++k) acc = fmaf(W[(long)i * width + k], last[k], acc);
+      x = fmaxf(acc, 0.f);
+    } else {
+      x = last[i];
+    }
+    v[i] = x;
+  }
+  __syncthreads();
+  float ss = 0.f;
+  for (int i = tid; i < P; i += blockDim.x) ss = fmaf(v[i], v[i], ss);
+  for (int off = 32; off > 0; off >>= 1) ss += __shfl_xor(ss, off, 64);
+  if ((tid & 63) == 0) red[tid >> 6] = ss;
+  __syncthreads();
+  const float nrm = fmaxf(sqrtf(red[0] + red[1] + red[2] + red[3]), 1e-12f);
+  for (int i = tid; i < P; i += blockDim.x) out[(long)b * P + i] = v[i] / nrm;
+}
+
+void ge2e_finalize(tts_ctx* c, int in_dim, int proj, int lstm, int nl, int with_proj) {
+  auto& G = c->ge2e;
+  const auto& h = c->ge2e_host;
+  G.ready = false;
+  TTS_CHECK(lstm == 768, "speaker encoder: lstm_dim must be 768 (the persistent LSTM kernel's width)");
+  TTS_CHECK(nl >= 1 && nl <= 4 && in_dim >= 1 && in_dim <= 1024 && proj >= 1 && proj <= 1024, "speaker encoder sizes");
+  G.in_dim = in_dim;
+  G.in_pad = (in_dim + 15) / 16 * 16;
+  G.proj = proj;
+  G.H = lstm;
+  G.nl = nl;
+  G.with_proj = with_proj;
+  const int H = lstm;
+  int pl0[8] = {0};
+  for (int l = 0; l < nl; ++l) {
+    const std::string pfx = with_proj ? "layers." + std::to_string(l) + ".lstm." : "layers.lstm.";
+    const std::string sfx = with_proj ? "_l0" : "_l" + std::to_string(l);
+    const int din = l == 0 ? in_dim : (with_proj ? proj : H);
+    const int dpad = l == 0 ? G.in_pad : din;
+    TTS_CHECK(dpad % 16 == 0, "speaker encoder: layer input width must be a multiple of 16");
+    const auto& wih = need(h, pfx + "weight_ih" + sfx, {4 * H, din}).d;
+    const auto& whh = need(h, pfx + "weight_hh" + sfx, {4 * H, H}).d;
+    const auto& bih = need(h, pfx + "bias_ih" + sfx, {4 * H}).d;
+    const auto& bhh = need(h, pfx + "bias_hh" + sfx, {4 * H}).d;
+    std::vector<float> wt = lstm_tile_rows(wih, H, din), w2((size_t)4 * H * dpad, 0.f);
+    for (int r = 0; r < 4 * H; ++r)
+      for (int k = 0; k < din; ++k) w2[(size_t)r * dpad + k] = wt[(size_t)r * din + k];
+    std::vector<float> bs(4 * H);
+    for (int i = 0; i < 4 * H; ++i) bs[i] = bih[i] + bhh[i];
+    pack_conv(G.gin[l], w2, lstm_tile_rows(bs, H, 1), dpad, 4 * H, 1, 1, 1, pl0);
+    G.whh[l].upload(swz(lstm_tile_rows(whh, H, H), 4 * H, H));
+    if (with_proj) {
+      const auto& wl = need(h, "layers." + std::to_string(l) + ".linear.weight", {proj, H}).d;
+      pack_conv(G.proj_l[l], wl, std::vector<float>(proj, 0.f), H, proj, 1, 1, 1, pl0);
+    }
+  }
+  if (!with_proj) {
+    G.lin_w.upload(need(h, "layers.linear.weight", {proj, H}).d);
+    G.lin_b.upload(need(h, "layers.linear.bias", {proj}).d);
+  }
+  HIP_OK(hipDeviceSynchronize());
+  G.ready = true;
+}
+
+void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int T_max, float* d_out) {
+  auto& G = c->ge2e;
+  auto& W = c->gws;
+  TTS_CHECK(G.ready, "speaker encoder weights not finalized");
+  TTS_CHECK(B >= 1 && B <= 64, "speaker encoder: B must be in [1, 64]");
+  TTS_CHECK(T_max >= 1 && T_max <= 100000, "speaker encoder: bad T_max");
+  for (int b = 0; b < B; ++b) TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= T_max, "speaker encoder: lens out of range");
+  hipStream_t s = c->s;
+  const int H = G.H;
+  long gen = 0;
+  grow<float>(W.x, (size_t)B * T_max * G.in_pad, gen);
+  grow<int>(W.lens, 64, gen);
+  grow<float>(W.g, (size_t)B * T_max * 4 * H, gen);
+  grow<float>(W.o, (size_t)B * T_max * H, gen);
+  grow<float>(W.p, (size_t)B * T_max * G.proj, gen);
+  grow<unsigned>(W.bar, 512, gen);
+  grow<float>(W.hbuf, (size_t)2 * 64 * H, gen);
+  std::vector<int> lens(h_lens, h_lens + B);
+  HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  pad_channels_kernel<<<1024, 256, 0, s>>>(d_x, G.in_dim, G.in_pad, (long)B * T_max, W.x.f());
+  HIP_OK(hipGetLastError());
+  const float* in = W.x.f();
+  int din = G.in_pad;
+  for (int l = 0; l < G.nl; ++l) {
+    ConvCall cc;  // gates_in = x W_ih^T + b  (time-major rows, K = 1)
+    cc.lens = W.lens.i();
+    cc.B = B;
+    cc.max_q = T_max;
+    cc.s[0] = src_of(in, (long)T_max * din, 1, din, din, 0);
+    cc.out = W.g.f();
+    cc.ob = (long)T_max * 4 * H;
+    cc.oc = 1;
+    cc.ot = 4 * H;
+    run_conv(G.gin[l], cc, s);
+    const bool ok = launch_lstm768_persist(W.g.f(), G.whh[l].f(), W.lens.i(), T_max, B, W.hbuf.f(),
+                                           reinterpret_cast<unsigned*>(W.bar.p), W.o.f(), s);
+    TTS_CHECK(ok, "speaker encoder: cooperative launch unavailable");
+    if (G.with_proj) {
+      ConvCall cp;
+      cp.lens = W.lens.i();
+      cp.B = B;
+      cp.max_q = T_max;
+      cp.s[0] = src_of(W.o.f(), (long)T_max * H, 1, H, H, 0);
+      cp.out = W.p.f();
+      cp.ob = (long)T_max * G.proj;
+      cp.oc = 1;
+      cp.ot = G.proj;
+      run_conv(G.proj_l[l], cp, s);
+      in = W.p.f();
+      din = G.proj;
+    } else {
+      in = W.o.f();
+      din = H;
+    }
+  }
+  if (G.with_proj)
+    ge2e_final_kernel<<<B, 256, 0, s>>>(W.p.f(), (long)T_max * G.proj, G.proj, W.lens.i(), T_max, nullptr, nullptr,
+                                        G.proj, d_out);
+  else
+    ge2e_final_kernel<<<B, 256, 0, s>>>(W.o.f(), (long)T_max * H, H, W.lens.i(), T_max, G.lin_w.f(), G.lin_b.f(),
+                                        G.proj, d_out);
+  HIP_OK(hipGetLastError());
+  HIP_OK(hipStreamSynchronize(s));
+  unsigned err = 0;
+  HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(W.bar.p) + 16, 4, hipMemcpyDeviceToHost));
+  TTS_CHECK(err == 0, "speaker encoder: grid barrier timed out (workgroups not co-resident)");
+}
+
 void set_tensor(HostMap& m, const char* name, const float* h, const int64_t* shape, int ndim) {
   TTS_CHECK(name && (h || ndim == 0), "set_tensor: null argument");
   HostT t;
@@ -1627,6 +1799,34 @@ int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int 
     HIP_OK(hipMemsetAsync(d_out, 0, (size_t)B * M_max * 80 * 4, c->s));
     run_postnet(c, d_dec, (long)M_max * 80, W.mlens.i(), B, M_max, maxM, d_out, (long)M_max * 80, c->s);
     HIP_OK(hipStreamSynchronize(c->s));
+    leave(c, stream);
+  });
+}
+
+int tts_ge2e_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    set_tensor(c->ge2e_host, name, h, shape, ndim);
+  });
+}
+
+int tts_ge2e_finalize(tts_ctx* c, int input_dim, int proj_dim, int lstm_dim, int num_lstm_layers,
+                      int use_lstm_with_projection) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    DeviceGuard g(c->device);
+    HostMapConsumer consume{c->ge2e_host};
+    ge2e_finalize(c, input_dim, proj_dim, lstm_dim, num_lstm_layers, use_lstm_with_projection);
+  });
+}
+
+int tts_ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int T_max, float* d_out,
+                   void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_x && h_lens && d_out, "null argument");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    ge2e_infer(c, d_x, h_lens, B, T_max, d_out);
     leave(c, stream);
   });
 }

@@ -103,47 +103,54 @@ __global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restric
   out[((long)m * T_max + t) * 512 + dir * 256 + tl * 4 + u] = hn;
 }
 
-// The whole recurrence as ONE cooperative launch of the same 128 workgroups: W_hh fragments stay
-// in VGPRs, the cell state in a register of the thread that owns (row, unit), and a hierarchical
-// grid barrier (gsync.h) replaces the launch boundary between steps (per-step launches were
-// host-enqueue bound at ~8 us per step).
-template <int MT>
-__global__ __launch_bounds__(256) void bilstm_persist_kernel(const float* __restrict__ Whh,
-                                                             const float* __restrict__ Gin, const int* lens,
-                                                             int T_max, int B, float* hbuf, float* __restrict__ out,
-                                                             unsigned* bar) {
+// The whole recurrence as ONE cooperative launch: workgroup (dir, tile) owns gate tile `tile` (4
+// hidden units, gate-interleaved) of direction dir; its W_hh fragments stay in VGPRs, the cell
+// state in a register of the thread that owns (row, unit), and a hierarchical grid barrier
+// (gsync.h) per direction replaces the launch boundary between steps (per-step launches were
+// host-enqueue bound at ~8 us per step). Used by the Tacotron2 encoder BiLSTM (H = 256, 2
+// directions) and the GE2E speaker encoder LSTMs (H = 768, 1 direction).
+//   Whh : [dir][H/4 tiles][H/16 k-chunks][64 lanes][4]   Gin : (B, T_max, NDIR*4H) incl. biases
+//   hbuf: [2 ping-pong][dir][Bp x H] fragment order      out : (B, T_max, NDIR*H)
+template <int MT, int H, int NDIR>
+__global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restrict__ Whh,
+                                                           const float* __restrict__ Gin, const int* lens,
+                                                           int T_max, int B, float* hbuf, float* __restrict__ out,
+                                                           unsigned* bar) {
   constexpr int Bp = MT * 16;
-  constexpr int H = 256, NKC = H / 16, KPW = NKC / 4;  // 4 k-chunks per wave
+  constexpr int NT = H / 4;                   // gate tiles per direction
+  constexpr int NKC = H / 16, KPW = NKC / 4;  // k-chunks, per wave
+  constexpr int G = NDIR * 4 * H, O = NDIR * H;
+  static_assert(NKC % 4 == 0 && NT % 8 == 0, "LSTM geometry");
   __shared__ float part[4 * Bp * 17];
   __shared__ int sflag;
-  const int dir = blockIdx.x >> 6, tl = blockIdx.x & 63;
+  const int dir = blockIdx.x / NT, tl = blockIdx.x % NT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   f32x4 w[KPW];
   {
-    const f32x4* Wv = reinterpret_cast<const f32x4*>(Whh) + ((long)(dir * 64 + tl) * NKC + wave * KPW) * 64 + lane;
+    const f32x4* Wv = reinterpret_cast<const f32x4*>(Whh) + ((long)(dir * NT + tl) * NKC + wave * KPW) * 64 + lane;
 #pragma unroll
     for (int k = 0; k < KPW; ++k) w[k] = Wv[(long)k * 64];
   }
   const int m = min(tid >> 2, Bp - 1), u = tid & 3;
   const bool row = (tid >> 2) < Bp && m < B;
   const int Tm = lens[min(m, B - 1)];
-  const float* gbase = Gin + (long)min(m, B - 1) * T_max * 2048 + dir * 1024 + tl * 16 + u;
+  const float* gbase = Gin + (long)min(m, B - 1) * T_max * G + dir * 4 * H + tl * 16 + u;
   float cst = 0.f;
   unsigned gen = 0;
   // input-projection gates of a step do not depend on h: loaded one step ahead, under the barrier
   auto tpos = [&](int step) { return min(max(dir ? Tm - 1 - step : step, 0), T_max - 1); };
   float gin[4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(0) * 2048 + q * 4];
+  for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(0) * G + q * 4];
   for (int step = 0; step < T_max; ++step) {
-    const float* hi = hbuf + (size_t)(step & 1) * 2 * Bp * H + (long)dir * Bp * H;
-    float* ho = hbuf + (size_t)((step + 1) & 1) * 2 * Bp * H + (long)dir * Bp * H;
+    const float* hi = hbuf + (size_t)(step & 1) * NDIR * Bp * H + (long)dir * Bp * H;
+    float* ho = hbuf + (size_t)((step + 1) & 1) * NDIR * Bp * H + (long)dir * Bp * H;
     const int t = tpos(step);
     f32x4 x[KPW][MT];
 #pragma unroll
     for (int k = 0; k < KPW; ++k)
 #pragma unroll
-      for (int mt = 0; mt < MT; ++mt) x[k][mt] = ldc4(hi, ((mt * 16 + wave * KPW + k) * 64 + lane) * 16);
+      for (int mt = 0; mt < MT; ++mt) x[k][mt] = ldc4(hi, ((mt * NKC + wave * KPW + k) * 64 + lane) * 16);
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -174,31 +181,45 @@ __global__ __launch_bounds__(256) void bilstm_persist_kernel(const float* __rest
       cst = fg * cst + ig * gg;
       const float hn = og * tanhf(cst);
       stc(ho + frag_idx(m, tl * 4 + u, H), hn);
-      out[((long)m * T_max + t) * 512 + dir * 256 + tl * 4 + u] = hn;
+      out[((long)m * T_max + t) * O + dir * H + tl * 4 + u] = hn;
     }
-    if (step + 1 < T_max) {  // the two directions are independent: one 64-workgroup barrier each
-      gsync_arrive(bar + dir * 512, gen, 64);
+    if (step + 1 < T_max) {  // directions are independent: one barrier each
+      gsync_arrive(bar + dir * 512, gen, NT);
 #pragma unroll
-      for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(step + 1) * 2048 + q * 4];
+      for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(step + 1) * G + q * 4];
       if (!gsync_wait(bar + dir * 512, gen, &sflag)) return;
     }
   }
 }
 
-bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
-                           unsigned* bar, float* out, hipStream_t s) {
+template <int H, int NDIR>
+static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
+                                  unsigned* bar, float* out, hipStream_t s) {
   int dev = 0, coop = 0;
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
   if (!coop) return false;
   const int MT = (B + 15) / 16, Bp = MT * 16;
-  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * 2 * Bp * 256 * 4, s));
-  HIP_OK(hipMemsetAsync(bar, 0, 1024 * 4, s));
+  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * NDIR * Bp * H * 4, s));
+  HIP_OK(hipMemsetAsync(bar, 0, (size_t)NDIR * 512 * 4, s));
   void* args[] = {(void*)&Whh, (void*)&Gin, (void*)&lens, (void*)&T_max, (void*)&B, (void*)&hbuf, (void*)&out, (void*)&bar};
-  const void* f = MT == 1 ? (const void*)bilstm_persist_kernel<1> : MT == 2 ? (const void*)bilstm_persist_kernel<2>
-                : MT == 3 ? (const void*)bilstm_persist_kernel<3> : (const void*)bilstm_persist_kernel<4>;
-  HIP_OK(hipLaunchCooperativeKernel(f, dim3(128), dim3(256), args, 0, s));
+  const void* f = MT == 1 ? (const void*)lstm_persist_kernel<1, H, NDIR> : MT == 2 ? (const void*)lstm_persist_kernel<2, H, NDIR>
+                : MT == 3 ? (const void*)lstm_persist_kernel<3, H, NDIR> : (const void*)lstm_persist_kernel<4, H, NDIR>;
+  HIP_OK(hipLaunchCooperativeKernel(f, dim3(NDIR * H / 4), dim3(256), args, 0, s));
   return true;
+}
+
+// encoder BiLSTM (H = 256, both directions); false = cooperative launch unavailable
+bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
+                           unsigned* bar, float* out, hipStream_t s) {
+  return launch_lstm_persist_t<256, 2>(Gin, Whh, lens, T_max, B, hbuf, bar, out, s);
+}
+
+// GE2E speaker-encoder LSTM layer (H = 768, forward only); hbuf >= 2 x 64 x 768 floats, bar >= 512 words
+bool launch_lstm768_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
+                            unsigned* bar, float* out, hipStream_t s) {
+  TTS_CHECK(B >= 1 && B <= 64, "speaker encoder: 1..64 sequences per launch");
+  return launch_lstm_persist_t<768, 1>(Gin, Whh, lens, T_max, B, hbuf, bar, out, s);
 }
 
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,

@@ -213,3 +213,43 @@ def melgan_spec(c: MelganConfig, weight_norm: bool = True) -> Spec:
               ("pqmf_layer.G", (1, N, taps + 1), "buffer"),
               ("pqmf_layer.updown_filter", (N, N, N), "buffer")]
     return s
+
+
+@dataclass
+class Ge2eConfig:
+    """``SpeakerEncoder(input_dim, proj_dim, lstm_dim, num_lstm_layers, use_lstm_with_projection)``
+    (``TTS/speaker_encoder/model.py:31-47``; config ``speaker_encoder/config.json:47-52``)."""
+    input_dim: int = 40
+    proj_dim: int = 256
+    lstm_dim: int = 768
+    num_lstm_layers: int = 3
+    use_lstm_with_projection: bool = True
+
+
+def ge2e_spec(c: Ge2eConfig) -> Spec:
+    """state_dict spec of ``SpeakerEncoder``: ``layers.{i}.lstm.*_l0`` + ``layers.{i}.linear.weight``
+    (LSTMWithProjection, model.py:5-17) or ``layers.lstm.*_l{k}`` + ``layers.linear.{weight,bias}``
+    (LSTMWithoutProjection, model.py:19-30)."""
+    H, P = c.lstm_dim, c.proj_dim
+    s: Spec = []
+    if c.use_lstm_with_projection:
+        for i in range(c.num_lstm_layers):
+            din = c.input_dim if i == 0 else P
+            s += [
+                (f"layers.{i}.lstm.weight_ih_l0", (4 * H, din), "xavier"),
+                (f"layers.{i}.lstm.weight_hh_l0", (4 * H, H), "xavier"),
+                (f"layers.{i}.lstm.bias_ih_l0", (4 * H,), "bias"),
+                (f"layers.{i}.lstm.bias_hh_l0", (4 * H,), "bias"),
+                (f"layers.{i}.linear.weight", (P, H), "xavier"),
+            ]
+    else:
+        for k in range(c.num_lstm_layers):
+            din = c.input_dim if k == 0 else H
+            s += [
+                (f"layers.lstm.weight_ih_l{k}", (4 * H, din), "xavier"),
+                (f"layers.lstm.weight_hh_l{k}", (4 * H, H), "xavier"),
+                (f"layers.lstm.bias_ih_l{k}", (4 * H,), "bias"),
+                (f"layers.lstm.bias_hh_l{k}", (4 * H,), "bias"),
+            ]
+        s += [("layers.linear.weight", (P, H), "xavier"), ("layers.linear.bias", (P,), "bias")]
+    return s

@@ -70,6 +70,9 @@ def synth_tensor(name: str, shape: Tuple[int, ...], kind: str, seed: int,
     elif kind in ("lstm", "lstm_enc"):
         H = shape[0] // 4
         x = u / math.sqrt(H)
+    elif kind == "xavier":  # xavier_normal_ in the reference (speaker_encoder/model.py:49-54): same std
+        fi, fo = _fans(shape)
+        x = u * math.sqrt(3.0) * math.sqrt(2.0 / (fi + fo))
     elif kind == "speaker_emb":  # normal_(0, 0.3) in the reference: same std, uniform
         x = u * (0.3 * math.sqrt(3.0))
     elif kind == "bias":
