@@ -1,9 +1,12 @@
-"""Per-launch HBM bytes of the decoder K4 kernel from two rocprofv3 --pmc passes.
+"""Per-launch HBM bytes of one decoder kernel from two rocprofv3 --pmc passes.
 
-K4 is the <1,4,MT> skinny kernel launched with 256 workgroups of 256 threads (grid 65536
-threads); the projection launch uses the same instantiation with 1 + 5r + 256 workgroups, so the
-grid size tells them apart. FETCH_SIZE is doubled (gfx950 tallies 128-B requests at 64 B,
-MI355X_MICROARCH.md §HBM); both counters are in KiB.
+  pmc_summary.py FETCH_DIR WRITE_DIR OUT.json [KERNEL_SUBSTRING]
+
+Default kernel: the graph path's K4 (<1,4,MT> skinny kernel, 256 x 256 grid; the projection
+launch uses the same instantiation with a different grid). With a substring (e.g.
+"persist_decoder_kernel<2>") every dispatch whose name contains it is averaged. FETCH_SIZE is
+doubled (gfx950 tallies 128-B requests at 64 B, MI355X_MICROARCH.md §HBM); both counters are in
+KiB; Infinity-Cache (MALL) hits are counted.
 """
 import csv
 import glob
@@ -12,7 +15,7 @@ import os
 import sys
 
 
-def load(d, counter):
+def load(d, counter, sub=None):
     files = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)
     if not files:
         raise SystemExit(f"no counter_collection.csv under {d}")
@@ -21,20 +24,22 @@ def load(d, counter):
         for row in csv.DictReader(open(f)):
             name = row.get("Kernel_Name", "")
             grid = int(row.get("Grid_Size", "0") or 0)
-            if "skinny_kernel<1, 4," in name and grid == 256 * 256 and row.get("Counter_Name") == counter:
+            hit = (sub in name) if sub else ("skinny_kernel<1, 4," in name and grid == 256 * 256)
+            if hit and row.get("Counter_Name") == counter:
                 vals.append(float(row["Counter_Value"]))
     return vals
 
 
 def main():
-    fetch = load(sys.argv[1], "FETCH_SIZE")
-    write = load(sys.argv[2], "WRITE_SIZE")
+    sub = sys.argv[4] if len(sys.argv) > 4 else None
+    fetch = load(sys.argv[1], "FETCH_SIZE", sub)
+    write = load(sys.argv[2], "WRITE_SIZE", sub)
     if not fetch or not write:
-        raise SystemExit("no K4 dispatches found")
+        raise SystemExit("no matching dispatches found")
     f_kb = sum(fetch) / len(fetch)
     w_kb = sum(write) / len(write)
     out = {
-        "kernel": "decoder K4 skinny_kernel<1,4,MT> (256 x 256 grid)",
+        "kernel": sub or "decoder K4 skinny_kernel<1,4,MT> (256 x 256 grid)",
         "dispatches": {"fetch": len(fetch), "write": len(write)},
         "fetch_size_kib_raw": f_kb,
         "write_size_kib": w_kb,
