@@ -67,12 +67,16 @@ def lstm_cell(x, h, c, w_ih, w_hh, b_ih, b_hh):
 
 
 class TacoOracle:
-    def __init__(self, sd, attn_norm="sigmoid", r_init=7, frame_channels=80):
+    def __init__(self, sd, attn_norm="sigmoid", r_init=7, frame_channels=80, windowing=False,
+                 forward_attn=False, trans_agent=False):
         self.sd = {k: (np.asarray(v, F32) if np.asarray(v).dtype != np.int64 else np.asarray(v))
                    for k, v in sd.items()}
         self.attn_norm = attn_norm
         self.r_init = r_init
         self.F = frame_channels
+        self.windowing = windowing
+        self.forward_attn = forward_attn
+        self.trans_agent = trans_agent
 
     def _bn(self, prefix):
         return {k: self.sd[f"{prefix}.batch_normalization.{k}"]
@@ -121,10 +125,15 @@ class TacoOracle:
 
     # ---- decoder -------------------------------------------------------------------
     def prenet(self, m):
-        """Prenet.forward (common_layers.py:76-82), eval mode (no dropout)."""
+        """Prenet.forward (common_layers.py:76-82), eval mode (no dropout); 'bn' type: LinearBN
+        (common_layers.py:25-46) = Linear(bias=False) then BatchNorm1d in eval."""
         for i in range(2):
-            m = np.maximum(m @ self.sd[f"decoder.prenet.linear_layers.{i}.linear_layer.weight"].T,
-                           F32(0)).astype(F32)
+            p = f"decoder.prenet.linear_layers.{i}."
+            m = (m @ self.sd[p + "linear_layer.weight"].T).astype(F32)
+            if p + "batch_normalization.weight" in self.sd:
+                m = batchnorm_eval(m[:, None], {k: self.sd[p + "batch_normalization." + k]
+                                                for k in ("weight", "bias", "running_mean", "running_var")})[:, 0]
+            m = np.maximum(m, F32(0)).astype(F32)
         return m
 
     def attention(self, query, inputs, pin, st):
@@ -137,6 +146,16 @@ class TacoOracle:
         loc = f.T @ self.sd[p + "location_layer.location_dense.linear_layer.weight"].T  # (T,128)
         e = np.tanh(pq[None, :] + loc + pin).astype(F32) @ self.sd[p + "v.linear_layer.weight"].T
         e = (e[:, 0] + self.sd[p + "v.linear_layer.bias"][0]).astype(F32)
+        if self.windowing:  # apply_windowing (common_layers.py:286-300), B = 1
+            w = st["win_idx"]
+            back, front = w - 2, w + 6
+            if back > 0:
+                e[:back] = -np.inf
+            if front < len(e):
+                e[front:] = -np.inf
+            if w == -1:
+                e[0] = e.max()
+            st["win_idx"] = int(np.argmax(e))
         if self.attn_norm == "softmax":
             z = np.exp(e - e.max()).astype(F32)
             a = (z / z.sum()).astype(F32)
@@ -146,8 +165,18 @@ class TacoOracle:
         else:
             raise ValueError("Unknown value for attention norm type")
         st["alpha_cum"] = (st["alpha_cum"] + a).astype(F32)
+        if self.forward_attn:  # apply_forward_attention (common_layers.py:302-323), no mask
+            prev = st["fwd_alpha"]
+            shifted = np.concatenate([np.zeros(1, F32), prev[:-1]])
+            a = (((F32(1) - st["u"]) * prev + st["u"] * shifted + F32(1e-8)) * a).astype(F32)
+            a = (a / a.sum()).astype(F32)
+            st["fwd_alpha"] = a
         st["alpha"] = a
-        return (a @ inputs).astype(F32)
+        ctx = (a @ inputs).astype(F32)
+        if self.forward_attn and self.trans_agent:  # u = sigmoid(ta([context, query]))
+            ta = np.concatenate([ctx, query]) @ self.sd[p + "ta.weight"].T + self.sd[p + "ta.bias"]
+            st["u"] = sigmoid(ta.astype(F32))[0]
+        return ctx
 
     def decode(self, mem, inputs, pin, st):
         """Decoder.decode (tacotron2.py:259-298)."""
@@ -178,7 +207,8 @@ class TacoOracle:
         pin = (inputs @ self.sd["decoder.attention.inputs_layer.linear_layer.weight"].T).astype(F32)
         st = dict(q=np.zeros(1024, F32), qc=np.zeros(1024, F32), h=np.zeros(1024, F32),
                   c=np.zeros(1024, F32), ctx=np.zeros(inputs.shape[1], F32),
-                  alpha=np.zeros(T, F32), alpha_cum=np.zeros(T, F32))
+                  alpha=np.zeros(T, F32), alpha_cum=np.zeros(T, F32), win_idx=-1, u=F32(0.5),
+                  fwd_alpha=np.concatenate([np.ones(1, F32), np.full(T - 1, 1e-7, F32)]))
         mem = np.zeros(F, F32)                 # go frame, after _update_memory
         outs, stops, aligns, logits, t = [], [], [], [], 0
         while True:

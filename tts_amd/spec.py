@@ -47,6 +47,11 @@ class TacotronConfig:
     # is given (external per-sample embeddings, tacotron_abstract.py:76-81)
     num_speakers: int = 0
     speaker_embedding_dim: Optional[int] = None
+    # decoder variants (layers/tacotron2.py:147-200, common_layers.py:49-74,196-372)
+    prenet_type: str = "original"   # 'original' | 'bn' (LinearBN: Linear(bias=False) + BatchNorm1d)
+    windowing: bool = False         # attention windowing at inference (common_layers.py:286-300)
+    forward_attn: bool = False      # forward attention (common_layers.py:302-323)
+    trans_agent: bool = False       # transition agent u = sigmoid(ta([ctx, query]))
 
     @property
     def spk_dim(self) -> int:
@@ -92,9 +97,15 @@ def _conv_bn(prefix: str, cin: int, cout: int, k: int) -> Spec:
 def _decoder(prefix: str, c: TacotronConfig, r: int) -> Spec:
     E, Q, D, P, A = c.decoder_in, c.query_dim, c.decoder_rnn_dim, c.prenet_dim, c.attn_dim
     F = c.frame_channels
-    s: Spec = [
-        (f"{prefix}.prenet.linear_layers.0.linear_layer.weight", (P, F), "linear_relu"),
-        (f"{prefix}.prenet.linear_layers.1.linear_layer.weight", (P, P), "linear_relu"),
+    s: Spec = []
+    for i, din in enumerate((F, P)):
+        s.append((f"{prefix}.prenet.linear_layers.{i}.linear_layer.weight", (P, din), "linear_relu"))
+        if c.prenet_type == "bn":
+            bn = f"{prefix}.prenet.linear_layers.{i}.batch_normalization"
+            s += [(f"{bn}.weight", (P,), "bn_w"), (f"{bn}.bias", (P,), "bn_b"),
+                  (f"{bn}.running_mean", (P,), "bn_mean"), (f"{bn}.running_var", (P,), "bn_var"),
+                  (f"{bn}.num_batches_tracked", (), "count")]
+    s += [
         (f"{prefix}.attention_rnn.weight_ih", (4 * Q, P + E), "lstm"),
         (f"{prefix}.attention_rnn.weight_hh", (4 * Q, Q), "lstm"),
         (f"{prefix}.attention_rnn.bias_ih", (4 * Q,), "lstm"),
@@ -104,6 +115,9 @@ def _decoder(prefix: str, c: TacotronConfig, r: int) -> Spec:
         (f"{prefix}.attention.v.linear_layer.weight", (1, A), "attn_v"),
         (f"{prefix}.attention.v.linear_layer.bias", (1,), "bias"),
     ]
+    if c.forward_attn and c.trans_agent:
+        s += [(f"{prefix}.attention.ta.weight", (1, Q + E), "linear_sigmoid"),
+              (f"{prefix}.attention.ta.bias", (1,), "bias")]
     if c.location_attn:
         s += [
             (f"{prefix}.attention.location_layer.location_conv1d.weight",
