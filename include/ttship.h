@@ -71,6 +71,13 @@ int tts_taco_infer_spk(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens
                        const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
                        int32_t* h_steps, int32_t* h_status, void* stream);
 
+/* Decoder options that no tensor reveals (layers/tacotron2.py:147-200 -> common_layers.py:196-372):
+   attention windowing at inference (attn_win) and forward attention (forward_attn; the transition
+   agent is on when decoder.attention.ta.* tensors are loaded). BN prenet is detected from the
+   decoder.prenet.linear_layers.N.batch_normalization.* tensors. Variants decode on the persistent
+   decoder only. Set before tts_taco_infer; kept across finalize. */
+int tts_taco_set_options(tts_ctx* ctx, int windowing, int forward_attn);
+
 /* speaker dimension of the finalized model (0 = single speaker) and its learned table size */
 int tts_taco_speaker_dim(tts_ctx* ctx, int* spk_dim, int* num_speakers);
 

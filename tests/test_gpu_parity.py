@@ -191,6 +191,28 @@ def test_tacotron2_multispeaker_matches_reference(name, n):
                 m.last_steps, range(n))
 
 
+@pytest.mark.parametrize("name", ["taco_bnprenet", "taco_window", "taco_window_softmax", "taco_fwdattn"])
+def test_tacotron2_decoder_variants_match_reference(name):
+    """SURVEY 8f rank 4 decoder variants on the persistent decoder, both fixture utterances in one
+    batched call: BN prenet, attention windowing (sigmoid / softmax), forward attention with the
+    transition agent."""
+    _dev()
+    fx = load_fixture(name)
+    r = 2
+    cfg, sd = taco_state_dict(fx, r=r)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(r)
+    m.decoder.max_decoder_steps = int(fx[f"r{r}_max_steps"])
+    ids = [fx[f"r{r}_u{i}_ids"] for i in range(2)]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((2, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=[len(x) for x in ids])
+    _check_taco(fx, r, dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy(), stop.cpu().numpy(),
+                m.last_steps, range(2))
+
+
 def test_tacotron2_multispeaker_requires_speaker():
     _dev()
     fx = load_fixture("taco_multispk")

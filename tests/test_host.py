@@ -77,8 +77,9 @@ def test_multispeaker_state_dict_keys_and_shapes():
     assert tuple(sd2["decoder.attention_rnn.weight_ih"].shape) == (4096, 256 + 768)
 
 
-@pytest.mark.parametrize("kw", [dict(gst=True), dict(attn_win=True), dict(forward_attn=True),
-                                dict(prenet_type="bn"), dict(attn_type="graves"), dict(location_attn=False)])
+@pytest.mark.parametrize("kw", [dict(gst=True), dict(forward_attn=True, forward_attn_mask=True),
+                                dict(trans_agent=True), dict(prenet_type="xyz"), dict(attn_type="graves"),
+                                dict(location_attn=False)])
 def test_unsupported_tacotron_variants_raise(kw):
     with pytest.raises(NotImplementedError):
         Tacotron2(num_chars=129, **kw)

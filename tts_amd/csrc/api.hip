@@ -204,6 +204,13 @@ struct TacoModel {
   // into its 512 encoder columns plus W_s s, a per-utterance bias. Host copies of the speaker
   // columns (rows in the kernels' order), spk_dim x ... each; spk_wT = [spk_dim][NSPK] for pj_r.
   int spk_dim = 0, num_spk = 0;
+  // decoder variants (common_layers.py:25-74, 196-372): BN prenet folded into the prenet weights
+  // (+ biases), windowing / forward attention / transition agent flags
+  bool prenet_bn = false, windowing = false, forward_attn = false, trans_agent = false;
+  std::vector<float> pre1_bias;  // b1' (BN), folded into the projection's prenet rows
+  DevBuf pre1_b0, pre2_b, ta_w;
+  float ta_b = 0.f;
+  bool variant() const { return prenet_bn || windowing || forward_attn; }
   DevBuf spk_table;  // speaker_embedding.weight (num_spk, 512) when learned
   std::vector<float> spk_att_h, spk_dec_h, spk_penc_h, proj_spk;
   DevBuf spk_wT;
@@ -220,6 +227,7 @@ struct TacoWS {
   DevBuf ids, post, map;       // rows in decode order (longest first), output scatter map
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
   DevBuf spk, spkid, spkb;     // speaker vectors (decode order), per-row biases [Bp][NSPK]
+  DevBuf win_idx, fwd_u, apf;  // windowing argmax, transition probability, forward chunk sums
   bool enc_persist = false;    // the last encoder ran the persistent BiLSTM (lc = its barrier words)
   // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
   // longest-first rows finish); all share one configuration key
@@ -434,8 +442,41 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     M.spk_penc_h = slice_cols(win_all, A, ES, E, ES);
   }
   M.pre1_host = need(h, "decoder.prenet.linear_layers.0.linear_layer.weight", {P, F}).d;
+  std::vector<float> w2 = need(h, "decoder.prenet.linear_layers.1.linear_layer.weight", {P, P}).d;
+  // BN prenet (LinearBN, common_layers.py:25-46, eval): relu(s (W x - mu) + beta) = relu(W' x + b')
+  M.prenet_bn = h.count("decoder.prenet.linear_layers.0.batch_normalization.weight") > 0;
+  std::vector<float> b2;
+  M.pre1_bias.assign(P, 0.f);
+  if (M.prenet_bn) {
+    for (int l = 0; l < 2; ++l) {
+      const std::string bn = "decoder.prenet.linear_layers." + std::to_string(l) + ".batch_normalization.";
+      const auto& g_ = need(h, bn + "weight", {P}).d;
+      const auto& b_ = need(h, bn + "bias", {P}).d;
+      const auto& mu = need(h, bn + "running_mean", {P}).d;
+      const auto& var = need(h, bn + "running_var", {P}).d;
+      std::vector<float>& W = l == 0 ? M.pre1_host : w2;
+      const int din = l == 0 ? F : P;
+      std::vector<float> bias(P);
+      for (int o = 0; o < P; ++o) {
+        const double sc = (double)g_[o] / std::sqrt((double)var[o] + 1e-5);
+        for (int k = 0; k < din; ++k) W[(size_t)o * din + k] = (float)(sc * W[(size_t)o * din + k]);
+        bias[o] = (float)((double)b_[o] - sc * mu[o]);
+      }
+      if (l == 0) M.pre1_bias = bias;
+      else b2 = bias;
+    }
+    M.pre1_b0.upload(M.pre1_bias);
+    M.pre2_b.upload(b2);
+  }
   M.pre1.upload(swz(M.pre1_host, P, F));
-  M.pre2.upload(swz(need(h, "decoder.prenet.linear_layers.1.linear_layer.weight", {P, P}).d, P, P));
+  M.pre2.upload(swz(w2, P, P));
+  // transition agent of forward attention (common_layers.py:215-217): ta over [context | query]
+  M.trans_agent = h.count("decoder.attention.ta.weight") > 0;
+  if (M.trans_agent) {
+    M.ta_w.upload(need(h, "decoder.attention.ta.weight", {1, E + S + Q}).d);
+    M.ta_b = need(h, "decoder.attention.ta.bias", {1}).d[0];
+    TTS_CHECK(S == 0, "transition agent with speaker embeddings is not implemented");
+  }
   {
     const auto& wih = need(h, "decoder.attention_rnn.weight_ih", {4 * Q, P + ES}).d;
     const auto& whh = need(h, "decoder.attention_rnn.weight_hh", {4 * Q, Q}).d;
@@ -583,6 +624,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.energy, (size_t)B * T_max, g);
   const int nch = (T_max + 15) / 16;
   grow<float>(W.aps, (size_t)B * nch, g);
+  grow<float>(W.apf, (size_t)B * nch, g);
   grow<float>(W.apm, (size_t)B * nch, g);
   grow<float>(W.apu, (size_t)B * nch * 512, g);
   grow<unsigned>(W.acnt, BMAX, g);
@@ -598,6 +640,8 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
   grow<unsigned>(W.pbar, 512, g);
   grow<float>(W.spk, (size_t)64 * 1024, g);
+  grow<int>(W.win_idx, 64, g);
+  grow<float>(W.fwd_u, 64, g);
   grow<int64_t>(W.spkid, 64, g);
   W.B = B;
   W.T_max = T_max;
@@ -950,7 +994,7 @@ void build_pj(tts_ctx* c, int r) {
     }
     float* dst = rows.data() + (size_t)(rows_p + k) * K;
     for (int j = 0; j < K; ++j) dst[j] = (float)acc[j];
-    bias[rows_p + k] = (float)bs;
+    bias[rows_p + k] = (float)(bs + (M.pre1_bias.empty() ? 0.0 : (double)M.pre1_bias[k]));
   }
   M.pj_w.upload(swz(rows, rows_p + P, K));
   M.pj_b.upload(bias);
@@ -1013,6 +1057,22 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     a.spk_att = M.spk_dim ? W.spkb.f() : nullptr;
     a.spk_dec = M.spk_dim ? W.spkb.f() + 4096 : nullptr;
     a.spk_penc = M.spk_dim ? W.spkb.f() + 8192 : nullptr;
+  }
+  // decoder variants
+  a.pre1_b0 = M.prenet_bn ? M.pre1_b0.f() : nullptr;
+  a.pre2_b = M.prenet_bn ? M.pre2_b.f() : nullptr;
+  a.win = M.windowing;
+  a.fwd = M.forward_attn;
+  a.trans = M.forward_attn && M.trans_agent;
+  a.ta_w = M.trans_agent ? M.ta_w.f() : nullptr;
+  a.ta_b = M.ta_b;
+  a.win_idx = W.win_idx.i();
+  a.fwd_u = W.fwd_u.f();
+  a.part_f = W.apf.f();
+  if (M.windowing) HIP_OK(hipMemsetAsync(W.win_idx.p, 0xff, 64 * 4, s));  // -1: before the first step
+  if (M.forward_attn) {
+    static const std::vector<float> half(64, 0.5f);  // u = 0.5 (common_layers.py:241)
+    HIP_OK(hipMemcpyAsync(W.fwd_u.p, half.data(), 64 * 4, hipMemcpyHostToDevice, s));
   }
   a.pre2_w = M.pre2.f();
   a.WqT = M.WqT.f();
@@ -1122,6 +1182,8 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
   W.thr = thr;
   // speaker vectors in decode order: external embeddings, or rows of the learned table
+  TTS_CHECK(!M.variant() || use_persistent(c), "BN prenet / attention windowing / forward attention run on the "
+                                               "persistent decoder only (<= 32 utterances per call on a 256-CU device)");
   if (M.spk_dim) {
     TTS_CHECK(d_spk_ids || d_spk_emb, "multi-speaker model: speaker ids or speaker embeddings are required");
     TTS_CHECK(use_persistent(c), "multi-speaker decoding runs on the persistent decoder only (<= 32 utterances "
@@ -1744,6 +1806,14 @@ int tts_taco_infer_spk(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, 
     DeviceGuard g(c->device);
     taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
                h_status, stream, d_spk_ids, d_spk_emb);
+  });
+}
+
+int tts_taco_set_options(tts_ctx* c, int windowing, int forward_attn) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    c->taco.windowing = windowing != 0;
+    c->taco.forward_attn = forward_attn != 0;
   });
 }
 

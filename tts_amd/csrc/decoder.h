@@ -119,6 +119,17 @@ struct PArgs {
   const float* spk_dec;
   const float* spk_penc;
   int spk_ld;
+  // decoder variants (common_layers.py:25-74, 286-372): BN prenet biases (null = original prenet),
+  // attention windowing, forward attention (+ transition agent)
+  const float* pre1_b0;  // [256] layer-1 bias b1' (BN folded): the prenet input of step 0 is relu(b1')
+  const float* pre2_b;   // [256] layer-2 bias b2'
+  int win;
+  int* win_idx;          // (B) previous argmax, -1 before the first step
+  int fwd, trans;
+  float* fwd_u;          // (B) transition probability u, 0.5 before the first step
+  float* part_f;         // (B, nchmax) chunk sums of the forward weights
+  const float* ta_w;     // [512 ctx | 1024 query]
+  float ta_b;
   const float* pre2_w;  // [16][16][64][4]
   const float* WqT;     // [1024][128]
   const float* Wcomb;   // [64][128]: location_dense . location_conv as one 62-tap filter per dim

@@ -186,6 +186,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   float* esum = Aw + 128;       // [8 waves][TC] partial energies
   float* sv = esum + 8 * TC;    // [TC] energies
   float* sw = sv + TC;          // [TC] normalised weights
+  float* swf = sw + TC;         // [TC] forward-attention weights
   if (!haveL) attn_loc(P, b, ch, Aw, wcomb, L);  // items beyond a workgroup's first
   const int tid = opaque_v(threadIdx.x);
   const int lane = tid & 63;
@@ -243,14 +244,31 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   ATRACE(3);
   const int nvalid = min(TC, T - t0);
   const long pidx = (long)b * P.nchmax + ch;
+  // attention windowing (common_layers.py:286-300): energies outside [lo, hi) around the previous
+  // step's argmax become -inf; on the first step (win_idx == -1) position 0 takes the max energy
+  int wlo = 0, whi = T, widx = 0;
+  if (P.win) {
+    widx = ldci(P.win_idx + b);
+    if (widx - 2 > 0) wlo = widx - 2;
+    if (widx + 6 < T) whi = widx + 6;
+  }
   if (tid < TC) {
     float e = P.bv;
 #pragma unroll
     for (int w = 0; w < 8; ++w) e += esum[w * TC + tid];
-    if (tid < nvalid) stc(P.energy + (long)b * D.T_max + t0 + tid, e);
+    if (P.win && (t0 + tid < wlo || t0 + tid >= whi)) e = -INFINITY;
     sv[tid] = e;
   }
   lds_barrier();
+  if (P.win && widx == -1 && ch == 0) {  // the first window [0, 5) lies in chunk 0
+    if (tid == 0) {
+      float mx = -INFINITY;
+      for (int i = 0; i < nvalid; ++i) mx = fmaxf(mx, sv[i]);
+      sv[0] = mx;
+    }
+    lds_barrier();
+  }
+  if (tid < nvalid) stc(P.energy + (long)b * D.T_max + t0 + tid, sv[tid]);
   ATRACE(4);
   // chunk-local normalisation terms (computed once, shared through LDS)
   float m_c = -INFINITY;
@@ -259,23 +277,37 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     for (int i = 0; i < TC; ++i)
       if (i < nvalid) m_c = fmaxf(m_c, sv[i]);
   }
+  // forward attention (common_layers.py:302-323): w = ((1-u) a[t] + u a[t-1] + 1e-8) * raw with
+  // raw = sigmoid(e) or exp(e - m_c); the normaliser of raw cancels in the renormalisation
+  const float fu = P.fwd ? ldc(P.fwd_u + b) : 0.f;
+  auto fwd_prev = [&](int pos) {  // previous forward alignment (init [1, 1e-7, ...], :236-241)
+    if (pos < 0) return 0.f;
+    return t == 0 ? (pos == 0 ? 1.f : 1e-7f) : ldc(P.alpha + (long)b * D.T_max + pos);
+  };
   if (tid < TC) {
     const float e = sv[tid];
-    const float x = P.softmax ? expf(e - m_c) : 1.f / (1.f + expf(-e));
-    sw[tid] = tid < nvalid ? x : 0.f;
+    float x = P.softmax ? (m_c == -INFINITY ? 0.f : expf(e - m_c)) : 1.f / (1.f + expf(-e));
+    if (tid >= nvalid) x = 0.f;
+    sw[tid] = x;
+    if (P.fwd) {
+      const int pos = t0 + tid;
+      swf[tid] = tid < nvalid ? ((1.f - fu) * fwd_prev(pos) + fu * fwd_prev(pos - 1) + 1e-8f) * x : 0.f;
+    }
   }
   lds_barrier();
-  float S_c = 0.f, u = 0.f;
+  const float* wsel = P.fwd ? swf : sw;
+  float S_c = 0.f, F_c = 0.f, u = 0.f;
 #pragma unroll
   for (int i = 0; i < TC; ++i) {
-    const float sl = sw[i];
-    S_c += sl;
-    u = fmaf(sl, ev[i], u);
+    S_c += sw[i];
+    F_c += swf[i];
+    u = fmaf(wsel[i], ev[i], u);
   }
   stc(P.part_u + pidx * 512 + tid, u);
   if (tid == 0) {
     stc(P.part_s + pidx, S_c);
     stc(P.part_m + pidx, m_c);
+    if (P.fwd) stc(P.part_f + pidx, F_c);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -291,14 +323,15 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   // combine: chunk partials in batches of 8, all loads of a batch in flight (clamped)
   const long pb0 = (long)b * P.nchmax;
   constexpr int CB = 8;
-  float m = -INFINITY, S = 0.f, cx = 0.f;
+  float m = -INFINITY, S = 0.f, Fz = 0.f, cx = 0.f;
   for (int cb = 0; cb < nch; cb += CB) {
-    float pm[CB], ps[CB], pu[CB];
+    float pm[CB], ps[CB], pf[CB], pu[CB];
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
       const long c = pb0 + min(cb + i, nch - 1);
       pm[i] = ldc(P.part_m + c);
       ps[i] = ldc(P.part_s + c);
+      pf[i] = P.fwd ? ldc(P.part_f + c) : 0.f;
       pu[i] = ldc(P.part_u + c * 512 + tid);
     }
     float wc[CB];
@@ -309,10 +342,11 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
         if (cb + i < nch) mb = fmaxf(mb, pm[i]);
       const float sc = (m == -INFINITY) ? 0.f : expf(m - mb);
       S *= sc;
+      Fz *= sc;
       cx *= sc;
       m = mb;
 #pragma unroll
-      for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch) ? expf(pm[i] - m) : 0.f;
+      for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch && pm[i] != -INFINITY) ? expf(pm[i] - m) : 0.f;
     } else {
 #pragma unroll
       for (int i = 0; i < CB; ++i) wc[i] = (cb + i < nch) ? 1.f : 0.f;
@@ -320,17 +354,85 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
 #pragma unroll
     for (int i = 0; i < CB; ++i) {
       S = fmaf(ps[i], wc[i], S);
+      Fz = fmaf(pf[i], wc[i], Fz);
       cx = fmaf(pu[i], wc[i], cx);
     }
   }
-  stc(P.ctx + frag_idx(b, tid, 512), cx / S);
+  const float ctx_v = cx / (P.fwd ? Fz : S);
+  stc(P.ctx + frag_idx(b, tid, 512), ctx_v);
   ATRACE(7);
+  const long ab = (long)b * D.T_max;
+  float bestv = -INFINITY;
+  int besti = 0x7fffffff;
   for (int tt = tid; tt < T; tt += NT) {
-    const float e = ldc(P.energy + (long)b * D.T_max + tt);
-    const float al = (P.softmax ? expf(e - m) : 1.f / (1.f + expf(-e))) / S;
-    stc(P.alpha + (long)b * D.T_max + tt, al);
-    stc(P.acum + (long)b * D.T_max + tt, ldc(P.acum + (long)b * D.T_max + tt) + al);
-    if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = al;
+    const float e = ldc(P.energy + ab + tt);
+    if (P.win && (e > bestv || (e == bestv && tt < besti))) {
+      bestv = e;
+      besti = tt;
+    }
+    const float raw = P.softmax ? (e == -INFINITY ? 0.f : expf(e - m)) : 1.f / (1.f + expf(-e));
+    const float al = raw / S;
+    stc(P.acum + ab + tt, ldc(P.acum + ab + tt) + al);  // location state accumulates the raw alignment
+    if (P.fwd) {  // forward alignment into the energy slot (alpha is still read as a[t-1] here)
+      stc(P.energy + ab + tt, ((1.f - fu) * fwd_prev(tt) + fu * fwd_prev(tt - 1) + 1e-8f) * raw / Fz);
+    } else {
+      stc(P.alpha + ab + tt, al);
+      if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = al;
+    }
+  }
+  if (P.fwd) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    for (int tt = tid; tt < T; tt += NT) {
+      const float af = ldc(P.energy + ab + tt);
+      stc(P.alpha + ab + tt, af);
+      if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = af;
+    }
+  }
+  if (P.win || (P.fwd && P.trans)) {
+    // block reductions over the 512 threads: window argmax (first index of the max energy) and the
+    // transition agent u = sigmoid(ta . [context, query] + b) for the next step
+    float tdot = 0.f;
+    if (P.fwd && P.trans) {
+      tdot = P.ta_w[tid] * ctx_v;
+#pragma unroll
+      for (int k = 0; k < 2; ++k) {
+        const int q = tid + k * NT;
+        tdot = fmaf(P.ta_w[512 + q], ldc(P.hatt + frag_idx(b, q, 1024)), tdot);
+      }
+    }
+    for (int off = 32; off > 0; off >>= 1) {
+      const float ov = __shfl_xor(bestv, off, 64);
+      const int oi = __shfl_xor(besti, off, 64);
+      if (ov > bestv || (ov == bestv && oi < besti)) {
+        bestv = ov;
+        besti = oi;
+      }
+      tdot += __shfl_xor(tdot, off, 64);
+    }
+    float* rv = red;  // the query-partial scratch is free by now
+    int* ri = reinterpret_cast<int*>(red + 16);
+    float* rt = red + 32;
+    lds_barrier();
+    if (lane == 0) {
+      rv[tid >> 6] = bestv;
+      ri[tid >> 6] = besti;
+      rt[tid >> 6] = tdot;
+    }
+    lds_barrier();
+    if (tid == 0) {
+      float bv = rv[0], ts = rt[0];
+      int bi = ri[0];
+      for (int w = 1; w < NT / 64; ++w) {
+        if (rv[w] > bv || (rv[w] == bv && ri[w] < bi)) {
+          bv = rv[w];
+          bi = ri[w];
+        }
+        ts += rt[w];
+      }
+      if (P.win) stci(P.win_idx + b, bi);
+      if (P.fwd && P.trans) stc(P.fwd_u + b, 1.f / (1.f + expf(-(ts + P.ta_b))));
+    }
   }
   if (tid == 0) __hip_atomic_store(&P.counter[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -530,14 +632,20 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-      if (t > 0) {  // t = 0: prenet input is the zero go-frame, layer 1 has no bias -> 0
+      // t = 0: the prenet input is the zero go-frame: layer 1 gives relu(b1') (BN prenet) or 0
+      if (t > 0 || P.pre1_b0) {
         const int kc = 8 * (g >> 4) + wave;
         const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int m = mt * 16 + (lane & 15);
-          const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pjb_rows + (long)m * P.spk_ld + col);
-          f32x4 x = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
+          f32x4 x;
+          if (t > 0) {
+            const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pjb_rows + (long)m * P.spk_ld + col);
+            x = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
+          } else {
+            x = *reinterpret_cast<const f32x4*>(P.pre1_b0 + kc * 16 + 4 * (lane >> 4));
+          }
 #pragma unroll
           for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
 #pragma unroll
@@ -548,7 +656,9 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       lds_barrier();
       for (int idx = tid; idx < Bp * 16; idx += PT) {
         const int m = idx >> 4, n = idx & 15;
-        stc(P.pb + (g >> 4) * PB_HALF + frag_idx(m, (g & 15) * 16 + n, 256), lds_sum<NWV, Bp>(red0, m, n));
+        float v = lds_sum<NWV, Bp>(red0, m, n);
+        if (P.pre2_b && (g >> 4) == 0) v += P.pre2_b[(g & 15) * 16 + n];  // BN prenet layer-2 bias, once
+        stc(P.pb + (g >> 4) * PB_HALF + frag_idx(m, (g & 15) * 16 + n, 256), v);
       }
       lds_barrier();
     }

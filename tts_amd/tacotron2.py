@@ -25,7 +25,7 @@ from .params import Container, host_tensors, new_token, populate
 from .spec import TacotronConfig, tacotron2_spec
 
 BATCH_LIMIT = 64
-SPEAKER_BATCH_LIMIT = 32  # multi-speaker decoding runs on the persistent decoder (<= 32 rows)
+SPEAKER_BATCH_LIMIT = 32  # multi-speaker / decoder variants run on the persistent decoder (<= 32 rows)
 
 
 class Decoder(Container):
@@ -57,13 +57,13 @@ class Tacotron2(nn.Module):
             unsupported.append("GST")
         if attn_type != "original":
             unsupported.append(f"attn_type={attn_type}")
-        if attn_win:
-            unsupported.append("attention windowing")
-        if forward_attn or trans_agent or forward_attn_mask:
-            unsupported.append("forward attention")
+        if forward_attn_mask:
+            unsupported.append("forward_attn_mask")
+        if trans_agent and not forward_attn:
+            unsupported.append("trans_agent without forward_attn")
         if not location_attn:
             unsupported.append("location_attn=False")
-        if prenet_type != "original":
+        if prenet_type not in ("original", "bn"):
             unsupported.append(f"prenet_type={prenet_type}")
         if bidirectional_decoder:
             unsupported.append("bidirectional_decoder")
@@ -84,7 +84,9 @@ class Tacotron2(nn.Module):
         self.cfg = TacotronConfig(num_chars=num_chars, r=r, attn_norm=attn_norm,
                                   double_decoder_consistency=double_decoder_consistency,
                                   ddc_r=ddc_r if ddc_r is not None else r,
-                                  num_speakers=num_speakers, speaker_embedding_dim=speaker_embedding_dim)
+                                  num_speakers=num_speakers, speaker_embedding_dim=speaker_embedding_dim,
+                                  prenet_type=prenet_type, windowing=bool(attn_win),
+                                  forward_attn=bool(forward_attn), trans_agent=bool(trans_agent))
         # models/tacotron2.py:50-58 / tacotron_abstract.py:76-81: a learned table unless the caller
         # gives per-sample embeddings of speaker_embedding_dim
         self.embeddings_per_sample = speaker_embedding_dim is not None
@@ -146,7 +148,7 @@ class Tacotron2(nn.Module):
         key = (self._token, self._version)
         if eng.taco_key != key:
             eng.load_tacotron(host_tensors(self, skip_prefixes=("coarse_decoder.",)), self.num_chars,
-                              self.decoder.r_init, self.attn_norm)
+                              self.decoder.r_init, self.attn_norm, self.cfg.windowing, self.cfg.forward_attn)
             eng.taco_key = key
 
     @torch.no_grad()
@@ -172,7 +174,8 @@ class Tacotron2(nn.Module):
         if not 1 <= r <= self.decoder.r_init:
             raise ValueError(f"r={r} must be in [1, r_init={self.decoder.r_init}]")
         spk_ids, spk_emb = self._speaker_args(speaker_ids, speaker_embeddings, B, dev)
-        limit = BATCH_LIMIT if self.num_speakers <= 1 else SPEAKER_BATCH_LIMIT
+        variant = self.cfg.prenet_type == "bn" or self.cfg.windowing or self.cfg.forward_attn
+        limit = BATCH_LIMIT if self.num_speakers <= 1 and not variant else SPEAKER_BATCH_LIMIT
         outs = []
         for b0 in range(0, B, limit):
             b1 = min(B, b0 + limit)
