@@ -172,9 +172,10 @@ __device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* A
   lds_barrier();  // window reads done before the scratch is reused
 }
 
-template <int MT>
+template <int MT, int VAR>
 __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
                                            int* is_last, float (&L)[8], bool haveL) {
+  constexpr bool WIN = VAR & 1, FWD = (VAR & 2) != 0;  // compiled-in decoder variants
   constexpr int NT = PT, TC = PTC;
   constexpr int NPT = NPQ_ / 16;  // query partials per thread (16 groups)
   constexpr int Bp = MT * 16;
@@ -247,7 +248,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   // attention windowing (common_layers.py:286-300): energies outside [lo, hi) around the previous
   // step's argmax become -inf; on the first step (win_idx == -1) position 0 takes the max energy
   int wlo = 0, whi = T, widx = 0;
-  if (P.win) {
+  if ((WIN && P.win)) {
     widx = ldci(P.win_idx + b);
     if (widx - 2 > 0) wlo = widx - 2;
     if (widx + 6 < T) whi = widx + 6;
@@ -256,11 +257,11 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     float e = P.bv;
 #pragma unroll
     for (int w = 0; w < 8; ++w) e += esum[w * TC + tid];
-    if (P.win && (t0 + tid < wlo || t0 + tid >= whi)) e = -INFINITY;
+    if ((WIN && P.win) && (t0 + tid < wlo || t0 + tid >= whi)) e = -INFINITY;
     sv[tid] = e;
   }
   lds_barrier();
-  if (P.win && widx == -1 && ch == 0) {  // the first window [0, 5) lies in chunk 0
+  if ((WIN && P.win) && widx == -1 && ch == 0) {  // the first window [0, 5) lies in chunk 0
     if (tid == 0) {
       float mx = -INFINITY;
       for (int i = 0; i < nvalid; ++i) mx = fmaxf(mx, sv[i]);
@@ -279,7 +280,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   }
   // forward attention (common_layers.py:302-323): w = ((1-u) a[t] + u a[t-1] + 1e-8) * raw with
   // raw = sigmoid(e) or exp(e - m_c); the normaliser of raw cancels in the renormalisation
-  const float fu = P.fwd ? ldc(P.fwd_u + b) : 0.f;
+  const float fu = (FWD && P.fwd) ? ldc(P.fwd_u + b) : 0.f;
   auto fwd_prev = [&](int pos) {  // previous forward alignment (init [1, 1e-7, ...], :236-241)
     if (pos < 0) return 0.f;
     return t == 0 ? (pos == 0 ? 1.f : 1e-7f) : ldc(P.alpha + (long)b * D.T_max + pos);
@@ -289,13 +290,13 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     float x = P.softmax ? (m_c == -INFINITY ? 0.f : expf(e - m_c)) : 1.f / (1.f + expf(-e));
     if (tid >= nvalid) x = 0.f;
     sw[tid] = x;
-    if (P.fwd) {
+    if ((FWD && P.fwd)) {
       const int pos = t0 + tid;
       swf[tid] = tid < nvalid ? ((1.f - fu) * fwd_prev(pos) + fu * fwd_prev(pos - 1) + 1e-8f) * x : 0.f;
     }
   }
   lds_barrier();
-  const float* wsel = P.fwd ? swf : sw;
+  const float* wsel = (FWD && P.fwd) ? swf : sw;
   float S_c = 0.f, F_c = 0.f, u = 0.f;
 #pragma unroll
   for (int i = 0; i < TC; ++i) {
@@ -307,7 +308,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   if (tid == 0) {
     stc(P.part_s + pidx, S_c);
     stc(P.part_m + pidx, m_c);
-    if (P.fwd) stc(P.part_f + pidx, F_c);
+    if ((FWD && P.fwd)) stc(P.part_f + pidx, F_c);
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -331,7 +332,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
       const long c = pb0 + min(cb + i, nch - 1);
       pm[i] = ldc(P.part_m + c);
       ps[i] = ldc(P.part_s + c);
-      pf[i] = P.fwd ? ldc(P.part_f + c) : 0.f;
+      pf[i] = (FWD && P.fwd) ? ldc(P.part_f + c) : 0.f;
       pu[i] = ldc(P.part_u + c * 512 + tid);
     }
     float wc[CB];
@@ -358,7 +359,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
       cx = fmaf(pu[i], wc[i], cx);
     }
   }
-  const float ctx_v = cx / (P.fwd ? Fz : S);
+  const float ctx_v = cx / ((FWD && P.fwd) ? Fz : S);
   stc(P.ctx + frag_idx(b, tid, 512), ctx_v);
   ATRACE(7);
   const long ab = (long)b * D.T_max;
@@ -366,21 +367,21 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   int besti = 0x7fffffff;
   for (int tt = tid; tt < T; tt += NT) {
     const float e = ldc(P.energy + ab + tt);
-    if (P.win && (e > bestv || (e == bestv && tt < besti))) {
+    if ((WIN && P.win) && (e > bestv || (e == bestv && tt < besti))) {
       bestv = e;
       besti = tt;
     }
     const float raw = P.softmax ? (e == -INFINITY ? 0.f : expf(e - m)) : 1.f / (1.f + expf(-e));
     const float al = raw / S;
     stc(P.acum + ab + tt, ldc(P.acum + ab + tt) + al);  // location state accumulates the raw alignment
-    if (P.fwd) {  // forward alignment into the energy slot (alpha is still read as a[t-1] here)
+    if ((FWD && P.fwd)) {  // forward alignment into the energy slot (alpha is still read as a[t-1] here)
       stc(P.energy + ab + tt, ((1.f - fu) * fwd_prev(tt) + fu * fwd_prev(tt - 1) + 1e-8f) * raw / Fz);
     } else {
       stc(P.alpha + ab + tt, al);
       if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = al;
     }
   }
-  if (P.fwd) {
+  if ((FWD && P.fwd)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     for (int tt = tid; tt < T; tt += NT) {
@@ -389,11 +390,11 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
       if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = af;
     }
   }
-  if (P.win || (P.fwd && P.trans)) {
+  if ((WIN && P.win) || ((FWD && P.fwd) && P.trans)) {
     // block reductions over the 512 threads: window argmax (first index of the max energy) and the
     // transition agent u = sigmoid(ta . [context, query] + b) for the next step
     float tdot = 0.f;
-    if (P.fwd && P.trans) {
+    if ((FWD && P.fwd) && P.trans) {
       tdot = P.ta_w[tid] * ctx_v;
 #pragma unroll
       for (int k = 0; k < 2; ++k) {
@@ -430,8 +431,8 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
         }
         ts += rt[w];
       }
-      if (P.win) stci(P.win_idx + b, bi);
-      if (P.fwd && P.trans) stc(P.fwd_u + b, 1.f / (1.f + expf(-(ts + P.ta_b))));
+      if ((WIN && P.win)) stci(P.win_idx + b, bi);
+      if ((FWD && P.fwd) && P.trans) stc(P.fwd_u + b, 1.f / (1.f + expf(-(ts + P.ta_b))));
     }
   }
   if (tid == 0) __hip_atomic_store(&P.counter[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -522,7 +523,7 @@ constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
   if (P.trace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                          \
   P.trace[((long)(t - P.trace_t0) * 16 + (k)) * PW + blockIdx.x] = __builtin_amdgcn_s_memrealtime()
 
-template <int MT>
+template <int MT, int VAR>
 __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
   __shared__ int sflag, is_last, dflag[64];
@@ -812,7 +813,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       if (g >= IW0) {  // items, then the decoder_rnn h_att part (attention_rnn's waits for P6)
         const int nitems = D.B * P.nchmax;
         for (int it = g - IW0; it < nitems; it += PW - IW0) {
-          pattn_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
+          pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
           lds_barrier();
         }
         gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
@@ -926,11 +927,18 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
   TTS_CHECK(a.D.B <= 64 && NATT * 4 * 4 == 1024, "persistent decoder: attention_rnn layout");
   TTS_CHECK(a.nchmax * PTC >= a.D.T_max, "persistent decoder: attention partial buffers too small");
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
-  const void* f = MT == 1 ? (const void*)persist_decoder_kernel<1> : (const void*)persist_decoder_kernel<2>;
-  static bool attr[3] = {false, false, false};
-  if (!attr[MT]) {
+  // decoder variants are compiled in only where used: VAR bit 0 windowing, bit 1 forward attention
+  const int var = (a.win ? 1 : 0) | (a.fwd ? 2 : 0);
+  static const void* const fns[2][4] = {
+      {(const void*)persist_decoder_kernel<1, 0>, (const void*)persist_decoder_kernel<1, 1>,
+       (const void*)persist_decoder_kernel<1, 2>, (const void*)persist_decoder_kernel<1, 3>},
+      {(const void*)persist_decoder_kernel<2, 0>, (const void*)persist_decoder_kernel<2, 1>,
+       (const void*)persist_decoder_kernel<2, 2>, (const void*)persist_decoder_kernel<2, 3>}};
+  const void* f = fns[MT - 1][var];
+  static bool attr[2][4] = {};
+  if (!attr[MT - 1][var]) {
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
-    attr[MT] = true;
+    attr[MT - 1][var] = true;
   }
   HIP_OK(hipMemsetAsync(a.bar, 0, 512 * 4, s));
   PArgs copy = a;
