@@ -110,6 +110,21 @@ int tts_melgan_generator(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens
 int tts_pqmf_synthesis(tts_ctx* ctx, const float* d_x, int B, int N, int L, const float* d_G, int taps,
                        float* d_y, void* stream);
 
+/* ---- Glow-TTS (TTS/tts/models/glow_tts.py, reference configs: gated-conv encoder) ----
+   tts_glow_set_tensor/finalize <- GlowTts(...).load_state_dict (enc_layers = 3 + num_layers_enc)
+   tts_glow_encode  <- GlowTts.inference up to the durations (glow_tts.py:166-176): encoder,
+                       duration predictor, w_ceil; h_ylens out: y_lengths per utterance
+   tts_glow_decode  <- the rest (:177-193) for Ty = max(h_ylens): generate_path, expanded means,
+                       z = y_mean + d_noise * noise_scale (d_noise (B, 80, Ty) standard normal),
+                       reverse flows; d_y (B, 80, 2*floor(Ty/2)), d_ymean (B, 80, Ty),
+                       d_attn (B, Ty, T_max), d_logw (B, T_max) = o_dur_log */
+int tts_glow_set_tensor(tts_ctx* ctx, const char* name, const float* host, const int64_t* shape, int ndim);
+int tts_glow_finalize(tts_ctx* ctx, int num_chars, int enc_layers, int num_flow_blocks, int num_block_layers);
+int tts_glow_encode(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max,
+                    float length_scale, int32_t* h_ylens, void* stream);
+int tts_glow_decode(tts_ctx* ctx, const float* d_noise, float noise_scale, int Ty, float* d_y, float* d_ymean,
+                    float* d_attn, float* d_logw, void* stream);
+
 /* ---- GE2E speaker encoder (TTS/speaker_encoder/model.py) ----
    tts_ge2e_set_tensor/finalize <- SpeakerEncoder(input_dim, proj_dim, lstm_dim, num_lstm_layers,
                                    use_lstm_with_projection).load_state_dict  (model.py:31-47)

@@ -1,0 +1,128 @@
+"""ORACLE (test infrastructure only): float32 numpy restatement of Glow-TTS inference for the
+reference configs (gated-conv encoder, mean_only, num_sqz 2, num_splits 4, dilation 1). Only
+``tests/`` may import it.
+
+Parity pin: ``tests/golden/glow.npz`` was produced in the build container by the reference's own
+``Encoder`` / ``Decoder`` modules (``TTS/tts/layers/glow_tts/{encoder,decoder}.py``) composed with
+the inference glue of ``TTS/tts/models/glow_tts.py:166-193`` (that module itself does not import
+here: its ``monotonic_align.core`` Cython extension is not built), see make_golden.py ``glow``.
+
+* ``layers/glow_tts/encoder.py:105-130``  embedding * sqrt(H), GatedConvBlock, proj_m, durations
+* ``layers/glow_tts/gated_conv.py:31-42``  conv -> LayerNorm -> GLU -> residual
+* ``layers/glow_tts/normalization.py:4-27,77-89``  LayerNorm (eps 1e-4), ActNorm reverse
+* ``layers/glow_tts/duration_predictor.py:29-40``
+* ``models/glow_tts.py:170-193``  w_ceil, y_lengths, generate_path, expanded means, noise
+* ``layers/glow_tts/decoder.py:6-33,81-95``  squeeze / unsqueeze, flows reversed
+* ``layers/glow_tts/glow.py:85-138,171-205,245-262``  WN, InvConvNear reverse, CouplingBlock reverse
+"""
+
+import numpy as np
+
+F32 = np.float32
+
+
+def conv1d(x, w, b=None, padding=0):
+    """x (Cin, L), w (Cout, Cin, K) -> (Cout, L + 2p - K + 1), zero padding."""
+    cin, L = x.shape
+    cout, _, K = w.shape
+    xp = np.pad(x, ((0, 0), (padding, padding))) if padding else x
+    Lo = xp.shape[1] - K + 1
+    cols = np.stack([xp[:, k:k + Lo] for k in range(K)], axis=1)  # (Cin, K, Lo)
+    y = w.reshape(cout, cin * K).astype(F32) @ cols.reshape(cin * K, Lo)
+    if b is not None:
+        y = y + b[:, None]
+    return y.astype(F32)
+
+
+def layer_norm(x, g, b, eps=1e-4):
+    m = x.mean(0, keepdims=True)
+    v = ((x - m) ** 2).mean(0, keepdims=True)
+    return ((x - m) / np.sqrt(v + F32(eps)) * g.reshape(-1, 1) + b.reshape(-1, 1)).astype(F32)
+
+
+def wn(sd, name):
+    if name + ".weight" in sd:
+        return sd[name + ".weight"]
+    v, g = sd[name + ".weight_v"].astype(np.float64), sd[name + ".weight_g"].astype(np.float64)
+    n = np.sqrt((v ** 2).reshape(v.shape[0], -1).sum(1)).reshape(-1, *([1] * (v.ndim - 1)))
+    return (v / n * g).astype(F32)
+
+
+class GlowOracle:
+    def __init__(self, sd, enc_layers=9, flows=12, wn_layers=4):
+        self.sd = {k: np.asarray(v, F32) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in sd.items()}
+        self.enc_layers, self.flows, self.wn_layers = enc_layers, flows, wn_layers
+
+    def encode(self, ids):
+        sd = self.sd
+        H = sd["encoder.emb.weight"].shape[1]
+        x = (sd["encoder.emb.weight"][ids] * F32(np.sqrt(H))).T.astype(F32)        # (H, T)
+        for i in range(self.enc_layers):
+            p = f"encoder.encoder."
+            o = conv1d(x, sd[p + f"conv_layers.{i}.weight"], sd[p + f"conv_layers.{i}.bias"], 2)
+            o = layer_norm(o, sd[p + f"norm_layers.{i}.gamma"], sd[p + f"norm_layers.{i}.beta"])
+            a, g = o[:H], o[H:]
+            x = (x + a * (F32(1) / (F32(1) + np.exp(-g)))).astype(F32)
+        o_mean = conv1d(x, sd["encoder.proj_m.weight"], sd["encoder.proj_m.bias"])
+        d = "encoder.duration_predictor."
+        h = np.maximum(conv1d(x, sd[d + "conv_1.weight"], sd[d + "conv_1.bias"], 1), F32(0))
+        h = layer_norm(h, sd[d + "norm_1.gamma"], sd[d + "norm_1.beta"])
+        h = np.maximum(conv1d(h, sd[d + "conv_2.weight"], sd[d + "conv_2.bias"], 1), F32(0))
+        h = layer_norm(h, sd[d + "norm_2.gamma"], sd[d + "norm_2.beta"])
+        logw = conv1d(h, sd[d + "proj.weight"], sd[d + "proj.bias"])[0]
+        return o_mean, logw
+
+    @staticmethod
+    def durations(logw, length_scale=1.0):
+        w_ceil = np.ceil(((np.exp(logw) - F32(1)) * F32(length_scale)).astype(F32))
+        return w_ceil, max(int(w_ceil.sum()), 1)
+
+    def inference(self, ids, noise=None, noise_scale=0.66, length_scale=1.0):
+        """one utterance: (y (80, 2*floor(Ty/2)), y_mean (80, Ty), attn (Ty, Tx), logw (Tx,), Ty)"""
+        sd = self.sd
+        o_mean, logw = self.encode(np.asarray(ids))
+        w_ceil, Ty = self.durations(logw, length_scale)
+        cum = np.cumsum(w_ceil)
+        j = np.arange(Ty, dtype=F32)[None, :]
+        path = (j < cum[:, None]).astype(F32)
+        path = path - np.concatenate([np.zeros((1, Ty), F32), path[:-1]], 0)          # (Tx, Ty)
+        y_mean = (o_mean @ path).astype(F32)                                            # (80, Ty)
+        z = y_mean if noise is None else (y_mean + noise[:, :Ty] * F32(noise_scale)).astype(F32)
+        C = z.shape[0]
+        K = Ty // 2
+        x = z[:, :2 * K].reshape(C, K, 2).transpose(2, 0, 1).reshape(2 * C, K)         # squeeze
+        for k in range(self.flows - 1, -1, -1):
+            x = self._coupling_rev(x, f"decoder.flows.{3 * k + 2}.")
+            x = self._invconv_rev(x, sd[f"decoder.flows.{3 * k + 1}.weight"])
+            a = f"decoder.flows.{3 * k}."
+            x = ((x - sd[a + "bias"].reshape(-1, 1)) * np.exp(-sd[a + "logs"].reshape(-1, 1))).astype(F32)
+        y = x.reshape(2, C, K).transpose(1, 2, 0).reshape(C, 2 * K)                    # unsqueeze
+        return y.astype(F32), y_mean, path.T.copy(), logw, Ty
+
+    def _coupling_rev(self, x, p):
+        sd = self.sd
+        C = x.shape[0] // 2
+        x0, x1 = x[:C], x[C:]
+        h = conv1d(x0, wn(sd, p + "start"), sd[p + "start.bias"])
+        H = h.shape[0]
+        out = np.zeros_like(h)
+        for i in range(self.wn_layers):
+            a = conv1d(h, wn(sd, p + f"wn.in_layers.{i}"), sd[p + f"wn.in_layers.{i}.bias"], 2)
+            acts = (np.tanh(a[:H]) * (F32(1) / (F32(1) + np.exp(-a[H:])))).astype(F32)
+            rs = conv1d(acts, wn(sd, p + f"wn.res_skip_layers.{i}"), sd[p + f"wn.res_skip_layers.{i}.bias"])
+            if i < self.wn_layers - 1:
+                h = (h + rs[:H]).astype(F32)
+                out = (out + rs[H:]).astype(F32)
+            else:
+                out = (out + rs).astype(F32)
+        mo = conv1d(out, sd[p + "end.weight"], sd[p + "end.bias"])
+        z1 = ((x1 - mo[:C]) * np.exp(-mo[C:])).astype(F32)
+        return np.concatenate([x0, z1], 0)
+
+    @staticmethod
+    def _invconv_rev(x, w):
+        c, t = x.shape
+        winv = np.linalg.inv(w.astype(np.float64)).astype(F32)
+        xs = x.reshape(2, c // 4, 2, t).transpose(0, 2, 1, 3).reshape(4, c // 4, t)
+        z = np.einsum("ab,bjt->ajt", winv, xs).astype(F32)
+        return z.reshape(2, 2, c // 4, t).transpose(0, 2, 1, 3).reshape(c, t)

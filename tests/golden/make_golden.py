@@ -239,6 +239,64 @@ def ge2e_case(name):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
+def glow_case(name):
+    """Glow-TTS (gated-conv encoder, as setup_model builds it, TTS/tts/utils/generic_utils.py:105-129).
+    The top-level GlowTts module does not import here (monotonic_align.core is an unbuilt Cython
+    extension), so the reference's Encoder and Decoder modules run under the inference glue of
+    glow_tts.py:166-193 restated below (durations, generate_path, expanded means, noise)."""
+    from TTS.tts.layers.glow_tts.encoder import Encoder
+    from TTS.tts.layers.glow_tts.decoder import Decoder
+    from tts_amd.spec import GlowConfig, glow_spec
+    cfg = GlowConfig()
+    enc = Encoder(cfg.num_chars, out_channels=80, hidden_channels=192, filter_channels=768, filter_channels_dp=256,
+                  encoder_type="gatedconv", num_heads=2, num_layers=6, kernel_size=3, dropout_p=0.1, mean_only=True,
+                  use_prenet=True, c_in_channels=0)
+    dec = Decoder(80, 192, 5, 1, 12, 4, dropout_p=0.05, num_splits=4, num_sqz=2, sigmoid_scale=False,
+                  c_in_channels=0)
+    ref_keys = {**{"encoder." + k: tuple(v.shape) for k, v in enc.state_dict().items()},
+                **{"decoder." + k: tuple(v.shape) for k, v in dec.state_dict().items()}}
+    spec = {n: tuple(sh) for n, sh, _ in glow_spec(cfg)}
+    assert spec == ref_keys, "glow_spec does not match the reference state_dict"
+    seed = 23
+    sd = synth_state_dict(glow_spec(cfg), seed)
+    enc.load_state_dict({k[8:]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("encoder.")})
+    dec.load_state_dict({k[8:]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("decoder.")})
+    enc.eval()
+    dec.eval()
+    rs = np.random.RandomState(24)
+    out = {"seed": np.int64(seed), "noise_scale": np.float32(0.66)}
+    for u, T in enumerate((17, 31)):
+        ids = rs.randint(1, cfg.num_chars, size=T).astype(np.int64)
+        with torch.no_grad():
+            x = torch.from_numpy(ids[None])
+            x_len = torch.tensor([T])
+            o_mean, o_log_scale, o_dur_log, x_mask = enc(x, x_len, g=None)
+            w = (torch.exp(o_dur_log) - 1) * x_mask * 1.0
+            w_ceil = torch.ceil(w)
+            y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
+            Ty = int(y_lengths.max())
+            y_mask = (torch.arange(Ty)[None] < y_lengths[:, None]).unsqueeze(1).to(x_mask.dtype)
+            attn_mask = torch.unsqueeze(x_mask, -1) * torch.unsqueeze(y_mask, 2)
+            cum = torch.cumsum(w_ceil.squeeze(1), 1)                       # generate_path
+            path = (torch.arange(Ty, dtype=cum.dtype)[None, None] < cum[:, :, None]).to(x_mask.dtype)
+            path = path - torch.nn.functional.pad(path, (0, 0, 1, 0))[:, :-1]
+            attn = (path * attn_mask.squeeze(1)).unsqueeze(1)
+            y_mean = torch.matmul(attn.squeeze(1).transpose(1, 2), o_mean.transpose(1, 2)).transpose(1, 2)
+            noise = torch.from_numpy(rs.normal(0, 1, size=(1, 80, Ty)).astype(np.float32))
+            z = (y_mean + torch.exp(torch.zeros_like(y_mean)) * noise * 0.66) * y_mask
+            y, _ = dec(z, y_mask, g=None, reverse=True)
+        k = f"u{u}"
+        out[f"{k}_ids"] = ids
+        out[f"{k}_noise"] = noise[0].numpy()
+        out[f"{k}_y"] = y[0].numpy()
+        out[f"{k}_ymean"] = y_mean[0].numpy()
+        out[f"{k}_attn"] = attn[0, 0].T.numpy()  # (Ty, Tx), as GlowTts.inference returns it
+        out[f"{k}_logw"] = o_dur_log[0, 0].numpy()
+        out[f"{k}_ylen"] = np.int64(y_lengths[0])
+        print(f"[{name}] u{u} T={T} Ty={Ty} y {tuple(y.shape)} |y|max {y.abs().max():.3f}")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
 def lj_profile():
     import scipy.io.wavfile as wavfile
     d = os.path.join(REF, "tests/data/ljspeech")
@@ -289,6 +347,8 @@ if __name__ == "__main__":
                   seed=19, utt_lens=[28, 17], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=20)
     if "ge2e" in which:
         ge2e_case("ge2e")
+    if "glow" in which:
+        glow_case("glow")
     if "taco_softmax" in which:
         taco_case("taco_softmax", TacotronConfig(attn_norm="softmax"), seed=2,
                   utt_lens=[25, 9], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=8)

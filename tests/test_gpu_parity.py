@@ -469,3 +469,42 @@ def test_ge2e_speaker_encoder_matches_reference(tag, proj):
     assert np.abs(emb[1] - fx[f"{tag}_emb2"][0]).max() <= 1e-5
     cemb = m.compute_embedding(torch.from_numpy(fx["x"]).cuda()).cpu().numpy()
     assert np.abs(cemb - fx[f"{tag}_cemb"]).max() <= 1e-5
+
+
+# --------------------------------------------------------------------------------- Glow-TTS
+def test_glow_tts_matches_reference():
+    """GlowTts.inference (glow_tts.py:166-193; gated-conv encoder, 12 reverse flow blocks) with the
+    fixture's prior noise, both utterances in ONE batched call: durations / y_lengths and the
+    monotonic path exact, means and mel <= 1e-4."""
+    from tts_amd import GlowTts
+    from tts_amd.spec import GlowConfig, glow_spec
+    from tts_amd.weights import synth_state_dict
+    _dev()
+    fx = load_fixture("glow")
+    m = GlowTts(num_chars=GlowConfig().num_chars)
+    sd = synth_state_dict(glow_spec(GlowConfig()), int(fx["seed"]))
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    ids = [fx["u0_ids"], fx["u1_ids"]]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((2, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    Ty = max(int(fx["u0_ylen"]), int(fx["u1_ylen"]))
+    noise = np.zeros((2, 80, Ty), np.float32)
+    for i in range(2):
+        nz = fx[f"u{i}_noise"]
+        noise[i, :, :nz.shape[1]] = nz
+    y, _, y_mean, _, attn, logw, _ = m.inference(torch.from_numpy(batch).cuda(), [len(x) for x in ids],
+                                                 noise=torch.from_numpy(noise).cuda())
+    y, y_mean, attn, logw = y.cpu().numpy(), y_mean.cpu().numpy(), attn.cpu().numpy(), logw.cpu().numpy()
+    for i in range(2):
+        k = f"u{i}"
+        ty, tx = int(fx[k + "_ylen"]), len(ids[i])
+        assert m.last_y_lengths[i] == ty
+        assert np.abs(logw[i, 0, :tx] - fx[k + "_logw"]).max() <= 1e-5
+        assert np.array_equal(attn[i, :ty, :tx], fx[k + "_attn"])
+        assert np.abs(y_mean[i, :, :ty] - fx[k + "_ymean"]).max() <= MEL_TOL
+        ref = fx[k + "_y"]
+        assert np.abs(y[i, :, :ref.shape[1]] - ref).max() <= MEL_TOL
+        assert not y[i, :, ref.shape[1]:].any()

@@ -174,3 +174,19 @@ def test_replicated_workload_weak_scaling():
         assert len(shards) == n and all(len(s) == 32 for s in shards)
         assert sorted(i for s in shards for i in s) == list(range(32 * n))
         assert sum(M[i] for i in shards[-1]) == 19112
+
+
+def test_glow_tts_constructor_and_keys():
+    """glow_tts.py:17-95 with the gated-conv encoder: checkpoint key layout; other encoders raise."""
+    from tts_amd import GlowTts
+    m = GlowTts(num_chars=130)
+    sd = m.state_dict()
+    assert tuple(sd["encoder.emb.weight"].shape) == (130, 192)
+    assert tuple(sd["encoder.proj_m.weight"].shape) == (80, 192, 1)
+    assert tuple(sd["decoder.flows.1.weight"].shape) == (4, 4)
+    assert m.noise_scale == 0.66 and m.length_scale == 1.
+    for kw in (dict(encoder_type="transformer"), dict(num_speakers=4, c_in_channels=256), dict(mean_only=False)):
+        with pytest.raises(NotImplementedError):
+            GlowTts(num_chars=130, **kw)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        m.inference(torch.ones(1, 5, dtype=torch.long), [5])

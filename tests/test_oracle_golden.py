@@ -142,3 +142,21 @@ def test_tacotron2_oracle_decoder_variants_match_reference(name):
         assert np.abs(post - fx[k + "_post"]).max() <= 1e-5
         # forward attention multiplies by the previous alignment every step: 1e-5 on alignments
         assert np.abs(align - fx[k + "_align"]).max() <= (1e-5 if cfg.forward_attn else 1e-6)
+
+
+def test_glow_oracle_matches_reference():
+    """Glow-TTS (gated-conv encoder): the reference's Encoder / Decoder modules under the inference
+    glue of glow_tts.py:166-193 (make_golden.py glow); fixed prior noise."""
+    from oracle.glow_np import GlowOracle
+    from tts_amd.spec import GlowConfig, glow_spec
+    from tts_amd.weights import synth_state_dict
+    fx = load_fixture("glow")
+    orc = GlowOracle(synth_state_dict(glow_spec(GlowConfig()), int(fx["seed"])))
+    for u in range(2):
+        k = f"u{u}"
+        y, ym, attn, logw, Ty = orc.inference(fx[k + "_ids"], fx[k + "_noise"], float(fx["noise_scale"]))
+        assert Ty == int(fx[k + "_ylen"])
+        assert np.abs(logw - fx[k + "_logw"]).max() <= 1e-5
+        assert np.array_equal(attn, fx[k + "_attn"])
+        assert np.abs(ym - fx[k + "_ymean"]).max() <= 1e-5
+        assert np.abs(y - fx[k + "_y"]).max() <= 5e-5

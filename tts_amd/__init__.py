@@ -5,6 +5,7 @@ Drop-in replacements for the reference's hot-path modules; compute runs in the H
 """
 
 from .factories import AttrDict, load_config, setup_generator, setup_model  # noqa: F401
+from .glow_tts import GlowTts  # noqa: F401
 from .speaker_encoder import SpeakerEncoder  # noqa: F401
 from .tacotron2 import Tacotron2  # noqa: F401
 from .vocoder import FullbandMelganGenerator, MelganGenerator, MultibandMelganGenerator, PQMF  # noqa: F401

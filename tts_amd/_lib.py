@@ -54,6 +54,11 @@ SIGNATURES = [
     ("tts_ge2e_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int]),
     ("tts_ge2e_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    ("tts_glow_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
+    ("tts_glow_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
+    ("tts_glow_encode", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, _c_int_p,
+                                       _vp]),
+    ("tts_glow_decode", ctypes.c_int, [_vp, _vp, ctypes.c_float, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("tts_time_decoder_kernel", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_f_p]),
     ("tts_decoder_stats", ctypes.c_int, [_vp, _c_i_p, _c_i_p, _c_f_p, _c_i_p]),
 ]
@@ -108,6 +113,7 @@ class Engine:
         self.taco_key = None
         self.melgan_key = None
         self.ge2e_key = None
+        self.glow_key = None
 
     def close(self):
         if self.h:
@@ -171,6 +177,23 @@ class Engine:
         B, M, _ = dec.shape
         lens_a, lens_p = _i32(lens)
         _check(self.lib.tts_taco_postnet(self.h, _ptr(dec), lens_p, B, M, _ptr(out), _stream(dec.device)))
+
+    def load_glow(self, tensors: Dict[str, np.ndarray], num_chars, enc_layers, flows, wn_layers):
+        for k, v in tensors.items():
+            self._set(self.lib.tts_glow_set_tensor, k, v)
+        _check(self.lib.tts_glow_finalize(self.h, num_chars, enc_layers, flows, wn_layers))
+
+    def glow_encode(self, ids, lens, length_scale):
+        B, T = ids.shape
+        lens_a, lens_p = _i32(lens)
+        ylens = np.zeros(B, np.int32)
+        _check(self.lib.tts_glow_encode(self.h, _ptr(ids), lens_p, B, T, float(length_scale),
+                                        ylens.ctypes.data_as(_c_int_p), _stream(ids.device)))
+        return ylens
+
+    def glow_decode(self, noise, noise_scale, Ty, y, y_mean, attn, logw):
+        _check(self.lib.tts_glow_decode(self.h, _ptr(noise), float(noise_scale), Ty, _ptr(y), _ptr(y_mean),
+                                        _ptr(attn), _ptr(logw), _stream(y.device)))
 
     def load_ge2e(self, tensors: Dict[str, np.ndarray], input_dim, proj_dim, lstm_dim, num_layers, with_proj):
         for k, v in tensors.items():

@@ -19,6 +19,21 @@ void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int 
                          const int* lens, int B, float* out, hipStream_t s);
 bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
                            unsigned* bar, float* out, hipStream_t s);
+void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, const float* beta, const float* res,
+                       long rb, float* out, long ob, const int* lens, int B, int T, hipStream_t s);
+void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, const int* lens, int B, int T,
+               hipStream_t s);
+void launch_glow_durations(const float* logw, int T, const int* lens, float length_scale, float* cum, int* ylen,
+                           float* wceil, int B, hipStream_t s);
+void launch_glow_expand(const float* o_mean, int C, int Tx, const int* xlens, const float* cum, const int* ylens,
+                        int Ty, const float* noise, float noise_scale, float* y_mean, float* z, float* attn, int B,
+                        hipStream_t s);
+void launch_glow_squeeze(const float* x, int C, int T, const int* ylens, float* y, int K, int B, hipStream_t s);
+void launch_glow_unsqueeze(const float* x, int C2, int K, const int* ylens, float* y, int T, int B, hipStream_t s);
+void launch_glow_gate(const float* a, int H, int K, const int* klens, float* acts, int B, hipStream_t s);
+void launch_glow_coupling(float* x, const float* mo, int Ch, int K, const int* klens, int B, hipStream_t s);
+void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
+                       int B, hipStream_t s);
 bool launch_lstm768_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
                             unsigned* bar, float* out, hipStream_t s);
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
@@ -279,6 +294,28 @@ struct Ge2eWS {
   DevBuf x, lens, g, o, p, bar, hbuf;
 };
 
+// Glow-TTS (TTS/tts/models/glow_tts.py, the reference configs' gated-conv encoder, mean_only,
+// num_sqz 2, num_splits 4, dilation 1, no speaker conditioning)
+struct GlowModel {
+  bool ready = false;
+  int num_chars = 0, H = 192, Fdp = 256, C = 80, enc_layers = 9, flows = 12, wn_layers = 4;
+  DevBuf emb;                                   // scaled by sqrt(H)
+  std::vector<ConvLayer> enc_conv;              // H -> 2H, k5
+  std::vector<DevBuf> enc_g, enc_b;             // LayerNorm(2H)
+  ConvLayer proj_m, dp1, dp2, dp_proj;
+  DevBuf dp_g1, dp_b1, dp_g2, dp_b2;
+  // per flow block (index = block): start (C -> H), WN in (H -> 2H, k5), res (H -> H), skip (H -> H),
+  // end (H -> 2C), inverse invconv + actnorm folded (2C -> 2C, 1x1 + bias)
+  std::vector<ConvLayer> start, end, invact;
+  std::vector<ConvLayer> wn_in, wn_res, wn_skip;  // [block * wn_layers + i]
+};
+
+struct GlowWS {
+  int B = 0, Tx = 0, Ty = 0;
+  DevBuf ids, lens, klens, ylens, xa, xb, h2, hdp, logw, cum, wceil, om, ym, z, attn, sq, sq2, wh, wa, wacts, wskip,
+      wmo, noise;
+};
+
 struct tts_ctx {
   int device = 0;
   hipStream_t s = nullptr;
@@ -295,6 +332,9 @@ struct tts_ctx {
   HostMap ge2e_host;
   Ge2eModel ge2e;
   Ge2eWS gws;
+  HostMap glow_host;
+  GlowModel glow;
+  GlowWS glws;
   // last decode configuration (for tts_time_decoder_kernel)
   int last_B = 0, last_T = 0, last_S = 0, last_r = 0;
 };
@@ -1693,6 +1733,263 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
   TTS_CHECK(err == 0, "speaker encoder: grid barrier timed out (workgroups not co-resident)");
 }
 
+// ------------------------------------------------------------------------------------ Glow-TTS
+void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_layers) {
+  auto& G = c->glow;
+  const auto& h = c->glow_host;
+  G.ready = false;
+  const int H = G.H, C = G.C, F = G.Fdp, C2 = 2 * C;
+  TTS_CHECK(enc_layers >= 1 && enc_layers <= 32 && flows >= 1 && flows <= 32 && wn_layers >= 1 && wn_layers <= 8,
+            "glow: layer counts");
+  G.num_chars = num_chars;
+  G.enc_layers = enc_layers;
+  G.flows = flows;
+  G.wn_layers = wn_layers;
+  int p2[8] = {2}, p1[8] = {1}, p0[8] = {0};
+  {
+    auto e = need(h, "encoder.emb.weight", {num_chars, H}).d;
+    const float sc = std::sqrt((float)H);  // encoder.py:107, x * math.sqrt(hidden) in fp32
+    for (auto& v : e) v *= sc;
+    G.emb.upload(e);
+  }
+  G.enc_conv.clear();
+  G.enc_conv.resize(enc_layers);
+  G.enc_g.clear();
+  G.enc_g.resize(enc_layers);
+  G.enc_b.clear();
+  G.enc_b.resize(enc_layers);
+  for (int i = 0; i < enc_layers; ++i) {
+    const std::string pf = "encoder.encoder.";
+    pack_conv(G.enc_conv[i], need(h, pf + "conv_layers." + std::to_string(i) + ".weight", {2 * H, H, 5}).d,
+              need(h, pf + "conv_layers." + std::to_string(i) + ".bias", {2 * H}).d, H, 2 * H, 5, 1, 1, p2);
+    G.enc_g[i].upload(need(h, pf + "norm_layers." + std::to_string(i) + ".gamma", {1, 2 * H, 1}).d);
+    G.enc_b[i].upload(need(h, pf + "norm_layers." + std::to_string(i) + ".beta", {1, 2 * H, 1}).d);
+  }
+  pack_conv(G.proj_m, need(h, "encoder.proj_m.weight", {C, H, 1}).d, need(h, "encoder.proj_m.bias", {C}).d, H, C, 1, 1,
+            1, p0);
+  const std::string dp = "encoder.duration_predictor.";
+  pack_conv(G.dp1, need(h, dp + "conv_1.weight", {F, H, 3}).d, need(h, dp + "conv_1.bias", {F}).d, H, F, 3, 1, 1, p1);
+  pack_conv(G.dp2, need(h, dp + "conv_2.weight", {F, F, 3}).d, need(h, dp + "conv_2.bias", {F}).d, F, F, 3, 1, 1, p1);
+  pack_conv(G.dp_proj, need(h, dp + "proj.weight", {1, F, 1}).d, need(h, dp + "proj.bias", {1}).d, F, 1, 1, 1, 1, p0);
+  G.dp_g1.upload(need(h, dp + "norm_1.gamma", {1, F, 1}).d);
+  G.dp_b1.upload(need(h, dp + "norm_1.beta", {1, F, 1}).d);
+  G.dp_g2.upload(need(h, dp + "norm_2.gamma", {1, F, 1}).d);
+  G.dp_b2.upload(need(h, dp + "norm_2.beta", {1, F, 1}).d);
+  G.start.clear();
+  G.start.resize(flows);
+  G.end.clear();
+  G.end.resize(flows);
+  G.invact.clear();
+  G.invact.resize(flows);
+  G.wn_in.clear();
+  G.wn_in.resize(flows * wn_layers);
+  G.wn_res.clear();
+  G.wn_res.resize(flows * wn_layers);
+  G.wn_skip.clear();
+  G.wn_skip.resize(flows * wn_layers);
+  for (int k = 0; k < flows; ++k) {
+    const std::string an = "decoder.flows." + std::to_string(3 * k) + ".";
+    const std::string ic = "decoder.flows." + std::to_string(3 * k + 1) + ".";
+    const std::string cp = "decoder.flows." + std::to_string(3 * k + 2) + ".";
+    pack_conv(G.start[k], wn_weight(h, cp + "start", {H, C, 1}), need(h, cp + "start.bias", {H}).d, C, H, 1, 1, 1, p0);
+    pack_conv(G.end[k], need(h, cp + "end.weight", {C2, H, 1}).d, need(h, cp + "end.bias", {C2}).d, H, C2, 1, 1, 1, p0);
+    for (int i = 0; i < wn_layers; ++i) {
+      const std::string wi = cp + "wn.in_layers." + std::to_string(i);
+      const std::string wr = cp + "wn.res_skip_layers." + std::to_string(i);
+      pack_conv(G.wn_in[k * wn_layers + i], wn_weight(h, wi, {2 * H, H, 5}), need(h, wi + ".bias", {2 * H}).d, H,
+                2 * H, 5, 1, 1, p2);
+      const bool last = i == wn_layers - 1;
+      const int rsc = last ? H : 2 * H;
+      const auto w = wn_weight(h, wr, {rsc, H, 1});
+      const auto& bb = need(h, wr + ".bias", {rsc}).d;
+      if (!last) {  // rows [0, H): residual, [H, 2H): skip
+        pack_conv(G.wn_res[k * wn_layers + i], std::vector<float>(w.begin(), w.begin() + (size_t)H * H),
+                  std::vector<float>(bb.begin(), bb.begin() + H), H, H, 1, 1, 1, p0);
+        pack_conv(G.wn_skip[k * wn_layers + i], std::vector<float>(w.begin() + (size_t)H * H, w.end()),
+                  std::vector<float>(bb.begin() + H, bb.end()), H, H, 1, 1, 1, p0);
+      } else {
+        pack_conv(G.wn_skip[k * wn_layers + i], w, bb, H, H, 1, 1, 1, p0);
+      }
+    }
+    // reverse of [ActNorm, InvConvNear]: z = exp(-logs) * (M x - bias), M the 2C x 2C matrix of the
+    // inverse 4 x 4 split mixing (glow.py:184-201: channel c = i*C + j*2 + k <-> split s = 2i + k)
+    const auto& w4 = need(h, ic + "weight", {4, 4}).d;
+    double a[4][8];
+    for (int r = 0; r < 4; ++r)
+      for (int q = 0; q < 8; ++q) a[r][q] = q < 4 ? w4[r * 4 + q] : (q - 4 == r ? 1.0 : 0.0);
+    for (int col = 0; col < 4; ++col) {  // Gauss-Jordan with partial pivoting
+      int piv = col;
+      for (int r = col + 1; r < 4; ++r)
+        if (std::fabs(a[r][col]) > std::fabs(a[piv][col])) piv = r;
+      for (int q = 0; q < 8; ++q) std::swap(a[col][q], a[piv][q]);
+      TTS_CHECK(std::fabs(a[col][col]) > 1e-12, "glow: singular InvConvNear weight");
+      const double d = a[col][col];
+      for (int q = 0; q < 8; ++q) a[col][q] /= d;
+      for (int r = 0; r < 4; ++r)
+        if (r != col) {
+          const double f = a[r][col];
+          for (int q = 0; q < 8; ++q) a[r][q] -= f * a[col][q];
+        }
+    }
+    // the reference inverts in fp32 and casts (glow.py:190-193): round the inverse to float
+    float winv[4][4];
+    for (int r = 0; r < 4; ++r)
+      for (int q = 0; q < 4; ++q) winv[r][q] = (float)a[r][4 + q];
+    const auto& logs = need(h, an + "logs", {1, C2, 1}).d;
+    const auto& abias = need(h, an + "bias", {1, C2, 1}).d;
+    std::vector<float> M((size_t)C2 * C2, 0.f), mb(C2);
+    const int J = C2 / 4;
+    for (int cp2 = 0; cp2 < C2; ++cp2) {
+      const int i2 = cp2 / (2 * J), j = (cp2 % (2 * J)) / 2, k2 = cp2 % 2;
+      const int s2 = 2 * i2 + k2;
+      const float e = std::exp(-logs[cp2]);
+      for (int s1 = 0; s1 < 4; ++s1) {
+        const int i1 = s1 / 2, k1 = s1 % 2;
+        const int c1 = i1 * 2 * J + j * 2 + k1;
+        M[(size_t)cp2 * C2 + c1] = e * winv[s2][s1];
+      }
+      mb[cp2] = -e * abias[cp2];
+    }
+    pack_conv(G.invact[k], M, mb, C2, C2, 1, 1, 1, p0);
+  }
+  HIP_OK(hipDeviceSynchronize());
+  G.ready = true;
+}
+
+// encoder + duration predictor + durations: h_ylens out (per-utterance frames)
+void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T, float length_scale,
+                 int32_t* h_ylens) {
+  auto& G = c->glow;
+  auto& W = c->glws;
+  TTS_CHECK(G.ready, "glow weights not finalized");
+  TTS_CHECK(B >= 1 && B <= 64 && T >= 1 && T <= 4096, "glow: bad sizes");
+  for (int b = 0; b < B; ++b) TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= T, "glow: lens out of range");
+  hipStream_t s = c->s;
+  const int H = G.H, C = G.C, F = G.Fdp;
+  long gen = 0;
+  grow<int>(W.lens, 64, gen);
+  grow<int>(W.ylens, 64, gen);
+  grow<int>(W.klens, 64, gen);
+  grow<float>(W.xa, (size_t)B * 2 * H * T, gen);
+  grow<float>(W.xb, (size_t)B * H * T, gen);
+  grow<float>(W.h2, (size_t)B * 2 * H * T, gen);
+  grow<float>(W.hdp, (size_t)B * F * T, gen);
+  grow<float>(W.logw, (size_t)B * T, gen);
+  grow<float>(W.cum, (size_t)B * T, gen);
+  grow<float>(W.wceil, (size_t)B * T, gen);
+  grow<float>(W.om, (size_t)B * C * T, gen);
+  W.B = B;
+  W.Tx = T;
+  std::vector<int> lens(h_lens, h_lens + B);
+  HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  const int* dl = W.lens.i();
+  float* x = W.xa.f();   // (B, H, T) current activations
+  float* x2 = W.xb.f();  // ping-pong
+  launch_glow_embed(d_ids, T, G.emb.f(), G.num_chars, H, dl, x, B, s);
+  auto conv = [&](const ConvLayer& L, const float* in, int cin, float* out, int cout, int epi) {
+    ConvCall cc;
+    cc.lens = dl;
+    cc.B = B;
+    cc.max_q = T;
+    cc.s[0] = src_of(in, (long)cin * T, T, 1, cin, 0);
+    cc.out = out;
+    cc.ob = (long)cout * T;
+    cc.oc = T;
+    cc.ot = 1;
+    cc.epi = epi;
+    run_conv(L, cc, s);
+  };
+  for (int i = 0; i < G.enc_layers; ++i) {  // GatedConvBlock (gated_conv.py:31-42)
+    conv(G.enc_conv[i], x, H, W.h2.f(), 2 * H, 0);
+    launch_glu_ln_res(W.h2.f(), (long)2 * H * T, 2 * H, G.enc_g[i].f(), G.enc_b[i].f(), x, (long)H * T, x2,
+                      (long)H * T, dl, B, T, s);
+    std::swap(x, x2);
+  }
+  conv(G.proj_m, x, H, W.om.f(), C, 0);  // o_mean (encoder.py:125)
+  // DurationPredictor (duration_predictor.py:29-40): conv -> relu -> LN, twice, then proj
+  conv(G.dp1, x, H, W.hdp.f(), F, 1);
+  launch_ln(W.hdp.f(), (long)F * T, F, G.dp_g1.f(), G.dp_b1.f(), dl, B, T, s);
+  conv(G.dp2, W.hdp.f(), F, W.h2.f(), F, 1);
+  launch_ln(W.h2.f(), (long)F * T, F, G.dp_g2.f(), G.dp_b2.f(), dl, B, T, s);
+  conv(G.dp_proj, W.h2.f(), F, W.logw.f(), 1, 0);
+  launch_glow_durations(W.logw.f(), T, dl, length_scale, W.cum.f(), W.ylens.i(), W.wceil.f(), B, s);
+  HIP_OK(hipMemcpyAsync(h_ylens, W.ylens.p, B * 4, hipMemcpyDeviceToHost, s));
+  HIP_OK(hipStreamSynchronize(s));
+  int mx = 1;
+  for (int b = 0; b < B; ++b) mx = std::max(mx, (int)h_ylens[b]);
+  W.Ty = mx;
+}
+
+// expand + noise + reverse flows after glow_encode: d_y (B, 80, 2*(Ty/2)), d_ymean (B, 80, Ty),
+// d_attn (B, Ty, Tx), d_logw (B, Tx) = o_dur_log; d_noise (B, 80, Ty) standard normal or null
+void glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, float* d_y, float* d_ymean,
+                 float* d_attn, float* d_logw) {
+  auto& G = c->glow;
+  auto& W = c->glws;
+  TTS_CHECK(W.B > 0 && Ty == W.Ty, "glow: decode after encode with Ty = max(y_lengths)");
+  hipStream_t s = c->s;
+  const int B = W.B, Tx = W.Tx, H = G.H, C = G.C, C2 = 2 * C, K = Ty / 2;
+  long gen = 0;
+  grow<float>(W.z, (size_t)B * C * Ty, gen);
+  grow<float>(W.sq, (size_t)B * C2 * std::max(K, 1), gen);
+  grow<float>(W.sq2, (size_t)B * C2 * std::max(K, 1), gen);
+  grow<float>(W.wh, (size_t)B * H * std::max(K, 1), gen);
+  grow<float>(W.wa, (size_t)B * 2 * H * std::max(K, 1), gen);
+  grow<float>(W.wacts, (size_t)B * H * std::max(K, 1), gen);
+  grow<float>(W.wskip, (size_t)B * H * std::max(K, 1), gen);
+  grow<float>(W.wmo, (size_t)B * C2 * std::max(K, 1), gen);
+  launch_glow_expand(W.om.f(), C, Tx, W.lens.i(), W.cum.f(), W.ylens.i(), Ty, d_noise, noise_scale, d_ymean, W.z.f(),
+                     d_attn, B, s);
+  HIP_OK(hipMemcpyAsync(d_logw, W.logw.p, (size_t)B * Tx * 4, hipMemcpyDeviceToDevice, s));
+  HIP_OK(hipMemsetAsync(d_y, 0, (size_t)B * C * 2 * K * 4, s));
+  if (K == 0) return;
+  {  // squeezed lengths floor(y_len / 2) (decoder.py:13-15)
+    std::vector<int> yl(B);
+    HIP_OK(hipMemcpy(yl.data(), W.ylens.p, B * 4, hipMemcpyDeviceToHost));
+    for (auto& v : yl) v /= 2;
+    HIP_OK(hipMemcpyAsync(W.klens.p, yl.data(), B * 4, hipMemcpyHostToDevice, s));
+  }
+  const int* kl = W.klens.i();
+  launch_glow_squeeze(W.z.f(), C, Ty, W.ylens.i(), W.sq.f(), K, B, s);
+  auto conv = [&](const ConvLayer& L, const float* in, int cin, float* out, int cout, const float* resid) {
+    ConvCall cc;
+    cc.lens = kl;
+    cc.B = B;
+    cc.max_q = K;
+    cc.s[0] = src_of(in, (long)(in == W.sq.f() || in == W.sq2.f() ? C2 : cin) * K, K, 1, cin, 0);
+    cc.out = out;
+    cc.ob = (long)cout * K;
+    cc.oc = K;
+    cc.ot = 1;
+    cc.resid = resid;
+    cc.rb = (long)cout * K;
+    cc.rc = K;
+    cc.rt = 1;
+    run_conv(L, cc, s);
+  };
+  float* x = W.sq.f();
+  float* x2 = W.sq2.f();
+  for (int k = G.flows - 1; k >= 0; --k) {
+    // CouplingBlock reverse (glow.py:245-262): WN over start(x0), then z1 = (x1 - m) exp(-logs)
+    conv(G.start[k], x, C, W.wh.f(), H, nullptr);
+    HIP_OK(hipMemsetAsync(W.wskip.p, 0, (size_t)B * H * K * 4, s));
+    for (int i = 0; i < G.wn_layers; ++i) {  // WN (glow.py:118-138), g = None
+      const int li = k * G.wn_layers + i;
+      conv(G.wn_in[li], W.wh.f(), H, W.wa.f(), 2 * H, nullptr);
+      launch_glow_gate(W.wa.f(), H, K, kl, W.wacts.f(), B, s);
+      if (i < G.wn_layers - 1) conv(G.wn_res[li], W.wacts.f(), H, W.wh.f(), H, W.wh.f());
+      conv(G.wn_skip[li], W.wacts.f(), H, W.wskip.f(), H, W.wskip.f());
+    }
+    conv(G.end[k], W.wskip.f(), H, W.wmo.f(), C2, nullptr);
+    launch_glow_coupling(x, W.wmo.f(), C, K, kl, B, s);
+    // InvConvNear + ActNorm reverse as one 1x1 conv
+    conv(G.invact[k], x, C2, x2, C2, nullptr);
+    std::swap(x, x2);
+  }
+  launch_glow_unsqueeze(x, C2, K, W.ylens.i(), d_y, 2 * K, B, s);
+  HIP_OK(hipStreamSynchronize(s));
+}
+
 void set_tensor(HostMap& m, const char* name, const float* h, const int64_t* shape, int ndim) {
   TTS_CHECK(name && (h || ndim == 0), "set_tensor: null argument");
   HostT t;
@@ -1869,6 +2166,44 @@ int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int 
     HIP_OK(hipMemsetAsync(d_out, 0, (size_t)B * M_max * 80 * 4, c->s));
     run_postnet(c, d_dec, (long)M_max * 80, W.mlens.i(), B, M_max, maxM, d_out, (long)M_max * 80, c->s);
     HIP_OK(hipStreamSynchronize(c->s));
+    leave(c, stream);
+  });
+}
+
+int tts_glow_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    set_tensor(c->glow_host, name, h, shape, ndim);
+  });
+}
+
+int tts_glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int num_flow_blocks, int num_block_layers) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    DeviceGuard g(c->device);
+    HostMapConsumer consume{c->glow_host};
+    glow_finalize(c, num_chars, enc_layers, num_flow_blocks, num_block_layers);
+  });
+}
+
+int tts_glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, float length_scale,
+                    int32_t* h_ylens, void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_ids && h_lens && h_ylens, "null argument");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    glow_encode(c, d_ids, h_lens, B, T_max, length_scale, h_ylens);
+    leave(c, stream);
+  });
+}
+
+int tts_glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, float* d_y, float* d_ymean,
+                    float* d_attn, float* d_logw, void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_y && d_ymean && d_attn && d_logw, "null argument");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    glow_decode(c, d_noise, noise_scale, Ty, d_y, d_ymean, d_attn, d_logw);
     leave(c, stream);
   });
 }

@@ -262,7 +262,7 @@ int conv_tile_for_cout(int cout) {
   if (cout % 128 == 0) return TILE_128x64;
   if (cout == 192) return TILE_192x64;
   if (cout == 96) return TILE_96x64;
-  if (cout == 80) return TILE_80x64;
+  if (cout % 80 == 0) return TILE_80x64;
   if (cout == 48) return TILE_48x128;
   if (cout % 64 == 0) return TILE_64x64;
   return TILE_16x256;

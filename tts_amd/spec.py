@@ -267,3 +267,58 @@ def ge2e_spec(c: Ge2eConfig) -> Spec:
             ]
         s += [("layers.linear.weight", (P, H), "xavier"), ("layers.linear.bias", (P,), "bias")]
     return s
+
+
+@dataclass
+class GlowConfig:
+    """``GlowTts`` as ``setup_model`` builds it for the reference configs
+    (``TTS/tts/utils/generic_utils.py:105-129``; ``configs/glow_tts_gated_conv.json``): hidden 192,
+    duration-predictor filters 256, 80 mel channels, gated-conv encoder with 3 + 6 layers, 12 flow
+    blocks of 4 WN layers (kernel 5, dilation 1), num_sqz 2, num_splits 4, mean_only."""
+    num_chars: int = 129
+    hidden_channels: int = 192
+    filter_channels_dp: int = 256
+    out_channels: int = 80
+    num_layers_enc: int = 6
+    num_flow_blocks_dec: int = 12
+    num_block_layers: int = 4
+    kernel_size_dec: int = 5
+
+
+def glow_spec(c: GlowConfig) -> Spec:
+    """state_dict spec of ``GlowTts`` (encoder_type 'gatedconv'): ``encoder.*`` from
+    ``layers/glow_tts/encoder.py:59-104`` + ``gated_conv.py`` + ``duration_predictor.py``,
+    ``decoder.flows.*`` from ``layers/glow_tts/decoder.py:60-79`` + ``glow.py`` + ``normalization.py``."""
+    H, F, C = c.hidden_channels, c.filter_channels_dp, c.out_channels
+    s: Spec = [("encoder.emb.weight", (c.num_chars, H), "glow_emb")]
+    for i in range(3 + c.num_layers_enc):
+        s += [(f"encoder.encoder.conv_layers.{i}.weight", (2 * H, H, 5), "conv"),
+              (f"encoder.encoder.conv_layers.{i}.bias", (2 * H,), "bias"),
+              (f"encoder.encoder.norm_layers.{i}.gamma", (1, 2 * H, 1), "ln_g"),
+              (f"encoder.encoder.norm_layers.{i}.beta", (1, 2 * H, 1), "bias")]
+    dp = "encoder.duration_predictor"
+    s += [("encoder.proj_m.weight", (C, H, 1), "conv"), ("encoder.proj_m.bias", (C,), "bias"),
+          (f"{dp}.conv_1.weight", (F, H, 3), "conv"), (f"{dp}.conv_1.bias", (F,), "bias"),
+          (f"{dp}.norm_1.gamma", (1, F, 1), "ln_g"), (f"{dp}.norm_1.beta", (1, F, 1), "bias"),
+          (f"{dp}.conv_2.weight", (F, F, 3), "conv"), (f"{dp}.conv_2.bias", (F,), "bias"),
+          (f"{dp}.norm_2.gamma", (1, F, 1), "ln_g"), (f"{dp}.norm_2.beta", (1, F, 1), "bias"),
+          (f"{dp}.proj.weight", (1, F, 1), "conv"), (f"{dp}.proj.bias", (1,), "bias")]
+    C2 = 2 * C
+    for k in range(c.num_flow_blocks_dec):
+        f = f"decoder.flows.{3 * k}"
+        s += [(f"{f}.logs", (1, C2, 1), "actnorm"), (f"{f}.bias", (1, C2, 1), "bias")]
+        s += [(f"decoder.flows.{3 * k + 1}.weight", (4, 4), "orthogonal")]
+        f = f"decoder.flows.{3 * k + 2}"
+        s += [(f"{f}.start.bias", (H,), "bias"), (f"{f}.start.weight_g", (H, 1, 1), "wn_g"),
+              (f"{f}.start.weight_v", (H, C, 1), "conv"),
+              (f"{f}.end.weight", (C2, H, 1), "glow_end"), (f"{f}.end.bias", (C2,), "bias")]
+        for i in range(c.num_block_layers):
+            s += [(f"{f}.wn.in_layers.{i}.bias", (2 * H,), "bias"),
+                  (f"{f}.wn.in_layers.{i}.weight_g", (2 * H, 1, 1), "wn_g"),
+                  (f"{f}.wn.in_layers.{i}.weight_v", (2 * H, H, c.kernel_size_dec), "conv")]
+        for i in range(c.num_block_layers):
+            rs = H if i == c.num_block_layers - 1 else 2 * H
+            s += [(f"{f}.wn.res_skip_layers.{i}.bias", (rs,), "bias"),
+                  (f"{f}.wn.res_skip_layers.{i}.weight_g", (rs, 1, 1), "wn_g"),
+                  (f"{f}.wn.res_skip_layers.{i}.weight_v", (rs, H, 1), "conv")]
+    return s

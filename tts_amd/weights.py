@@ -73,6 +73,21 @@ def synth_tensor(name: str, shape: Tuple[int, ...], kind: str, seed: int,
     elif kind == "xavier":  # xavier_normal_ in the reference (speaker_encoder/model.py:49-54): same std
         fi, fo = _fans(shape)
         x = u * math.sqrt(3.0) * math.sqrt(2.0 / (fi + fo))
+    elif kind == "glow_emb":  # normal_(0, hidden ** -0.5) (glow_tts/encoder.py:61): same std
+        x = u * math.sqrt(3.0) * shape[1] ** -0.5
+    elif kind == "ln_g":
+        x = 1.0 + 0.1 * u
+    elif kind == "actnorm":
+        x = 0.05 * u
+    elif kind == "glow_end":  # zero-initialised in the reference; small so the flows stay tame
+        fi, fo = _fans(shape)
+        x = 0.1 * u * math.sqrt(6.0 / (fi + fo))
+    elif kind == "orthogonal":  # a rotation (QR of a splitmix64 matrix), det > 0 as in glow.py:172-175
+        q, r = np.linalg.qr(u.reshape(shape))
+        q = q * np.sign(np.diag(r))[None, :]
+        if np.linalg.det(q) < 0:
+            q[:, 0] = -q[:, 0]
+        x = q.reshape(-1)
     elif kind == "speaker_emb":  # normal_(0, 0.3) in the reference: same std, uniform
         x = u * (0.3 * math.sqrt(3.0))
     elif kind == "bias":
