@@ -30,8 +30,6 @@ void launch_glow_expand(const float* o_mean, int C, int Tx, const int* xlens, co
                         hipStream_t s);
 void launch_glow_squeeze(const float* x, int C, int T, const int* ylens, float* y, int K, int B, hipStream_t s);
 void launch_glow_unsqueeze(const float* x, int C2, int K, const int* ylens, float* y, int T, int B, hipStream_t s);
-void launch_glow_gate(const float* a, int H, int K, const int* klens, float* acts, int B, hipStream_t s);
-void launch_glow_coupling(float* x, const float* mo, int Ch, int K, const int* klens, int B, hipStream_t s);
 void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
                        int B, hipStream_t s);
 bool launch_lstm768_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
@@ -115,6 +113,7 @@ void pack_conv(ConvLayer& L, const std::vector<float>& Wm, const std::vector<flo
   L.dil = dil;
   L.nphase = nphase;
   L.tile = conv_tile_for_cout(Cout);
+  if (K == 1 && Cout % 64 == 0) L.tile = TILE_64x64;  // 1x1 convs are short: more workgroups
   const int TC = conv_tile_tc(L.tile);
   L.Cout_pad = (Cout + TC - 1) / TC * TC;
   const int Kdim = Cin * K;
@@ -147,7 +146,8 @@ struct ConvCall {
   int epi = 0;
   const float* resid = nullptr;
   long rb = 0;
-  int rc = 0, rt = 0;
+  int rc = 0, rt = 0, resid_rows = 0;
+  const float* aux = nullptr;
   int max_q = 0, B = 0;
 };
 
@@ -183,6 +183,8 @@ void run_conv(const ConvLayer& L, const ConvCall& c, hipStream_t st) {
   a.rb = c.rb;
   a.rc = c.rc;
   a.rt = c.rt;
+  a.resid_rows = c.resid_rows;
+  a.aux = c.aux;
   a.max_q = c.max_q;
   a.B = c.B;
   launch_conv(a, L.tile, st);
@@ -304,16 +306,18 @@ struct GlowModel {
   std::vector<DevBuf> enc_g, enc_b;             // LayerNorm(2H)
   ConvLayer proj_m, dp1, dp2, dp_proj;
   DevBuf dp_g1, dp_b1, dp_g2, dp_b2;
-  // per flow block (index = block): start (C -> H), WN in (H -> 2H, k5), res (H -> H), skip (H -> H),
-  // end (H -> 2C), inverse invconv + actnorm folded (2C -> 2C, 1x1 + bias)
-  std::vector<ConvLayer> start, end, invact;
-  std::vector<ConvLayer> wn_in, wn_res, wn_skip;  // [block * wn_layers + i]
+  // per flow block (index = block): start (C -> H), WN in (H -> 2H, k5, rows interleaved), res+skip
+  // (H -> 2H, last layer H -> H skip), end (H -> 2C, rows interleaved) whose epilogue also applies
+  // the inverse InvConvNear + ActNorm from invtab (2C x {w[4], bias, exp(-logs)})
+  std::vector<ConvLayer> start, end;
+  std::vector<DevBuf> invtab;
+  std::vector<ConvLayer> wn_in, wn_rs;  // [block * wn_layers + i]
 };
 
 struct GlowWS {
   int B = 0, Tx = 0, Ty = 0;
-  DevBuf ids, lens, klens, ylens, xa, xb, h2, hdp, logw, cum, wceil, om, ym, z, attn, sq, sq2, wh, wa, wacts, wskip,
-      wmo, noise;
+  DevBuf ids, lens, klens, ylens, xa, xb, h2, hdp, logw, cum, wceil, om, z, sq, sq2, whs, wacts;
+  std::vector<int> h_ylens, h_klens;
 };
 
 struct tts_ctx {
@@ -1734,6 +1738,19 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
 }
 
 // ------------------------------------------------------------------------------------ Glow-TTS
+// rows (r, half + r) -> (2r, 2r + 1) of a (2 * half, rowlen) weight and its bias
+static std::pair<std::vector<float>, std::vector<float>> interleave_halves(const std::vector<float>& w,
+                                                                           const std::vector<float>& b, int half,
+                                                                           int rowlen) {
+  std::vector<float> wo(w.size()), bo(b.size());
+  for (int r = 0; r < 2 * half; ++r) {
+    const int src = (r & 1) ? half + r / 2 : r / 2;
+    std::copy(w.begin() + (size_t)src * rowlen, w.begin() + (size_t)(src + 1) * rowlen, wo.begin() + (size_t)r * rowlen);
+    bo[r] = b[src];
+  }
+  return {wo, bo};
+}
+
 void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_layers) {
   auto& G = c->glow;
   const auto& h = c->glow_host;
@@ -1779,40 +1796,34 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
   G.start.resize(flows);
   G.end.clear();
   G.end.resize(flows);
-  G.invact.clear();
-  G.invact.resize(flows);
+  G.invtab.clear();
+  G.invtab.resize(flows);
   G.wn_in.clear();
   G.wn_in.resize(flows * wn_layers);
-  G.wn_res.clear();
-  G.wn_res.resize(flows * wn_layers);
-  G.wn_skip.clear();
-  G.wn_skip.resize(flows * wn_layers);
+  G.wn_rs.clear();
+  G.wn_rs.resize(flows * wn_layers);
   for (int k = 0; k < flows; ++k) {
     const std::string an = "decoder.flows." + std::to_string(3 * k) + ".";
     const std::string ic = "decoder.flows." + std::to_string(3 * k + 1) + ".";
     const std::string cp = "decoder.flows." + std::to_string(3 * k + 2) + ".";
     pack_conv(G.start[k], wn_weight(h, cp + "start", {H, C, 1}), need(h, cp + "start.bias", {H}).d, C, H, 1, 1, 1, p0);
-    pack_conv(G.end[k], need(h, cp + "end.weight", {C2, H, 1}).d, need(h, cp + "end.bias", {C2}).d, H, C2, 1, 1, 1, p0);
+    // end rows interleaved (m_c, logs_c) for the conv's coupling-pair epilogue
+    auto [we, be] = interleave_halves(need(h, cp + "end.weight", {C2, H, 1}).d, need(h, cp + "end.bias", {C2}).d, C, H);
+    pack_conv(G.end[k], we, be, H, C2, 1, 1, 1, p0);
     for (int i = 0; i < wn_layers; ++i) {
       const std::string wi = cp + "wn.in_layers." + std::to_string(i);
       const std::string wr = cp + "wn.res_skip_layers." + std::to_string(i);
-      pack_conv(G.wn_in[k * wn_layers + i], wn_weight(h, wi, {2 * H, H, 5}), need(h, wi + ".bias", {2 * H}).d, H,
-                2 * H, 5, 1, 1, p2);
-      const bool last = i == wn_layers - 1;
-      const int rsc = last ? H : 2 * H;
-      const auto w = wn_weight(h, wr, {rsc, H, 1});
-      const auto& bb = need(h, wr + ".bias", {rsc}).d;
-      if (!last) {  // rows [0, H): residual, [H, 2H): skip
-        pack_conv(G.wn_res[k * wn_layers + i], std::vector<float>(w.begin(), w.begin() + (size_t)H * H),
-                  std::vector<float>(bb.begin(), bb.begin() + H), H, H, 1, 1, 1, p0);
-        pack_conv(G.wn_skip[k * wn_layers + i], std::vector<float>(w.begin() + (size_t)H * H, w.end()),
-                  std::vector<float>(bb.begin() + H, bb.end()), H, H, 1, 1, 1, p0);
-      } else {
-        pack_conv(G.wn_skip[k * wn_layers + i], w, bb, H, H, 1, 1, 1, p0);
-      }
+      // in rows interleaved (tanh_c, sigmoid_c) for the gate-pair epilogue
+      auto [wg, bg] = interleave_halves(wn_weight(h, wi, {2 * H, H, 5}), need(h, wi + ".bias", {2 * H}).d, H, H * 5);
+      pack_conv(G.wn_in[k * wn_layers + i], wg, bg, H, 2 * H, 5, 1, 1, p2);
+      // rows [0, H): residual, [H, 2H): skip -- one conv into the [hidden | skip] buffer; the last
+      // layer has the skip rows only
+      const int rsc = i == wn_layers - 1 ? H : 2 * H;
+      pack_conv(G.wn_rs[k * wn_layers + i], wn_weight(h, wr, {rsc, H, 1}), need(h, wr + ".bias", {rsc}).d, H, rsc, 1,
+                1, 1, p0);
     }
-    // reverse of [ActNorm, InvConvNear]: z = exp(-logs) * (M x - bias), M the 2C x 2C matrix of the
-    // inverse 4 x 4 split mixing (glow.py:184-201: channel c = i*C + j*2 + k <-> split s = 2i + k)
+    // reverse of [ActNorm, InvConvNear] (glow.py:48-58, 184-201): output channel c' = i*C + 2j + k
+    // (split s' = 2i + k) = (sum_s winv[s'][s] x[c_s] - bias[c']) * exp(-logs[c']), c_s = i_s*C + 2j + k_s
     const auto& w4 = need(h, ic + "weight", {4, 4}).d;
     double a[4][8];
     for (int r = 0; r < 4; ++r)
@@ -1832,25 +1843,16 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
         }
     }
     // the reference inverts in fp32 and casts (glow.py:190-193): round the inverse to float
-    float winv[4][4];
-    for (int r = 0; r < 4; ++r)
-      for (int q = 0; q < 4; ++q) winv[r][q] = (float)a[r][4 + q];
     const auto& logs = need(h, an + "logs", {1, C2, 1}).d;
     const auto& abias = need(h, an + "bias", {1, C2, 1}).d;
-    std::vector<float> M((size_t)C2 * C2, 0.f), mb(C2);
-    const int J = C2 / 4;
+    std::vector<float> tab((size_t)C2 * 6);
     for (int cp2 = 0; cp2 < C2; ++cp2) {
-      const int i2 = cp2 / (2 * J), j = (cp2 % (2 * J)) / 2, k2 = cp2 % 2;
-      const int s2 = 2 * i2 + k2;
-      const float e = std::exp(-logs[cp2]);
-      for (int s1 = 0; s1 < 4; ++s1) {
-        const int i1 = s1 / 2, k1 = s1 % 2;
-        const int c1 = i1 * 2 * J + j * 2 + k1;
-        M[(size_t)cp2 * C2 + c1] = e * winv[s2][s1];
-      }
-      mb[cp2] = -e * abias[cp2];
+      const int s2 = 2 * (cp2 / C) + cp2 % 2;
+      for (int s1 = 0; s1 < 4; ++s1) tab[cp2 * 6 + s1] = (float)a[s2][4 + s1];
+      tab[cp2 * 6 + 4] = abias[cp2];
+      tab[cp2 * 6 + 5] = std::exp(-logs[cp2]);
     }
-    pack_conv(G.invact[k], M, mb, C2, C2, 1, 1, 1, p0);
+    G.invtab[k].upload(tab);
   }
   HIP_OK(hipDeviceSynchronize());
   G.ready = true;
@@ -1916,6 +1918,8 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
   HIP_OK(hipMemcpyAsync(h_ylens, W.ylens.p, B * 4, hipMemcpyDeviceToHost, s));
   HIP_OK(hipStreamSynchronize(s));
   int mx = 1;
+  W.h_ylens.assign(h_ylens, h_ylens + B);
+  W.h_klens.resize(B);
   for (int b = 0; b < B; ++b) mx = std::max(mx, (int)h_ylens[b]);
   W.Ty = mx;
 }
@@ -1930,60 +1934,60 @@ void glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, fl
   hipStream_t s = c->s;
   const int B = W.B, Tx = W.Tx, H = G.H, C = G.C, C2 = 2 * C, K = Ty / 2;
   long gen = 0;
+  const int K1 = std::max(K, 1);
   grow<float>(W.z, (size_t)B * C * Ty, gen);
-  grow<float>(W.sq, (size_t)B * C2 * std::max(K, 1), gen);
-  grow<float>(W.sq2, (size_t)B * C2 * std::max(K, 1), gen);
-  grow<float>(W.wh, (size_t)B * H * std::max(K, 1), gen);
-  grow<float>(W.wa, (size_t)B * 2 * H * std::max(K, 1), gen);
-  grow<float>(W.wacts, (size_t)B * H * std::max(K, 1), gen);
-  grow<float>(W.wskip, (size_t)B * H * std::max(K, 1), gen);
-  grow<float>(W.wmo, (size_t)B * C2 * std::max(K, 1), gen);
+  grow<float>(W.sq, (size_t)B * C2 * K1, gen);
+  grow<float>(W.sq2, (size_t)B * C2 * K1, gen);
+  grow<float>(W.whs, (size_t)B * 2 * H * K1, gen);
+  grow<float>(W.wacts, (size_t)B * H * K1, gen);
   launch_glow_expand(W.om.f(), C, Tx, W.lens.i(), W.cum.f(), W.ylens.i(), Ty, d_noise, noise_scale, d_ymean, W.z.f(),
                      d_attn, B, s);
   HIP_OK(hipMemcpyAsync(d_logw, W.logw.p, (size_t)B * Tx * 4, hipMemcpyDeviceToDevice, s));
   HIP_OK(hipMemsetAsync(d_y, 0, (size_t)B * C * 2 * K * 4, s));
   if (K == 0) return;
-  {  // squeezed lengths floor(y_len / 2) (decoder.py:13-15)
-    std::vector<int> yl(B);
-    HIP_OK(hipMemcpy(yl.data(), W.ylens.p, B * 4, hipMemcpyDeviceToHost));
-    for (auto& v : yl) v /= 2;
-    HIP_OK(hipMemcpyAsync(W.klens.p, yl.data(), B * 4, hipMemcpyHostToDevice, s));
-  }
+  // squeezed lengths floor(y_len / 2) (decoder.py:13-15); the staging vector lives in the
+  // workspace so the async copy never reads a dead host buffer
+  for (int b = 0; b < B; ++b) W.h_klens[b] = W.h_ylens[b] / 2;
+  HIP_OK(hipMemcpyAsync(W.klens.p, W.h_klens.data(), B * 4, hipMemcpyHostToDevice, s));
   const int* kl = W.klens.i();
   launch_glow_squeeze(W.z.f(), C, Ty, W.ylens.i(), W.sq.f(), K, B, s);
-  auto conv = [&](const ConvLayer& L, const float* in, int cin, float* out, int cout, const float* resid) {
+  // every activation is (B, rows, K) with a per-buffer batch stride (in rows)
+  auto conv = [&](const ConvLayer& L, const float* in, int in_rows, float* out, int out_rows, const float* resid,
+                  int epi, int resid_rows = 0, const float* aux = nullptr) {
     ConvCall cc;
     cc.lens = kl;
     cc.B = B;
     cc.max_q = K;
-    cc.s[0] = src_of(in, (long)(in == W.sq.f() || in == W.sq2.f() ? C2 : cin) * K, K, 1, cin, 0);
+    cc.s[0] = src_of(in, (long)in_rows * K, K, 1, L.Cin, 0);
     cc.out = out;
-    cc.ob = (long)cout * K;
+    cc.ob = (long)out_rows * K;
     cc.oc = K;
     cc.ot = 1;
     cc.resid = resid;
-    cc.rb = (long)cout * K;
+    cc.rb = (long)out_rows * K;
     cc.rc = K;
     cc.rt = 1;
+    cc.epi = epi;
+    cc.resid_rows = resid_rows;
+    cc.aux = aux;
     run_conv(L, cc, s);
   };
   float* x = W.sq.f();
   float* x2 = W.sq2.f();
+  float* hid = W.whs.f();                 // [hidden | skip] (B, 2H, K)
+  float* skip = W.whs.f() + (size_t)H * K;
   for (int k = G.flows - 1; k >= 0; --k) {
     // CouplingBlock reverse (glow.py:245-262): WN over start(x0), then z1 = (x1 - m) exp(-logs)
-    conv(G.start[k], x, C, W.wh.f(), H, nullptr);
-    HIP_OK(hipMemsetAsync(W.wskip.p, 0, (size_t)B * H * K * 4, s));
+    conv(G.start[k], x, C2, hid, 2 * H, nullptr, 0);
     for (int i = 0; i < G.wn_layers; ++i) {  // WN (glow.py:118-138), g = None
       const int li = k * G.wn_layers + i;
-      conv(G.wn_in[li], W.wh.f(), H, W.wa.f(), 2 * H, nullptr);
-      launch_glow_gate(W.wa.f(), H, K, kl, W.wacts.f(), B, s);
-      if (i < G.wn_layers - 1) conv(G.wn_res[li], W.wacts.f(), H, W.wh.f(), H, W.wh.f());
-      conv(G.wn_skip[li], W.wacts.f(), H, W.wskip.f(), H, W.wskip.f());
+      conv(G.wn_in[li], hid, 2 * H, W.wacts.f(), H, nullptr, 3);  // gate fused
+      // skip rows start at the first layer's output (no accumulate), hidden rows add the residual
+      if (i < G.wn_layers - 1) conv(G.wn_rs[li], W.wacts.f(), H, hid, 2 * H, hid, 0, i == 0 ? H : 0);
+      else conv(G.wn_rs[li], W.wacts.f(), H, skip, 2 * H, i == 0 ? nullptr : skip, 0);
     }
-    conv(G.end[k], W.wskip.f(), H, W.wmo.f(), C2, nullptr);
-    launch_glow_coupling(x, W.wmo.f(), C, K, kl, B, s);
-    // InvConvNear + ActNorm reverse as one 1x1 conv
-    conv(G.invact[k], x, C2, x2, C2, nullptr);
+    // end conv + coupling + inverse InvConvNear / ActNorm: reads x, writes the next x
+    conv(G.end[k], skip, 2 * H, x2, C2, x, 5, 0, G.invtab[k].f());
     std::swap(x, x2);
   }
   launch_glow_unsqueeze(x, C2, K, W.ylens.i(), d_y, 2 * K, B, s);

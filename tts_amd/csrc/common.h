@@ -66,10 +66,13 @@ struct ConvArgs {
   long ob;
   int oc, ot;
   int out_mul;        // t_out = q*out_mul + phase
-  int epi_act;        // 0 none, 1 relu, 2 tanh
+  int epi_act;        // 0 none, 1 relu, 2 tanh, 3 gate pair, 4 coupling pair, 5 coupling +
+                      // inverse InvConvNear / ActNorm (see conv.hip)
   const float* resid; // optional residual added after activation
   long rb;
   int rc, rt;
+  int resid_rows;     // > 0: the residual applies to output rows < resid_rows only
+  const float* aux;   // epi 5: per output channel {w[4], actnorm bias, exp(-logs)}
   int max_q;          // max over batch of output positions per phase (grid x extent)
   int B;
 };

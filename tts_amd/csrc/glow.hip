@@ -1,56 +1,66 @@
 // Glow-TTS inference pieces that are not convolutions (gfx950), SURVEY.md §8f rank 3:
 //   TTS/tts/layers/glow_tts/{gated_conv,normalization,duration_predictor,glow,decoder}.py and the
 //   inference glue of TTS/tts/models/glow_tts.py:170-193 (durations -> monotonic path -> expanded
-//   means + noise). Activations are channel-major (B, C, T); a thread owns one time position and
-//   walks the channels, so every channel step is one coalesced row access across the wave. Only
+//   means + noise). Activations are channel-major (B, C, T); lanes run along time, so every channel
+//   step is one coalesced row access per wave, and the 4 waves of a workgroup split the channels.
+//   The WN gate and the coupling reverse are conv epilogues (conv.hip, epi 3 / 4). Only
 //   positions t < length are written: the convolutions (conv.hip) read positions >= length as zero
 //   padding, which is what the reference's masks produce.
 #include "common.h"
 
-// LayerNorm over the channel dim (normalization.py:4-27, eps 1e-4), then GLU (dim 1) and the
-// residual of GatedConvBlock (gated_conv.py:31-42): out = res + a * sigmoid(b), [a | b] = LN(x)
-__global__ __launch_bounds__(256) void glu_ln_res_kernel(const float* __restrict__ x, long xb, int C2,
-                                                         const float* __restrict__ gamma,
-                                                         const float* __restrict__ beta, const float* res,
-                                                         long rb, float* out, long ob, const int* lens, int T) {
-  const int b = blockIdx.y, t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T || t >= lens[b]) return;
-  const float* xp = x + b * xb + t;
-  float mean = 0.f;
-  for (int c = 0; c < C2; ++c) mean += xp[(long)c * T];
-  mean /= (float)C2;
-  float var = 0.f;
-  for (int c = 0; c < C2; ++c) {
-    const float d = xp[(long)c * T] - mean;
-    var = fmaf(d, d, var);
+// LayerNorm over the channel dim (normalization.py:4-27, eps 1e-4). A workgroup owns 64 time
+// positions (one per lane, coalesced rows) x 4 channel groups (one per wave); the column's values
+// stay in registers (NPT per thread) and the mean / variance partials meet in LDS.
+//   GLU:  GatedConvBlock (gated_conv.py:31-42): out = res + a * sigmoid(g), [a | g] = LN(x), wave w
+//         holds a-channels [w*NPT/2, (w+1)*NPT/2) and the matching g-channels (C2 = 4 * NPT)
+//   !GLU: in-place LN (DurationPredictor norm_1 / norm_2 after the conv's ReLU), C = 4 * NPT
+template <int NPT, bool GLU>
+__global__ __launch_bounds__(256) void ln_chan_kernel(const float* x, long xb, const float* __restrict__ gamma,
+                                                      const float* __restrict__ beta, const float* res, long rb,
+                                                      float* out, long ob, const int* lens, int T) {
+  constexpr int CN = 4 * NPT, HALF = NPT / 2;
+  __shared__ float part[2][4][64];
+  const int b = blockIdx.y, lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int t = blockIdx.x * 64 + lane;
+  const bool valid = t < T && t < lens[b];
+  const float* xp = x + b * xb + (valid ? t : 0);
+  auto chan = [&](int i) { return GLU ? (i < HALF ? w * HALF + i : CN / 2 + w * HALF + i - HALF) : w * NPT + i; };
+  float v[NPT];
+  float s = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    v[i] = valid ? xp[(long)chan(i) * T] : 0.f;
+    s += v[i];
   }
-  var /= (float)C2;
+  part[0][w][lane] = s;
+  __syncthreads();
+  const float mean = (part[0][0][lane] + part[0][1][lane] + part[0][2][lane] + part[0][3][lane]) / (float)CN;
+  float q = 0.f;
+#pragma unroll
+  for (int i = 0; i < NPT; ++i) {
+    const float d = v[i] - mean;
+    q = fmaf(d, d, q);
+  }
+  part[1][w][lane] = q;
+  __syncthreads();
+  const float var = (part[1][0][lane] + part[1][1][lane] + part[1][2][lane] + part[1][3][lane]) / (float)CN;
+  if (!valid) return;
   const float rs = rsqrtf(var + 1e-4f);
-  const int C = C2 / 2;
-  for (int c = 0; c < C; ++c) {
-    const float a = (xp[(long)c * T] - mean) * rs * gamma[c] + beta[c];
-    const float g = (xp[(long)(c + C) * T] - mean) * rs * gamma[c + C] + beta[c + C];
-    out[b * ob + (long)c * T + t] = res[b * rb + (long)c * T + t] + a / (1.f + expf(-g));
+  if constexpr (GLU) {
+#pragma unroll
+    for (int i = 0; i < HALF; ++i) {
+      const int ca = chan(i), cg = chan(i + HALF);
+      const float a = (v[i] - mean) * rs * gamma[ca] + beta[ca];
+      const float g = (v[i + HALF] - mean) * rs * gamma[cg] + beta[cg];
+      out[b * ob + (long)ca * T + t] = res[b * rb + (long)ca * T + t] + a / (1.f + expf(-g));
+    }
+  } else {
+#pragma unroll
+    for (int i = 0; i < NPT; ++i) {
+      const int c = chan(i);
+      out[b * ob + (long)c * T + t] = (v[i] - mean) * rs * gamma[c] + beta[c];
+    }
   }
-}
-
-// in-place LayerNorm over channels (DurationPredictor norm_1 / norm_2, after the conv's ReLU)
-__global__ __launch_bounds__(256) void ln_kernel(float* x, long xb, int C, const float* __restrict__ gamma,
-                                                 const float* __restrict__ beta, const int* lens, int T) {
-  const int b = blockIdx.y, t = blockIdx.x * blockDim.x + threadIdx.x;
-  if (t >= T || t >= lens[b]) return;
-  float* xp = x + b * xb + t;
-  float mean = 0.f;
-  for (int c = 0; c < C; ++c) mean += xp[(long)c * T];
-  mean /= (float)C;
-  float var = 0.f;
-  for (int c = 0; c < C; ++c) {
-    const float d = xp[(long)c * T] - mean;
-    var = fmaf(d, d, var);
-  }
-  var /= (float)C;
-  const float rs = rsqrtf(var + 1e-4f);
-  for (int c = 0; c < C; ++c) xp[(long)c * T] = (xp[(long)c * T] - mean) * rs * gamma[c] + beta[c];
 }
 
 // glow_tts.py:172-176: w = (exp(logw) - 1) * x_mask * length_scale, w_ceil = ceil(w),
@@ -73,91 +83,91 @@ __global__ __launch_bounds__(64) void glow_durations_kernel(const float* __restr
   ylen[b] = max((int)c, 1);  // clamp_min(sum, 1).long()
 }
 
-// path[t, j] = [j < cum_t] - [j < cum_{t-1}] (generate_path), masked by t < x_len, j < y_len;
-// y_mean[c, j] = sum_t path[t, j] o_mean[c, t]; z = (y_mean + noise * noise_scale) * y_mask
-// (mean_only: y_log_scale = 0, glow_tts.py:184-186). Also writes attn (B, T_y, T_x) and y_mean.
+// path[t, j] = [j < cum_t] - [j < cum_{t-1}] (generate_path), masked by t < x_len, j < y_len: with
+// cum non-decreasing, row j has one 1 at t_j = the first t with cum_t > j (none past sum w_ceil).
+// y_mean[c, j] = o_mean[c, t_j]; z = (y_mean + noise * noise_scale) * y_mask (mean_only:
+// y_log_scale = 0, glow_tts.py:184-186). A workgroup owns 64 frames: t_j by binary search, then
+// y_mean / z with lanes along j, then the 64 attn rows (B, T_y, T_x) with lanes along t.
 __global__ __launch_bounds__(256) void glow_expand_kernel(const float* __restrict__ o_mean, int C, int Tx,
                                                           const int* xlens, const float* __restrict__ cum,
                                                           const int* ylens, int Ty, const float* noise,
                                                           float noise_scale, float* __restrict__ y_mean,
                                                           float* __restrict__ z, float* __restrict__ attn) {
-  const int b = blockIdx.y, j = blockIdx.x * blockDim.x + threadIdx.x;
-  if (j >= Ty) return;
-  const int xl = xlens[b], yl = ylens[b];
-  const bool yv = j < yl;
+  __shared__ int tj[64];
+  const int b = blockIdx.y, j0 = blockIdx.x * 64, tid = threadIdx.x;
+  const int xl = xlens[b];
   const float* cb = cum + (long)b * Tx;
-  const float jf = (float)j;
-  float* arow = attn + ((long)b * Ty + j) * Tx;
-  for (int c = 0; c < C; ++c) y_mean[((long)b * C + c) * Ty + j] = 0.f;
-  for (int t = 0; t < Tx; ++t) {
-    const float hi = jf < cb[t] ? 1.f : 0.f;
-    const float lo = t > 0 && jf < cb[t - 1] ? 1.f : 0.f;
-    const float p = (yv && t < xl) ? hi - lo : 0.f;
-    arow[t] = p;
-    if (p != 0.f)
-      for (int c = 0; c < C; ++c) y_mean[((long)b * C + c) * Ty + j] += p * o_mean[((long)b * C + c) * Tx + t];
+  if (tid < 64) {
+    const int j = j0 + tid;
+    int lo = 0, hi = xl;  // first t in [0, xl) with cum_t > j, xl if none
+    const float jf = (float)j;
+    while (lo < hi) {
+      const int mid = (lo + hi) >> 1;
+      if (cb[mid] > jf) hi = mid;
+      else lo = mid + 1;
+    }
+    tj[tid] = (j < Ty && j < ylens[b] && lo < xl) ? lo : -1;
   }
-  for (int c = 0; c < C; ++c) {
-    const long i = ((long)b * C + c) * Ty + j;
-    const float nz = noise ? noise[i] * noise_scale : 0.f;
-    z[i] = yv ? y_mean[i] + nz : 0.f;
+  __syncthreads();
+  {
+    const int jj = tid & 63, j = j0 + jj;
+    if (j < Ty) {
+      const int t = tj[jj];
+      const bool yv = j < ylens[b];
+      for (int c = tid >> 6; c < C; c += 4) {
+        const long i = ((long)b * C + c) * Ty + j;
+        const float m = t >= 0 ? o_mean[((long)b * C + c) * Tx + t] : 0.f;
+        y_mean[i] = m;
+        const float nz = noise ? noise[i] * noise_scale : 0.f;
+        z[i] = yv ? m + nz : 0.f;
+      }
+    }
+  }
+  const int nj = min(64, Ty - j0);
+  for (int r = 0; r < nj; ++r) {
+    float* arow = attn + ((long)b * Ty + j0 + r) * Tx;
+    const int t1 = tj[r];
+    for (int t = tid; t < Tx; t += 256) arow[t] = t == t1 ? 1.f : 0.f;
   }
 }
 
 // decoder.py:6-19: (B, C, T) -> (B, 2C, T/2), x_sqz[s*C + c][k] = x[c][2k + s], masked by
-// y_mask[2k + 1]; unsqueeze (decoder.py:22-33) is the inverse, masked by the repeated mask
+// y_mask[2k + 1]; unsqueeze (decoder.py:22-33) is the inverse, masked by the repeated mask.
+// 64 positions x 4 channel groups per workgroup.
 __global__ __launch_bounds__(256) void glow_squeeze_kernel(const float* __restrict__ x, int C, int T,
                                                            const int* ylens, float* __restrict__ y, int K) {
-  const int b = blockIdx.y, k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y, k = blockIdx.x * 64 + (threadIdx.x & 63);
   if (k >= K) return;
   const bool v = 2 * k + 1 < ylens[b];
-  for (int s = 0; s < 2; ++s)
-    for (int c = 0; c < C; ++c)
-      y[((long)b * 2 * C + s * C + c) * K + k] = v ? x[((long)b * C + c) * T + 2 * k + s] : 0.f;
+  for (int sc = threadIdx.x >> 6; sc < 2 * C; sc += 4) {
+    const int s = sc / C, c = sc % C;
+    y[((long)b * 2 * C + sc) * K + k] = v ? x[((long)b * C + c) * T + 2 * k + s] : 0.f;
+  }
 }
 __global__ __launch_bounds__(256) void glow_unsqueeze_kernel(const float* __restrict__ x, int C2, int K,
                                                              const int* ylens, float* __restrict__ y, int T) {
-  const int b = blockIdx.y, k = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y, k = blockIdx.x * 64 + (threadIdx.x & 63);
   if (k >= K) return;
   const int C = C2 / 2;
   const bool v = 2 * k + 1 < ylens[b];
-  for (int s = 0; s < 2; ++s)
-    for (int c = 0; c < C; ++c)
-      y[((long)b * C + c) * T + 2 * k + s] = v ? x[((long)b * C2 + s * C + c) * K + k] : 0.f;
-}
-
-// WN gate (glow.py fused_add_tanh_sigmoid_multiply, g = None): acts = tanh(a[:H]) * sigmoid(a[H:])
-__global__ __launch_bounds__(256) void glow_gate_kernel(const float* __restrict__ a, int H, int K, const int* klens,
-                                                        float* __restrict__ acts) {
-  const int b = blockIdx.y, k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K || k >= klens[b]) return;
-  for (int c = 0; c < H; ++c) {
-    const float x = a[((long)b * 2 * H + c) * K + k], g = a[((long)b * 2 * H + c + H) * K + k];
-    acts[((long)b * H + c) * K + k] = tanhf(x) / (1.f + expf(-g));
-  }
-}
-
-// CouplingBlock reverse (glow.py:245-262, sigmoid_scale False): z1 = (x1 - m) * exp(-logs), in place
-// on the second half of x; mo = end(wn(...)) = [m | logs]
-__global__ __launch_bounds__(256) void glow_coupling_kernel(float* x, const float* __restrict__ mo, int Ch, int K,
-                                                            const int* klens) {
-  const int b = blockIdx.y, k = blockIdx.x * blockDim.x + threadIdx.x;
-  if (k >= K || k >= klens[b]) return;
-  for (int c = 0; c < Ch; ++c) {
-    const long ix = ((long)b * 2 * Ch + Ch + c) * K + k;
-    const float m = mo[((long)b * 2 * Ch + c) * K + k], ls = mo[((long)b * 2 * Ch + Ch + c) * K + k];
-    x[ix] = (x[ix] - m) * expf(-ls);
+  for (int c = threadIdx.x >> 6; c < C; c += 4) {
+    float2 o;
+    o.x = v ? x[((long)b * C2 + c) * K + k] : 0.f;
+    o.y = v ? x[((long)b * C2 + C + c) * K + k] : 0.f;
+    *reinterpret_cast<float2*>(y + ((long)b * C + c) * T + 2 * k) = o;
   }
 }
 
 void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, const float* beta, const float* res,
                        long rb, float* out, long ob, const int* lens, int B, int T, hipStream_t s) {
-  glu_ln_res_kernel<<<dim3((T + 255) / 256, B), 256, 0, s>>>(x, xb, C2, gamma, beta, res, rb, out, ob, lens, T);
+  TTS_CHECK(C2 == 384, "glow encoder LayerNorm: 2 * hidden must be 384");
+  ln_chan_kernel<96, true><<<dim3((T + 63) / 64, B), 256, 0, s>>>(x, xb, gamma, beta, res, rb, out, ob, lens, T);
   HIP_OK(hipGetLastError());
 }
 void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, const int* lens, int B, int T,
                hipStream_t s) {
-  ln_kernel<<<dim3((T + 255) / 256, B), 256, 0, s>>>(x, xb, C, gamma, beta, lens, T);
+  TTS_CHECK(C == 256, "glow duration-predictor LayerNorm: filter channels must be 256");
+  ln_chan_kernel<64, false><<<dim3((T + 63) / 64, B), 256, 0, s>>>(x, xb, gamma, beta, nullptr, 0, x, xb, lens, T);
   HIP_OK(hipGetLastError());
 }
 void launch_glow_durations(const float* logw, int T, const int* lens, float length_scale, float* cum, int* ylen,
@@ -168,39 +178,30 @@ void launch_glow_durations(const float* logw, int T, const int* lens, float leng
 void launch_glow_expand(const float* o_mean, int C, int Tx, const int* xlens, const float* cum, const int* ylens,
                         int Ty, const float* noise, float noise_scale, float* y_mean, float* z, float* attn, int B,
                         hipStream_t s) {
-  glow_expand_kernel<<<dim3((Ty + 255) / 256, B), 256, 0, s>>>(o_mean, C, Tx, xlens, cum, ylens, Ty, noise,
+  glow_expand_kernel<<<dim3((Ty + 63) / 64, B), 256, 0, s>>>(o_mean, C, Tx, xlens, cum, ylens, Ty, noise,
                                                                 noise_scale, y_mean, z, attn);
   HIP_OK(hipGetLastError());
 }
 void launch_glow_squeeze(const float* x, int C, int T, const int* ylens, float* y, int K, int B, hipStream_t s) {
-  glow_squeeze_kernel<<<dim3((K + 255) / 256, B), 256, 0, s>>>(x, C, T, ylens, y, K);
+  glow_squeeze_kernel<<<dim3((K + 63) / 64, B), 256, 0, s>>>(x, C, T, ylens, y, K);
   HIP_OK(hipGetLastError());
 }
 void launch_glow_unsqueeze(const float* x, int C2, int K, const int* ylens, float* y, int T, int B, hipStream_t s) {
-  glow_unsqueeze_kernel<<<dim3((K + 255) / 256, B), 256, 0, s>>>(x, C2, K, ylens, y, T);
+  glow_unsqueeze_kernel<<<dim3((K + 63) / 64, B), 256, 0, s>>>(x, C2, K, ylens, y, T);
   HIP_OK(hipGetLastError());
 }
-void launch_glow_gate(const float* a, int H, int K, const int* klens, float* acts, int B, hipStream_t s) {
-  glow_gate_kernel<<<dim3((K + 255) / 256, B), 256, 0, s>>>(a, H, K, klens, acts);
-  HIP_OK(hipGetLastError());
-}
-void launch_glow_coupling(float* x, const float* mo, int Ch, int K, const int* klens, int B, hipStream_t s) {
-  glow_coupling_kernel<<<dim3((K + 255) / 256, B), 256, 0, s>>>(x, mo, Ch, K, klens);
-  HIP_OK(hipGetLastError());
-}
-
 // encoder.py:107: emb(x) * sqrt(hidden) (the scale is folded into the table), channel-major out
 __global__ __launch_bounds__(256) void glow_embed_kernel(const int64_t* __restrict__ ids, int T, const float* table,
                                                          int rows, int D, const int* lens, float* __restrict__ out) {
-  const int b = blockIdx.y, t = blockIdx.x * blockDim.x + threadIdx.x;
+  const int b = blockIdx.y, t = blockIdx.x * 64 + (threadIdx.x & 63);
   if (t >= T) return;
   const bool v = t < lens[b];
   long id = v ? ids[(long)b * T + t] : 0;
   if (id < 0 || id >= rows) id = 0;
-  for (int c = 0; c < D; ++c) out[((long)b * D + c) * T + t] = v ? table[id * D + c] : 0.f;
+  for (int c = threadIdx.x >> 6; c < D; c += 4) out[((long)b * D + c) * T + t] = v ? table[id * D + c] : 0.f;
 }
 void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
                        int B, hipStream_t s) {
-  glow_embed_kernel<<<dim3((T + 255) / 256, B), 256, 0, s>>>(ids, T, table, rows, D, lens, out);
+  glow_embed_kernel<<<dim3((T + 63) / 64, B), 256, 0, s>>>(ids, T, table, rows, D, lens, out);
   HIP_OK(hipGetLastError());
 }
