@@ -110,6 +110,19 @@ int tts_melgan_generator(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens
 int tts_pqmf_synthesis(tts_ctx* ctx, const float* d_x, int B, int N, int L, const float* d_G, int taps,
                        float* d_y, void* stream);
 
+/* ---- ParallelWaveGAN generator (TTS/vocoder/models/parallel_wavegan_generator.py) ----
+   tts_pwgan_set_tensor/finalize <- ParallelWaveganGenerator(...) as setup_generator builds it
+                       (vocoder/utils/generic_utils.py:79-92: 64 res / 128 gate / 64 skip / 80 aux
+                       channels, kernel 3) + load_state_dict (weight_g / weight_v or folded weight)
+   tts_pwgan_infer  <- ParallelWaveganGenerator.inference (:120-125): replicate pad `pad`, ConvUpsample,
+                       first_conv on d_noise (B, 1, hop*(M_max + 2*pad)) standard normal, residual
+                       blocks, output convs -> d_out (B, 1, hop*(M_max + 2*pad)); row b is zero past
+                       hop*(h_lens[b] + 2*pad) */
+int tts_pwgan_set_tensor(tts_ctx* ctx, const char* name, const float* host, const int64_t* shape, int ndim);
+int tts_pwgan_finalize(tts_ctx* ctx, int num_res_blocks, int stacks, const int32_t* upsample_factors, int n_up);
+int tts_pwgan_infer(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
+                    const float* d_noise, float* d_out, void* stream);
+
 /* ---- Glow-TTS (TTS/tts/models/glow_tts.py, reference configs: gated-conv encoder) ----
    tts_glow_set_tensor/finalize <- GlowTts(...).load_state_dict (enc_layers = 3 + num_layers_enc)
    tts_glow_encode  <- GlowTts.inference up to the durations (glow_tts.py:166-176): encoder,

@@ -297,6 +297,41 @@ def glow_case(name):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
+def pwgan_case(name):
+    """ParallelWaveGAN generator (setup_generator's parallel_wavegan config). The prior noise is
+    drawn inside forward() with torch.randn: re-seeding torch reproduces it for the fixture."""
+    from TTS.vocoder.models.parallel_wavegan_generator import ParallelWaveganGenerator
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    cfg = PwganConfig()
+    m = ParallelWaveganGenerator(in_channels=1, out_channels=1, kernel_size=3, num_res_blocks=cfg.num_res_blocks,
+                                 stacks=cfg.stacks, res_channels=64, gate_channels=128, skip_channels=64,
+                                 aux_channels=80, dropout=0.0, bias=True, use_weight_norm=True,
+                                 upsample_factors=list(cfg.upsample_factors))
+    ref = [(k, tuple(v.shape)) for k, v in m.state_dict().items()]
+    spec = [(n, tuple(sh)) for n, sh, _ in pwgan_spec(cfg)]
+    assert ref == spec, "pwgan_spec does not match the reference state_dict"
+    seed = 31
+    sd = synth_state_dict(pwgan_spec(cfg), seed)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.eval()
+    out = {"seed": np.int64(seed)}
+    rs = np.random.RandomState(32)
+    for M in (5, 11):
+        mel = (rs.uniform(-1, 1, size=(1, 80, M)) * 2.0).astype(np.float32)
+        T = (M + 2 * cfg.inference_padding) * 256
+        torch.manual_seed(1000 + M)
+        noise = torch.randn([1, 1, T])
+        torch.manual_seed(1000 + M)
+        with torch.no_grad():
+            wav = m.inference(torch.from_numpy(mel))
+        k = f"M{M}"
+        out[f"{k}_mel"] = mel
+        out[f"{k}_noise"] = noise.numpy()
+        out[f"{k}_wav"] = wav.numpy()
+        print(f"[{name}] M={M} wav {tuple(wav.shape)} |w|max {wav.abs().max():.4f} std {wav.std():.4f}")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
 def lj_profile():
     import scipy.io.wavfile as wavfile
     d = os.path.join(REF, "tests/data/ljspeech")
@@ -315,6 +350,8 @@ def lj_profile():
 
 if __name__ == "__main__":
     which = sys.argv[1:] or ["lj", "pqmf", "vocoder", "taco_sigmoid", "taco_softmax"]
+    if "pwgan" in which:
+        pwgan_case("pwgan")
     if "lj" in which:
         lj_profile()
     if "pqmf" in which:

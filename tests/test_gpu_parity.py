@@ -508,3 +508,39 @@ def test_glow_tts_matches_reference():
         ref = fx[k + "_y"]
         assert np.abs(y[i, :, :ref.shape[1]] - ref).max() <= MEL_TOL
         assert not y[i, :, ref.shape[1]:].any()
+
+
+# --------------------------------------------------------------------------------- ParallelWaveGAN
+def test_pwgan_matches_reference():
+    """ParallelWaveganGenerator.inference with the reference's own prior noise, both fixture mels in
+    ONE ragged batch: waveform <= 1e-4 of the reference, zero past each row's length; then the
+    weight-norm-folded model gives the same samples."""
+    from tts_amd import ParallelWaveganGenerator
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    from tts_amd.weights import synth_state_dict
+    _dev()
+    fx = load_fixture("pwgan")
+    g = ParallelWaveganGenerator()
+    g.load_state_dict({k: torch.from_numpy(v) for k, v in
+                       synth_state_dict(pwgan_spec(PwganConfig()), int(fx["seed"])).items()})
+    g = g.cuda().eval()
+    Ms = (5, 11)
+    M = max(Ms)
+    mel = np.zeros((2, 80, M), np.float32)
+    T = 256 * (M + 4)
+    noise = np.zeros((2, 1, T), np.float32)
+    for i, m in enumerate(Ms):
+        mel[i, :, :m] = fx[f"M{m}_mel"][0]
+        noise[i, 0, :256 * (m + 4)] = fx[f"M{m}_noise"][0, 0]
+    outs = []
+    for fold in (False, True):
+        if fold:
+            g.remove_weight_norm()
+        y = g.inference(torch.from_numpy(mel).cuda(), lengths=list(Ms), noise=torch.from_numpy(noise).cuda())
+        y = y.cpu().numpy()
+        for i, m in enumerate(Ms):
+            ref = fx[f"M{m}_wav"][0, 0]
+            assert np.abs(y[i, 0, :len(ref)] - ref).max() <= 1e-4
+            assert not y[i, 0, len(ref):].any()
+        outs.append(y)
+    assert np.abs(outs[0] - outs[1]).max() <= 1e-5

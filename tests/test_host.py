@@ -190,3 +190,25 @@ def test_glow_tts_constructor_and_keys():
             GlowTts(num_chars=130, **kw)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         m.inference(torch.ones(1, 5, dtype=torch.long), [5])
+
+
+def test_pwgan_keys_match_reference_and_factory():
+    """parallel_wavegan_generator.py:16-88 checkpoint keys (pinned against the reference module by
+    make_golden.py pwgan), remove_weight_norm folding, setup_generator dispatch."""
+    from tts_amd import ParallelWaveganGenerator
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    g = ParallelWaveganGenerator()
+    assert [(k, tuple(v.shape)) for k, v in g.state_dict().items()] == \
+        [(n, tuple(s)) for n, s, _ in pwgan_spec(PwganConfig())]
+    assert tuple(g.state_dict()["upsample_net.upsample.up_layers.7.weight_v"].shape) == (1, 1, 1, 9)
+    g.remove_weight_norm()
+    sd = g.state_dict()
+    assert "conv_layers.29.conv.weight" in sd and "conv_layers.29.conv.weight_g" not in sd
+    c = {"generator_model": "parallel_wavegan_generator", "audio": {"num_mels": 80},
+         "generator_model_params": {"upsample_factors": [4, 4, 4, 4], "stacks": 3, "num_res_blocks": 30}}
+    v = setup_generator(c)
+    assert isinstance(v, ParallelWaveganGenerator) and v.hop == 256
+    with pytest.raises(NotImplementedError):
+        ParallelWaveganGenerator(res_channels=32)
+    with pytest.raises(RuntimeError, match="no CPU fallback"):
+        v.inference(torch.zeros(1, 80, 4))

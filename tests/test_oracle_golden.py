@@ -160,3 +160,18 @@ def test_glow_oracle_matches_reference():
         assert np.array_equal(attn, fx[k + "_attn"])
         assert np.abs(ym - fx[k + "_ymean"]).max() <= 1e-5
         assert np.abs(y - fx[k + "_y"]).max() <= 5e-5
+
+
+def test_pwgan_oracle_matches_reference():
+    """ParallelWaveGAN generator: ParallelWaveganGenerator.inference (parallel_wavegan_generator.py:
+    120-125) run by make_golden.py with its torch.randn prior captured; fp32 restatement <= 2e-6."""
+    from oracle.pwgan_np import PwganOracle
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    from tts_amd.weights import synth_state_dict
+    fx = load_fixture("pwgan")
+    cfg = PwganConfig()
+    orc = PwganOracle(synth_state_dict(pwgan_spec(cfg), int(fx["seed"])), cfg)
+    for M in (5,):  # (11 is covered on the GPU; the numpy WaveNet takes seconds per case)
+        y = orc.inference(fx[f"M{M}_mel"][0], fx[f"M{M}_noise"][0, 0])
+        assert y.shape == fx[f"M{M}_wav"][0, 0].shape
+        assert np.abs(y - fx[f"M{M}_wav"][0, 0]).max() <= 2e-6

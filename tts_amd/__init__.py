@@ -8,6 +8,7 @@ from .factories import AttrDict, load_config, setup_generator, setup_model  # no
 from .glow_tts import GlowTts  # noqa: F401
 from .speaker_encoder import SpeakerEncoder  # noqa: F401
 from .tacotron2 import Tacotron2  # noqa: F401
-from .vocoder import FullbandMelganGenerator, MelganGenerator, MultibandMelganGenerator, PQMF  # noqa: F401
+from .vocoder import (FullbandMelganGenerator, MelganGenerator, MultibandMelganGenerator, ParallelWaveganGenerator,  # noqa: F401
+                      PQMF)
 
 __version__ = "0.1.0"

@@ -54,6 +54,10 @@ SIGNATURES = [
     ("tts_ge2e_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                          ctypes.c_int]),
     ("tts_ge2e_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    ("tts_pwgan_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
+    ("tts_pwgan_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_int]),
+    ("tts_pwgan_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp,
+                                       _vp]),
     ("tts_glow_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
     ("tts_glow_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_glow_encode", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, _c_int_p,
@@ -112,6 +116,7 @@ class Engine:
         self.h = h
         self.taco_key = None
         self.melgan_key = None
+        self.pwgan_key = None
         self.ge2e_key = None
         self.glow_key = None
 
@@ -177,6 +182,18 @@ class Engine:
         B, M, _ = dec.shape
         lens_a, lens_p = _i32(lens)
         _check(self.lib.tts_taco_postnet(self.h, _ptr(dec), lens_p, B, M, _ptr(out), _stream(dec.device)))
+
+    def load_pwgan(self, tensors: Dict[str, np.ndarray], num_res_blocks, stacks, upsample_factors):
+        for k, v in tensors.items():
+            self._set(self.lib.tts_pwgan_set_tensor, k, v)
+        ups, ups_p = _i32(list(upsample_factors))
+        _check(self.lib.tts_pwgan_finalize(self.h, num_res_blocks, stacks, ups_p, len(ups)))
+
+    def pwgan_infer(self, mel, lens, pad, noise, out):
+        B, _, M = mel.shape
+        lens_a, lens_p = _i32(lens)
+        _check(self.lib.tts_pwgan_infer(self.h, _ptr(mel), lens_p, B, M, pad, _ptr(noise), _ptr(out),
+                                        _stream(mel.device)))
 
     def load_glow(self, tensors: Dict[str, np.ndarray], num_chars, enc_layers, flows, wn_layers):
         for k, v in tensors.items():

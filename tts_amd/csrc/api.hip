@@ -30,6 +30,16 @@ void launch_glow_expand(const float* o_mean, int C, int Tx, const int* xlens, co
                         hipStream_t s);
 void launch_glow_squeeze(const float* x, int C, int T, const int* ylens, float* y, int K, int B, hipStream_t s);
 void launch_glow_unsqueeze(const float* x, int C2, int K, const int* ylens, float* y, int T, int B, hipStream_t s);
+void launch_pw_upsample(const float* in, long ib, int Lin_max, const int* lens, int len_add, int in_mul, int s,
+                        const float* h, float* out, long ob, int Lout_max, int C, int B, hipStream_t st);
+void launch_pw_first(const float* noise, long nb, const float* w, const float* bias, const int* lens, int len_add,
+                     int hop, float* x, int Tmax, int B, hipStream_t st);
+void launch_pw_layer(const float* x, const float* c, float* xn, float* skip, const float* W1, const float* b1,
+                     const float* W2, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
+                     int first, int B, hipStream_t st);
+void launch_pw_out(const float* skip, float scale, const float* W3, const float* b3, const float* w4,
+                   const float* b4, const int* lens, int len_add, int hop, int Tmax, float* out, int B,
+                   hipStream_t st);
 void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
                        int B, hipStream_t s);
 bool launch_lstm768_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
@@ -320,6 +330,23 @@ struct GlowWS {
   std::vector<int> h_ylens, h_klens;
 };
 
+// ParallelWaveGAN generator (TTS/vocoder/models/parallel_wavegan_generator.py, setup_generator's
+// configuration: 64 res / 128 gate / 64 skip / 80 aux channels, kernel 3)
+struct PwganModel {
+  bool ready = false;
+  int layers = 30, stacks = 3;
+  std::vector<int> ups;
+  DevBuf first_w, first_b;
+  ConvLayer conv_in;                 // 80 -> 80, k1, no bias
+  std::vector<DevBuf> up_h;          // per factor s: 2s + 1 taps
+  std::vector<DevBuf> W1, b1, W2, b2;  // per residual block (pw_layer_kernel layouts)
+  DevBuf W3, b3, w4, b4;
+};
+
+struct PwganWS {
+  DevBuf lens, ca, cb, xa, xb, skip;
+};
+
 struct tts_ctx {
   int device = 0;
   hipStream_t s = nullptr;
@@ -336,6 +363,9 @@ struct tts_ctx {
   HostMap ge2e_host;
   Ge2eModel ge2e;
   Ge2eWS gws;
+  HostMap pw_host;
+  PwganModel pw;
+  PwganWS pws;
   HostMap glow_host;
   GlowModel glow;
   GlowWS glws;
@@ -1351,7 +1381,9 @@ std::vector<float> wn_weight(const HostMap& m, const std::string& name, std::vec
   auto itw = m.find(name + ".weight");
   if (itw != m.end()) return need(m, name + ".weight", shape).d;
   const auto& v = need(m, name + ".weight_v", shape).d;
-  const auto& g = need(m, name + ".weight_g", {shape[0], 1, 1}).d;
+  std::vector<int64_t> gshape(shape.size(), 1);
+  gshape[0] = shape[0];
+  const auto& g = need(m, name + ".weight_g", gshape).d;
   const size_t per = v.size() / shape[0];
   std::vector<float> w(v.size());
   for (int64_t o = 0; o < shape[0]; ++o) {
@@ -1994,6 +2026,140 @@ void glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, fl
   HIP_OK(hipStreamSynchronize(s));
 }
 
+void pwgan_finalize(tts_ctx* c, int layers, int stacks, const int32_t* ups, int n_up) {
+  auto& P = c->pw;
+  const auto& h = c->pw_host;
+  P.ready = false;
+  TTS_CHECK(layers >= 1 && layers <= 64 && stacks >= 1 && layers % stacks == 0, "pwgan: layers / stacks");
+  TTS_CHECK(n_up >= 1 && n_up <= 6, "pwgan: upsample factors");
+  const int R = 64, G = 128, A = 80, S = 64, K1 = 3 * R + A;
+  P.layers = layers;
+  P.stacks = stacks;
+  P.ups.assign(ups, ups + n_up);
+  P.first_w.upload(wn_weight(h, "first_conv", {R, 1, 1}));
+  P.first_b.upload(need(h, "first_conv.bias", {R}).d);
+  int p0[8] = {0};
+  pack_conv(P.conv_in, wn_weight(h, "upsample_net.conv_in", {A, A, 1}), std::vector<float>(A, 0.f), A, A, 1, 1, 1,
+            p0);
+  P.up_h.clear();
+  P.up_h.resize(n_up);
+  for (int i = 0; i < n_up; ++i) {
+    TTS_CHECK(ups[i] >= 1 && ups[i] <= 16, "pwgan: upsample factor");
+    P.up_h[i].upload(
+        wn_weight(h, "upsample_net.upsample.up_layers." + std::to_string(2 * i + 1), {1, 1, 1, 2 * ups[i] + 1}));
+  }
+  P.W1.clear();
+  P.W1.resize(layers);
+  P.b1.clear();
+  P.b1.resize(layers);
+  P.W2.clear();
+  P.W2.resize(layers);
+  P.b2.clear();
+  P.b2.resize(layers);
+  for (int l = 0; l < layers; ++l) {
+    const std::string q = "conv_layers." + std::to_string(l) + ".";
+    const auto wd = wn_weight(h, q + "conv", {G, R, 3});
+    const auto& bd = need(h, q + "conv.bias", {G}).d;
+    const auto wa = wn_weight(h, q + "conv1x1_aux", {G, A, 1});
+    // GEMM1 matrix (128 x 272): row r = gate row (r even: r/2, odd: 64 + r/2); column k = tap*64 + ch
+    // for the dilated taps, 192 + ch for the aux features
+    std::vector<float> m1((size_t)G * K1), bb1(G);
+    for (int r = 0; r < G; ++r) {
+      const int src = (r & 1) ? G / 2 + r / 2 : r / 2;
+      for (int tap = 0; tap < 3; ++tap)
+        for (int ch = 0; ch < R; ++ch) m1[(size_t)r * K1 + tap * R + ch] = wd[((size_t)src * R + ch) * 3 + tap];
+      for (int ch = 0; ch < A; ++ch) m1[(size_t)r * K1 + 3 * R + ch] = wa[(size_t)src * A + ch];
+      bb1[r] = bd[src];
+    }
+    std::vector<float> sw1((size_t)G * K1);
+    swizzle_rows16(m1.data(), G, G, K1, sw1.data());
+    P.W1[l].upload(sw1);
+    P.b1[l].upload(bb1);
+    const auto wo = wn_weight(h, q + "conv1x1_out", {R, G / 2, 1});
+    const auto ws = wn_weight(h, q + "conv1x1_skip", {S, G / 2, 1});
+    std::vector<float> m2((size_t)(R + S) * (G / 2)), bb2(R + S);
+    std::copy(wo.begin(), wo.end(), m2.begin());
+    std::copy(ws.begin(), ws.end(), m2.begin() + (size_t)R * (G / 2));
+    const auto& bo = need(h, q + "conv1x1_out.bias", {R}).d;
+    const auto& bs = need(h, q + "conv1x1_skip.bias", {S}).d;
+    std::copy(bo.begin(), bo.end(), bb2.begin());
+    std::copy(bs.begin(), bs.end(), bb2.begin() + R);
+    std::vector<float> sw2(m2.size());
+    swizzle_rows16(m2.data(), R + S, R + S, G / 2, sw2.data());
+    P.W2[l].upload(sw2);
+    P.b2[l].upload(bb2);
+  }
+  P.W3.upload(wn_weight(h, "last_conv_layers.1", {S, S, 1}));
+  P.b3.upload(need(h, "last_conv_layers.1.bias", {S}).d);
+  P.w4.upload(wn_weight(h, "last_conv_layers.3", {1, S, 1}));
+  P.b4.upload(need(h, "last_conv_layers.3.bias", {1}).d);
+  HIP_OK(hipDeviceSynchronize());
+  P.ready = true;
+}
+
+// ParallelWaveganGenerator.inference (parallel_wavegan_generator.py:120-125) for B mels of
+// h_lens[b] frames: replicate pad p, upsample, WaveNet, output (B, 1, hop * (M_max + 2p)),
+// row b zero past hop * (h_lens[b] + 2p). d_noise (B, 1, hop * (M_max + 2p)) standard normal.
+void pwgan_infer(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int M_max, int pad, const float* noise,
+                 float* out) {
+  auto& P = c->pw;
+  auto& W = c->pws;
+  TTS_CHECK(P.ready, "pwgan weights not finalized");
+  TTS_CHECK(B >= 1 && M_max >= 1 && pad >= 0 && pad <= 64, "pwgan: bad sizes");
+  for (int b = 0; b < B; ++b) TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= M_max, "pwgan: mel lens out of range");
+  hipStream_t s = c->s;
+  int hop = 1;
+  for (int u : P.ups) hop *= u;
+  const int Lf = M_max + 2 * pad, Tmax = Lf * hop;
+  W.lens.ensure(B * 4);
+  W.ca.ensure((size_t)B * 80 * Tmax * 4);
+  W.cb.ensure((size_t)B * 80 * Tmax * 4);
+  W.xa.ensure((size_t)B * 64 * Tmax * 4);
+  W.xb.ensure((size_t)B * 64 * Tmax * 4);
+  W.skip.ensure((size_t)B * 64 * Tmax * 4);
+  std::vector<int> lens(h_lens, h_lens + B);
+  HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  const int* dl = W.lens.i();
+  // replicate pad + ConvUpsample.conv_in (1x1, frame rate)
+  ConvCall cc;
+  cc.lens = dl;
+  cc.B = B;
+  cc.len_add = 2 * pad;
+  cc.s[0] = src_of(mel, (long)80 * M_max, M_max, 1, 80, 0);
+  cc.pad_mode = 2;
+  cc.rep_pad = pad;
+  cc.max_q = Lf;
+  float* cin = W.cb.f();
+  float* cout = W.ca.f();
+  cc.out = cin;
+  cc.ob = (long)80 * Lf;
+  cc.oc = Lf;
+  cc.ot = 1;
+  run_conv(P.conv_in, cc, s);
+  int L = Lf, mul = 1;
+  for (size_t i = 0; i < P.ups.size(); ++i) {
+    const int u = P.ups[i];
+    launch_pw_upsample(cin, (long)80 * L, L, dl, 2 * pad, mul, u, P.up_h[i].f(), cout, (long)80 * L * u, L * u, 80, B,
+                       s);
+    std::swap(cin, cout);
+    L *= u;
+    mul *= u;
+  }
+  const float* cfeat = cin;  // (B, 80, Tmax)
+  float* x = W.xa.f();
+  float* xn = W.xb.f();
+  launch_pw_first(noise, Tmax, P.first_w.f(), P.first_b.f(), dl, 2 * pad, hop, x, Tmax, B, s);
+  const int per_stack = P.layers / P.stacks;
+  for (int l = 0; l < P.layers; ++l) {
+    launch_pw_layer(x, cfeat, xn, W.skip.f(), P.W1[l].f(), P.b1[l].f(), P.W2[l].f(), P.b2[l].f(), dl, 2 * pad, hop,
+                    Tmax, 1 << (l % per_stack), l == 0, B, s);
+    std::swap(x, xn);
+  }
+  launch_pw_out(W.skip.f(), std::sqrt(1.0f / P.layers), P.W3.f(), P.b3.f(), P.w4.f(), P.b4.f(), dl, 2 * pad, hop,
+                Tmax, out, B, s);
+  HIP_OK(hipStreamSynchronize(s));
+}
+
 void set_tensor(HostMap& m, const char* name, const float* h, const int64_t* shape, int ndim) {
   TTS_CHECK(name && (h || ndim == 0), "set_tensor: null argument");
   HostT t;
@@ -2170,6 +2336,33 @@ int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int 
     HIP_OK(hipMemsetAsync(d_out, 0, (size_t)B * M_max * 80 * 4, c->s));
     run_postnet(c, d_dec, (long)M_max * 80, W.mlens.i(), B, M_max, maxM, d_out, (long)M_max * 80, c->s);
     HIP_OK(hipStreamSynchronize(c->s));
+    leave(c, stream);
+  });
+}
+
+int tts_pwgan_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
+  return guarded([&] {
+    TTS_CHECK(c, "null ctx");
+    set_tensor(c->pw_host, name, h, shape, ndim);
+  });
+}
+
+int tts_pwgan_finalize(tts_ctx* c, int num_res_blocks, int stacks, const int32_t* upsample_factors, int n_up) {
+  return guarded([&] {
+    TTS_CHECK(c && upsample_factors, "null argument");
+    DeviceGuard g(c->device);
+    HostMapConsumer consume{c->pw_host};
+    pwgan_finalize(c, num_res_blocks, stacks, upsample_factors, n_up);
+  });
+}
+
+int tts_pwgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
+                    const float* d_noise, float* d_out, void* stream) {
+  return guarded([&] {
+    TTS_CHECK(c && d_mel && h_lens && d_noise && d_out, "null argument");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    pwgan_infer(c, d_mel, h_lens, B, M_max, pad, d_noise, d_out);
     leave(c, stream);
   });
 }

@@ -1,0 +1,266 @@
+// ParallelWaveGAN generator inference (gfx950), SURVEY.md §8f rank 3 (config C4):
+//   TTS/vocoder/models/parallel_wavegan_generator.py:90-125, layers/parallel_wavegan.py:56-87,
+//   layers/upsample.py:5-101.
+//
+// Layout: every signal is channel-major (B, C, T) fp32 at the sample rate, T_b = hop * (M_b + 2p).
+// The 30 WaveNet residual blocks are the cost (86 kFLOP per sample per block): one fused kernel per
+// block, an implicit GEMM on v_mfma_f32_16x16x4_f32 with
+//   GEMM1  a (128 x TQ) = Wd (128 x 3*64, the 3 dilated taps) . x  +  Wa (128 x 80) . c
+//          (17 k-chunks of 16, staged through LDS with the dilation offsets and the zero padding
+//          resolved at staging time; gate rows interleaved (tanh_j, sigmoid_j) so the gate
+//          z = tanh * sigmoid is a lane-local epilogue written straight into LDS)
+//   GEMM2  [out | skip] (128 x TQ) = W2 (128 x 64) . z   (z read from LDS, never from HBM)
+//   epilogue  x' = (out + b + x) / 4  -> ping-pong buffer;  skip (+)= s + b  (in place)
+// HBM per sample per block: x (+halo, L2) 256 B, c 320 B, skip r/w 512 B, x' 256 B.
+#include "common.h"
+
+namespace {
+constexpr int PW_TQ = 128;          // time columns per workgroup
+constexpr int PW_ROW = PW_TQ + 4;   // LDS row stride (conflict-free B-operand reads)
+constexpr int PW_R = 64, PW_G = 128, PW_A = 80, PW_S = 64;
+constexpr int PW_KC1 = (3 * PW_R + PW_A) / 16;  // 17
+constexpr int PW_KC2 = (PW_G / 2) / 16;         // 4
+}  // namespace
+
+// upsample.py:5-63: nearest stretch by s along time, then the (1, 2s + 1) Conv2d with zero padding
+// s (one filter for every channel): out[t] = sum_k h[k] * in[(t + k - s) / s], 0 <= t + k - s < L*s
+__global__ __launch_bounds__(256) void pw_upsample_kernel(const float* __restrict__ in, long ib, int Lin_max,
+                                                          const int* lens, int len_add, int in_mul, int s,
+                                                          const float* __restrict__ h, float* __restrict__ out,
+                                                          long ob, int Lout_max) {
+  const int b = blockIdx.z, ch = blockIdx.y, t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= Lout_max) return;
+  const int Lin = (lens[b] + len_add) * in_mul, Lout = Lin * s;
+  float acc = 0.f;
+  if (t < Lout) {
+    const float* ip = in + b * ib + (long)ch * Lin_max;
+    for (int k = 0; k <= 2 * s; ++k) {
+      const int u = t + k - s;
+      if (u >= 0 && u < Lout) acc = fmaf(h[k], ip[u / s], acc);
+    }
+  }
+  out[b * ob + (long)ch * Lout_max + t] = acc;
+}
+
+// first_conv (1 -> 64, k1) on the prior noise
+__global__ __launch_bounds__(256) void pw_first_kernel(const float* __restrict__ noise, long nb,
+                                                       const float* __restrict__ w, const float* __restrict__ bias,
+                                                       const int* lens, int len_add, int hop,
+                                                       float* __restrict__ x, int Tmax) {
+  const int b = blockIdx.y, t = blockIdx.x * 64 + (threadIdx.x & 63);
+  if (t >= Tmax) return;
+  const int T = (lens[b] + len_add) * hop;
+  const float n = t < T ? noise[b * nb + t] : 0.f;
+  for (int ch = threadIdx.x >> 6; ch < PW_R; ch += 4)
+    x[((long)b * PW_R + ch) * Tmax + t] = t < T ? fmaf(w[ch], n, bias[ch]) : 0.f;
+}
+
+// tanh(u) * sigmoid(g) on the hardware exp / rcp (|error| ~1e-7 absolute; tanh = 1 - 2 / (1 + e^2u)
+// saturates cleanly at both ends)
+__device__ __forceinline__ float pw_gate(float u, float g) {
+  const float t = 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * u));
+  return t * __frcp_rn(1.f + __expf(-g));
+}
+
+struct PwLayerArgs {
+  const float* x;      // (B, 64, Tmax)
+  const float* c;      // (B, 80, Tmax) upsampled features
+  float* xn;           // next x
+  float* skip;         // (B, 64, Tmax)
+  const f32x4* W1;     // [8 m16][17 kc][64] swizzled, rows interleaved (tanh_j, sigmoid_j)
+  const float* b1;     // [128] interleaved
+  const f32x4* W2;     // [8 m16][4 kc][64]: rows 0..63 conv1x1_out, 64..127 conv1x1_skip
+  const float* b2;     // [128]
+  const int* lens;
+  int len_add, hop, Tmax, dil, first;
+};
+
+__global__ __launch_bounds__(256) void pw_layer_kernel(PwLayerArgs a) {
+  __shared__ __attribute__((aligned(16))) float Xs[2][16 * PW_ROW];
+  __shared__ __attribute__((aligned(16))) float Zs[(PW_G / 2) * PW_ROW];
+  const int b = blockIdx.y;
+  const int T = (a.lens[b] + a.len_add) * a.hop;
+  const int t0 = blockIdx.x * PW_TQ;
+  if (t0 >= T) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;  // 2 x 2 waves, each 64 rows x 64 columns
+  const int g4 = 4 * (lane >> 4), col = lane & 15;
+  const float* xb = a.x + (long)b * PW_R * a.Tmax;
+  const float* cb = a.c + (long)b * PW_A * a.Tmax;
+
+  // staging: chunk kc < 12 -> x rows 16*(kc%4).. at tap kc/4 (offset (tap-1)*dil); else c rows.
+  // Two register sets, loads two chunks ahead: chunk kc+2's global loads go into the set chunk kc
+  // vacated (written to LDS one iteration earlier) while chunk kc's MFMAs run; chunk kc+1's set
+  // goes to LDS after them. Weight fragments run one chunk ahead (L2-resident).
+  float st[2][8];
+  auto stage_load = [&](float (&r8)[8], int kc) {
+    const float* src;
+    int off;
+    if (kc < 12) {
+      src = xb + (long)(16 * (kc & 3)) * a.Tmax;
+      off = (kc / 4 - 1) * a.dil;
+    } else {
+      src = cb + (long)(16 * (kc - 12)) * a.Tmax;
+      off = 0;
+    }
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = tid + 256 * j;
+      const int r = e >> 7, q = e & 127;
+      const int t = t0 + q + off;
+      const bool ok = t >= 0 && t < T;
+      const float v = src[(long)r * a.Tmax + (ok ? t : 0)];
+      r8[j] = ok ? v : 0.f;
+    }
+  };
+  auto stage_store = [&](float* X, const float (&r8)[8]) {
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e = tid + 256 * j;
+      X[(e >> 7) * PW_ROW + (e & 127)] = r8[j];
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+
+  const int mt0 = wm * 4;
+  f32x4 Ar[2][4];
+  auto aload = [&](f32x4 (&r)[4], int kc) {
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) r[mi] = a.W1[((mt0 + mi) * PW_KC1 + kc) * 64 + lane];
+  };
+  aload(Ar[0], 0);
+  stage_load(st[0], 0);
+  stage_load(st[1], 1);
+  stage_store(Xs[0], st[0]);
+  __syncthreads();
+#pragma unroll 2
+  for (int kc = 0; kc < PW_KC1; ++kc) {
+    const float* X = Xs[kc & 1];
+    const int p = kc & 1, q = p ^ 1;
+    if (kc + 2 < PW_KC1) stage_load(st[p], kc + 2);
+    if (kc + 1 < PW_KC1) aload(Ar[q], kc + 1);
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float bv[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bv[ni] = X[(g4 + s) * PW_ROW + wn * 64 + ni * 16 + col];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = MFMA16(Ar[p][mi][s], bv[ni], acc[mi][ni]);
+    }
+    if (kc + 1 < PW_KC1) stage_store(Xs[q], st[q]);
+    __syncthreads();
+  }
+
+  // gate epilogue: rows R = wm*64 + mi*16 + g4 + j, (R even, R + 1) -> z[R / 2] into LDS
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int R = wm * 64 + mi * 16 + g4;
+    const float b0 = a.b1[R], b1 = a.b1[R + 1], b2 = a.b1[R + 2], b3 = a.b1[R + 3];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int q = wn * 64 + ni * 16 + col;
+      const f32x4 v = acc[mi][ni];
+      Zs[(R >> 1) * PW_ROW + q] = pw_gate(v[0] + b0, v[1] + b1);
+      Zs[((R >> 1) + 1) * PW_ROW + q] = pw_gate(v[2] + b2, v[3] + b3);
+    }
+  }
+  __syncthreads();
+
+  // GEMM2: wave row half wm = 0 -> conv1x1_out rows, wm = 1 -> conv1x1_skip rows
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < PW_KC2; ++kc) {
+    f32x4 A[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) A[mi] = a.W2[((mt0 + mi) * PW_KC2 + kc) * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float bv[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bv[ni] = Zs[(kc * 16 + g4 + s) * PW_ROW + wn * 64 + ni * 16 + col];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
+    }
+  }
+  // x' = (out + b + x) * 0.25 (parallel_wavegan.py:85); skip (+)= s + b
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int t = t0 + wn * 64 + ni * 16 + col;
+      if (t >= T) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = mi * 16 + g4 + j;
+        const float v = acc[mi][ni][j] + a.b2[wm * 64 + ch];
+        const long i = ((long)b * 64 + ch) * a.Tmax + t;
+        if (wm == 0) a.xn[i] = (v + a.x[i]) * 0.25f;
+        else a.skip[i] = a.first ? v : a.skip[i] + v;
+      }
+    }
+  }
+}
+
+// parallel_wavegan_generator.py:111-116: skips * sqrt(1 / layers) -> ReLU -> 1x1 (64) -> ReLU -> 1x1 (1)
+__global__ __launch_bounds__(256) void pw_out_kernel(const float* __restrict__ skip, float scale,
+                                                     const float* __restrict__ W3, const float* __restrict__ b3,
+                                                     const float* __restrict__ w4, const float* __restrict__ b4,
+                                                     const int* lens, int len_add, int hop, int Tmax,
+                                                     float* __restrict__ out) {
+  const int b = blockIdx.y, t = blockIdx.x * 256 + threadIdx.x;
+  if (t >= Tmax) return;
+  const int T = (lens[b] + len_add) * hop;
+  if (t >= T) {
+    out[(long)b * Tmax + t] = 0.f;
+    return;
+  }
+  float h[PW_S];
+#pragma unroll
+  for (int ch = 0; ch < PW_S; ++ch) h[ch] = fmaxf(skip[((long)b * PW_S + ch) * Tmax + t] * scale, 0.f);
+  float y = b4[0];
+  for (int o = 0; o < PW_S; ++o) {
+    float v = b3[o];
+#pragma unroll
+    for (int ch = 0; ch < PW_S; ++ch) v = fmaf(W3[o * PW_S + ch], h[ch], v);
+    y = fmaf(w4[o], fmaxf(v, 0.f), y);
+  }
+  out[(long)b * Tmax + t] = y;
+}
+
+void launch_pw_upsample(const float* in, long ib, int Lin_max, const int* lens, int len_add, int in_mul, int s,
+                        const float* h, float* out, long ob, int Lout_max, int C, int B, hipStream_t st) {
+  pw_upsample_kernel<<<dim3((Lout_max + 255) / 256, C, B), 256, 0, st>>>(in, ib, Lin_max, lens, len_add, in_mul, s,
+                                                                         h, out, ob, Lout_max);
+  HIP_OK(hipGetLastError());
+}
+void launch_pw_first(const float* noise, long nb, const float* w, const float* bias, const int* lens, int len_add,
+                     int hop, float* x, int Tmax, int B, hipStream_t st) {
+  pw_first_kernel<<<dim3((Tmax + 63) / 64, B), 256, 0, st>>>(noise, nb, w, bias, lens, len_add, hop, x, Tmax);
+  HIP_OK(hipGetLastError());
+}
+void launch_pw_layer(const float* x, const float* c, float* xn, float* skip, const float* W1, const float* b1,
+                     const float* W2, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
+                     int first, int B, hipStream_t st) {
+  PwLayerArgs a{x, c, xn, skip, reinterpret_cast<const f32x4*>(W1), b1, reinterpret_cast<const f32x4*>(W2), b2,
+                lens, len_add, hop, Tmax, dil, first};
+  pw_layer_kernel<<<dim3((Tmax + PW_TQ - 1) / PW_TQ, B), 256, 0, st>>>(a);
+  HIP_OK(hipGetLastError());
+}
+void launch_pw_out(const float* skip, float scale, const float* W3, const float* b3, const float* w4,
+                   const float* b4, const int* lens, int len_add, int hop, int Tmax, float* out, int B,
+                   hipStream_t st) {
+  pw_out_kernel<<<dim3((Tmax + 255) / 256, B), 256, 0, st>>>(skip, scale, W3, b3, w4, b4, lens, len_add, hop, Tmax,
+                                                             out);
+  HIP_OK(hipGetLastError());
+}

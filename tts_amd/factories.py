@@ -9,7 +9,7 @@ import json
 import re
 
 from .tacotron2 import Tacotron2
-from .vocoder import FullbandMelganGenerator, MelganGenerator, MultibandMelganGenerator
+from .vocoder import FullbandMelganGenerator, MelganGenerator, MultibandMelganGenerator, ParallelWaveganGenerator
 
 
 class AttrDict(dict):
@@ -71,4 +71,9 @@ def setup_generator(c):
         return FullbandMelganGenerator(in_channels=n_mels, out_channels=1, proj_kernel=7, base_channels=512,
                                        upsample_factors=p["upsample_factors"], res_kernel=3,
                                        num_res_blocks=p["num_res_blocks"])
+    if name == "parallel_wavegan_generator":  # generic_utils.py:79-92
+        return ParallelWaveganGenerator(in_channels=1, out_channels=1, kernel_size=3,
+                                        num_res_blocks=p["num_res_blocks"], stacks=p["stacks"], res_channels=64,
+                                        gate_channels=128, skip_channels=64, aux_channels=n_mels, dropout=0.0,
+                                        bias=True, use_weight_norm=True, upsample_factors=p["upsample_factors"])
     raise NotImplementedError(f"generator {name} is outside the MI355X hot path (SURVEY.md §8f)")

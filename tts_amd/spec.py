@@ -322,3 +322,54 @@ def glow_spec(c: GlowConfig) -> Spec:
                   (f"{f}.wn.res_skip_layers.{i}.weight_g", (rs, 1, 1), "wn_g"),
                   (f"{f}.wn.res_skip_layers.{i}.weight_v", (rs, H, 1), "conv")]
     return s
+
+
+@dataclass
+class PwganConfig:
+    """``ParallelWaveganGenerator`` as ``setup_generator`` builds it
+    (``TTS/vocoder/utils/generic_utils.py:79-92``, ``configs/parallel_wavegan_config.json:84-88``):
+    30 WaveNet residual blocks in 3 stacks (dilation 2 ** (i % 10)), kernel 3, res / skip 64,
+    gate 128, aux 80, weight norm, ConvUpsample 4 x 4 x 4 x 4, inference_padding 2."""
+    num_res_blocks: int = 30
+    stacks: int = 3
+    kernel_size: int = 3
+    res_channels: int = 64
+    gate_channels: int = 128
+    skip_channels: int = 64
+    aux_channels: int = 80
+    upsample_factors: Tuple[int, ...] = (4, 4, 4, 4)
+    inference_padding: int = 2
+
+    def dilation(self, i: int) -> int:
+        return 2 ** (i % (self.num_res_blocks // self.stacks))
+
+
+def pwgan_spec(c: PwganConfig, weight_norm: bool = True) -> Spec:
+    """state_dict spec (``parallel_wavegan_generator.py:47-88``, ``layers/parallel_wavegan.py:29-54``,
+    ``layers/upsample.py:33-92``); ``weight_norm=True`` is the checkpoint naming (bias, weight_g,
+    weight_v per conv, torch.nn.utils.weight_norm dim 0)."""
+    s: Spec = []
+
+    def conv(name, shape, bias):
+        if bias:
+            s.append((f"{name}.bias", (shape[0],), "bias"))
+        if weight_norm:
+            s.append((f"{name}.weight_g", (shape[0],) + (1,) * (len(shape) - 1), "wn_g"))
+            s.append((f"{name}.weight_v", shape, "conv"))
+        else:
+            s.append((f"{name}.weight", shape, "conv"))
+
+    R, G, S, A = c.res_channels, c.gate_channels, c.skip_channels, c.aux_channels
+    conv("first_conv", (R, 1, 1), True)
+    conv("upsample_net.conv_in", (A, A, 1), False)
+    for i, u in enumerate(c.upsample_factors):
+        conv(f"upsample_net.upsample.up_layers.{2 * i + 1}", (1, 1, 1, 2 * u + 1), False)
+    for i in range(c.num_res_blocks):
+        p = f"conv_layers.{i}."
+        conv(p + "conv", (G, R, c.kernel_size), True)
+        conv(p + "conv1x1_aux", (G, A, 1), False)
+        conv(p + "conv1x1_out", (R, G // 2, 1), True)
+        conv(p + "conv1x1_skip", (S, G // 2, 1), True)
+    conv("last_conv_layers.1", (S, S, 1), True)
+    conv("last_conv_layers.3", (1, S, 1), True)
+    return s

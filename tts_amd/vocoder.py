@@ -17,7 +17,7 @@ from torch import nn
 from ._lib import get_engine
 from .params import Container, host_tensors, new_token, populate
 from .pqmf import pqmf_filters
-from .spec import MelganConfig, melgan_layers, melgan_spec
+from .spec import MelganConfig, PwganConfig, melgan_layers, melgan_spec, pwgan_spec
 
 
 class PQMF(Container):
@@ -178,3 +178,105 @@ class FullbandMelganGenerator(MelganGenerator):
         super().__init__(in_channels=in_channels, out_channels=out_channels, proj_kernel=proj_kernel,
                          base_channels=base_channels, upsample_factors=upsample_factors, res_kernel=res_kernel,
                          num_res_blocks=num_res_blocks)
+
+
+class ParallelWaveganGenerator(nn.Module):
+    """``TTS/vocoder/models/parallel_wavegan_generator.py:9-158`` for the configuration
+    ``setup_generator`` builds (64 res / 128 gate / 64 skip / 80 aux channels, kernel 3, bias,
+    no dropout at inference): constructor, checkpoint keys (weight_g / weight_v until
+    ``remove_weight_norm()``), ``inference(c)`` -> (B, 1, hop * (M + 2 * inference_padding)).
+
+    The prior noise is ``torch.randn([B, 1, T])`` on the CPU generator, as the reference draws it
+    (``:96``), so a seeded call reproduces the reference's noise; pass ``noise=`` to fix it.
+    Batching (new, optional): ``lengths=`` gives per-row mel frames of a padded batch."""
+
+    def __init__(self, in_channels=1, out_channels=1, kernel_size=3, num_res_blocks=30, stacks=3, res_channels=64,
+                 gate_channels=128, skip_channels=64, aux_channels=80, dropout=0.0, bias=True, use_weight_norm=True,
+                 upsample_factors=(4, 4, 4, 4), inference_padding=2):
+        super().__init__()
+        if (in_channels, out_channels, kernel_size, res_channels, gate_channels, skip_channels, aux_channels) != \
+                (1, 1, 3, 64, 128, 64, 80) or not bias:
+            raise NotImplementedError("tts_amd ParallelWaveganGenerator implements the reference configuration "
+                                      "(1/1 channels, kernel 3, res 64, gate 128, skip 64, aux 80, bias)")
+        if num_res_blocks % stacks:
+            raise ValueError("num_res_blocks must be a multiple of stacks")
+        self.cfg = PwganConfig(num_res_blocks=num_res_blocks, stacks=stacks, upsample_factors=tuple(upsample_factors),
+                               inference_padding=inference_padding)
+        self.in_channels, self.out_channels, self.aux_channels = in_channels, out_channels, aux_channels
+        self.num_res_blocks, self.stacks, self.kernel_size = num_res_blocks, stacks, kernel_size
+        self.upsample_factors = list(upsample_factors)
+        self.upsample_scale = int(np.prod(upsample_factors))
+        self.inference_padding = inference_padding
+        self.dropout = dropout
+        self._wn = use_weight_norm
+        populate(self, pwgan_spec(self.cfg, weight_norm=use_weight_norm))
+        self._version = 0
+        self._token = new_token()
+
+    @property
+    def hop(self):
+        return self.upsample_scale
+
+    def load_state_dict(self, state_dict, strict=True, **kw):
+        res = super().load_state_dict(state_dict, strict=strict, **kw)
+        self._version += 1
+        return res
+
+    def _apply(self, fn, *args, **kwargs):
+        res = super()._apply(fn, *args, **kwargs)
+        self._version += 1
+        return res
+
+    def invalidate(self):
+        self._version += 1
+
+    def remove_weight_norm(self):
+        """Fold w = g * v / ||v|| for every weight-normed conv (parallel_wavegan_generator.py:127-135)."""
+        if not self._wn:
+            return
+        for name, shape, kind in pwgan_spec(self.cfg, weight_norm=True):
+            if not name.endswith(".weight_v"):
+                continue
+            path = name[:-len(".weight_v")].split(".")
+            m = self
+            for p in path:
+                m = m._modules[p]
+            w = torch._weight_norm(m.weight_v.data, m.weight_g.data, 0)
+            del m._parameters["weight_g"]
+            del m._parameters["weight_v"]
+            m.weight = nn.Parameter(w.contiguous(), requires_grad=False)
+        self._wn = False
+        self._version += 1
+
+    def _sync(self, eng):
+        key = (self._token, self._version)
+        if eng.pwgan_key != key:
+            eng.load_pwgan(host_tensors(self), self.cfg.num_res_blocks, self.cfg.stacks, self.cfg.upsample_factors)
+            eng.pwgan_key = key
+
+    def forward(self, c):
+        raise NotImplementedError("training forward is out of scope; use inference()")
+
+    @torch.no_grad()
+    def inference(self, c, lengths: Optional[Sequence[int]] = None, noise: Optional[torch.Tensor] = None):
+        dev = self.first_conv.bias.device
+        eng = get_engine(dev)
+        self._sync(eng)
+        c = torch.as_tensor(c).to(dev, torch.float32)
+        if c.dim() == 2:
+            c = c[None]
+        c = c.contiguous()
+        B, C, M = c.shape
+        if C != self.aux_channels:
+            raise ValueError(f"expected {self.aux_channels} mel channels, got {C}")
+        lens = np.full(B, M, np.int64) if lengths is None else np.asarray(torch.as_tensor(lengths).cpu(), np.int64)
+        pad = int(self.inference_padding)
+        T = self.hop * (M + 2 * pad)
+        if noise is None:
+            noise = torch.randn([B, 1, T])
+        noise = torch.as_tensor(noise).to(dev, torch.float32).contiguous()
+        if tuple(noise.shape) != (B, 1, T):
+            raise ValueError(f"noise must be (B, 1, {T})")
+        out = torch.empty(B, 1, T, device=dev)
+        eng.pwgan_infer(c, lens, pad, noise, out)
+        return out
