@@ -123,7 +123,7 @@ void pack_conv(ConvLayer& L, const std::vector<float>& Wm, const std::vector<flo
   L.dil = dil;
   L.nphase = nphase;
   L.tile = conv_tile_for_cout(Cout);
-  if (K == 1 && Cout % 64 == 0) L.tile = TILE_64x64;  // 1x1 convs are short: more workgroups
+  if (K == 1 && Cout % 64 == 0 && Cout <= 384) L.tile = TILE_64x64;  // short 1x1 convs: more workgroups
   const int TC = conv_tile_tc(L.tile);
   L.Cout_pad = (Cout + TC - 1) / TC * TC;
   const int Kdim = Cin * K;
