@@ -544,3 +544,36 @@ def test_pwgan_matches_reference():
             assert not y[i, 0, len(ref):].any()
         outs.append(y)
     assert np.abs(outs[0] - outs[1]).max() <= 1e-5
+
+
+def test_synthesizer_glow_tts_and_pwgan(tmp_path):
+    """Config C4 through the server path: model "glow_tts" + "parallel_wavegan_generator"
+    (setup_model / setup_generator), all sentences in one Glow call and one PWGAN call; each
+    waveform is hop * 2 * floor(y_length / 2) samples (a B = 1 reference call's length)."""
+    import json as _json
+    from tts_amd import GlowTts, ParallelWaveganGenerator
+    from tts_amd.spec import GlowConfig, PwganConfig, glow_spec, pwgan_spec
+    from tts_amd.synthesizer import Synthesizer
+    from tts_amd.text import symbols
+    from tts_amd.weights import synth_state_dict
+    _dev()
+    conf = _synth_files(tmp_path, with_vocoder=False)
+    tcfg = _json.loads((tmp_path / "tts.json").read_text())
+    tcfg.update({"model": "glow_tts", "encoder_type": "gatedconv"})
+    (tmp_path / "glow.json").write_text(_json.dumps(tcfg))
+    gsd = synth_state_dict(glow_spec(GlowConfig(num_chars=len(symbols))), 23)
+    torch.save({"model": {k: torch.from_numpy(v) for k, v in gsd.items()}}, str(tmp_path / "glow.pth"))
+    vcfg = {"generator_model": "parallel_wavegan_generator", "audio": tcfg["audio"],
+            "generator_model_params": {"upsample_factors": [4, 4, 4, 4], "stacks": 3, "num_res_blocks": 30}}
+    (tmp_path / "pwg.json").write_text(_json.dumps(vcfg))
+    psd = synth_state_dict(pwgan_spec(PwganConfig()), 31)
+    torch.save({"model": {k: torch.from_numpy(v) for k, v in psd.items()}}, str(tmp_path / "pwg.pth"))
+    conf.update({"tts_checkpoint": str(tmp_path / "glow.pth"), "tts_config": str(tmp_path / "glow.json"),
+                 "vocoder_checkpoint": str(tmp_path / "pwg.pth"), "vocoder_config": str(tmp_path / "pwg.json")})
+    synth = Synthesizer(conf)
+    assert isinstance(synth.tts_model, GlowTts) and isinstance(synth.vocoder_model, ParallelWaveganGenerator)
+    sens = ["Hello world.", "A longer sentence for the flow decoder!"]
+    wavs = synth.synthesize_batch(sens)
+    ylens = synth.tts_model.last_y_lengths
+    for w, yl in zip(wavs, ylens):
+        assert w.shape == (256 * 2 * (int(yl) // 2),) and np.isfinite(w).all() and np.abs(w).max() > 0

@@ -8,6 +8,7 @@
 import json
 import re
 
+from .glow_tts import GlowTts
 from .tacotron2 import Tacotron2
 from .vocoder import FullbandMelganGenerator, MelganGenerator, MultibandMelganGenerator, ParallelWaveganGenerator
 
@@ -34,6 +35,13 @@ def _get(c, k, default=None):
 
 def setup_model(num_chars, num_speakers, c, speaker_embedding_dim=None):
     print(" > Using model: {}".format(c["model"]))
+    if c["model"].lower() == "glow_tts":  # TTS/tts/utils/generic_utils.py:105-129
+        return GlowTts(num_chars=num_chars, hidden_channels=192, filter_channels=768, filter_channels_dp=256,
+                       out_channels=80, kernel_size=3, num_heads=2, num_layers_enc=6,
+                       encoder_type=_get(c, "encoder_type", "gatedconv"), dropout_p=0.1, num_flow_blocks_dec=12,
+                       kernel_size_dec=5, dilation_rate=1, num_block_layers=4, dropout_p_dec=0.05,
+                       num_speakers=num_speakers, c_in_channels=0, num_splits=4, num_sqz=2, sigmoid_scale=False,
+                       mean_only=True, hidden_channels_enc=192, hidden_channels_dec=192, use_encoder_prenet=True)
     if c["model"].lower() != "tacotron2":
         raise NotImplementedError(f"model {c['model']} is outside the MI355X hot path (SURVEY.md §8f)")
     gst = _get(c, "gst", {}) or {}

@@ -18,6 +18,7 @@ import torch
 
 from .audio import AudioProcessor, wav_bytes
 from .factories import load_config, setup_generator, setup_model
+from .glow_tts import GlowTts
 from .text import make_symbols, phonemes, split_into_sentences, symbols, text_to_seqvec
 
 
@@ -53,6 +54,8 @@ class Synthesizer:
         if use_cuda:
             self.tts_model.cuda()
         self.tts_model.eval()
+        if isinstance(self.tts_model, GlowTts):
+            return
         self.tts_model.decoder.max_decoder_steps = 3000
         if "r" in cp:
             self.tts_model.decoder.set_r(int(cp["r"]))
@@ -85,8 +88,14 @@ class Synthesizer:
         for i, q in enumerate(seqs):
             batch[i, :len(q)] = q
         with torch.no_grad():
-            _, post, _, _ = self.tts_model.inference(torch.from_numpy(batch).to(dev), text_lengths=lens)
-            mel_lens = [int(m) for m in self.tts_model.last_mel_lengths]
+            if isinstance(self.tts_model, GlowTts):  # synthesis.py:60-66
+                y = self.tts_model.inference(torch.from_numpy(batch).to(dev), lens)[0]
+                post = y.transpose(1, 2)
+                # a B = 1 reference call returns 2 * floor(y_length / 2) frames (decoder squeeze)
+                mel_lens = [2 * (int(m) // 2) for m in self.tts_model.last_y_lengths]
+            else:
+                _, post, _, _ = self.tts_model.inference(torch.from_numpy(batch).to(dev), text_lengths=lens)
+                mel_lens = [int(m) for m in self.tts_model.last_mel_lengths]
             if self.vocoder_model is not None:
                 wav = self.vocoder_model.inference(post.transpose(1, 2).contiguous(), lengths=mel_lens)
                 hop = wav.shape[-1] // post.shape[1]
