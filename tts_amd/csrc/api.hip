@@ -35,8 +35,8 @@ void launch_pw_upsample(const float* in, long ib, int Lin_max, const int* lens, 
 void launch_pw_first(const float* noise, long nb, const float* w, const float* bias, const int* lens, int len_add,
                      int hop, float* x, int Tmax, int B, hipStream_t st);
 void launch_pw_layer(const float* x, const float* c, float* xn, float* skip, const float* W1, const float* b1,
-                     const float* W2, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
-                     int first, int B, hipStream_t st);
+                     const float* W2, const float* b2, const int* lens, const float* zeros, int len_add, int hop,
+                     int Tmax, int dil, int first, int B, int variant, hipStream_t st);
 void launch_pw_out(const float* skip, float scale, const float* W3, const float* b3, const float* w4,
                    const float* b4, const int* lens, int len_add, int hop, int Tmax, float* out, int B,
                    hipStream_t st);
@@ -344,7 +344,7 @@ struct PwganModel {
 };
 
 struct PwganWS {
-  DevBuf lens, ca, cb, xa, xb, skip;
+  DevBuf lens, ca, cb, xa, xb, skip, zeros;
 };
 
 struct tts_ctx {
@@ -2149,10 +2149,21 @@ void pwgan_infer(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int
   float* x = W.xa.f();
   float* xn = W.xb.f();
   launch_pw_first(noise, Tmax, P.first_w.f(), P.first_b.f(), dl, 2 * pad, hop, x, Tmax, B, s);
+  if (!W.zeros.p) {
+    W.zeros.ensure(256 * 4);
+    HIP_OK(hipMemsetAsync(W.zeros.p, 0, 256 * 4, s));
+  }
+  // residual-block kernel: LDS-DMA ring (default) or register staging (TTS_PWGAN_STAGING=regs)
+  static const int variant = [] {
+    const char* e = std::getenv("TTS_PWGAN_STAGING");
+    if (e && std::string(e) == "regs") return 0;
+    if (e && std::string(e) == "ring4") return 2;
+    return 1;
+  }();
   const int per_stack = P.layers / P.stacks;
   for (int l = 0; l < P.layers; ++l) {
-    launch_pw_layer(x, cfeat, xn, W.skip.f(), P.W1[l].f(), P.b1[l].f(), P.W2[l].f(), P.b2[l].f(), dl, 2 * pad, hop,
-                    Tmax, 1 << (l % per_stack), l == 0, B, s);
+    launch_pw_layer(x, cfeat, xn, W.skip.f(), P.W1[l].f(), P.b1[l].f(), P.W2[l].f(), P.b2[l].f(), dl, W.zeros.f(),
+                    2 * pad, hop, Tmax, 1 << (l % per_stack), l == 0, B, variant, s);
     std::swap(x, xn);
   }
   launch_pw_out(W.skip.f(), std::sqrt(1.0f / P.layers), P.W3.f(), P.b3.f(), P.w4.f(), P.b4.f(), dl, 2 * pad, hop,

@@ -72,6 +72,7 @@ struct PwLayerArgs {
   const f32x4* W2;     // [8 m16][4 kc][64]: rows 0..63 conv1x1_out, 64..127 conv1x1_skip
   const float* b2;     // [128]
   const int* lens;
+  const float* zeros;  // >= 64 zero floats: the source of out-of-range staging lanes (LDS-DMA path)
   int len_add, hop, Tmax, dil, first;
 };
 
@@ -212,6 +213,154 @@ __global__ __launch_bounds__(256) void pw_layer_kernel(PwLayerArgs a) {
   }
 }
 
+// s_waitcnt with vmcnt = n and no lgkm / exp wait (gfx9 encoding: vmcnt[3:0] | vmcnt[5:4] << 14)
+#define PW_WAIT_VM(n) __builtin_amdgcn_s_waitcnt(((n) & 15) | (((n) >> 4) << 14) | (7 << 4) | (0xF << 8))
+
+// The same residual block with LDS-DMA staging: both GEMM1 operands go global -> LDS with
+// global_load_lds (no staging registers), through a 3-deep ring, two chunks ahead. Every wave
+// issues exactly 10 LDS-DMA loads per chunk (8 x 4 B for its quarter of the 16 x 128 activation
+// tile -- out-of-range lanes read a zero buffer --, 2 x 16 B for two of the 8 weight tiles), so a
+// counted vmcnt(10) retires chunk kc while kc+1 stays in flight, and a raw s_barrier (no vmcnt(0)
+// drain) publishes it. The weight fragments are read from LDS (ds_read_b128); GEMM2 and the
+// epilogues are those of pw_layer_kernel, with z in LDS aliasing the ring.
+constexpr int PW_RB = 16 * PW_ROW;  // activation slot (floats)
+constexpr int PW_RA = 8 * 256;      // weight slot: 8 m16 tiles x 64 lanes x 4
+template <int PW_NS>
+__global__ __launch_bounds__(256, PW_NS == 3 ? 3 : 2) void pw_layer_glds_kernel(PwLayerArgs a) {
+  constexpr int PW_LDS =
+      PW_NS * (PW_RB + PW_RA) > (PW_G / 2) * PW_ROW ? PW_NS * (PW_RB + PW_RA) : (PW_G / 2) * PW_ROW;
+  constexpr int AHEAD = PW_NS - 1;  // chunks in flight beyond the one being consumed
+  __shared__ __attribute__((aligned(16))) float pool[PW_LDS];
+  float* ringA = pool;                 // [NS][PW_RA]
+  float* ringB = pool + PW_NS * PW_RA;  // [NS][PW_RB]
+  float* Zs = pool;                    // after GEMM1
+  const int b = blockIdx.y;
+  const int T = (a.lens[b] + a.len_add) * a.hop;
+  const int t0 = blockIdx.x * PW_TQ;
+  if (t0 >= T) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int wm = wave >> 1, wn = wave & 1;
+  const int g4 = 4 * (lane >> 4), col = lane & 15;
+  const float* xb = a.x + (long)b * PW_R * a.Tmax;
+  const float* cb = a.c + (long)b * PW_A * a.Tmax;
+  const float* W1f = reinterpret_cast<const float*>(a.W1);
+
+  auto issue = [&](int kc) {
+    const int sl = kc % PW_NS;
+    const float* src;
+    int off;
+    if (kc < 12) {
+      src = xb + (long)(16 * (kc & 3)) * a.Tmax;
+      off = (kc / 4 - 1) * a.dil;
+    } else {
+      src = cb + (long)(16 * (kc - 12)) * a.Tmax;
+      off = 0;
+    }
+    float* dstB = ringB + sl * PW_RB;
+#pragma unroll
+    for (int j = 0; j < 8; ++j) {
+      const int e0 = j * 256 + wave * 64;  // this wave's 64 consecutive elements of the tile
+      const int r = e0 >> 7, q = (e0 & 127) + lane;
+      const int t = t0 + q + off;
+      const float* g = (t >= 0 && t < T) ? src + (long)r * a.Tmax + t : a.zeros + lane;
+      __builtin_amdgcn_global_load_lds(g, dstB + r * PW_ROW + (e0 & 127), 4, 0, 0);
+    }
+    float* dstA = ringA + sl * PW_RA;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) {
+      const int m16 = wave * 2 + i;
+      __builtin_amdgcn_global_load_lds(W1f + ((long)(m16 * PW_KC1 + kc) * 64 + lane) * 4, dstA + m16 * 256, 16, 0,
+                                       0);
+    }
+  };
+
+  f32x4 acc[4][4];
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const int mt0 = wm * 4;
+
+#pragma unroll
+  for (int k = 0; k < AHEAD; ++k) issue(k);
+  for (int kc = 0; kc < PW_KC1; ++kc) {
+    // chunks issued after kc: min(AHEAD - 1, PW_KC1 - 1 - kc), 10 LDS-DMA loads each
+    const int after = min(AHEAD - 1, PW_KC1 - 1 - kc);
+    if (after >= 2) PW_WAIT_VM(20);
+    else if (after == 1) PW_WAIT_VM(10);
+    else PW_WAIT_VM(0);
+    __builtin_amdgcn_s_barrier();
+    asm volatile("" ::: "memory");
+    if (kc + AHEAD < PW_KC1) issue(kc + AHEAD);
+    const int sl = kc % PW_NS;
+    const float* X = ringB + sl * PW_RB;
+    const f32x4* As = reinterpret_cast<const f32x4*>(ringA + sl * PW_RA);
+    f32x4 A[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) A[mi] = As[(mt0 + mi) * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float bv[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bv[ni] = X[(g4 + s) * PW_ROW + wn * 64 + ni * 16 + col];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
+    }
+  }
+  __syncthreads();  // every wave is done with the ring before z overwrites it
+
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+    const int R = wm * 64 + mi * 16 + g4;
+    const float b0 = a.b1[R], b1 = a.b1[R + 1], b2 = a.b1[R + 2], b3 = a.b1[R + 3];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int q = wn * 64 + ni * 16 + col;
+      const f32x4 v = acc[mi][ni];
+      Zs[(R >> 1) * PW_ROW + q] = pw_gate(v[0] + b0, v[1] + b1);
+      Zs[((R >> 1) + 1) * PW_ROW + q] = pw_gate(v[2] + b2, v[3] + b3);
+    }
+  }
+  __syncthreads();
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int kc = 0; kc < PW_KC2; ++kc) {
+    f32x4 A[4];
+#pragma unroll
+    for (int mi = 0; mi < 4; ++mi) A[mi] = a.W2[((mt0 + mi) * PW_KC2 + kc) * 64 + lane];
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      float bv[4];
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) bv[ni] = Zs[(kc * 16 + g4 + s) * PW_ROW + wn * 64 + ni * 16 + col];
+#pragma unroll
+      for (int mi = 0; mi < 4; ++mi)
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) acc[mi][ni] = MFMA16(A[mi][s], bv[ni], acc[mi][ni]);
+    }
+  }
+#pragma unroll
+  for (int mi = 0; mi < 4; ++mi) {
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int t = t0 + wn * 64 + ni * 16 + col;
+      if (t >= T) continue;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = mi * 16 + g4 + j;
+        const float v = acc[mi][ni][j] + a.b2[wm * 64 + ch];
+        const long i = ((long)b * 64 + ch) * a.Tmax + t;
+        if (wm == 0) a.xn[i] = (v + a.x[i]) * 0.25f;
+        else a.skip[i] = a.first ? v : a.skip[i] + v;
+      }
+    }
+  }
+}
+
 // parallel_wavegan_generator.py:111-116: skips * sqrt(1 / layers) -> ReLU -> 1x1 (64) -> ReLU -> 1x1 (1)
 __global__ __launch_bounds__(256) void pw_out_kernel(const float* __restrict__ skip, float scale,
                                                      const float* __restrict__ W3, const float* __restrict__ b3,
@@ -250,11 +399,14 @@ void launch_pw_first(const float* noise, long nb, const float* w, const float* b
   HIP_OK(hipGetLastError());
 }
 void launch_pw_layer(const float* x, const float* c, float* xn, float* skip, const float* W1, const float* b1,
-                     const float* W2, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
-                     int first, int B, hipStream_t st) {
+                     const float* W2, const float* b2, const int* lens, const float* zeros, int len_add, int hop,
+                     int Tmax, int dil, int first, int B, int variant, hipStream_t st) {
   PwLayerArgs a{x, c, xn, skip, reinterpret_cast<const f32x4*>(W1), b1, reinterpret_cast<const f32x4*>(W2), b2,
-                lens, len_add, hop, Tmax, dil, first};
-  pw_layer_kernel<<<dim3((Tmax + PW_TQ - 1) / PW_TQ, B), 256, 0, st>>>(a);
+                lens, zeros, len_add, hop, Tmax, dil, first};
+  const dim3 grid((Tmax + PW_TQ - 1) / PW_TQ, B);
+  if (variant == 1) pw_layer_glds_kernel<3><<<grid, 256, 0, st>>>(a);
+  else if (variant == 2) pw_layer_glds_kernel<4><<<grid, 256, 0, st>>>(a);
+  else pw_layer_kernel<<<grid, 256, 0, st>>>(a);
   HIP_OK(hipGetLastError());
 }
 void launch_pw_out(const float* skip, float scale, const float* W3, const float* b3, const float* w4,
