@@ -75,8 +75,9 @@ int tts_taco_infer_spk(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens
    attention windowing at inference (attn_win) and forward attention (forward_attn; the transition
    agent is on when decoder.attention.ta.* tensors are loaded). BN prenet is detected from the
    decoder.prenet.linear_layers.N.batch_normalization.* tensors. Variants decode on the persistent
-   decoder only. Set before tts_taco_infer; kept across finalize. */
-int tts_taco_set_options(tts_ctx* ctx, int windowing, int forward_attn);
+   decoder only. forward_attn_mask keeps the forward alignment to [n-1, n+2] around the shifted
+   previous argmax n (common_layers.py:309-318). Set before tts_taco_infer; kept across finalize. */
+int tts_taco_set_options(tts_ctx* ctx, int windowing, int forward_attn, int forward_attn_mask);
 
 /* speaker dimension of the finalized model (0 = single speaker) and its learned table size */
 int tts_taco_speaker_dim(tts_ctx* ctx, int* spk_dim, int* num_speakers);

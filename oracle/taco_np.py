@@ -68,7 +68,7 @@ def lstm_cell(x, h, c, w_ih, w_hh, b_ih, b_hh):
 
 class TacoOracle:
     def __init__(self, sd, attn_norm="sigmoid", r_init=7, frame_channels=80, windowing=False,
-                 forward_attn=False, trans_agent=False):
+                 forward_attn=False, trans_agent=False, forward_attn_mask=False):
         self.sd = {k: (np.asarray(v, F32) if np.asarray(v).dtype != np.int64 else np.asarray(v))
                    for k, v in sd.items()}
         self.attn_norm = attn_norm
@@ -77,6 +77,7 @@ class TacoOracle:
         self.windowing = windowing
         self.forward_attn = forward_attn
         self.trans_agent = trans_agent
+        self.forward_attn_mask = forward_attn_mask
 
     def _bn(self, prefix):
         return {k: self.sd[f"{prefix}.batch_normalization.{k}"]
@@ -165,10 +166,16 @@ class TacoOracle:
         else:
             raise ValueError("Unknown value for attention norm type")
         st["alpha_cum"] = (st["alpha_cum"] + a).astype(F32)
-        if self.forward_attn:  # apply_forward_attention (common_layers.py:302-323), no mask
+        if self.forward_attn:  # apply_forward_attention (common_layers.py:302-323)
             prev = st["fwd_alpha"]
             shifted = np.concatenate([np.zeros(1, F32), prev[:-1]])
             a = (((F32(1) - st["u"]) * prev + st["u"] * shifted + F32(1e-8)) * a).astype(F32)
+            if self.forward_attn_mask:  # :309-318, Python slice / negative-index semantics kept
+                n = int(np.argmax(shifted))
+                val = a.max()
+                a[n + 3:] = 0
+                a[:n - 1] = 0
+                a[n - 2] = F32(0.01) * val
             a = (a / a.sum()).astype(F32)
             st["fwd_alpha"] = a
         st["alpha"] = a

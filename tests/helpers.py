@@ -36,7 +36,8 @@ def build_taco(cfg, sd, device="cuda"):
     m = Tacotron2(num_chars=cfg.num_chars, num_speakers=cfg.num_speakers, r=cfg.r, attn_norm=cfg.attn_norm,
                   double_decoder_consistency=cfg.double_decoder_consistency, ddc_r=cfg.ddc_r,
                   speaker_embedding_dim=cfg.speaker_embedding_dim, prenet_type=cfg.prenet_type,
-                  attn_win=cfg.windowing, forward_attn=cfg.forward_attn, trans_agent=cfg.trans_agent)
+                  attn_win=cfg.windowing, forward_attn=cfg.forward_attn, trans_agent=cfg.trans_agent,
+                  forward_attn_mask=cfg.forward_attn_mask)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     return m.to(device).eval()
 

@@ -191,7 +191,8 @@ def test_tacotron2_multispeaker_matches_reference(name, n):
                 m.last_steps, range(n))
 
 
-@pytest.mark.parametrize("name", ["taco_bnprenet", "taco_window", "taco_window_softmax", "taco_fwdattn"])
+@pytest.mark.parametrize("name", ["taco_bnprenet", "taco_window", "taco_window_softmax", "taco_fwdattn",
+                                  "taco_fwdmask"])
 def test_tacotron2_decoder_variants_match_reference(name):
     """SURVEY 8f rank 4 decoder variants on the persistent decoder, both fixture utterances in one
     batched call: BN prenet, attention windowing (sigmoid / softmax), forward attention with the

@@ -106,7 +106,7 @@ def test_tacotron2_oracle_multispeaker_matches_reference(name, n):
 def test_fixture_fp64_drift_is_small():
     """Every Tacotron2 fixture records its fp32-vs-fp64 drift; the 1e-4 tolerance needs it tiny."""
     for name in ("taco_sigmoid", "taco_softmax", "taco_multispk", "taco_extspk", "taco_bnprenet", "taco_window",
-                 "taco_window_softmax", "taco_fwdattn"):
+                 "taco_window_softmax", "taco_fwdattn", "taco_fwdmask"):
         fx = load_fixture(name)
         drifts = [float(fx[k]) for k in fx.files if k.endswith("_drift64")]
         assert drifts and max(drifts) < 1e-6
@@ -127,14 +127,15 @@ def test_ge2e_oracle_matches_reference(tag, proj):
     assert np.abs(orc.compute_embedding(fx["x"][0]) - fx[f"{tag}_cemb"][0]).max() <= 2e-6
 
 
-@pytest.mark.parametrize("name", ["taco_bnprenet", "taco_window", "taco_window_softmax", "taco_fwdattn"])
+@pytest.mark.parametrize("name", ["taco_bnprenet", "taco_window", "taco_window_softmax", "taco_fwdattn",
+                                  "taco_fwdmask"])
 def test_tacotron2_oracle_decoder_variants_match_reference(name):
     """Decoder variants: BN prenet (common_layers.py:25-74), attention windowing
     (:286-300) with sigmoid and softmax norms, forward attention + transition agent (:302-372)."""
     fx = load_fixture(name)
     cfg, sd = taco_state_dict(fx, r=2)
     orc = TacoOracle(sd, cfg.attn_norm, cfg.r, windowing=cfg.windowing, forward_attn=cfg.forward_attn,
-                     trans_agent=cfg.trans_agent)
+                     trans_agent=cfg.trans_agent, forward_attn_mask=cfg.forward_attn_mask)
     for u in range(2):
         k = f"r2_u{u}"
         dec, post, align, stop = orc.inference(fx[k + "_ids"], 2, int(fx["r2_max_steps"]))

@@ -39,7 +39,7 @@ SIGNATURES = [
                                           ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_int_p,
                                           _c_int_p, _vp]),
     ("tts_taco_speaker_dim", ctypes.c_int, [_vp, _c_i_p, _c_i_p]),
-    ("tts_taco_set_options", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int]),
+    ("tts_taco_set_options", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_taco_encoder", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_taco_postnet", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_melgan_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
@@ -132,8 +132,9 @@ class Engine:
         _check(fn(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p), shape, a.ndim))
 
     def load_tacotron(self, tensors: Dict[str, np.ndarray], num_chars: int, r_init: int, attn_norm: str,
-                      windowing: bool = False, forward_attn: bool = False):
-        _check(self.lib.tts_taco_set_options(self.h, int(bool(windowing)), int(bool(forward_attn))))
+                      windowing: bool = False, forward_attn: bool = False, forward_attn_mask: bool = False):
+        _check(self.lib.tts_taco_set_options(self.h, int(bool(windowing)), int(bool(forward_attn)),
+                                             int(bool(forward_attn and forward_attn_mask))))
         for k, v in tensors.items():
             self._set(self.lib.tts_taco_set_tensor, k, v)
         _check(self.lib.tts_taco_finalize(self.h, num_chars, r_init, 1 if attn_norm == "softmax" else 0))

@@ -233,7 +233,7 @@ struct TacoModel {
   int spk_dim = 0, num_spk = 0;
   // decoder variants (common_layers.py:25-74, 196-372): BN prenet folded into the prenet weights
   // (+ biases), windowing / forward attention / transition agent flags
-  bool prenet_bn = false, windowing = false, forward_attn = false, trans_agent = false;
+  bool prenet_bn = false, windowing = false, forward_attn = false, trans_agent = false, forward_attn_mask = false;
   std::vector<float> pre1_bias;  // b1' (BN), folded into the projection's prenet rows
   DevBuf pre1_b0, pre2_b, ta_w;
   float ta_b = 0.f;
@@ -1138,6 +1138,7 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.win = M.windowing;
   a.fwd = M.forward_attn;
   a.trans = M.forward_attn && M.trans_agent;
+  a.fwd_mask = M.forward_attn && M.forward_attn_mask;
   a.ta_w = M.trans_agent ? M.ta_w.f() : nullptr;
   a.ta_b = M.ta_b;
   a.win_idx = W.win_idx.i();
@@ -2287,11 +2288,12 @@ int tts_taco_infer_spk(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, 
   });
 }
 
-int tts_taco_set_options(tts_ctx* c, int windowing, int forward_attn) {
+int tts_taco_set_options(tts_ctx* c, int windowing, int forward_attn, int forward_attn_mask) {
   return guarded([&] {
     TTS_CHECK(c, "null ctx");
     c->taco.windowing = windowing != 0;
     c->taco.forward_attn = forward_attn != 0;
+    c->taco.forward_attn_mask = forward_attn_mask != 0;
   });
 }
 

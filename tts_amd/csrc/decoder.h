@@ -125,7 +125,7 @@ struct PArgs {
   const float* pre2_b;   // [256] layer-2 bias b2'
   int win;
   int* win_idx;          // (B) previous argmax, -1 before the first step
-  int fwd, trans;
+  int fwd, trans, fwd_mask;
   float* fwd_u;          // (B) transition probability u, 0.5 before the first step
   float* part_f;         // (B, nchmax) chunk sums of the forward weights
   const float* ta_w;     // [512 ctx | 1024 query]

@@ -359,12 +359,16 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
       cx = fmaf(pu[i], wc[i], cx);
     }
   }
-  const float ctx_v = cx / ((FWD && P.fwd) ? Fz : S);
+  float ctx_v = cx / ((FWD && P.fwd) ? Fz : S);
   stc(P.ctx + frag_idx(b, tid, 512), ctx_v);
   ATRACE(7);
   const long ab = (long)b * D.T_max;
   float bestv = -INFINITY;
   int besti = 0x7fffffff;
+  // forward_attn_mask (common_layers.py:309-318): argmax of the shifted previous alignment
+  // (1 + first argmax of a[0 .. T-2]; 0 when that max is 0) and the max of the unmasked one
+  float prv_m = 0.f, vmax = 0.f;
+  int prv_i = 0x7fffffff;
   for (int tt = tid; tt < T; tt += NT) {
     const float e = ldc(P.energy + ab + tt);
     if ((WIN && P.win) && (e > bestv || (e == bestv && tt < besti))) {
@@ -375,7 +379,16 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     const float al = raw / S;
     stc(P.acum + ab + tt, ldc(P.acum + ab + tt) + al);  // location state accumulates the raw alignment
     if ((FWD && P.fwd)) {  // forward alignment into the energy slot (alpha is still read as a[t-1] here)
-      stc(P.energy + ab + tt, ((1.f - fu) * fwd_prev(tt) + fu * fwd_prev(tt - 1) + 1e-8f) * raw / Fz);
+      const float ap = fwd_prev(tt);
+      const float fa = ((1.f - fu) * ap + fu * fwd_prev(tt - 1) + 1e-8f) * raw / Fz;
+      stc(P.energy + ab + tt, fa);
+      if (P.fwd_mask) {
+        vmax = fmaxf(vmax, fa);
+        if (tt <= T - 2 && ap > prv_m) {  // strictly greater: the first index of the max
+          prv_m = ap;
+          prv_i = tt;
+        }
+      }
     } else {
       stc(P.alpha + ab + tt, al);
       if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = al;
@@ -384,10 +397,64 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   if ((FWD && P.fwd)) {
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
+    // mask: keep [lo, n + 2] (lo = n - 1, or T - 1 when n = 0: Python's a[:-1] = 0), then
+    // a[n - 2] (negative index wraps) = 0.01 max, renormalise; the context is recomputed from the
+    // at most 5 surviving positions
+    int lo = 0, hi = T - 1, pp = -1;
+    float vz = 0.f, zsum = 1.f;
+    if (P.fwd_mask) {
+      for (int off = 32; off > 0; off >>= 1) {
+        const float ov = __shfl_xor(prv_m, off, 64);
+        const int oi = __shfl_xor(prv_i, off, 64);
+        if (ov > prv_m || (ov == prv_m && oi < prv_i)) {
+          prv_m = ov;
+          prv_i = oi;
+        }
+        vmax = fmaxf(vmax, __shfl_xor(vmax, off, 64));
+      }
+      float* rv = red;
+      int* ri = reinterpret_cast<int*>(red + 16);
+      float* rm = red + 32;
+      if (lane == 0) {
+        rv[tid >> 6] = prv_m;
+        ri[tid >> 6] = prv_i;
+        rm[tid >> 6] = vmax;
+      }
+      lds_barrier();
+      float pv = rv[0], vm = rm[0];
+      int pi = ri[0];
+      for (int w = 1; w < NT / 64; ++w) {
+        if (rv[w] > pv || (rv[w] == pv && ri[w] < pi)) {
+          pv = rv[w];
+          pi = ri[w];
+        }
+        vm = fmaxf(vm, rm[w]);
+      }
+      const int n = pv > 0.f ? pi + 1 : 0;
+      lo = n >= 1 ? n - 1 : T - 1;
+      hi = min(n + 2, T - 1);
+      pp = n - 2 < 0 ? n - 2 + T : n - 2;
+      vz = 0.01f * vm;
+      zsum = 0.f;
+      for (int j = lo; j <= hi; ++j)
+        if (j != pp) zsum += ldc(P.energy + ab + j);
+      if (pp >= 0) zsum += vz;
+      lds_barrier();  // the reduction scratch is reused below
+    }
     for (int tt = tid; tt < T; tt += NT) {
-      const float af = ldc(P.energy + ab + tt);
+      float af = ldc(P.energy + ab + tt);
+      if (P.fwd_mask) af = tt == pp ? vz / zsum : (tt >= lo && tt <= hi ? af / zsum : 0.f);
       stc(P.alpha + ab + tt, af);
       if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + tt] = af;
+    }
+    if (P.fwd_mask) {
+      const float* eb = P.enc + (long)b * D.T_max * 512 + tid;
+      float c2 = 0.f;
+      for (int j = lo; j <= hi; ++j)
+        if (j != pp) c2 = fmaf(ldc(P.energy + ab + j) / zsum, eb[(long)j * 512], c2);
+      if (pp >= 0) c2 = fmaf(vz / zsum, eb[(long)pp * 512], c2);
+      ctx_v = c2;
+      stc(P.ctx + frag_idx(b, tid, 512), ctx_v);
     }
   }
   if ((WIN && P.win) || ((FWD && P.fwd) && P.trans)) {

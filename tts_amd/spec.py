@@ -52,6 +52,7 @@ class TacotronConfig:
     windowing: bool = False         # attention windowing at inference (common_layers.py:286-300)
     forward_attn: bool = False      # forward attention (common_layers.py:302-323)
     trans_agent: bool = False       # transition agent u = sigmoid(ta([ctx, query]))
+    forward_attn_mask: bool = False  # forward attention kept to [n-1, n+2] (common_layers.py:309-318)
 
     @property
     def spk_dim(self) -> int:

@@ -57,8 +57,6 @@ class Tacotron2(nn.Module):
             unsupported.append("GST")
         if attn_type != "original":
             unsupported.append(f"attn_type={attn_type}")
-        if forward_attn_mask:
-            unsupported.append("forward_attn_mask")
         if trans_agent and not forward_attn:
             unsupported.append("trans_agent without forward_attn")
         if not location_attn:
@@ -86,7 +84,8 @@ class Tacotron2(nn.Module):
                                   ddc_r=ddc_r if ddc_r is not None else r,
                                   num_speakers=num_speakers, speaker_embedding_dim=speaker_embedding_dim,
                                   prenet_type=prenet_type, windowing=bool(attn_win),
-                                  forward_attn=bool(forward_attn), trans_agent=bool(trans_agent))
+                                  forward_attn=bool(forward_attn), trans_agent=bool(trans_agent),
+                                  forward_attn_mask=bool(forward_attn and forward_attn_mask))
         # models/tacotron2.py:50-58 / tacotron_abstract.py:76-81: a learned table unless the caller
         # gives per-sample embeddings of speaker_embedding_dim
         self.embeddings_per_sample = speaker_embedding_dim is not None
@@ -148,7 +147,8 @@ class Tacotron2(nn.Module):
         key = (self._token, self._version)
         if eng.taco_key != key:
             eng.load_tacotron(host_tensors(self, skip_prefixes=("coarse_decoder.",)), self.num_chars,
-                              self.decoder.r_init, self.attn_norm, self.cfg.windowing, self.cfg.forward_attn)
+                              self.decoder.r_init, self.attn_norm, self.cfg.windowing, self.cfg.forward_attn,
+                              self.cfg.forward_attn_mask)
             eng.taco_key = key
 
     @torch.no_grad()
