@@ -49,15 +49,48 @@ def wn(sd, name):
 
 
 class GlowOracle:
-    def __init__(self, sd, enc_layers=9, flows=12, wn_layers=4):
+    def __init__(self, sd, enc_layers=9, flows=12, wn_layers=4, encoder_type="gatedconv"):
         self.sd = {k: np.asarray(v, F32) if np.asarray(v).dtype != np.int64 else np.asarray(v) for k, v in sd.items()}
         self.enc_layers, self.flows, self.wn_layers = enc_layers, flows, wn_layers
+        self.encoder_type = encoder_type
+
+    def _bn(self, x, name, eps=1e-5):
+        sd = self.sd
+        sc = sd[name + ".weight"] / np.sqrt(sd[name + ".running_var"] + F32(eps))
+        return ((x - sd[name + ".running_mean"][:, None]) * sc[:, None] + sd[name + ".bias"][:, None]).astype(F32)
+
+    def _tdsep(self, x):
+        """encoder.py:118-121 with use_prenet: ConvLayerNorm (glow.py:43-50) then the
+        TimeDepthSeparableConvBlock (time_depth_sep_conv.py:51-63,93-96); B = 1, so masks are 1."""
+        sd = self.sd
+        H = x.shape[0]
+        h = x
+        for i in range(3):
+            p = "encoder.pre."
+            h = conv1d(h, sd[p + f"conv_layers.{i}.weight"], sd[p + f"conv_layers.{i}.bias"], 2)
+            h = np.maximum(layer_norm(h, sd[p + f"norm_layers.{i}.gamma"], sd[p + f"norm_layers.{i}.beta"]), F32(0))
+        x = (x + conv1d(h, sd["encoder.pre.proj.weight"], sd["encoder.pre.proj.bias"])).astype(F32)
+        for i in range(self.enc_layers):
+            q = f"encoder.encoder.layers.{i}."
+            h = self._bn(conv1d(x, sd[q + "time_conv.weight"], sd[q + "time_conv.bias"]), q + "norm1")
+            h = (h[:H] * (F32(1) / (F32(1) + np.exp(-h[H:])))).astype(F32)               # GLU
+            wd = sd[q + "depth_conv.weight"][:, 0, :]                                      # (H, 5)
+            hp = np.pad(h, ((0, 0), (2, 2)))
+            L = h.shape[1]
+            d = sum(wd[:, k:k + 1] * hp[:, k:k + L] for k in range(5)) + sd[q + "depth_conv.bias"][:, None]
+            d = self._bn(d.astype(F32), q + "norm2")
+            d = (d * (F32(1) / (F32(1) + np.exp(-d)))).astype(F32)                         # x * sigmoid(x)
+            o = self._bn(conv1d(d, sd[q + "time_conv2.weight"], sd[q + "time_conv2.bias"]), q + "norm3")
+            x = (x + o).astype(F32)
+        return x
 
     def encode(self, ids):
         sd = self.sd
         H = sd["encoder.emb.weight"].shape[1]
         x = (sd["encoder.emb.weight"][ids] * F32(np.sqrt(H))).T.astype(F32)        # (H, T)
-        for i in range(self.enc_layers):
+        if self.encoder_type == "time-depth-separable":
+            x = self._tdsep(x)
+        for i in range(self.enc_layers if self.encoder_type == "gatedconv" else 0):
             p = f"encoder.encoder."
             o = conv1d(x, sd[p + f"conv_layers.{i}.weight"], sd[p + f"conv_layers.{i}.bias"], 2)
             o = layer_norm(o, sd[p + f"norm_layers.{i}.gamma"], sd[p + f"norm_layers.{i}.beta"])

@@ -239,7 +239,7 @@ def ge2e_case(name):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
-def glow_case(name):
+def glow_case(name, encoder_type="gatedconv", seed=23, data_seed=24):
     """Glow-TTS (gated-conv encoder, as setup_model builds it, TTS/tts/utils/generic_utils.py:105-129).
     The top-level GlowTts module does not import here (monotonic_align.core is an unbuilt Cython
     extension), so the reference's Encoder and Decoder modules run under the inference glue of
@@ -247,9 +247,9 @@ def glow_case(name):
     from TTS.tts.layers.glow_tts.encoder import Encoder
     from TTS.tts.layers.glow_tts.decoder import Decoder
     from tts_amd.spec import GlowConfig, glow_spec
-    cfg = GlowConfig()
+    cfg = GlowConfig(encoder_type=encoder_type)
     enc = Encoder(cfg.num_chars, out_channels=80, hidden_channels=192, filter_channels=768, filter_channels_dp=256,
-                  encoder_type="gatedconv", num_heads=2, num_layers=6, kernel_size=3, dropout_p=0.1, mean_only=True,
+                  encoder_type=encoder_type, num_heads=2, num_layers=6, kernel_size=3, dropout_p=0.1, mean_only=True,
                   use_prenet=True, c_in_channels=0)
     dec = Decoder(80, 192, 5, 1, 12, 4, dropout_p=0.05, num_splits=4, num_sqz=2, sigmoid_scale=False,
                   c_in_channels=0)
@@ -257,14 +257,13 @@ def glow_case(name):
                 **{"decoder." + k: tuple(v.shape) for k, v in dec.state_dict().items()}}
     spec = {n: tuple(sh) for n, sh, _ in glow_spec(cfg)}
     assert spec == ref_keys, "glow_spec does not match the reference state_dict"
-    seed = 23
     sd = synth_state_dict(glow_spec(cfg), seed)
     enc.load_state_dict({k[8:]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("encoder.")})
     dec.load_state_dict({k[8:]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("decoder.")})
     enc.eval()
     dec.eval()
-    rs = np.random.RandomState(24)
-    out = {"seed": np.int64(seed), "noise_scale": np.float32(0.66)}
+    rs = np.random.RandomState(data_seed)
+    out = {"seed": np.int64(seed), "noise_scale": np.float32(0.66), "encoder_type": encoder_type}
     for u, T in enumerate((17, 31)):
         ids = rs.randint(1, cfg.num_chars, size=T).astype(np.int64)
         with torch.no_grad():
@@ -390,6 +389,8 @@ if __name__ == "__main__":
         ge2e_case("ge2e")
     if "glow" in which:
         glow_case("glow")
+    if "glow_tdsep" in which:
+        glow_case("glow_tdsep", "time-depth-separable", seed=27, data_seed=28)
     if "taco_softmax" in which:
         taco_case("taco_softmax", TacotronConfig(attn_norm="softmax"), seed=2,
                   utt_lens=[25, 9], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=8)

@@ -473,17 +473,18 @@ def test_ge2e_speaker_encoder_matches_reference(tag, proj):
 
 
 # --------------------------------------------------------------------------------- Glow-TTS
-def test_glow_tts_matches_reference():
-    """GlowTts.inference (glow_tts.py:166-193; gated-conv encoder, 12 reverse flow blocks) with the
-    fixture's prior noise, both utterances in ONE batched call: durations / y_lengths and the
-    monotonic path exact, means and mel <= 1e-4."""
+@pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable")])
+def test_glow_tts_matches_reference(name, enc):
+    """GlowTts.inference (glow_tts.py:166-193; gated-conv or time-depth-separable encoder, 12 reverse
+    flow blocks) with the fixture's prior noise, both utterances in ONE batched call: durations /
+    y_lengths and the monotonic path exact, means and mel <= 1e-4."""
     from tts_amd import GlowTts
     from tts_amd.spec import GlowConfig, glow_spec
     from tts_amd.weights import synth_state_dict
     _dev()
-    fx = load_fixture("glow")
-    m = GlowTts(num_chars=GlowConfig().num_chars)
-    sd = synth_state_dict(glow_spec(GlowConfig()), int(fx["seed"]))
+    fx = load_fixture(name)
+    m = GlowTts(num_chars=GlowConfig().num_chars, encoder_type=enc, use_encoder_prenet=True)
+    sd = synth_state_dict(glow_spec(GlowConfig(encoder_type=enc)), int(fx["seed"]))
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     m = m.cuda().eval()
     ids = [fx["u0_ids"], fx["u1_ids"]]

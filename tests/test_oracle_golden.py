@@ -145,14 +145,16 @@ def test_tacotron2_oracle_decoder_variants_match_reference(name):
         assert np.abs(align - fx[k + "_align"]).max() <= (1e-5 if cfg.forward_attn else 1e-6)
 
 
-def test_glow_oracle_matches_reference():
-    """Glow-TTS (gated-conv encoder): the reference's Encoder / Decoder modules under the inference
-    glue of glow_tts.py:166-193 (make_golden.py glow); fixed prior noise."""
+@pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable")])
+def test_glow_oracle_matches_reference(name, enc):
+    """Glow-TTS, both encoders the reference configs use (gated conv; time-depth-separable with the
+    ConvLayerNorm prenet): the reference's Encoder / Decoder modules under the inference glue of
+    glow_tts.py:166-193 (make_golden.py glow / glow_tdsep); fixed prior noise."""
     from oracle.glow_np import GlowOracle
     from tts_amd.spec import GlowConfig, glow_spec
     from tts_amd.weights import synth_state_dict
-    fx = load_fixture("glow")
-    orc = GlowOracle(synth_state_dict(glow_spec(GlowConfig()), int(fx["seed"])))
+    fx = load_fixture(name)
+    orc = GlowOracle(synth_state_dict(glow_spec(GlowConfig(encoder_type=enc)), int(fx["seed"])), encoder_type=enc)
     for u in range(2):
         k = f"u{u}"
         y, ym, attn, logw, Ty = orc.inference(fx[k + "_ids"], fx[k + "_noise"], float(fx["noise_scale"]))

@@ -22,7 +22,9 @@ bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, 
 void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, const float* beta, const float* res,
                        long rb, float* out, long ob, const int* lens, int B, int T, hipStream_t s);
 void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, const int* lens, int B, int T,
-               hipStream_t s);
+               hipStream_t s, bool relu = false);
+void launch_tds_depthwise(const float* x, int C, int T, const float* w, const float* bias, const int* lens, float* y,
+                          int B, hipStream_t s);
 void launch_glow_durations(const float* logw, int T, const int* lens, float length_scale, float* cum, int* ylen,
                            float* wceil, int B, hipStream_t s);
 void launch_glow_expand(const float* o_mean, int C, int Tx, const int* xlens, const float* cum, const int* ylens,
@@ -314,6 +316,13 @@ struct GlowModel {
   DevBuf emb;                                   // scaled by sqrt(H)
   std::vector<ConvLayer> enc_conv;              // H -> 2H, k5
   std::vector<DevBuf> enc_g, enc_b;             // LayerNorm(2H)
+  // time-depth-separable encoder (configs/glow_tts_tdsep.json): ConvLayerNorm prenet, then per
+  // layer time_conv (H -> 2H, BN folded, rows interleaved for the GLU epilogue), depthwise k5 (BN
+  // folded) + swish, time_conv2 (BN folded) + residual
+  bool tdsep = false;
+  std::vector<ConvLayer> pre_conv, tds_tc, tds_tc2;
+  std::vector<DevBuf> pre_g, pre_b, tds_dw, tds_dwb;
+  ConvLayer pre_proj;
   ConvLayer proj_m, dp1, dp2, dp_proj;
   DevBuf dp_g1, dp_b1, dp_g2, dp_b2;
   // per flow block (index = block): start (C -> H), WN in (H -> 2H, k5, rows interleaved), res+skip
@@ -1803,12 +1812,67 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
     G.emb.upload(e);
   }
   G.enc_conv.clear();
-  G.enc_conv.resize(enc_layers);
   G.enc_g.clear();
-  G.enc_g.resize(enc_layers);
   G.enc_b.clear();
-  G.enc_b.resize(enc_layers);
-  for (int i = 0; i < enc_layers; ++i) {
+  G.tdsep = h.count("encoder.encoder.layers.0.time_conv.weight") > 0;
+  if (G.tdsep) {
+    G.pre_conv.clear();
+    G.pre_conv.resize(3);
+    G.pre_g.clear();
+    G.pre_g.resize(3);
+    G.pre_b.clear();
+    G.pre_b.resize(3);
+    for (int i = 0; i < 3; ++i) {
+      const std::string q = "encoder.pre.";
+      pack_conv(G.pre_conv[i], need(h, q + "conv_layers." + std::to_string(i) + ".weight", {H, H, 5}).d,
+                need(h, q + "conv_layers." + std::to_string(i) + ".bias", {H}).d, H, H, 5, 1, 1, p2);
+      G.pre_g[i].upload(need(h, q + "norm_layers." + std::to_string(i) + ".gamma", {1, H, 1}).d);
+      G.pre_b[i].upload(need(h, q + "norm_layers." + std::to_string(i) + ".beta", {1, H, 1}).d);
+    }
+    pack_conv(G.pre_proj, need(h, "encoder.pre.proj.weight", {H, H, 1}).d, need(h, "encoder.pre.proj.bias", {H}).d, H,
+              H, 1, 1, 1, p0);
+    // eval BatchNorm: y = (x - mean) * w / sqrt(var + 1e-5) + b, folded in double
+    auto bn_fold = [&](const std::string& name, int n, std::vector<float>& W, std::vector<float>& bias, int rowlen) {
+      const auto& w = need(h, name + ".weight", {n}).d;
+      const auto& bb = need(h, name + ".bias", {n}).d;
+      const auto& mu = need(h, name + ".running_mean", {n}).d;
+      const auto& var = need(h, name + ".running_var", {n}).d;
+      for (int r = 0; r < n; ++r) {
+        const double sc = (double)w[r] / std::sqrt((double)var[r] + 1e-5);
+        for (int k = 0; k < rowlen; ++k) W[(size_t)r * rowlen + k] = (float)(W[(size_t)r * rowlen + k] * sc);
+        bias[r] = (float)(((double)bias[r] - mu[r]) * sc + bb[r]);
+      }
+    };
+    G.tds_tc.clear();
+    G.tds_tc.resize(enc_layers);
+    G.tds_tc2.clear();
+    G.tds_tc2.resize(enc_layers);
+    G.tds_dw.clear();
+    G.tds_dw.resize(enc_layers);
+    G.tds_dwb.clear();
+    G.tds_dwb.resize(enc_layers);
+    for (int i = 0; i < enc_layers; ++i) {
+      const std::string q = "encoder.encoder.layers." + std::to_string(i) + ".";
+      auto w1 = need(h, q + "time_conv.weight", {2 * H, H, 1}).d;
+      auto b1 = need(h, q + "time_conv.bias", {2 * H}).d;
+      bn_fold(q + "norm1", 2 * H, w1, b1, H);
+      auto [w1i, b1i] = interleave_halves(w1, b1, H, H);  // (a_c, g_c) pairs for the GLU epilogue
+      pack_conv(G.tds_tc[i], w1i, b1i, H, 2 * H, 1, 1, 1, p0);
+      auto wd = need(h, q + "depth_conv.weight", {H, 1, 5}).d;
+      auto bd = need(h, q + "depth_conv.bias", {H}).d;
+      bn_fold(q + "norm2", H, wd, bd, 5);
+      G.tds_dw[i].upload(wd);
+      G.tds_dwb[i].upload(bd);
+      auto w2 = need(h, q + "time_conv2.weight", {H, H, 1}).d;
+      auto b2 = need(h, q + "time_conv2.bias", {H}).d;
+      bn_fold(q + "norm3", H, w2, b2, H);
+      pack_conv(G.tds_tc2[i], w2, b2, H, H, 1, 1, 1, p0);
+    }
+  }
+  G.enc_conv.resize(G.tdsep ? 0 : enc_layers);
+  G.enc_g.resize(G.tdsep ? 0 : enc_layers);
+  G.enc_b.resize(G.tdsep ? 0 : enc_layers);
+  for (int i = 0; i < (G.tdsep ? 0 : enc_layers); ++i) {
     const std::string pf = "encoder.encoder.";
     pack_conv(G.enc_conv[i], need(h, pf + "conv_layers." + std::to_string(i) + ".weight", {2 * H, H, 5}).d,
               need(h, pf + "conv_layers." + std::to_string(i) + ".bias", {2 * H}).d, H, 2 * H, 5, 1, 1, p2);
@@ -1921,7 +1985,8 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
   float* x = W.xa.f();   // (B, H, T) current activations
   float* x2 = W.xb.f();  // ping-pong
   launch_glow_embed(d_ids, T, G.emb.f(), G.num_chars, H, dl, x, B, s);
-  auto conv = [&](const ConvLayer& L, const float* in, int cin, float* out, int cout, int epi) {
+  auto conv = [&](const ConvLayer& L, const float* in, int cin, float* out, int cout, int epi,
+                  const float* resid = nullptr) {
     ConvCall cc;
     cc.lens = dl;
     cc.B = B;
@@ -1932,9 +1997,33 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
     cc.oc = T;
     cc.ot = 1;
     cc.epi = epi;
+    cc.resid = resid;
+    cc.rb = (long)cout * T;
+    cc.rc = T;
+    cc.rt = 1;
     run_conv(L, cc, s);
   };
-  for (int i = 0; i < G.enc_layers; ++i) {  // GatedConvBlock (gated_conv.py:31-42)
+  if (G.tdsep) {
+    // ConvLayerNorm prenet (glow.py:43-50): 3 x (conv k5 -> LayerNorm -> ReLU), x + proj(.)
+    float* h0 = W.h2.f();
+    float* h1 = W.hdp.f();
+    conv(G.pre_conv[0], x, H, h0, H, 0);
+    launch_ln(h0, (long)H * T, H, G.pre_g[0].f(), G.pre_b[0].f(), dl, B, T, s, true);
+    conv(G.pre_conv[1], h0, H, h1, H, 0);
+    launch_ln(h1, (long)H * T, H, G.pre_g[1].f(), G.pre_b[1].f(), dl, B, T, s, true);
+    conv(G.pre_conv[2], h1, H, h0, H, 0);
+    launch_ln(h0, (long)H * T, H, G.pre_g[2].f(), G.pre_b[2].f(), dl, B, T, s, true);
+    conv(G.pre_proj, h0, H, x2, H, 0, x);
+    std::swap(x, x2);
+    // TimeDepthSeparableConvBlock (time_depth_sep_conv.py:51-63, 93-96)
+    for (int i = 0; i < G.enc_layers; ++i) {
+      conv(G.tds_tc[i], x, H, h0, H, 6);  // time_conv + BN + GLU -> H rows
+      launch_tds_depthwise(h0, H, T, G.tds_dw[i].f(), G.tds_dwb[i].f(), dl, h1, B, s);
+      conv(G.tds_tc2[i], h1, H, x2, H, 0, x);  // time_conv2 + BN + residual
+      std::swap(x, x2);
+    }
+  }
+  for (int i = 0; i < (G.tdsep ? 0 : G.enc_layers); ++i) {  // GatedConvBlock (gated_conv.py:31-42)
     conv(G.enc_conv[i], x, H, W.h2.f(), 2 * H, 0);
     launch_glu_ln_res(W.h2.f(), (long)2 * H * T, 2 * H, G.enc_g[i].f(), G.enc_b[i].f(), x, (long)H * T, x2,
                       (long)H * T, dl, B, T, s);

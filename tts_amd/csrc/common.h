@@ -67,7 +67,7 @@ struct ConvArgs {
   int oc, ot;
   int out_mul;        // t_out = q*out_mul + phase
   int epi_act;        // 0 none, 1 relu, 2 tanh, 3 gate pair, 4 coupling pair, 5 coupling +
-                      // inverse InvConvNear / ActNorm (see conv.hip)
+                      // inverse InvConvNear / ActNorm, 6 GLU pair (see conv.hip)
   const float* resid; // optional residual added after activation
   long rb;
   int rc, rt;

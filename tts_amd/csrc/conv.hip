@@ -257,6 +257,7 @@ __global__ __launch_bounds__(256) void conv_mfma_kernel(ConvArgs a) {
           const float u = acc[mi][ni][j] + bias4[j], g = acc[mi][ni][j + 1] + bias4[j + 1];
           float v;
           if (a.epi_act == 3) v = tanhf(u) / (1.f + expf(-g));
+          else if (a.epi_act == 6) v = u / (1.f + expf(-g));  // GLU
           else v = (a.resid[(long)b * a.rb + (long)c * a.rc + (long)t * a.rt] - u) * expf(-g);
           a.out[(long)b * a.ob + (long)c * a.oc + (long)t * a.ot] = v;
         }

@@ -14,7 +14,7 @@
 //   GLU:  GatedConvBlock (gated_conv.py:31-42): out = res + a * sigmoid(g), [a | g] = LN(x), wave w
 //         holds a-channels [w*NPT/2, (w+1)*NPT/2) and the matching g-channels (C2 = 4 * NPT)
 //   !GLU: in-place LN (DurationPredictor norm_1 / norm_2 after the conv's ReLU), C = 4 * NPT
-template <int NPT, bool GLU>
+template <int NPT, bool GLU, bool RELU = false>
 __global__ __launch_bounds__(256) void ln_chan_kernel(const float* x, long xb, const float* __restrict__ gamma,
                                                       const float* __restrict__ beta, const float* res, long rb,
                                                       float* out, long ob, const int* lens, int T) {
@@ -58,7 +58,8 @@ __global__ __launch_bounds__(256) void ln_chan_kernel(const float* x, long xb, c
 #pragma unroll
     for (int i = 0; i < NPT; ++i) {
       const int c = chan(i);
-      out[b * ob + (long)c * T + t] = (v[i] - mean) * rs * gamma[c] + beta[c];
+      const float y = (v[i] - mean) * rs * gamma[c] + beta[c];
+      out[b * ob + (long)c * T + t] = RELU ? fmaxf(y, 0.f) : y;
     }
   }
 }
@@ -165,9 +166,39 @@ void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, cons
   HIP_OK(hipGetLastError());
 }
 void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, const int* lens, int B, int T,
-               hipStream_t s) {
-  TTS_CHECK(C == 256, "glow duration-predictor LayerNorm: filter channels must be 256");
-  ln_chan_kernel<64, false><<<dim3((T + 63) / 64, B), 256, 0, s>>>(x, xb, gamma, beta, nullptr, 0, x, xb, lens, T);
+               hipStream_t s, bool relu) {
+  const dim3 grid((T + 63) / 64, B);
+  if (C == 256 && !relu) ln_chan_kernel<64, false><<<grid, 256, 0, s>>>(x, xb, gamma, beta, nullptr, 0, x, xb, lens, T);
+  else if (C == 192 && relu)
+    ln_chan_kernel<48, false, true><<<grid, 256, 0, s>>>(x, xb, gamma, beta, nullptr, 0, x, xb, lens, T);
+  else TTS_CHECK(false, "glow LayerNorm: unsupported channel count");
+  HIP_OK(hipGetLastError());
+}
+
+// TimeDepthSeparableConv middle (time_depth_sep_conv.py:51-58): depthwise k5 conv (zero padding at
+// the utterance's own length, as a B = 1 call sees it) with BatchNorm folded into w / bias, then
+// x * sigmoid(x). 64 positions x 4 channel groups per workgroup.
+__global__ __launch_bounds__(256) void tds_depthwise_kernel(const float* __restrict__ x, int C, int T,
+                                                            const float* __restrict__ w,
+                                                            const float* __restrict__ bias, const int* lens,
+                                                            float* __restrict__ y) {
+  const int b = blockIdx.y, t = blockIdx.x * 64 + (threadIdx.x & 63);
+  const int L = lens[b];
+  if (t >= T || t >= L) return;
+  for (int c = threadIdx.x >> 6; c < C; c += 4) {
+    const float* xp = x + ((long)b * C + c) * T;
+    float acc = bias[c];
+#pragma unroll
+    for (int k = 0; k < 5; ++k) {
+      const int u = t + k - 2;
+      if (u >= 0 && u < L) acc = fmaf(w[c * 5 + k], xp[u], acc);
+    }
+    y[((long)b * C + c) * T + t] = acc / (1.f + expf(-acc));
+  }
+}
+void launch_tds_depthwise(const float* x, int C, int T, const float* w, const float* bias, const int* lens, float* y,
+                          int B, hipStream_t s) {
+  tds_depthwise_kernel<<<dim3((T + 63) / 64, B), 256, 0, s>>>(x, C, T, w, bias, lens, y);
   HIP_OK(hipGetLastError());
 }
 void launch_glow_durations(const float* logw, int T, const int* lens, float length_scale, float* cum, int* ylen,

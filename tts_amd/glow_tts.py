@@ -1,7 +1,8 @@
 """Drop-in ``GlowTts`` whose ``inference`` runs on MI355X through ``libttship.so``.
 
 Mirrors ``TTS/tts/models/glow_tts.py`` as ``setup_model`` builds it for the reference configs
-(``TTS/tts/utils/generic_utils.py:105-129``: gated-conv encoder of 3 + 6 layers, hidden 192,
+(``TTS/tts/utils/generic_utils.py:105-129``: gated-conv or time-depth-separable (with the
+ConvLayerNorm prenet) encoder of 3 + 6 layers, hidden 192,
 duration predictor 256, 12 flow blocks x 4 WN layers, kernel 5, dilation 1, num_sqz 2,
 num_splits 4, mean_only): the constructor signature, the checkpoint keys (``encoder.*``,
 ``decoder.flows.*``), the ``noise_scale`` / ``length_scale`` attributes and
@@ -32,8 +33,10 @@ class GlowTts(nn.Module):
                  use_encoder_prenet=False, encoder_type="gatedconv"):
         super().__init__()
         bad = []
-        if encoder_type.lower() != "gatedconv":
+        if encoder_type.lower() not in ("gatedconv", "time-depth-separable"):
             bad.append(f"encoder_type={encoder_type}")
+        if encoder_type.lower() == "time-depth-separable" and not use_encoder_prenet:
+            bad.append("time-depth-separable encoder without the prenet")
         if hidden_channels != 192 or (hidden_channels_enc or 192) != 192 or (hidden_channels_dec or 192) != 192:
             bad.append("hidden channels != 192")
         if filter_channels_dp != 256 or out_channels != 80 or kernel_size != 3 or kernel_size_dec != 5:
@@ -46,7 +49,8 @@ class GlowTts(nn.Module):
             raise NotImplementedError("tts_amd GlowTts implements the reference configs only: " + ", ".join(bad))
         self.num_chars = num_chars
         self.cfg = GlowConfig(num_chars=num_chars, num_layers_enc=num_layers_enc,
-                              num_flow_blocks_dec=num_flow_blocks_dec, num_block_layers=num_block_layers)
+                              num_flow_blocks_dec=num_flow_blocks_dec, num_block_layers=num_block_layers,
+                              encoder_type=encoder_type.lower())
         self.noise_scale = 0.66
         self.length_scale = 1.
         populate(self, glow_spec(self.cfg))

@@ -281,6 +281,7 @@ class GlowConfig:
     filter_channels_dp: int = 256
     out_channels: int = 80
     num_layers_enc: int = 6
+    encoder_type: str = "gatedconv"  # or "time-depth-separable" (configs/glow_tts_tdsep.json)
     num_flow_blocks_dec: int = 12
     num_block_layers: int = 4
     kernel_size_dec: int = 5
@@ -292,11 +293,34 @@ def glow_spec(c: GlowConfig) -> Spec:
     ``decoder.flows.*`` from ``layers/glow_tts/decoder.py:60-79`` + ``glow.py`` + ``normalization.py``."""
     H, F, C = c.hidden_channels, c.filter_channels_dp, c.out_channels
     s: Spec = [("encoder.emb.weight", (c.num_chars, H), "glow_emb")]
-    for i in range(3 + c.num_layers_enc):
-        s += [(f"encoder.encoder.conv_layers.{i}.weight", (2 * H, H, 5), "conv"),
-              (f"encoder.encoder.conv_layers.{i}.bias", (2 * H,), "bias"),
-              (f"encoder.encoder.norm_layers.{i}.gamma", (1, 2 * H, 1), "ln_g"),
-              (f"encoder.encoder.norm_layers.{i}.beta", (1, 2 * H, 1), "bias")]
+    if c.encoder_type == "time-depth-separable":
+        # ConvLayerNorm prenet (glow.py:8-50) + TimeDepthSeparableConvBlock (time_depth_sep_conv.py)
+        for i in range(3):
+            s += [(f"encoder.pre.conv_layers.{i}.weight", (H, H, 5), "conv"),
+                  (f"encoder.pre.conv_layers.{i}.bias", (H,), "bias")]
+        for i in range(3):
+            s += [(f"encoder.pre.norm_layers.{i}.gamma", (1, H, 1), "ln_g"),
+                  (f"encoder.pre.norm_layers.{i}.beta", (1, H, 1), "bias")]
+        s += [("encoder.pre.proj.weight", (H, H, 1), "conv"), ("encoder.pre.proj.bias", (H,), "bias")]
+
+        def bn(name, n):
+            return [(f"{name}.weight", (n,), "bn_w"), (f"{name}.bias", (n,), "bn_b"),
+                    (f"{name}.running_mean", (n,), "bn_mean"), (f"{name}.running_var", (n,), "bn_var"),
+                    (f"{name}.num_batches_tracked", (), "count")]
+        for i in range(3 + c.num_layers_enc):
+            q = f"encoder.encoder.layers.{i}"
+            s += [(f"{q}.time_conv.weight", (2 * H, H, 1), "conv"), (f"{q}.time_conv.bias", (2 * H,), "bias")]
+            s += bn(f"{q}.norm1", 2 * H)
+            s += [(f"{q}.depth_conv.weight", (H, 1, 5), "dwconv"), (f"{q}.depth_conv.bias", (H,), "bias")]
+            s += bn(f"{q}.norm2", H)
+            s += [(f"{q}.time_conv2.weight", (H, H, 1), "conv"), (f"{q}.time_conv2.bias", (H,), "bias")]
+            s += bn(f"{q}.norm3", H)
+    else:
+        for i in range(3 + c.num_layers_enc):
+            s += [(f"encoder.encoder.conv_layers.{i}.weight", (2 * H, H, 5), "conv"),
+                  (f"encoder.encoder.conv_layers.{i}.bias", (2 * H,), "bias"),
+                  (f"encoder.encoder.norm_layers.{i}.gamma", (1, 2 * H, 1), "ln_g"),
+                  (f"encoder.encoder.norm_layers.{i}.beta", (1, 2 * H, 1), "bias")]
     dp = "encoder.duration_predictor"
     s += [("encoder.proj_m.weight", (C, H, 1), "conv"), ("encoder.proj_m.bias", (C,), "bias"),
           (f"{dp}.conv_1.weight", (F, H, 3), "conv"), (f"{dp}.conv_1.bias", (F,), "bias"),

@@ -75,6 +75,8 @@ def synth_tensor(name: str, shape: Tuple[int, ...], kind: str, seed: int,
         x = u * math.sqrt(3.0) * math.sqrt(2.0 / (fi + fo))
     elif kind == "glow_emb":  # normal_(0, hidden ** -0.5) (glow_tts/encoder.py:61): same std
         x = u * math.sqrt(3.0) * shape[1] ** -0.5
+    elif kind == "dwconv":  # depthwise conv (groups = channels): fan_in = taps, kaiming-uniform scale
+        x = u * math.sqrt(1.0 / shape[-1])
     elif kind == "ln_g":
         x = 1.0 + 0.1 * u
     elif kind == "actnorm":
