@@ -7,7 +7,8 @@ Parity pin: ``tests/golden/glow.npz`` was produced in the build container by the
 the inference glue of ``TTS/tts/models/glow_tts.py:166-193`` (that module itself does not import
 here: its ``monotonic_align.core`` Cython extension is not built), see make_golden.py ``glow``.
 
-* ``layers/glow_tts/encoder.py:105-130``  embedding * sqrt(H), GatedConvBlock, proj_m, durations
+* ``layers/glow_tts/encoder.py:105-130``  embedding * sqrt(H), GatedConvBlock / ConvLayerNorm prenet +
+  TimeDepthSeparableConvBlock / Transformer (``transformer.py:9-127,228-319``), proj_m, durations
 * ``layers/glow_tts/gated_conv.py:31-42``  conv -> LayerNorm -> GLU -> residual
 * ``layers/glow_tts/normalization.py:4-27,77-89``  LayerNorm (eps 1e-4), ActNorm reverse
 * ``layers/glow_tts/duration_predictor.py:29-40``
@@ -64,12 +65,7 @@ class GlowOracle:
         TimeDepthSeparableConvBlock (time_depth_sep_conv.py:51-63,93-96); B = 1, so masks are 1."""
         sd = self.sd
         H = x.shape[0]
-        h = x
-        for i in range(3):
-            p = "encoder.pre."
-            h = conv1d(h, sd[p + f"conv_layers.{i}.weight"], sd[p + f"conv_layers.{i}.bias"], 2)
-            h = np.maximum(layer_norm(h, sd[p + f"norm_layers.{i}.gamma"], sd[p + f"norm_layers.{i}.beta"]), F32(0))
-        x = (x + conv1d(h, sd["encoder.pre.proj.weight"], sd["encoder.pre.proj.bias"])).astype(F32)
+        x = self._prenet(x)
         for i in range(self.enc_layers):
             q = f"encoder.encoder.layers.{i}."
             h = self._bn(conv1d(x, sd[q + "time_conv.weight"], sd[q + "time_conv.bias"]), q + "norm1")
@@ -84,12 +80,53 @@ class GlowOracle:
             x = (x + o).astype(F32)
         return x
 
+    def _prenet(self, x):
+        """ConvLayerNorm (glow.py:43-50): 3 x (conv k5 -> LayerNorm -> ReLU), x + proj(.)."""
+        sd = self.sd
+        h = x
+        for i in range(3):
+            p = "encoder.pre."
+            h = conv1d(h, sd[p + f"conv_layers.{i}.weight"], sd[p + f"conv_layers.{i}.bias"], 2)
+            h = np.maximum(layer_norm(h, sd[p + f"norm_layers.{i}.gamma"], sd[p + f"norm_layers.{i}.beta"]), F32(0))
+        return (x + conv1d(h, sd["encoder.pre.proj.weight"], sd["encoder.pre.proj.bias"])).astype(F32)
+
+    def _transformer(self, x, heads=2):
+        """Transformer.forward (transformer.py:307-319) without relative-position tables: B = 1, so
+        the attention mask is all ones."""
+        sd = self.sd
+        H, T = x.shape
+        dk = H // heads
+        L = len([k for k in sd if k.endswith(".conv_q.weight")])
+        for i in range(L):
+            a = f"encoder.encoder.attn_layers.{i}."
+            q = conv1d(x, sd[a + "conv_q.weight"], sd[a + "conv_q.bias"])
+            k = conv1d(x, sd[a + "conv_k.weight"], sd[a + "conv_k.bias"])
+            v = conv1d(x, sd[a + "conv_v.weight"], sd[a + "conv_v.bias"])
+            o = np.zeros_like(x)
+            for hh in range(heads):
+                sl = slice(hh * dk, (hh + 1) * dk)
+                sc = (q[sl].T @ k[sl] / F32(np.sqrt(dk))).astype(F32)          # (T_t, T_s)
+                sc = np.exp(sc - sc.max(1, keepdims=True))
+                p = (sc / sc.sum(1, keepdims=True)).astype(F32)
+                o[sl] = (v[sl] @ p.T).astype(F32)
+            y = conv1d(o, sd[a + "conv_o.weight"], sd[a + "conv_o.bias"])
+            x = layer_norm((x + y).astype(F32), sd[f"encoder.encoder.norm_layers_1.{i}.gamma"],
+                           sd[f"encoder.encoder.norm_layers_1.{i}.beta"])
+            f = f"encoder.encoder.ffn_layers.{i}."
+            h = np.maximum(conv1d(x, sd[f + "conv_1.weight"], sd[f + "conv_1.bias"], 1), F32(0))
+            y = conv1d(h, sd[f + "conv_2.weight"], sd[f + "conv_2.bias"], 1)
+            x = layer_norm((x + y).astype(F32), sd[f"encoder.encoder.norm_layers_2.{i}.gamma"],
+                           sd[f"encoder.encoder.norm_layers_2.{i}.beta"])
+        return x
+
     def encode(self, ids):
         sd = self.sd
         H = sd["encoder.emb.weight"].shape[1]
         x = (sd["encoder.emb.weight"][ids] * F32(np.sqrt(H))).T.astype(F32)        # (H, T)
         if self.encoder_type == "time-depth-separable":
             x = self._tdsep(x)
+        elif self.encoder_type == "transformer":
+            x = self._transformer(self._prenet(x))
         for i in range(self.enc_layers if self.encoder_type == "gatedconv" else 0):
             p = f"encoder.encoder."
             o = conv1d(x, sd[p + f"conv_layers.{i}.weight"], sd[p + f"conv_layers.{i}.bias"], 2)

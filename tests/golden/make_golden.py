@@ -391,6 +391,8 @@ if __name__ == "__main__":
         glow_case("glow")
     if "glow_tdsep" in which:
         glow_case("glow_tdsep", "time-depth-separable", seed=27, data_seed=28)
+    if "glow_tfm" in which:
+        glow_case("glow_tfm", "transformer", seed=33, data_seed=30)  # seed 29: all durations 0
     if "taco_softmax" in which:
         taco_case("taco_softmax", TacotronConfig(attn_norm="softmax"), seed=2,
                   utt_lens=[25, 9], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=8)

@@ -473,7 +473,8 @@ def test_ge2e_speaker_encoder_matches_reference(tag, proj):
 
 
 # --------------------------------------------------------------------------------- Glow-TTS
-@pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable")])
+@pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable"),
+                                      ("glow_tfm", "transformer")])
 def test_glow_tts_matches_reference(name, enc):
     """GlowTts.inference (glow_tts.py:166-193; gated-conv or time-depth-separable encoder, 12 reverse
     flow blocks) with the fixture's prior noise, both utterances in ONE batched call: durations /

@@ -184,7 +184,8 @@ def test_glow_tts_constructor_and_keys():
     assert tuple(sd["encoder.proj_m.weight"].shape) == (80, 192, 1)
     assert tuple(sd["decoder.flows.1.weight"].shape) == (4, 4)
     assert m.noise_scale == 0.66 and m.length_scale == 1.
-    for kw in (dict(encoder_type="transformer"), dict(num_speakers=4, c_in_channels=256), dict(mean_only=False)):
+    for kw in (dict(encoder_type="transformer", rel_attn_window_size=4, use_encoder_prenet=True),
+               dict(encoder_type="transformer"), dict(num_speakers=4, c_in_channels=256), dict(mean_only=False)):
         with pytest.raises(NotImplementedError):
             GlowTts(num_chars=130, **kw)
     with pytest.raises(RuntimeError, match="no CPU fallback"):

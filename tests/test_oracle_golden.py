@@ -145,7 +145,8 @@ def test_tacotron2_oracle_decoder_variants_match_reference(name):
         assert np.abs(align - fx[k + "_align"]).max() <= (1e-5 if cfg.forward_attn else 1e-6)
 
 
-@pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable")])
+@pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable"),
+                                      ("glow_tfm", "transformer")])
 def test_glow_oracle_matches_reference(name, enc):
     """Glow-TTS, both encoders the reference configs use (gated conv; time-depth-separable with the
     ConvLayerNorm prenet): the reference's Encoder / Decoder modules under the inference glue of
@@ -154,7 +155,8 @@ def test_glow_oracle_matches_reference(name, enc):
     from tts_amd.spec import GlowConfig, glow_spec
     from tts_amd.weights import synth_state_dict
     fx = load_fixture(name)
-    orc = GlowOracle(synth_state_dict(glow_spec(GlowConfig(encoder_type=enc)), int(fx["seed"])), encoder_type=enc)
+    orc = GlowOracle(synth_state_dict(glow_spec(GlowConfig(encoder_type=enc)), int(fx["seed"])), encoder_type=enc,
+                     enc_layers=6 if enc == "transformer" else 9)
     for u in range(2):
         k = f"u{u}"
         y, ym, attn, logw, Ty = orc.inference(fx[k + "_ids"], fx[k + "_noise"], float(fx["noise_scale"]))

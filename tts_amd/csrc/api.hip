@@ -23,6 +23,7 @@ void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, cons
                        long rb, float* out, long ob, const int* lens, int B, int T, hipStream_t s);
 void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, const int* lens, int B, int T,
                hipStream_t s, bool relu = false);
+void launch_glow_mha(const float* qkv, int H, int heads, int T, const int* lens, float* out, int B, hipStream_t s);
 void launch_tds_depthwise(const float* x, int C, int T, const float* w, const float* bias, const int* lens, float* y,
                           int B, hipStream_t s);
 void launch_glow_durations(const float* logw, int T, const int* lens, float length_scale, float* cum, int* ylen,
@@ -319,7 +320,10 @@ struct GlowModel {
   // time-depth-separable encoder (configs/glow_tts_tdsep.json): ConvLayerNorm prenet, then per
   // layer time_conv (H -> 2H, BN folded, rows interleaved for the GLU epilogue), depthwise k5 (BN
   // folded) + swish, time_conv2 (BN folded) + residual
-  bool tdsep = false;
+  bool tdsep = false, tfm = false;
+  // transformer encoder: per layer q|k|v as one 1x1 conv (H -> 3H), o (1x1), FFN k3 (H -> 768 -> H)
+  std::vector<ConvLayer> tfm_qkv, tfm_o, tfm_f1, tfm_f2;
+  std::vector<DevBuf> tfm_g1, tfm_b1, tfm_g2, tfm_b2;
   std::vector<ConvLayer> pre_conv, tds_tc, tds_tc2;
   std::vector<DevBuf> pre_g, pre_b, tds_dw, tds_dwb;
   ConvLayer pre_proj;
@@ -335,7 +339,7 @@ struct GlowModel {
 
 struct GlowWS {
   int B = 0, Tx = 0, Ty = 0;
-  DevBuf ids, lens, klens, ylens, xa, xb, h2, hdp, logw, cum, wceil, om, z, sq, sq2, whs, wacts;
+  DevBuf ids, lens, klens, ylens, xa, xb, h2, hdp, logw, cum, wceil, om, z, sq, sq2, whs, wacts, big;
   std::vector<int> h_ylens, h_klens;
 };
 
@@ -1815,7 +1819,8 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
   G.enc_g.clear();
   G.enc_b.clear();
   G.tdsep = h.count("encoder.encoder.layers.0.time_conv.weight") > 0;
-  if (G.tdsep) {
+  G.tfm = h.count("encoder.encoder.attn_layers.0.conv_q.weight") > 0;
+  if (G.tdsep || G.tfm) {
     G.pre_conv.clear();
     G.pre_conv.resize(3);
     G.pre_g.clear();
@@ -1831,6 +1836,43 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
     }
     pack_conv(G.pre_proj, need(h, "encoder.pre.proj.weight", {H, H, 1}).d, need(h, "encoder.pre.proj.bias", {H}).d, H,
               H, 1, 1, 1, p0);
+  }
+  if (G.tfm) {  // transformer.py:265-319, num_layers = enc_layers
+    for (auto* v : {&G.tfm_qkv, &G.tfm_o, &G.tfm_f1, &G.tfm_f2}) {
+      v->clear();
+      v->resize(enc_layers);
+    }
+    for (auto* v : {&G.tfm_g1, &G.tfm_b1, &G.tfm_g2, &G.tfm_b2}) {
+      v->clear();
+      v->resize(enc_layers);
+    }
+    const int Fc = 768;
+    for (int i = 0; i < enc_layers; ++i) {
+      const std::string a = "encoder.encoder.attn_layers." + std::to_string(i) + ".";
+      std::vector<float> wqkv, bqkv;
+      for (const char* n : {"q", "k", "v"}) {
+        const auto& w = need(h, a + "conv_" + n + ".weight", {H, H, 1}).d;
+        const auto& bb = need(h, a + "conv_" + n + ".bias", {H}).d;
+        wqkv.insert(wqkv.end(), w.begin(), w.end());
+        bqkv.insert(bqkv.end(), bb.begin(), bb.end());
+      }
+      pack_conv(G.tfm_qkv[i], wqkv, bqkv, H, 3 * H, 1, 1, 1, p0);
+      pack_conv(G.tfm_o[i], need(h, a + "conv_o.weight", {H, H, 1}).d, need(h, a + "conv_o.bias", {H}).d, H, H, 1, 1,
+                1, p0);
+      const std::string f = "encoder.encoder.ffn_layers." + std::to_string(i) + ".";
+      pack_conv(G.tfm_f1[i], need(h, f + "conv_1.weight", {Fc, H, 3}).d, need(h, f + "conv_1.bias", {Fc}).d, H, Fc, 3,
+                1, 1, p1);
+      pack_conv(G.tfm_f2[i], need(h, f + "conv_2.weight", {H, Fc, 3}).d, need(h, f + "conv_2.bias", {H}).d, Fc, H, 3,
+                1, 1, p1);
+      const std::string n1 = "encoder.encoder.norm_layers_1." + std::to_string(i) + ".";
+      const std::string n2 = "encoder.encoder.norm_layers_2." + std::to_string(i) + ".";
+      G.tfm_g1[i].upload(need(h, n1 + "gamma", {1, H, 1}).d);
+      G.tfm_b1[i].upload(need(h, n1 + "beta", {1, H, 1}).d);
+      G.tfm_g2[i].upload(need(h, n2 + "gamma", {1, H, 1}).d);
+      G.tfm_b2[i].upload(need(h, n2 + "beta", {1, H, 1}).d);
+    }
+  }
+  if (G.tdsep) {
     // eval BatchNorm: y = (x - mean) * w / sqrt(var + 1e-5) + b, folded in double
     auto bn_fold = [&](const std::string& name, int n, std::vector<float>& W, std::vector<float>& bias, int rowlen) {
       const auto& w = need(h, name + ".weight", {n}).d;
@@ -1869,10 +1911,11 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
       pack_conv(G.tds_tc2[i], w2, b2, H, H, 1, 1, 1, p0);
     }
   }
-  G.enc_conv.resize(G.tdsep ? 0 : enc_layers);
-  G.enc_g.resize(G.tdsep ? 0 : enc_layers);
-  G.enc_b.resize(G.tdsep ? 0 : enc_layers);
-  for (int i = 0; i < (G.tdsep ? 0 : enc_layers); ++i) {
+  const bool gated = !G.tdsep && !G.tfm;
+  G.enc_conv.resize(gated ? enc_layers : 0);
+  G.enc_g.resize(gated ? enc_layers : 0);
+  G.enc_b.resize(gated ? enc_layers : 0);
+  for (int i = 0; i < (gated ? enc_layers : 0); ++i) {
     const std::string pf = "encoder.encoder.";
     pack_conv(G.enc_conv[i], need(h, pf + "conv_layers." + std::to_string(i) + ".weight", {2 * H, H, 5}).d,
               need(h, pf + "conv_layers." + std::to_string(i) + ".bias", {2 * H}).d, H, 2 * H, 5, 1, 1, p2);
@@ -1977,6 +2020,7 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
   grow<float>(W.cum, (size_t)B * T, gen);
   grow<float>(W.wceil, (size_t)B * T, gen);
   grow<float>(W.om, (size_t)B * C * T, gen);
+  if (G.tfm) grow<float>(W.big, (size_t)B * 768 * T, gen);
   W.B = B;
   W.Tx = T;
   std::vector<int> lens(h_lens, h_lens + B);
@@ -2003,7 +2047,7 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
     cc.rt = 1;
     run_conv(L, cc, s);
   };
-  if (G.tdsep) {
+  if (G.tdsep || G.tfm) {
     // ConvLayerNorm prenet (glow.py:43-50): 3 x (conv k5 -> LayerNorm -> ReLU), x + proj(.)
     float* h0 = W.h2.f();
     float* h1 = W.hdp.f();
@@ -2015,15 +2059,26 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
     launch_ln(h0, (long)H * T, H, G.pre_g[2].f(), G.pre_b[2].f(), dl, B, T, s, true);
     conv(G.pre_proj, h0, H, x2, H, 0, x);
     std::swap(x, x2);
+    // Transformer (transformer.py:307-319): x = LN1(x + o(attn(x))), x = LN2(x + FFN(x))
+    for (int i = 0; i < (G.tfm ? G.enc_layers : 0); ++i) {
+      float* big = W.big.f();
+      conv(G.tfm_qkv[i], x, H, big, 3 * H, 0);
+      launch_glow_mha(big, H, H / 96, T, dl, h0, B, s);
+      conv(G.tfm_o[i], h0, H, x2, H, 0, x);
+      launch_ln(x2, (long)H * T, H, G.tfm_g1[i].f(), G.tfm_b1[i].f(), dl, B, T, s);
+      conv(G.tfm_f1[i], x2, H, big, 768, 1);
+      conv(G.tfm_f2[i], big, 768, x, H, 0, x2);
+      launch_ln(x, (long)H * T, H, G.tfm_g2[i].f(), G.tfm_b2[i].f(), dl, B, T, s);
+    }
     // TimeDepthSeparableConvBlock (time_depth_sep_conv.py:51-63, 93-96)
-    for (int i = 0; i < G.enc_layers; ++i) {
+    for (int i = 0; i < (G.tdsep ? G.enc_layers : 0); ++i) {
       conv(G.tds_tc[i], x, H, h0, H, 6);  // time_conv + BN + GLU -> H rows
       launch_tds_depthwise(h0, H, T, G.tds_dw[i].f(), G.tds_dwb[i].f(), dl, h1, B, s);
       conv(G.tds_tc2[i], h1, H, x2, H, 0, x);  // time_conv2 + BN + residual
       std::swap(x, x2);
     }
   }
-  for (int i = 0; i < (G.tdsep ? 0 : G.enc_layers); ++i) {  // GatedConvBlock (gated_conv.py:31-42)
+  for (int i = 0; i < (G.tdsep || G.tfm ? 0 : G.enc_layers); ++i) {  // GatedConvBlock (gated_conv.py:31-42)
     conv(G.enc_conv[i], x, H, W.h2.f(), 2 * H, 0);
     launch_glu_ln_res(W.h2.f(), (long)2 * H * T, 2 * H, G.enc_g[i].f(), G.enc_b[i].f(), x, (long)H * T, x2,
                       (long)H * T, dl, B, T, s);

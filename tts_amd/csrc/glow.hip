@@ -171,6 +171,7 @@ void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, 
   if (C == 256 && !relu) ln_chan_kernel<64, false><<<grid, 256, 0, s>>>(x, xb, gamma, beta, nullptr, 0, x, xb, lens, T);
   else if (C == 192 && relu)
     ln_chan_kernel<48, false, true><<<grid, 256, 0, s>>>(x, xb, gamma, beta, nullptr, 0, x, xb, lens, T);
+  else if (C == 192) ln_chan_kernel<48, false><<<grid, 256, 0, s>>>(x, xb, gamma, beta, nullptr, 0, x, xb, lens, T);
   else TTS_CHECK(false, "glow LayerNorm: unsupported channel count");
   HIP_OK(hipGetLastError());
 }
@@ -234,5 +235,66 @@ __global__ __launch_bounds__(256) void glow_embed_kernel(const int64_t* __restri
 void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
                        int B, hipStream_t s) {
   glow_embed_kernel<<<dim3((T + 63) / 64, B), 256, 0, s>>>(ids, T, table, rows, D, lens, out);
+  HIP_OK(hipGetLastError());
+}
+
+// Self-attention of the Glow-TTS Transformer encoder (transformer.py:73-127; no relative-position
+// tables, no proximal bias, as setup_model builds it): per (utterance, head) softmax(q k^T / sqrt(dk))
+// v over the utterance's own keys (the reference's -1e4 mask makes padded keys exactly 0 after the
+// softmax). One lane per query; keys and values staged through LDS in blocks of 32 and read as
+// broadcasts; online softmax (running max / sum, rescaled accumulator).
+constexpr int MHA_DK = 96, MHA_KB = 32;
+__global__ __launch_bounds__(64) void glow_mha_kernel(const float* __restrict__ qkv, int H, int T, const int* lens,
+                                                      float* __restrict__ out) {
+  __shared__ float Ks[MHA_DK][MHA_KB];
+  __shared__ float Vs[MHA_DK][MHA_KB];
+  const int b = blockIdx.z, head = blockIdx.y, lane = threadIdx.x;
+  const int t = blockIdx.x * 64 + lane;
+  const int L = lens[b];
+  if (blockIdx.x * 64 >= L) return;
+  const float* qb = qkv + ((long)b * 3 * H + head * MHA_DK) * T;
+  const float* kb = qb + (long)H * T;
+  const float* vb = qb + (long)2 * H * T;
+  const bool valid = t < L;
+  float q[MHA_DK], o[MHA_DK];
+  const float inv = 1.f / sqrtf((float)MHA_DK);
+#pragma unroll
+  for (int d = 0; d < MHA_DK; ++d) {
+    q[d] = valid ? qb[(long)d * T + t] : 0.f;
+    o[d] = 0.f;
+  }
+  float m = -INFINITY, l = 0.f;
+  for (int s0 = 0; s0 < L; s0 += MHA_KB) {
+    __syncthreads();
+    for (int e = lane; e < MHA_DK * MHA_KB; e += 64) {
+      const int d = e / MHA_KB, j = e % MHA_KB;
+      const int sidx = min(s0 + j, L - 1);
+      Ks[d][j] = kb[(long)d * T + sidx];
+      Vs[d][j] = vb[(long)d * T + sidx];
+    }
+    __syncthreads();
+    const int nb = min(MHA_KB, L - s0);
+    for (int j = 0; j < nb; ++j) {
+      float sc = 0.f;
+#pragma unroll
+      for (int d = 0; d < MHA_DK; ++d) sc = fmaf(q[d], Ks[d][j], sc);
+      sc *= inv;
+      const float mn = fmaxf(m, sc);
+      const float r = expf(m - mn), p = expf(sc - mn);
+      l = l * r + p;
+#pragma unroll
+      for (int d = 0; d < MHA_DK; ++d) o[d] = fmaf(o[d], r, p * Vs[d][j]);
+      m = mn;
+    }
+  }
+  if (!valid) return;
+  const float il = 1.f / l;
+  float* ob = out + ((long)b * H + head * MHA_DK) * T + t;
+#pragma unroll
+  for (int d = 0; d < MHA_DK; ++d) ob[(long)d * T] = o[d] * il;
+}
+void launch_glow_mha(const float* qkv, int H, int heads, int T, const int* lens, float* out, int B, hipStream_t s) {
+  TTS_CHECK(H == heads * MHA_DK, "glow attention: head size must be 96");
+  glow_mha_kernel<<<dim3((T + 63) / 64, heads, B), 64, 0, s>>>(qkv, H, T, lens, out);
   HIP_OK(hipGetLastError());
 }

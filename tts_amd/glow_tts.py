@@ -1,8 +1,8 @@
 """Drop-in ``GlowTts`` whose ``inference`` runs on MI355X through ``libttship.so``.
 
 Mirrors ``TTS/tts/models/glow_tts.py`` as ``setup_model`` builds it for the reference configs
-(``TTS/tts/utils/generic_utils.py:105-129``: gated-conv or time-depth-separable (with the
-ConvLayerNorm prenet) encoder of 3 + 6 layers, hidden 192,
+(``TTS/tts/utils/generic_utils.py:105-129``: transformer (6 layers, 2 heads) or time-depth-separable
+(both with the ConvLayerNorm prenet) or gated-conv encoder, hidden 192,
 duration predictor 256, 12 flow blocks x 4 WN layers, kernel 5, dilation 1, num_sqz 2,
 num_splits 4, mean_only): the constructor signature, the checkpoint keys (``encoder.*``,
 ``decoder.flows.*``), the ``noise_scale`` / ``length_scale`` attributes and
@@ -33,10 +33,14 @@ class GlowTts(nn.Module):
                  use_encoder_prenet=False, encoder_type="gatedconv"):
         super().__init__()
         bad = []
-        if encoder_type.lower() not in ("gatedconv", "time-depth-separable"):
+        if encoder_type.lower() not in ("gatedconv", "time-depth-separable", "transformer"):
             bad.append(f"encoder_type={encoder_type}")
-        if encoder_type.lower() == "time-depth-separable" and not use_encoder_prenet:
-            bad.append("time-depth-separable encoder without the prenet")
+        if encoder_type.lower() in ("time-depth-separable", "transformer") and not use_encoder_prenet:
+            bad.append(f"{encoder_type} encoder without the prenet")
+        if encoder_type.lower() == "transformer" and (rel_attn_window_size is not None or input_length is not None
+                                                      or num_heads * 96 != hidden_channels or filter_channels != 768
+                                                      or kernel_size != 3):
+            bad.append("transformer options other than setup_model's")
         if hidden_channels != 192 or (hidden_channels_enc or 192) != 192 or (hidden_channels_dec or 192) != 192:
             bad.append("hidden channels != 192")
         if filter_channels_dp != 256 or out_channels != 80 or kernel_size != 3 or kernel_size_dec != 5:
@@ -80,7 +84,8 @@ class GlowTts(nn.Module):
         key = (self._token, self._version)
         if eng.glow_key != key:
             c = self.cfg
-            eng.load_glow(host_tensors(self), c.num_chars, 3 + c.num_layers_enc, c.num_flow_blocks_dec,
+            enc_layers = c.num_layers_enc if c.encoder_type == "transformer" else 3 + c.num_layers_enc
+            eng.load_glow(host_tensors(self), c.num_chars, enc_layers, c.num_flow_blocks_dec,
                           c.num_block_layers)
             eng.glow_key = key
 

@@ -281,7 +281,8 @@ class GlowConfig:
     filter_channels_dp: int = 256
     out_channels: int = 80
     num_layers_enc: int = 6
-    encoder_type: str = "gatedconv"  # or "time-depth-separable" (configs/glow_tts_tdsep.json)
+    filter_channels: int = 768       # transformer FFN width
+    encoder_type: str = "gatedconv"  # "time-depth-separable" (configs/glow_tts_tdsep.json), "transformer"
     num_flow_blocks_dec: int = 12
     num_block_layers: int = 4
     kernel_size_dec: int = 5
@@ -293,8 +294,8 @@ def glow_spec(c: GlowConfig) -> Spec:
     ``decoder.flows.*`` from ``layers/glow_tts/decoder.py:60-79`` + ``glow.py`` + ``normalization.py``."""
     H, F, C = c.hidden_channels, c.filter_channels_dp, c.out_channels
     s: Spec = [("encoder.emb.weight", (c.num_chars, H), "glow_emb")]
-    if c.encoder_type == "time-depth-separable":
-        # ConvLayerNorm prenet (glow.py:8-50) + TimeDepthSeparableConvBlock (time_depth_sep_conv.py)
+    if c.encoder_type in ("time-depth-separable", "transformer"):
+        # ConvLayerNorm prenet (glow.py:8-50; setup_model passes use_encoder_prenet=True)
         for i in range(3):
             s += [(f"encoder.pre.conv_layers.{i}.weight", (H, H, 5), "conv"),
                   (f"encoder.pre.conv_layers.{i}.bias", (H,), "bias")]
@@ -307,6 +308,26 @@ def glow_spec(c: GlowConfig) -> Spec:
             return [(f"{name}.weight", (n,), "bn_w"), (f"{name}.bias", (n,), "bn_b"),
                     (f"{name}.running_mean", (n,), "bn_mean"), (f"{name}.running_var", (n,), "bn_var"),
                     (f"{name}.num_batches_tracked", (), "count")]
+    if c.encoder_type == "transformer":
+        # Transformer (glow_tts/transformer.py:265-319), no relative-position tables (setup_model
+        # passes no rel_attn_window_size), FFN kernel 3, filter 768
+        L, Fc = c.num_layers_enc, c.filter_channels
+        for i in range(L):
+            for n in ("q", "k", "v", "o"):
+                s += [(f"encoder.encoder.attn_layers.{i}.conv_{n}.weight", (H, H, 1), "xavier"),
+                      (f"encoder.encoder.attn_layers.{i}.conv_{n}.bias", (H,), "bias")]
+        for i in range(L):
+            s += [(f"encoder.encoder.norm_layers_1.{i}.gamma", (1, H, 1), "ln_g"),
+                  (f"encoder.encoder.norm_layers_1.{i}.beta", (1, H, 1), "bias")]
+        for i in range(L):
+            s += [(f"encoder.encoder.ffn_layers.{i}.conv_1.weight", (Fc, H, 3), "conv"),
+                  (f"encoder.encoder.ffn_layers.{i}.conv_1.bias", (Fc,), "bias"),
+                  (f"encoder.encoder.ffn_layers.{i}.conv_2.weight", (H, Fc, 3), "conv"),
+                  (f"encoder.encoder.ffn_layers.{i}.conv_2.bias", (H,), "bias")]
+        for i in range(L):
+            s += [(f"encoder.encoder.norm_layers_2.{i}.gamma", (1, H, 1), "ln_g"),
+                  (f"encoder.encoder.norm_layers_2.{i}.beta", (1, H, 1), "bias")]
+    elif c.encoder_type == "time-depth-separable":
         for i in range(3 + c.num_layers_enc):
             q = f"encoder.encoder.layers.{i}"
             s += [(f"{q}.time_conv.weight", (2 * H, H, 1), "conv"), (f"{q}.time_conv.bias", (2 * H,), "bias")]
