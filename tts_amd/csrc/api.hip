@@ -2189,7 +2189,7 @@ void pwgan_finalize(tts_ctx* c, int layers, int stacks, const int32_t* ups, int 
   P.up_h.clear();
   P.up_h.resize(n_up);
   for (int i = 0; i < n_up; ++i) {
-    TTS_CHECK(ups[i] >= 1 && ups[i] <= 16, "pwgan: upsample factor");
+    TTS_CHECK(ups[i] == 2 || ups[i] == 4 || ups[i] == 8, "pwgan: upsample factors must be 2, 4 or 8");
     P.up_h[i].upload(
         wn_weight(h, "upsample_net.upsample.up_layers." + std::to_string(2 * i + 1), {1, 1, 1, 2 * ups[i] + 1}));
   }

@@ -22,24 +22,36 @@ constexpr int PW_KC1 = (3 * PW_R + PW_A) / 16;  // 17
 constexpr int PW_KC2 = (PW_G / 2) / 16;         // 4
 }  // namespace
 
-// upsample.py:5-63: nearest stretch by s along time, then the (1, 2s + 1) Conv2d with zero padding
-// s (one filter for every channel): out[t] = sum_k h[k] * in[(t + k - s) / s], 0 <= t + k - s < L*s
+// upsample.py:5-63: nearest stretch by S along time, then the (1, 2S + 1) Conv2d with zero padding
+// S (one filter for every channel): out[t] = sum_k h[k] * in[(t + k - S) / S], 0 <= t + k - S < L*S.
+// A thread makes S consecutive outputs, so its 2S + 1 taps touch 3 input samples; positions past
+// the row's length are not written (every reader bounds its reads by the length).
+template <int S>
 __global__ __launch_bounds__(256) void pw_upsample_kernel(const float* __restrict__ in, long ib, int Lin_max,
-                                                          const int* lens, int len_add, int in_mul, int s,
+                                                          const int* lens, int len_add, int in_mul,
                                                           const float* __restrict__ h, float* __restrict__ out,
                                                           long ob, int Lout_max) {
-  const int b = blockIdx.z, ch = blockIdx.y, t = blockIdx.x * 256 + threadIdx.x;
-  if (t >= Lout_max) return;
-  const int Lin = (lens[b] + len_add) * in_mul, Lout = Lin * s;
-  float acc = 0.f;
-  if (t < Lout) {
-    const float* ip = in + b * ib + (long)ch * Lin_max;
-    for (int k = 0; k <= 2 * s; ++k) {
-      const int u = t + k - s;
-      if (u >= 0 && u < Lout) acc = fmaf(h[k], ip[u / s], acc);
+  const int b = blockIdx.z, ch = blockIdx.y, u = blockIdx.x * 256 + threadIdx.x;  // input sample u
+  const int Lin = (lens[b] + len_add) * in_mul, Lout = Lin * S;
+  if (u >= Lin) return;
+  const float* ip = in + b * ib + (long)ch * Lin_max;
+  const float xm = u > 0 ? ip[u - 1] : 0.f, x0 = ip[u], xp = u + 1 < Lin ? ip[u + 1] : 0.f;
+  float hk[2 * S + 1];
+#pragma unroll
+  for (int k = 0; k <= 2 * S; ++k) hk[k] = h[k];
+  float* op = out + b * ob + (long)ch * Lout_max + (long)u * S;
+#pragma unroll
+  for (int r = 0; r < S; ++r) {  // t = u S + r; tap k reads stretched sample t + k - S
+    float acc = 0.f;
+#pragma unroll
+    for (int k = 0; k <= 2 * S; ++k) {
+      const int v = r + k - S;  // offset from u S, in [-S, 2S - 1]
+      const float x = v < 0 ? xm : (v < S ? x0 : xp);
+      const int tt = u * S + v;
+      if (tt >= 0 && tt < Lout) acc = fmaf(hk[k], x, acc);
     }
+    op[r] = acc;
   }
-  out[b * ob + (long)ch * Lout_max + t] = acc;
 }
 
 // first_conv (1 -> 64, k1) on the prior noise
@@ -389,8 +401,13 @@ __global__ __launch_bounds__(256) void pw_out_kernel(const float* __restrict__ s
 
 void launch_pw_upsample(const float* in, long ib, int Lin_max, const int* lens, int len_add, int in_mul, int s,
                         const float* h, float* out, long ob, int Lout_max, int C, int B, hipStream_t st) {
-  pw_upsample_kernel<<<dim3((Lout_max + 255) / 256, C, B), 256, 0, st>>>(in, ib, Lin_max, lens, len_add, in_mul, s,
-                                                                         h, out, ob, Lout_max);
+  const dim3 grid((Lin_max + 255) / 256, C, B);
+  switch (s) {
+    case 2: pw_upsample_kernel<2><<<grid, 256, 0, st>>>(in, ib, Lin_max, lens, len_add, in_mul, h, out, ob, Lout_max); break;
+    case 4: pw_upsample_kernel<4><<<grid, 256, 0, st>>>(in, ib, Lin_max, lens, len_add, in_mul, h, out, ob, Lout_max); break;
+    case 8: pw_upsample_kernel<8><<<grid, 256, 0, st>>>(in, ib, Lin_max, lens, len_add, in_mul, h, out, ob, Lout_max); break;
+    default: TTS_CHECK(false, "pwgan: upsample factors must be 2, 4 or 8");
+  }
   HIP_OK(hipGetLastError());
 }
 void launch_pw_first(const float* noise, long nb, const float* w, const float* bias, const int* lens, int len_add,
