@@ -68,7 +68,7 @@ def lstm_cell(x, h, c, w_ih, w_hh, b_ih, b_hh):
 
 class TacoOracle:
     def __init__(self, sd, attn_norm="sigmoid", r_init=7, frame_channels=80, windowing=False,
-                 forward_attn=False, trans_agent=False, forward_attn_mask=False):
+                 forward_attn=False, trans_agent=False, forward_attn_mask=False, attn_type="original", attn_K=5):
         self.sd = {k: (np.asarray(v, F32) if np.asarray(v).dtype != np.int64 else np.asarray(v))
                    for k, v in sd.items()}
         self.attn_norm = attn_norm
@@ -78,6 +78,8 @@ class TacoOracle:
         self.forward_attn = forward_attn
         self.trans_agent = trans_agent
         self.forward_attn_mask = forward_attn_mask
+        self.attn_type = attn_type
+        self.attn_K = attn_K
 
     def _bn(self, prefix):
         return {k: self.sd[f"{prefix}.batch_normalization.{k}"]
@@ -137,8 +139,34 @@ class TacoOracle:
             m = np.maximum(m, F32(0)).astype(F32)
         return m
 
+    def graves(self, query, inputs, st):
+        """GravesAttention.forward (common_layers.py:150-193), eval mode (no dropout), mask None."""
+        p = "decoder.attention.N_a."
+        K = self.attn_K
+        hid = np.maximum(query @ self.sd[p + "0.weight"].T + self.sd[p + "0.bias"], F32(0)).astype(F32)
+        gbk = (hid @ self.sd[p + "2.weight"].T + self.sd[p + "2.bias"]).astype(F32)
+        g, b, k = gbk[:K], gbk[K:2 * K], gbk[2 * K:]
+
+        def softplus(x):  # torch: x above the threshold 20, log1p(exp(x)) otherwise
+            return np.where(x > 20, x, np.log1p(np.exp(np.minimum(x, 20)))).astype(F32)
+        sig = (softplus(b) + F32(1e-5)).astype(F32)
+        mu = (st["mu"] + softplus(k)).astype(F32)
+        e = np.exp(g - g.max())
+        g = (e / e.sum() + F32(1e-5)).astype(F32)
+        T = inputs.shape[0]
+        j = np.arange(T + 1, dtype=F32) + F32(0.5)
+        phi = g[:, None] * (F32(1) / (F32(1) + sigmoid((mu[:, None] - j[None, :]) / sig[:, None])))
+        a = phi.astype(F32).sum(0)
+        a = (a[1:] - a[:-1]).astype(F32)
+        a[a == 0] = F32(1e-8)
+        st["mu"] = mu
+        st["alpha"] = a
+        return (a @ inputs).astype(F32)
+
     def attention(self, query, inputs, pin, st):
         """OriginalAttention.forward (common_layers.py:325-372), location-sensitive."""
+        if self.attn_type == "graves":
+            return self.graves(query, inputs, st)
         p = "decoder.attention."
         cat = np.stack([st["alpha"], st["alpha_cum"]])              # (2, T)
         pq = query @ self.sd[p + "query_layer.linear_layer.weight"].T       # (128,)
@@ -211,8 +239,9 @@ class TacoOracle:
         """Decoder.inference (tacotron2.py:335-374) at B=1 (stop iff sigma>thr and t>0)."""
         F = self.F
         T = inputs.shape[0]
-        pin = (inputs @ self.sd["decoder.attention.inputs_layer.linear_layer.weight"].T).astype(F32)
-        st = dict(q=np.zeros(1024, F32), qc=np.zeros(1024, F32), h=np.zeros(1024, F32),
+        pin = None if self.attn_type == "graves" else \
+            (inputs @ self.sd["decoder.attention.inputs_layer.linear_layer.weight"].T).astype(F32)
+        st = dict(q=np.zeros(1024, F32), qc=np.zeros(1024, F32), h=np.zeros(1024, F32), mu=np.zeros(self.attn_K, F32),
                   c=np.zeros(1024, F32), ctx=np.zeros(inputs.shape[1], F32),
                   alpha=np.zeros(T, F32), alpha_cum=np.zeros(T, F32), win_idx=-1, u=F32(0.5),
                   fwd_alpha=np.concatenate([np.ones(1, F32), np.full(T - 1, 1e-7, F32)]))

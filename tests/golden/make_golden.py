@@ -49,7 +49,8 @@ def build_taco(cfg: TacotronConfig, seed: int, stop_bias: float, dtype=torch.flo
                   double_decoder_consistency=cfg.double_decoder_consistency, ddc_r=cfg.ddc_r,
                   separate_stopnet=True, speaker_embedding_dim=cfg.speaker_embedding_dim,
                   prenet_type=cfg.prenet_type, attn_win=cfg.windowing, forward_attn=cfg.forward_attn,
-                  trans_agent=cfg.trans_agent, forward_attn_mask=cfg.forward_attn_mask)
+                  trans_agent=cfg.trans_agent, forward_attn_mask=cfg.forward_attn_mask, attn_type=cfg.attn_type,
+                  attn_K=cfg.attn_K)
     sd = synth_state_dict(tacotron2_spec(cfg), seed, STOP_GAIN)
     sd["decoder.stopnet.1.linear_layer.bias"] = np.array([stop_bias], np.float32)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
@@ -385,6 +386,9 @@ if __name__ == "__main__":
         taco_case("taco_fwdmask", TacotronConfig(attn_norm="sigmoid", forward_attn=True, trans_agent=True,
                                                  forward_attn_mask=True),
                   seed=25, utt_lens=[27, 16], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=26)
+    if "taco_graves" in which:  # GravesAttention (common_layers.py:113-193)
+        taco_case("taco_graves", TacotronConfig(attn_norm="sigmoid", attn_type="graves"), seed=41,
+                  utt_lens=[24, 15], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=42)
     if "ge2e" in which:
         ge2e_case("ge2e")
     if "glow" in which:

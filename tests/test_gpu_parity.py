@@ -192,7 +192,7 @@ def test_tacotron2_multispeaker_matches_reference(name, n):
 
 
 @pytest.mark.parametrize("name", ["taco_bnprenet", "taco_window", "taco_window_softmax", "taco_fwdattn",
-                                  "taco_fwdmask"])
+                                  "taco_fwdmask", "taco_graves"])
 def test_tacotron2_decoder_variants_match_reference(name):
     """SURVEY 8f rank 4 decoder variants on the persistent decoder, both fixture utterances in one
     batched call: BN prenet, attention windowing (sigmoid / softmax), forward attention with the

@@ -77,7 +77,7 @@ def test_multispeaker_state_dict_keys_and_shapes():
     assert tuple(sd2["decoder.attention_rnn.weight_ih"].shape) == (4096, 256 + 768)
 
 
-@pytest.mark.parametrize("kw", [dict(gst=True), dict(trans_agent=True), dict(prenet_type="xyz"), dict(attn_type="graves"),
+@pytest.mark.parametrize("kw", [dict(gst=True), dict(trans_agent=True), dict(prenet_type="xyz"), dict(attn_type="graves", num_speakers=4),
                                 dict(location_attn=False)])
 def test_unsupported_tacotron_variants_raise(kw):
     with pytest.raises(NotImplementedError):

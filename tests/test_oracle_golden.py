@@ -106,7 +106,7 @@ def test_tacotron2_oracle_multispeaker_matches_reference(name, n):
 def test_fixture_fp64_drift_is_small():
     """Every Tacotron2 fixture records its fp32-vs-fp64 drift; the 1e-4 tolerance needs it tiny."""
     for name in ("taco_sigmoid", "taco_softmax", "taco_multispk", "taco_extspk", "taco_bnprenet", "taco_window",
-                 "taco_window_softmax", "taco_fwdattn", "taco_fwdmask"):
+                 "taco_window_softmax", "taco_fwdattn", "taco_fwdmask", "taco_graves"):
         fx = load_fixture(name)
         drifts = [float(fx[k]) for k in fx.files if k.endswith("_drift64")]
         assert drifts and max(drifts) < 1e-6
@@ -128,14 +128,15 @@ def test_ge2e_oracle_matches_reference(tag, proj):
 
 
 @pytest.mark.parametrize("name", ["taco_bnprenet", "taco_window", "taco_window_softmax", "taco_fwdattn",
-                                  "taco_fwdmask"])
+                                  "taco_fwdmask", "taco_graves"])
 def test_tacotron2_oracle_decoder_variants_match_reference(name):
     """Decoder variants: BN prenet (common_layers.py:25-74), attention windowing
     (:286-300) with sigmoid and softmax norms, forward attention + transition agent (:302-372)."""
     fx = load_fixture(name)
     cfg, sd = taco_state_dict(fx, r=2)
     orc = TacoOracle(sd, cfg.attn_norm, cfg.r, windowing=cfg.windowing, forward_attn=cfg.forward_attn,
-                     trans_agent=cfg.trans_agent, forward_attn_mask=cfg.forward_attn_mask)
+                     trans_agent=cfg.trans_agent, forward_attn_mask=cfg.forward_attn_mask, attn_type=cfg.attn_type,
+                     attn_K=cfg.attn_K)
     for u in range(2):
         k = f"r2_u{u}"
         dec, post, align, stop = orc.inference(fx[k + "_ids"], 2, int(fx["r2_max_steps"]))

@@ -240,7 +240,12 @@ struct TacoModel {
   std::vector<float> pre1_bias;  // b1' (BN), folded into the projection's prenet rows
   DevBuf pre1_b0, pre2_b, ta_w;
   float ta_b = 0.f;
-  bool variant() const { return prenet_bn || windowing || forward_attn; }
+  bool variant() const { return prenet_bn || windowing || forward_attn || graves; }
+  // Graves attention (common_layers.py:113-193): N_a layer 1 as 64 swizzled 16-row tiles of the
+  // P3g GEMM (K = 1024), its bias, layer 2 (3K x 1024, row-major) and bias
+  bool graves = false;
+  int graves_K = 0;
+  DevBuf na1_w, na1_b, na2_w, na2_b;
   DevBuf spk_table;  // speaker_embedding.weight (num_spk, 512) when learned
   std::vector<float> spk_att_h, spk_dec_h, spk_penc_h, proj_spk;
   DevBuf spk_wT;
@@ -258,6 +263,7 @@ struct TacoWS {
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
   DevBuf spk, spkid, spkb;     // speaker vectors (decode order), per-row biases [Bp][NSPK]
   DevBuf win_idx, fwd_u, apf;  // windowing argmax, transition probability, forward chunk sums
+  DevBuf gh, gmu;              // Graves: N_a hidden (32 x 1024), mixture means (64 x 16)
   bool enc_persist = false;    // the last encoder ran the persistent BiLSTM (lc = its barrier words)
   // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
   // longest-first rows finish); all share one configuration key
@@ -469,8 +475,41 @@ void fold_convbn(const HostMap& m, const std::string& pfx, int Cin, int Cout, in
 
 void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
   auto& M = c->taco;
+  M.graves = c->taco_host.count("decoder.attention.N_a.0.weight") > 0;
+  if (M.graves) {
+    // Graves attention has no location-sensitive tensors: zero stand-ins keep the shared packing
+    // (processed inputs, query projection, location filters, energies) well defined; the Graves
+    // variant of the persistent decoder never reads what they produce
+    const auto it = c->taco_host.find("decoder.attention_rnn.weight_ih");
+    TTS_CHECK(it != c->taco_host.end() && it->second.shape.size() == 2 && it->second.shape[1] > 256,
+              "missing tensor: decoder.attention_rnn.weight_ih");
+    const int64_t ES = it->second.shape[1] - 256;
+    auto zero = [&](const std::string& k, std::vector<int64_t> shape) {
+      size_t n = 1;
+      for (auto d : shape) n *= (size_t)d;
+      c->taco_host[k] = HostT{std::vector<float>(n, 0.f), shape};
+    };
+    zero("decoder.attention.inputs_layer.linear_layer.weight", {128, ES});
+    zero("decoder.attention.query_layer.linear_layer.weight", {128, 1024});
+    zero("decoder.attention.location_layer.location_conv1d.weight", {32, 2, 31});
+    zero("decoder.attention.location_layer.location_dense.linear_layer.weight", {128, 32});
+    zero("decoder.attention.v.linear_layer.weight", {1, 128});
+    zero("decoder.attention.v.linear_layer.bias", {1});
+  }
   const auto& h = c->taco_host;
   M.ready = false;
+  if (M.graves) {
+    const auto& w2 = need(h, "decoder.attention.N_a.2.weight", {}).d;
+    M.graves_K = (int)(w2.size() / 1024 / 3);
+    TTS_CHECK(M.graves_K >= 1 && M.graves_K <= 16 && (size_t)M.graves_K * 3 * 1024 == w2.size(),
+              "Graves attention: N_a.2.weight must be (3K, 1024), K <= 16");
+    std::vector<float> sw((size_t)1024 * 1024);
+    swizzle_rows16(need(h, "decoder.attention.N_a.0.weight", {1024, 1024}).d.data(), 1024, 1024, 1024, sw.data());
+    M.na1_w.upload(sw);
+    M.na1_b.upload(need(h, "decoder.attention.N_a.0.bias", {1024}).d);
+    M.na2_w.upload(w2);
+    M.na2_b.upload(need(h, "decoder.attention.N_a.2.bias", {3 * M.graves_K}).d);
+  }
   M.num_chars = num_chars;
   M.r_init = r_init;
   M.softmax = attn_norm;
@@ -728,6 +767,8 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<unsigned>(W.pbar, 512, g);
   grow<float>(W.spk, (size_t)64 * 1024, g);
   grow<int>(W.win_idx, 64, g);
+  grow<float>(W.gh, 32 * 1024, g);
+  grow<float>(W.gmu, 64 * 16, g);
   grow<float>(W.fwd_u, 64, g);
   grow<int64_t>(W.spkid, 64, g);
   W.B = B;
@@ -1158,6 +1199,14 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.fwd_u = W.fwd_u.f();
   a.part_f = W.apf.f();
   if (M.windowing) HIP_OK(hipMemsetAsync(W.win_idx.p, 0xff, 64 * 4, s));  // -1: before the first step
+  a.gK = M.graves ? M.graves_K : 0;
+  a.na1_w = M.na1_w.f();
+  a.na1_b = M.na1_b.f();
+  a.na2_w = M.na2_w.f();
+  a.na2_b = M.na2_b.f();
+  a.gh = W.gh.f();
+  a.gmu = W.gmu.f();
+  if (M.graves) HIP_OK(hipMemsetAsync(W.gmu.p, 0, 64 * 16 * 4, s));  // mu_prev = 0 (common_layers.py:143)
   if (M.forward_attn) {
     static const std::vector<float> half(64, 0.5f);  // u = 0.5 (common_layers.py:241)
     HIP_OK(hipMemcpyAsync(W.fwd_u.p, half.data(), 64 * 4, hipMemcpyHostToDevice, s));
@@ -1270,8 +1319,11 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
   W.thr = thr;
   // speaker vectors in decode order: external embeddings, or rows of the learned table
-  TTS_CHECK(!M.variant() || use_persistent(c), "BN prenet / attention windowing / forward attention run on the "
-                                               "persistent decoder only (<= 32 utterances per call on a 256-CU device)");
+  TTS_CHECK(!M.variant() || use_persistent(c), "BN prenet / attention windowing / forward / Graves attention run on "
+                                               "the persistent decoder only (<= 32 utterances per call on a 256-CU "
+                                               "device)");
+  TTS_CHECK(!(M.graves && M.spk_dim), "Graves attention with speaker embeddings is not supported (its weights do "
+                                      "not sum to 1, so the speaker columns do not fold into biases)");
   if (M.spk_dim) {
     TTS_CHECK(d_spk_ids || d_spk_emb, "multi-speaker model: speaker ids or speaker embeddings are required");
     TTS_CHECK(use_persistent(c), "multi-speaker decoding runs on the persistent decoder only (<= 32 utterances "

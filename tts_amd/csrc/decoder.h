@@ -128,6 +128,11 @@ struct PArgs {
   int fwd, trans, fwd_mask;
   float* fwd_u;          // (B) transition probability u, 0.5 before the first step
   float* part_f;         // (B, nchmax) chunk sums of the forward weights
+  // Graves attention (VAR bit 2): N_a layer 1 tiles / bias, layer 2 (3K x 1024) / bias, hidden
+  // (Bp x 1024, row-major), mixture means carried across steps (B x 16)
+  int gK;
+  const float *na1_w, *na1_b, *na2_w, *na2_b;
+  float *gh, *gmu;
   const float* ta_w;     // [512 ctx | 1024 query]
   float ta_b;
   const float* pre2_w;  // [16][16][64][4]

@@ -506,6 +506,90 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
 }
 
 
+// Graves attention item (common_layers.py:150-193, eval: no dropout; mask None at B = 1): utterance
+// b, positions [PTC ch, PTC ch + PTC). gbk = N_a.2(hidden) from the P3g hidden row, the mixture
+// (softmax(g) + eps, softplus(b) + eps, mu_prev + softplus(k)), alpha_j = F(j + 1) - F(j) with
+// F(i) = sum_k g_k / (1 + sigmoid((mu_k - i - 0.5) / sig_k)) (0 -> 1e-8), the partial context
+// (alpha is not normalised); the last arriver sums the partials and carries mu to the next step.
+__device__ __forceinline__ float softplus_t(float x) { return x > 20.f ? x : log1pf(expf(x)); }
+
+template <int MT>
+__device__ __forceinline__ void graves_item(const PArgs& P, int t, int b, int ch, float* sm, int* is_last) {
+  constexpr int NT = PT, TC = PTC;
+  const DecDev& D = P.D;
+  const int t0 = ch * TC;
+  const int tid = opaque_v(threadIdx.x);
+  const int lane = tid & 63;
+  const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int T = D.lens[b];
+  const int K = P.gK;
+  float* red = sm;             // [48][8] wave partials of gbk
+  float* gbk = red + 48 * 8;   // [48]
+  float* sw = gbk + 48;        // [TC] alpha of this chunk
+  const int dn = ldci(D.done + b);
+  const float hv0 = ldc(P.gh + (long)b * 1024 + tid), hv1 = ldc(P.gh + (long)b * 1024 + tid + NT);
+  if (t0 >= T || dn) return;  // workgroup-uniform
+  for (int o = 0; o < 3 * K; ++o) {
+    const float v = wave64_sum(fmaf(P.na2_w[(long)o * 1024 + tid], hv0, P.na2_w[(long)o * 1024 + tid + NT] * hv1));
+    if (lane == 0) red[o * 8 + wave] = v;
+  }
+  lds_barrier();
+  if (tid < 3 * K) {
+    float v = P.na2_b[tid];
+#pragma unroll
+    for (int w = 0; w < 8; ++w) v += red[tid * 8 + w];
+    gbk[tid] = v;
+  }
+  lds_barrier();
+  // mixture parameters (every thread, K <= 16)
+  float gm = -INFINITY;
+  for (int k = 0; k < K; ++k) gm = fmaxf(gm, gbk[k]);
+  float gs = 0.f;
+  for (int k = 0; k < K; ++k) gs += expf(gbk[k] - gm);
+  const long pidx = (long)b * P.nchmax + ch;
+  const int nvalid = min(TC, T - t0);
+  if (tid < TC) {
+    float al = 0.f;
+    if (tid < nvalid) {
+      const float j0 = (float)(t0 + tid) + 0.5f, j1 = j0 + 1.f;
+      float f0 = 0.f, f1 = 0.f;
+      for (int k = 0; k < K; ++k) {
+        const float gk = expf(gbk[k] - gm) / gs + 1e-5f;
+        const float sg = softplus_t(gbk[K + k]) + 1e-5f;
+        const float mu = ldc(P.gmu + (long)b * 16 + k) + softplus_t(gbk[2 * K + k]);
+        f0 += gk * (1.f / (1.f + 1.f / (1.f + expf(-((mu - j0) / sg)))));
+        f1 += gk * (1.f / (1.f + 1.f / (1.f + expf(-((mu - j1) / sg)))));
+      }
+      al = f1 - f0;
+      if (al == 0.f) al = 1e-8f;
+      if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + t0 + tid] = al;
+    }
+    sw[tid] = al;
+  }
+  lds_barrier();
+  {
+    const float* eb = P.enc + ((long)b * D.T_max + t0) * 512 + tid;
+    float u = 0.f;
+    for (int i = 0; i < nvalid; ++i) u = fmaf(sw[i], eb[(long)i * 512], u);
+    stc(P.part_u + pidx * 512 + tid, u);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const int nch = (T + TC - 1) / TC;
+  if (tid == 0) {
+    const unsigned prev = __hip_atomic_fetch_add(&P.counter[b], 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    *is_last = (prev == (unsigned)(nch - 1));
+  }
+  lds_barrier();
+  if (!*is_last) return;
+  const long pb0 = (long)b * P.nchmax;
+  float cx = 0.f;
+  for (int c = 0; c < nch; ++c) cx += ldc(P.part_u + (pb0 + c) * 512 + tid);
+  stc(P.ctx + frag_idx(b, tid, 512), cx);
+  if (tid < K) stc(P.gmu + (long)b * 16 + tid, ldc(P.gmu + (long)b * 16 + tid) + softplus_t(gbk[2 * K + tid]));
+  if (tid == 0) __hip_atomic_store(&P.counter[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 // acc[MT] += act[:, chunks kc0 .. kc0+NC) . W^T for one fragment-order activation with nk 16-column
 // chunks; wf(i) gives the weight fragment of local chunk i (registers or LDS). Activation loads
 // run G chunks ahead (two register stages).
@@ -592,6 +676,7 @@ constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
 
 template <int MT, int VAR>
 __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
+  constexpr bool GRAVES = (VAR & 4) != 0;  // Graves attention replaces the location-sensitive one
   extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
   __shared__ int sflag, is_last, dflag[64];
   constexpr int Bp = MT * 16;
@@ -733,7 +818,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     // location features of this workgroup's first attention item for step t (alpha of t-1 is
     // final); items sit on workgroups IW0.. so that they miss the prenet workgroups
     const int it0 = g - IW0;
-    if (it0 >= 0 && it0 < D.B * P.nchmax) attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
+    if (!GRAVES && it0 >= 0 && it0 < D.B * P.nchmax)
+      attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
     if (g == IW0 - 1) {  // stop decision: an attention_rnn workgroup that is not a prenet one
       if (tid < D.B) {
         const int m = tid;
@@ -851,7 +937,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
       lds_barrier();
       PTRACE(11);
-      {  // partial query projection over this workgroup's 16 units
+      if (!GRAVES) {  // partial query projection over this workgroup's 16 units
         const int a = tid & 127;
         for (int m = tid >> 7; m < Bp; m += PT / 128) {
           float s = 0.f;
@@ -868,6 +954,33 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     PTRACE(3);
     gsync_arrive(P.bar, gen);
     if (!gsync_wait(P.bar, gen, &sflag)) return;
+    if constexpr (GRAVES) {
+      // ======== P3g: N_a hidden = relu(W1 h_att + b1), 16 units per workgroup IW0 .. IW0+63 ========
+      tid = opaque_v(tid0);
+      lane = opaque_v(lane0);
+      wave = opaque_s(wave0);
+      const int gt = g - IW0;
+      if (gt >= 0 && gt < 64) {
+        f32x4 wn[8];
+        const f32x4* src = reinterpret_cast<const f32x4*>(P.na1_w) + ((long)gt * 64 + 8 * wave) * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < 8; ++i) wn[i] = src[(long)i * 64];
+        f32x4 acc[MT];
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+        gemm_seg<MT, 8, 2>(acc, P.hatt, 64, 8 * wave, lane, [&](int i) { return wn[i]; });
+        acc_to_lds<MT>(red0, wave, lane, acc);
+        lds_barrier();
+        for (int idx = tid; idx < Bp * 16; idx += PT) {
+          const int m = idx >> 4, n = idx & 15;
+          const float v = lds_sum<NWV, Bp>(red0, m, n) + P.na1_b[gt * 16 + n];
+          stc(P.gh + (long)m * 1024 + gt * 16 + n, fmaxf(v, 0.f));
+        }
+        lds_barrier();
+      }
+      gsync_arrive(P.bar, gen);
+      if (!gsync_wait(P.bar, gen, &sflag)) return;
+    }
     PTRACE(4);
     // ======== P4: attention || the h_att parts of decoder_rnn and attention_rnn ========
     tid = opaque_v(tid0);
@@ -880,7 +993,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       if (g >= IW0) {  // items, then the decoder_rnn h_att part (attention_rnn's waits for P6)
         const int nitems = D.B * P.nchmax;
         for (int it = g - IW0; it < nitems; it += PW - IW0) {
-          pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
+          if constexpr (GRAVES) graves_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, &is_last);
+          else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
           lds_barrier();
         }
         gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
@@ -995,14 +1109,17 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
   TTS_CHECK(a.nchmax * PTC >= a.D.T_max, "persistent decoder: attention partial buffers too small");
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
   // decoder variants are compiled in only where used: VAR bit 0 windowing, bit 1 forward attention
-  const int var = (a.win ? 1 : 0) | (a.fwd ? 2 : 0);
-  static const void* const fns[2][4] = {
+  // (bit 2: Graves attention, exclusive of the others)
+  const int var = a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0);
+  static const void* const fns[2][5] = {
       {(const void*)persist_decoder_kernel<1, 0>, (const void*)persist_decoder_kernel<1, 1>,
-       (const void*)persist_decoder_kernel<1, 2>, (const void*)persist_decoder_kernel<1, 3>},
+       (const void*)persist_decoder_kernel<1, 2>, (const void*)persist_decoder_kernel<1, 3>,
+       (const void*)persist_decoder_kernel<1, 4>},
       {(const void*)persist_decoder_kernel<2, 0>, (const void*)persist_decoder_kernel<2, 1>,
-       (const void*)persist_decoder_kernel<2, 2>, (const void*)persist_decoder_kernel<2, 3>}};
+       (const void*)persist_decoder_kernel<2, 2>, (const void*)persist_decoder_kernel<2, 3>,
+       (const void*)persist_decoder_kernel<2, 4>}};
   const void* f = fns[MT - 1][var];
-  static bool attr[2][4] = {};
+  static bool attr[2][5] = {};
   if (!attr[MT - 1][var]) {
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
     attr[MT - 1][var] = true;

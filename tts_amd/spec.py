@@ -53,6 +53,8 @@ class TacotronConfig:
     forward_attn: bool = False      # forward attention (common_layers.py:302-323)
     trans_agent: bool = False       # transition agent u = sigmoid(ta([ctx, query]))
     forward_attn_mask: bool = False  # forward attention kept to [n-1, n+2] (common_layers.py:309-318)
+    attn_type: str = "original"     # or "graves" (GravesAttention, common_layers.py:113-193)
+    attn_K: int = 5                 # Graves mixture components
 
     @property
     def spk_dim(self) -> int:
@@ -111,21 +113,29 @@ def _decoder(prefix: str, c: TacotronConfig, r: int) -> Spec:
         (f"{prefix}.attention_rnn.weight_hh", (4 * Q, Q), "lstm"),
         (f"{prefix}.attention_rnn.bias_ih", (4 * Q,), "lstm"),
         (f"{prefix}.attention_rnn.bias_hh", (4 * Q,), "lstm"),
-        (f"{prefix}.attention.query_layer.linear_layer.weight", (A, Q), "linear_tanh"),
-        (f"{prefix}.attention.inputs_layer.linear_layer.weight", (A, E), "linear_tanh"),
-        (f"{prefix}.attention.v.linear_layer.weight", (1, A), "attn_v"),
-        (f"{prefix}.attention.v.linear_layer.bias", (1,), "bias"),
     ]
-    if c.forward_attn and c.trans_agent:
-        s += [(f"{prefix}.attention.ta.weight", (1, Q + E), "linear_sigmoid"),
-              (f"{prefix}.attention.ta.bias", (1,), "bias")]
-    if c.location_attn:
+    if c.attn_type == "graves":  # N_a = Linear(Q, Q) -> ReLU -> Linear(Q, 3K)
+        s += [(f"{prefix}.attention.N_a.0.weight", (Q, Q), "linear_relu"),
+              (f"{prefix}.attention.N_a.0.bias", (Q,), "bias"),
+              (f"{prefix}.attention.N_a.2.weight", (3 * c.attn_K, Q), "linear"),
+              (f"{prefix}.attention.N_a.2.bias", (3 * c.attn_K,), "bias")]
+    else:  # OriginalAttention (common_layers.py:196-232)
         s += [
-            (f"{prefix}.attention.location_layer.location_conv1d.weight",
-             (c.loc_filters, 2, c.loc_kernel), "conv"),
-            (f"{prefix}.attention.location_layer.location_dense.linear_layer.weight",
-             (A, c.loc_filters), "linear_tanh"),
+            (f"{prefix}.attention.query_layer.linear_layer.weight", (A, Q), "linear_tanh"),
+            (f"{prefix}.attention.inputs_layer.linear_layer.weight", (A, E), "linear_tanh"),
+            (f"{prefix}.attention.v.linear_layer.weight", (1, A), "attn_v"),
+            (f"{prefix}.attention.v.linear_layer.bias", (1,), "bias"),
         ]
+        if c.forward_attn and c.trans_agent:
+            s += [(f"{prefix}.attention.ta.weight", (1, Q + E), "linear_sigmoid"),
+                  (f"{prefix}.attention.ta.bias", (1,), "bias")]
+        if c.location_attn:
+            s += [
+                (f"{prefix}.attention.location_layer.location_conv1d.weight",
+                 (c.loc_filters, 2, c.loc_kernel), "conv"),
+                (f"{prefix}.attention.location_layer.location_dense.linear_layer.weight",
+                 (A, c.loc_filters), "linear_tanh"),
+            ]
     s += [
         (f"{prefix}.decoder_rnn.weight_ih", (4 * D, Q + E), "lstm"),
         (f"{prefix}.decoder_rnn.weight_hh", (4 * D, D), "lstm"),

@@ -55,8 +55,10 @@ class Tacotron2(nn.Module):
         unsupported = []
         if gst:
             unsupported.append("GST")
-        if attn_type != "original":
+        if attn_type not in ("original", "graves"):
             unsupported.append(f"attn_type={attn_type}")
+        if attn_type == "graves" and num_speakers > 1:
+            unsupported.append("Graves attention with speaker embeddings")
         if trans_agent and not forward_attn:
             unsupported.append("trans_agent without forward_attn")
         if not location_attn:
@@ -83,9 +85,12 @@ class Tacotron2(nn.Module):
                                   double_decoder_consistency=double_decoder_consistency,
                                   ddc_r=ddc_r if ddc_r is not None else r,
                                   num_speakers=num_speakers, speaker_embedding_dim=speaker_embedding_dim,
-                                  prenet_type=prenet_type, windowing=bool(attn_win),
-                                  forward_attn=bool(forward_attn), trans_agent=bool(trans_agent),
-                                  forward_attn_mask=bool(forward_attn and forward_attn_mask))
+                                  prenet_type=prenet_type, attn_type=attn_type, attn_K=attn_K,
+                                  # GravesAttention ignores the location-attention options (tacotron2.py:177-188)
+                                  windowing=bool(attn_win) and attn_type != "graves",
+                                  forward_attn=bool(forward_attn) and attn_type != "graves",
+                                  trans_agent=bool(trans_agent) and attn_type != "graves",
+                                  forward_attn_mask=bool(forward_attn and forward_attn_mask) and attn_type != "graves")
         # models/tacotron2.py:50-58 / tacotron_abstract.py:76-81: a learned table unless the caller
         # gives per-sample embeddings of speaker_embedding_dim
         self.embeddings_per_sample = speaker_embedding_dim is not None
@@ -174,7 +179,8 @@ class Tacotron2(nn.Module):
         if not 1 <= r <= self.decoder.r_init:
             raise ValueError(f"r={r} must be in [1, r_init={self.decoder.r_init}]")
         spk_ids, spk_emb = self._speaker_args(speaker_ids, speaker_embeddings, B, dev)
-        variant = self.cfg.prenet_type == "bn" or self.cfg.windowing or self.cfg.forward_attn
+        variant = self.cfg.prenet_type == "bn" or self.cfg.windowing or self.cfg.forward_attn or \
+            self.cfg.attn_type == "graves"
         limit = BATCH_LIMIT if self.num_speakers <= 1 and not variant else SPEAKER_BATCH_LIMIT
         outs = []
         for b0 in range(0, B, limit):
