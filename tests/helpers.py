@@ -37,7 +37,8 @@ def build_taco(cfg, sd, device="cuda"):
                   double_decoder_consistency=cfg.double_decoder_consistency, ddc_r=cfg.ddc_r,
                   speaker_embedding_dim=cfg.speaker_embedding_dim, prenet_type=cfg.prenet_type,
                   attn_win=cfg.windowing, forward_attn=cfg.forward_attn, trans_agent=cfg.trans_agent,
-                  forward_attn_mask=cfg.forward_attn_mask, attn_type=cfg.attn_type, attn_K=cfg.attn_K)
+                  forward_attn_mask=cfg.forward_attn_mask, attn_type=cfg.attn_type, attn_K=cfg.attn_K,
+                  bidirectional_decoder=cfg.bidirectional_decoder)
     m.load_state_dict({k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()})
     return m.to(device).eval()
 

@@ -9,6 +9,8 @@ import torch
 
 from helpers import (build_melgan, build_taco, load_fixture, melgan_oracle, melgan_state_dict,
                      taco_state_dict)
+from tts_amd.spec import tacotron2_spec
+from tts_amd.weights import synth_state_dict
 
 pytestmark = pytest.mark.gpu
 
@@ -164,6 +166,28 @@ def test_tacotron2_batched_matches_reference(taco_sig, r):
         batch[i, :len(x)] = x
     dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=[len(x) for x in ids])
     _check_taco(fx, r, dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy(), stop.cpu().numpy(),
+                m.last_steps, range(3))
+
+
+def test_tacotron2_bidirectional_decoder_checkpoint(taco_sig):
+    """bidirectional_decoder=True adds decoder_backward.* (a deepcopy of the decoder,
+    tacotron_abstract.py:104-105) that inference never runs: same frames as the reference."""
+    import dataclasses
+    fx = taco_sig
+    cfg, sd = taco_state_dict(fx, r=2)
+    cfg = dataclasses.replace(cfg, bidirectional_decoder=True)
+    full = synth_state_dict(tacotron2_spec(cfg), 99)
+    full.update(sd)  # the fixture's weights; decoder_backward.* stay random
+    m = build_taco(cfg, full)
+    m.decoder.set_r(2)
+    m.decoder.max_decoder_steps = int(fx["r2_max_steps"])
+    ids = [fx[f"r2_u{i}_ids"] for i in range(3)]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((3, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=[len(x) for x in ids])
+    _check_taco(fx, 2, dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy(), stop.cpu().numpy(),
                 m.last_steps, range(3))
 
 

@@ -212,3 +212,14 @@ def test_pwgan_keys_match_reference_and_factory():
         ParallelWaveganGenerator(res_channels=32)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         v.inference(torch.zeros(1, 80, 4))
+
+
+def test_bidirectional_decoder_keys():
+    """bidirectional_decoder=True: decoder_backward.* mirrors decoder.* (tacotron_abstract.py:104-105),
+    registered before coarse_decoder (checked against the reference module when it was built)."""
+    m = Tacotron2(num_chars=129, r=7, double_decoder_consistency=True, ddc_r=7, bidirectional_decoder=True)
+    keys = list(m.state_dict().keys())
+    dec = [k for k in keys if k.startswith("decoder.")]
+    bwd = [k for k in keys if k.startswith("decoder_backward.")]
+    assert bwd == ["decoder_backward." + k[len("decoder."):] for k in dec]
+    assert keys.index(bwd[-1]) < keys.index("coarse_decoder.prenet.linear_layers.0.linear_layer.weight")

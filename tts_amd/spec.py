@@ -54,6 +54,7 @@ class TacotronConfig:
     trans_agent: bool = False       # transition agent u = sigmoid(ta([ctx, query]))
     forward_attn_mask: bool = False  # forward attention kept to [n-1, n+2] (common_layers.py:309-318)
     attn_type: str = "original"     # or "graves" (GravesAttention, common_layers.py:113-193)
+    bidirectional_decoder: bool = False  # decoder_backward: a training-time copy, unused at inference
     attn_K: int = 5                 # Graves mixture components
 
     @property
@@ -171,6 +172,8 @@ def tacotron2_spec(c: TacotronConfig) -> Spec:
     chans = [F, 512, 512, 512, 512, F]
     for i in range(5):
         s += _conv_bn(f"postnet.convolutions.{i}", chans[i], chans[i + 1], 5)
+    if c.bidirectional_decoder:  # tacotron_abstract.py:104-105 (deepcopy of the decoder)
+        s += _decoder("decoder_backward", c, c.r)
     if c.double_decoder_consistency:
         s += _decoder("coarse_decoder", c, c.ddc_r)
     return s

@@ -65,8 +65,6 @@ class Tacotron2(nn.Module):
             unsupported.append("location_attn=False")
         if prenet_type not in ("original", "bn"):
             unsupported.append(f"prenet_type={prenet_type}")
-        if bidirectional_decoder:
-            unsupported.append("bidirectional_decoder")
         if encoder_in_features != 512 or decoder_in_features != 512:  # before the speaker columns
             unsupported.append("non-default encoder/decoder feature sizes")
         if decoder_output_dim != 80 or postnet_output_dim != 80:
@@ -86,6 +84,7 @@ class Tacotron2(nn.Module):
                                   ddc_r=ddc_r if ddc_r is not None else r,
                                   num_speakers=num_speakers, speaker_embedding_dim=speaker_embedding_dim,
                                   prenet_type=prenet_type, attn_type=attn_type, attn_K=attn_K,
+                                  bidirectional_decoder=bool(bidirectional_decoder),
                                   # GravesAttention ignores the location-attention options (tacotron2.py:177-188)
                                   windowing=bool(attn_win) and attn_type != "graves",
                                   forward_attn=bool(forward_attn) and attn_type != "graves",
@@ -151,7 +150,7 @@ class Tacotron2(nn.Module):
     def _sync(self, eng):
         key = (self._token, self._version)
         if eng.taco_key != key:
-            eng.load_tacotron(host_tensors(self, skip_prefixes=("coarse_decoder.",)), self.num_chars,
+            eng.load_tacotron(host_tensors(self, skip_prefixes=("coarse_decoder.", "decoder_backward.")), self.num_chars,
                               self.decoder.r_init, self.attn_norm, self.cfg.windowing, self.cfg.forward_attn,
                               self.cfg.forward_attn_mask)
             eng.taco_key = key
