@@ -604,3 +604,54 @@ def test_synthesizer_glow_tts_and_pwgan(tmp_path):
     ylens = synth.tts_model.last_y_lengths
     for w, yl in zip(wavs, ylens):
         assert w.shape == (256 * 2 * (int(yl) // 2),) and np.isfinite(w).all() and np.abs(w).max() > 0
+
+
+def test_pwgan_inference_padding_zero_vs_oracle():
+    """inference_padding = 0 (what Synthesizer sets, server/synthesizer.py:86) against the fp32
+    oracle on the fixture weights and mel (parity pinned through the oracle, <= 2e-6 of the reference)."""
+    from oracle.pwgan_np import PwganOracle
+    from tts_amd import ParallelWaveganGenerator
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    _dev()
+    fx = load_fixture("pwgan")
+    cfg = PwganConfig(inference_padding=0)
+    sd = synth_state_dict(pwgan_spec(PwganConfig()), int(fx["seed"]))
+    g = ParallelWaveganGenerator(inference_padding=0)
+    g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    g = g.cuda().eval()
+    mel = fx["M5_mel"]
+    noise = np.random.RandomState(3).randn(1, 1, 5 * 256).astype(np.float32)
+    y = g.inference(torch.from_numpy(mel).cuda(), noise=torch.from_numpy(noise).cuda()).cpu().numpy()[0, 0]
+    ref = PwganOracle(sd, cfg).inference(mel[0], noise[0, 0])
+    assert y.shape == ref.shape == (5 * 256,)
+    assert np.abs(y - ref).max() <= 1e-4
+
+
+def test_glow_length_and_noise_scale_vs_oracle():
+    """GlowTts.length_scale / noise_scale (glow_tts.py:172-186) away from their defaults, against the
+    oracle: y_lengths and the path exact, mel <= 1e-4."""
+    from oracle.glow_np import GlowOracle
+    from tts_amd import GlowTts
+    from tts_amd.spec import GlowConfig, glow_spec
+    _dev()
+    fx = load_fixture("glow")
+    sd = synth_state_dict(glow_spec(GlowConfig()), int(fx["seed"]))
+    m = GlowTts(num_chars=GlowConfig().num_chars)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    ids = fx["u1_ids"]
+    orc = GlowOracle(sd)
+    # durations are ceil((exp(logw) - 1) * length_scale): take a scale that leaves every token's
+    # value >= 1e-3 away from an integer, so 1e-6-level differences in logw cannot flip a ceil
+    _, logw = orc.encode(ids)
+    w = np.exp(logw.astype(np.float64)) - 1
+    ls = next(x for x in (1.7, 1.45, 1.3, 0.85, 1.15) if np.abs(w * x - np.round(w * x)).min() > 1e-3)
+    m.length_scale, m.noise_scale = ls, 0.4
+    _, _, _, _, Ty0 = orc.inference(ids, None, 0.4, ls)
+    noise = np.random.RandomState(5).randn(1, 80, Ty0).astype(np.float32)
+    y_ref, ym_ref, attn_ref, logw_ref, Ty = orc.inference(ids, noise[0], 0.4, ls)
+    y, _, ym, _, attn, _, _ = m.inference(torch.from_numpy(ids[None]).cuda(), [len(ids)],
+                                          noise=torch.from_numpy(noise).cuda())
+    assert int(m.last_y_lengths[0]) == Ty
+    assert np.array_equal(attn.cpu().numpy()[0], attn_ref)
+    assert np.abs(y.cpu().numpy()[0] - y_ref).max() <= 1e-4

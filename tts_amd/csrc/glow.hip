@@ -84,51 +84,55 @@ __global__ __launch_bounds__(64) void glow_durations_kernel(const float* __restr
   ylen[b] = max((int)c, 1);  // clamp_min(sum, 1).long()
 }
 
-// path[t, j] = [j < cum_t] - [j < cum_{t-1}] (generate_path), masked by t < x_len, j < y_len: with
-// cum non-decreasing, row j has one 1 at t_j = the first t with cum_t > j (none past sum w_ceil).
-// y_mean[c, j] = o_mean[c, t_j]; z = (y_mean + noise * noise_scale) * y_mask (mean_only:
-// y_log_scale = 0, glow_tts.py:184-186). A workgroup owns 64 frames: t_j by binary search, then
-// y_mean / z with lanes along j, then the 64 attn rows (B, T_y, T_x) with lanes along t.
+// path[t, j] = [j < cum_t] - [j < cum_{t-1}] (generate_path), masked by t < x_len, j < y_len.
+// cum is not monotonic in general: with length_scale > 1 a token's ceil((exp(logw) - 1) * scale)
+// can be -1, and the reference's path then holds -1 entries; so every (j, t) pair is evaluated
+// (no search for a single t_j). y_mean[c, j] = sum_t path[t, j] o_mean[c, t]; z = (y_mean +
+// noise * noise_scale) * y_mask (mean_only: y_log_scale = 0, glow_tts.py:184-186). A workgroup owns
+// 64 frames: 4 threads per frame (a quarter of the channels each) accumulate over the nonzero
+// path entries, then the 64 attn rows (B, T_y, T_x) are written with lanes along t.
+__device__ __forceinline__ float glow_path(const float* cb, int t, int j, int xl, int yl) {
+  if (t >= xl || j >= yl) return 0.f;
+  const float jf = (float)j;
+  return (jf < cb[t] ? 1.f : 0.f) - (t > 0 && jf < cb[t - 1] ? 1.f : 0.f);
+}
+
 __global__ __launch_bounds__(256) void glow_expand_kernel(const float* __restrict__ o_mean, int C, int Tx,
                                                           const int* xlens, const float* __restrict__ cum,
                                                           const int* ylens, int Ty, const float* noise,
                                                           float noise_scale, float* __restrict__ y_mean,
                                                           float* __restrict__ z, float* __restrict__ attn) {
-  __shared__ int tj[64];
+  constexpr int CQ = 20;  // channels per thread (C = 80 = 4 x 20)
   const int b = blockIdx.y, j0 = blockIdx.x * 64, tid = threadIdx.x;
-  const int xl = xlens[b];
+  const int xl = xlens[b], yl = ylens[b];
   const float* cb = cum + (long)b * Tx;
-  if (tid < 64) {
-    const int j = j0 + tid;
-    int lo = 0, hi = xl;  // first t in [0, xl) with cum_t > j, xl if none
-    const float jf = (float)j;
-    while (lo < hi) {
-      const int mid = (lo + hi) >> 1;
-      if (cb[mid] > jf) hi = mid;
-      else lo = mid + 1;
-    }
-    tj[tid] = (j < Ty && j < ylens[b] && lo < xl) ? lo : -1;
-  }
-  __syncthreads();
   {
-    const int jj = tid & 63, j = j0 + jj;
+    const int jj = tid & 63, q = tid >> 6, j = j0 + jj;
     if (j < Ty) {
-      const int t = tj[jj];
-      const bool yv = j < ylens[b];
-      for (int c = tid >> 6; c < C; c += 4) {
-        const long i = ((long)b * C + c) * Ty + j;
-        const float m = t >= 0 ? o_mean[((long)b * C + c) * Tx + t] : 0.f;
-        y_mean[i] = m;
-        const float nz = noise ? noise[i] * noise_scale : 0.f;
-        z[i] = yv ? m + nz : 0.f;
+      float acc[CQ];
+#pragma unroll
+      for (int i = 0; i < CQ; ++i) acc[i] = 0.f;
+      for (int t = 0; t < xl; ++t) {
+        const float p = glow_path(cb, t, j, xl, yl);
+        if (p != 0.f) {
+#pragma unroll
+          for (int i = 0; i < CQ; ++i) acc[i] = fmaf(p, o_mean[((long)b * C + q * CQ + i) * Tx + t], acc[i]);
+        }
+      }
+      const bool yv = j < yl;
+#pragma unroll
+      for (int i = 0; i < CQ; ++i) {
+        const long ix = ((long)b * C + q * CQ + i) * Ty + j;
+        y_mean[ix] = acc[i];
+        const float nz = noise ? noise[ix] * noise_scale : 0.f;
+        z[ix] = yv ? acc[i] + nz : 0.f;
       }
     }
   }
   const int nj = min(64, Ty - j0);
   for (int r = 0; r < nj; ++r) {
     float* arow = attn + ((long)b * Ty + j0 + r) * Tx;
-    const int t1 = tj[r];
-    for (int t = tid; t < Tx; t += 256) arow[t] = t == t1 ? 1.f : 0.f;
+    for (int t = tid; t < Tx; t += 256) arow[t] = glow_path(cb, t, j0 + r, xl, yl);
   }
 }
 
@@ -210,6 +214,7 @@ void launch_glow_durations(const float* logw, int T, const int* lens, float leng
 void launch_glow_expand(const float* o_mean, int C, int Tx, const int* xlens, const float* cum, const int* ylens,
                         int Ty, const float* noise, float noise_scale, float* y_mean, float* z, float* attn, int B,
                         hipStream_t s) {
+  TTS_CHECK(C == 80, "glow: 80 mel channels");
   glow_expand_kernel<<<dim3((Ty + 63) / 64, B), 256, 0, s>>>(o_mean, C, Tx, xlens, cum, ylens, Ty, noise,
                                                                 noise_scale, y_mean, z, attn);
   HIP_OK(hipGetLastError());
