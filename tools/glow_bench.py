@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--steps", type=int, default=10)
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--cpu-utts", type=int, default=0)
     a = ap.parse_args()
     T, M = lj_profile()
     T, M = T[:a.batch], M[:a.batch]
@@ -46,9 +47,24 @@ def main():
         m.inference(x, lens)
     torch.cuda.synchronize()
     dt = (time.perf_counter() - t0) / a.steps
-    print(json.dumps({"metric": "glow_tts_mel_frames_per_sec", "value": frames / dt, "ms_per_call": dt * 1e3,
-                      "frames": frames, "chars": int(sum(T)), "batch": a.batch, "Ty": int(m.last_y_lengths.max()),
-                      "length_scale": m.length_scale}))
+    out = {"metric": "glow_tts_mel_frames_per_sec", "value": frames / dt, "ms_per_call": dt * 1e3,
+           "frames": frames, "chars": int(sum(T)), "batch": a.batch, "Ty": int(m.last_y_lengths.max()),
+           "length_scale": m.length_scale}
+    if a.cpu_utts:  # the numpy oracle (test infrastructure) on the first utterances, B = 1 each
+        from oracle.glow_np import GlowOracle
+        from threadpoolctl import threadpool_limits
+        cores = int(os.environ.get("OMP_NUM_THREADS", "16"))
+        orc = GlowOracle(sd)
+        ids = synthetic_ids(T)
+        n = 0
+        with threadpool_limits(cores):
+            t0 = time.perf_counter()
+            for i in range(a.cpu_utts):
+                n += orc.inference(ids[i], None, 0.66, m.length_scale)[4]
+            ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": n / ct, "unit": "mel-frames/s", "cores": cores, "kind": "port",
+                               "sample": f"first {a.cpu_utts} utterances, B=1, numpy fp32 oracle, {ct:.1f} s"}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":

@@ -23,6 +23,7 @@ def main():
     ap.add_argument("--steps", type=int, default=3)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32)
+    ap.add_argument("--cpu-frames", type=int, default=0)
     a = ap.parse_args()
     _, M = lj_profile()
     M = M[:a.batch]
@@ -47,9 +48,25 @@ def main():
     dt = (time.perf_counter() - t0) / a.steps
     samples = 256 * (sum(M) + 4 * len(M))
     flops = samples * 30 * 2 * (128 * 272 + 128 * 64)
-    print(json.dumps({"metric": "pwgan_samples_per_sec", "value": samples / dt, "ms_per_call": dt * 1e3,
-                      "samples": samples, "mel_frames": int(sum(M)), "batch": len(M),
-                      "residual_block_tflops": flops / dt / 1e12}))
+    out = {"metric": "pwgan_samples_per_sec", "value": samples / dt, "ms_per_call": dt * 1e3,
+           "samples": samples, "mel_frames": int(sum(M)), "batch": len(M),
+           "residual_block_tflops_lower_bound": flops / dt / 1e12}
+    if a.cpu_frames:  # the numpy oracle (test infrastructure) on a bounded sample, as bench.py does
+        sys.path.insert(0, os.path.join(os.path.dirname(os.path.abspath(__file__)), ".."))
+        from oracle.pwgan_np import PwganOracle
+        from threadpoolctl import threadpool_limits
+        cores = int(os.environ.get("OMP_NUM_THREADS", "16"))
+        sd = synth_state_dict(pwgan_spec(PwganConfig()), 5)
+        orc = PwganOracle(sd, PwganConfig())
+        m0 = np.random.RandomState(1).uniform(-1, 1, size=(80, a.cpu_frames)).astype(np.float32)
+        nz = np.random.RandomState(2).randn(256 * (a.cpu_frames + 4)).astype(np.float32)
+        with threadpool_limits(cores):
+            t0 = time.perf_counter()
+            orc.inference(m0, nz)
+            ct = time.perf_counter() - t0
+        out["cpu_baseline"] = {"value": 256 * (a.cpu_frames + 4) / ct, "unit": "samples/s", "cores": cores,
+                               "kind": "port", "sample": f"one {a.cpu_frames}-frame mel, numpy fp32 oracle, {ct:.1f} s"}
+    print(json.dumps(out))
 
 
 if __name__ == "__main__":
