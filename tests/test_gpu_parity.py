@@ -655,3 +655,30 @@ def test_glow_length_and_noise_scale_vs_oracle():
     assert int(m.last_y_lengths[0]) == Ty
     assert np.array_equal(attn.cpu().numpy()[0], attn_ref)
     assert np.abs(y.cpu().numpy()[0] - y_ref).max() <= 1e-4
+
+
+def test_synthesizer_multispeaker(tmp_path):
+    """tts_speakers mapping (synthesizer.py:62-67) -> num_speakers; tts(text, speaker_id) decodes every
+    sentence with that speaker's learned embedding: each equals the model's own B = 1 call."""
+    import json as _json
+    from tts_amd.spec import TacotronConfig
+    from tts_amd.synthesizer import Synthesizer
+    from tts_amd.text import symbols
+    _dev()
+    conf = _synth_files(tmp_path)
+    cfg = TacotronConfig(num_chars=len(symbols), num_speakers=4)
+    _, sd = taco_state_dict(None, seed=21, overrides={}, stop_bias=-1e4, cfg=cfg)
+    torch.save({"model": {k: torch.from_numpy(np.asarray(v)) for k, v in sd.items()}, "r": 2},
+               str(tmp_path / "tts_ms.pth"))
+    (tmp_path / "speakers.json").write_text(_json.dumps({f"spk{i}": i for i in range(4)}))
+    conf.update({"tts_checkpoint": str(tmp_path / "tts_ms.pth"), "tts_speakers": str(tmp_path)})
+    synth = Synthesizer(conf)
+    assert synth.tts_model.num_speakers == 4
+    synth.tts_model.decoder.max_decoder_steps = 12
+    sens = ["Hello world.", "Speaker two speaks here."]
+    wavs = synth.synthesize_batch(sens, speaker_id=2)
+    for s_, w in zip(sens, wavs):
+        ref = synth.synthesize_batch([s_], speaker_id=2)[0]
+        assert w.shape == ref.shape and np.abs(w - ref).max() <= 1e-4
+    other = synth.synthesize_batch(sens[:1], speaker_id=0)[0]
+    assert np.abs(other - wavs[0]).max() > 1e-3

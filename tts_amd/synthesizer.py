@@ -11,6 +11,8 @@ Follows `TTS/server/synthesizer.py:21-193`. What differs on purpose:
     phonemizer, unidecode and inflect are not in this image); phoneme configs need a
     `phonemize` callable.
 """
+import json
+import os
 import time
 
 import numpy as np
@@ -46,9 +48,20 @@ class Synthesizer:
         if "characters" in self.tts_config:
             syms, phs = make_symbols(**self.tts_config["characters"])
         self.input_size = len(phs) if self.use_phonemes else len(syms)
+        # synthesizer.py:62-67: a speaker mapping (speakers.json, or a directory holding one) sets
+        # num_speakers; tts(text, speaker_id) then conditions on the learned speaker table
+        num_speakers = 0
         if self.config.get("tts_speakers") is not None:
-            raise NotImplementedError("multi-speaker Tacotron2 is SURVEY.md §8f rank 2")
-        self.tts_model = setup_model(self.input_size, num_speakers=0, c=self.tts_config)
+            path = self.config["tts_speakers"]
+            if os.path.splitext(path)[1] != ".json":
+                path = os.path.join(path, "speakers.json")  # utils/speakers.py make_speakers_json_path
+            try:
+                with open(path) as f:
+                    self.tts_speakers = json.load(f)
+            except FileNotFoundError:
+                self.tts_speakers = {}
+            num_speakers = len(self.tts_speakers)
+        self.tts_model = setup_model(self.input_size, num_speakers=num_speakers, c=self.tts_config)
         cp = torch.load(tts_checkpoint, map_location=torch.device("cpu"), weights_only=True)
         self.tts_model.load_state_dict(cp["model"])
         if use_cuda:
@@ -79,7 +92,7 @@ class Synthesizer:
     def split_into_sentences(text):
         return split_into_sentences(text)
 
-    def synthesize_batch(self, sentences):
+    def synthesize_batch(self, sentences, speaker_id=None):
         """Sentences -> list of per-sentence waveforms (float32 numpy), one GPU call per model."""
         seqs = [text_to_seqvec(s, self.tts_config, self.phonemize) for s in sentences]
         lens = [max(1, len(q)) for q in seqs]
@@ -94,7 +107,9 @@ class Synthesizer:
                 # a B = 1 reference call returns 2 * floor(y_length / 2) frames (decoder squeeze)
                 mel_lens = [2 * (int(m) // 2) for m in self.tts_model.last_y_lengths]
             else:
-                _, post, _, _ = self.tts_model.inference(torch.from_numpy(batch).to(dev), text_lengths=lens)
+                spk = None if speaker_id is None else torch.full((len(seqs),), int(speaker_id), dtype=torch.long)
+                _, post, _, _ = self.tts_model.inference(torch.from_numpy(batch).to(dev), text_lengths=lens,
+                                                         speaker_ids=spk)
                 mel_lens = [int(m) for m in self.tts_model.last_mel_lengths]
             if self.vocoder_model is not None:
                 wav = self.vocoder_model.inference(post.transpose(1, 2).contiguous(), lengths=mel_lens)
@@ -106,13 +121,11 @@ class Synthesizer:
 
     def tts(self, text, speaker_id=None):
         """synthesizer.py:134-193"""
-        if speaker_id is not None:
-            raise NotImplementedError("multi-speaker Tacotron2 is SURVEY.md §8f rank 2")
         start_time = time.time()
         sens = self.split_into_sentences(text)
         print(sens)
         wavs = []
-        for wav in self.synthesize_batch(sens):
+        for wav in self.synthesize_batch(sens, speaker_id):
             wav = wav[:self.ap.find_endpoint(wav)]  # synthesis.py:130-131
             wavs += list(wav)
             wavs += [0] * 10000
