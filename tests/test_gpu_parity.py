@@ -682,3 +682,28 @@ def test_synthesizer_multispeaker(tmp_path):
         assert w.shape == ref.shape and np.abs(w - ref).max() <= 1e-4
     other = synth.synthesize_batch(sens[:1], speaker_id=0)[0]
     assert np.abs(other - wavs[0]).max() > 1e-3
+
+
+def test_synthesis_notebook_surface(tmp_path):
+    """synthesis(model, text, CONFIG, use_cuda, ap, ...) (tts/utils/synthesis.py:178-262), the
+    notebooks' entry: outputs are the model's own B = 1 inference, parsed as the reference parses
+    them; Griffin-Lim on request; truncated=True raises as the reference does."""
+    from tts_amd.audio import AudioProcessor
+    from tts_amd.factories import load_config
+    from tts_amd.synthesis import synthesis, text_to_seqvec
+    from tts_amd.synthesizer import Synthesizer
+    _dev()
+    conf = _synth_files(tmp_path, with_vocoder=False)
+    synth = Synthesizer(conf)
+    model = synth.tts_model
+    model.decoder.max_decoder_steps = 10
+    C = load_config(conf["tts_config"])
+    ap = AudioProcessor(**C["audio"])
+    wav, align, dec, post, stop, inputs = synthesis(model, "Hello there.", C, True, ap, use_griffin_lim=True)
+    ids = text_to_seqvec("Hello there.", C)
+    d2, p2, a2, s2 = model.inference(torch.from_numpy(ids[None].astype(np.int64)).cuda())
+    assert np.array_equal(post, p2[0].cpu().numpy()) and np.array_equal(dec, d2[0].cpu().numpy())
+    assert align.shape == a2[0].shape and stop.shape == s2[0].shape
+    assert wav is not None and np.isfinite(wav).all() and tuple(inputs.shape) == (1, len(ids))
+    with pytest.raises(AttributeError):
+        synthesis(model, "Hello there.", C, True, ap, truncated=True)
