@@ -3,6 +3,8 @@ oracle. Tolerances (fp32): mel / frames <= 1e-4 L-inf (north_star), waveforms <=
 stop steps and alignment argmax bit-exact (argmax only where the reference's top-2 margin
 exceeds 1e-5; ties below that are implementation-defined in fp32).
 """
+import os
+
 import numpy as np
 import pytest
 import torch
@@ -707,3 +709,17 @@ def test_synthesis_notebook_surface(tmp_path):
     assert wav is not None and np.isfinite(wav).all() and tuple(inputs.shape) == (1, len(ids))
     with pytest.raises(AttributeError):
         synthesis(model, "Hello there.", C, True, ap, truncated=True)
+
+
+def test_synthesize_cli(tmp_path):
+    """python -m tts_amd.synthesize (TTS/bin/synthesize.py): Tacotron2-DDC + MB-MelGAN from
+    checkpoint files; the 16-bit wav is named after the text as the reference names it."""
+    import scipy.io.wavfile
+    from tts_amd.synthesize import main
+    _dev()
+    conf = _synth_files(tmp_path)
+    out = main(["Hi there, MI355X.", conf["tts_config"], conf["tts_checkpoint"], str(tmp_path),
+                "--vocoder_path", conf["vocoder_checkpoint"], "--vocoder_config_path", conf["vocoder_config"]])
+    assert os.path.basename(out) == "Hi_there_MI355X.wav"
+    sr, x = scipy.io.wavfile.read(out)
+    assert sr == 22050 and len(x) > 0
