@@ -723,3 +723,58 @@ def test_synthesize_cli(tmp_path):
     assert os.path.basename(out) == "Hi_there_MI355X.wav"
     sr, x = scipy.io.wavfile.read(out)
     assert sr == 22050 and len(x) > 0
+
+
+def test_pwgan_single_frame_vs_oracle():
+    """Edge: a one-frame mel (5 frames after the replicate padding: 1280 samples, ten 128-sample
+    tiles of the residual-block grid) against the oracle."""
+    from oracle.pwgan_np import PwganOracle
+    from tts_amd import ParallelWaveganGenerator
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    _dev()
+    fx = load_fixture("pwgan")
+    sd = synth_state_dict(pwgan_spec(PwganConfig()), int(fx["seed"]))
+    g = ParallelWaveganGenerator()
+    g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    g = g.cuda().eval()
+    mel = fx["M5_mel"][:, :, :1]
+    noise = np.random.RandomState(7).randn(1, 1, 5 * 256).astype(np.float32)
+    y = g.inference(torch.from_numpy(mel).cuda(), noise=torch.from_numpy(noise).cuda()).cpu().numpy()[0, 0]
+    ref = PwganOracle(sd, PwganConfig()).inference(mel[0], noise[0, 0])
+    assert y.shape == ref.shape == (5 * 256,)
+    assert np.abs(y - ref).max() <= 1e-4
+
+
+def test_glow_short_utterances_vs_oracle():
+    """Edge: two-token and three-token utterances batched with a long one (ragged T_x, small T_y)."""
+    from oracle.glow_np import GlowOracle
+    from tts_amd import GlowTts
+    from tts_amd.spec import GlowConfig, glow_spec
+    _dev()
+    fx = load_fixture("glow")
+    sd = synth_state_dict(glow_spec(GlowConfig()), int(fx["seed"]))
+    m = GlowTts(num_chars=GlowConfig().num_chars)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    orc = GlowOracle(sd)
+    long_ids = fx["u1_ids"]
+
+    def short(n):  # the first n-token window whose T_y >= 2 (T_y < 2 leaves the reference's squeeze empty)
+        for s0 in range(len(long_ids) - n):
+            if orc.inference(long_ids[s0:s0 + n], None, 0.0, 1.0)[4] >= 2:
+                return long_ids[s0:s0 + n]
+        raise AssertionError("no usable window")
+    cands = [short(2), short(3), long_ids]
+    outs = [orc.inference(x, None, 0.0, 1.0) for x in cands]
+    Ty = max(o[4] for o in outs)
+    batch = np.zeros((3, len(long_ids)), np.int64)
+    for i, x in enumerate(cands):
+        batch[i, :len(x)] = x
+    m.noise_scale = 0.0
+    y, _, ym, _, attn, _, _ = m.inference(torch.from_numpy(batch).cuda(), [len(x) for x in cands],
+                                          noise=torch.zeros(3, 80, Ty).cuda())
+    y = y.cpu().numpy()
+    for i, (yr, ymr, ar, _, ty) in enumerate(outs):
+        assert int(m.last_y_lengths[i]) == ty
+        assert np.array_equal(attn.cpu().numpy()[i, :ty, :len(cands[i])], ar)
+        assert np.abs(y[i, :, :yr.shape[1]] - yr).max() <= 1e-4
