@@ -317,6 +317,41 @@ def test_tacotron2_random_batch_vs_oracle():
         assert not align[i, :, L:].any()
 
 
+@pytest.mark.parametrize("variant", ["graves", "fwdmask", "window_softmax"])
+def test_tacotron2_variant_random_batch_vs_oracle(variant):
+    """Decoder variants on 6 ragged utterances (1 to 40 tokens, forced lengths) against the oracle:
+    Graves attention, forward attention with the mask (its Python index wrap fires on short rows),
+    softmax windowing."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    kw = {"graves": dict(attn_type="graves"),
+          "fwdmask": dict(forward_attn=True, trans_agent=True, forward_attn_mask=True),
+          "window_softmax": dict(attn_norm="softmax", windowing=True)}[variant]
+    cfg = TacotronConfig(**kw)
+    _, sd = taco_state_dict(None, seed=13, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    r = 2
+    m.decoder.set_r(r)
+    rs = np.random.RandomState(6)
+    lens = [17, 5, 40, 2, 29, 12]
+    steps = [9, 14, 6, 3, 11, 7]
+    batch = np.zeros((len(lens), max(lens)), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, L)
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=lens, max_decoder_steps=steps)
+    assert list(m.last_steps) == steps
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r, windowing=cfg.windowing, forward_attn=cfg.forward_attn,
+                     trans_agent=cfg.trans_agent, forward_attn_mask=cfg.forward_attn_mask, attn_type=cfg.attn_type,
+                     attn_K=cfg.attn_K)
+    post, align = post.cpu().numpy(), align.cpu().numpy()
+    for i, L in enumerate(lens):
+        _, p, a, _ = orc.inference(batch[i, :L], r, steps[i])
+        M = steps[i] * r
+        assert np.abs(post[i, :M] - p).max() <= MEL_TOL
+        assert np.abs(align[i, :steps[i], :L] - a).max() <= 1e-5
+
+
 def test_tacotron2_batch_tiles_shrink_vs_oracle():
     """37 utterances (3 batch tiles) in caller order with the long ones scattered: the decoder
     decodes longest-first and drops to 2 and then 1 batch tile as rows finish; every row must
