@@ -813,3 +813,49 @@ def test_glow_short_utterances_vs_oracle():
         assert int(m.last_y_lengths[i]) == ty
         assert np.array_equal(attn.cpu().numpy()[i, :ty, :len(cands[i])], ar)
         assert np.abs(y[i, :, :yr.shape[1]] - yr).max() <= 1e-4
+
+
+def test_bench_workload_full_size_vs_oracle():
+    """The headline workload at its full size (bench.py: 32 LJ-profile utterances in one batch,
+    r = 2, forced lengths of up to 429 decoder steps, the bench's own weights), every utterance
+    checked against the oracle run at B = 1, like the reference CPU path: mel L-inf within 1e-4
+    (north_star), alignment argmax indices identical; and the MB-MelGAN waveform of the shortest
+    utterance within WAV_TOL. Measured: mel error ~1e-6 at 429 steps."""
+    import bench
+    from oracle.melgan_np import MelganOracle
+    from oracle.taco_np import TacoOracle
+    from tts_amd.pqmf import pqmf_filters
+    from tts_amd.spec import melgan_layers
+    from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids
+    dev = _dev()
+    taco, tsd, voc, vsd, tcfg, vcfg = bench.build_models(dev)
+    r = 2
+    taco.decoder.set_r(r)
+    taco.decoder.verbose = False
+    T_prof, M_prof = lj_profile()
+    ids = synthetic_ids(T_prof)
+    steps = forced_steps(M_prof, r)
+    batch, lens = pad_batch(ids)
+    with torch.no_grad():
+        dec, post, align, stop = taco.inference(torch.from_numpy(batch).to(dev), text_lengths=lens,
+                                                max_decoder_steps=steps)
+        assert list(taco.last_steps) == list(steps)
+        short = int(np.argmin(steps))  # vocoder on the shortest row alone (a padded batch would convolve the zeros)
+        mel = post[short:short + 1, :steps[short] * r].transpose(1, 2).contiguous()
+        wav = voc.inference(mel).cpu().numpy()
+    post, align = post.cpu().numpy(), align.cpu().numpy()
+    to = TacoOracle(tsd, tcfg.attn_norm, tcfg.r)
+    vo = MelganOracle(vsd, melgan_layers(vcfg), pqmf_filters()[1])
+    worst = 0.0
+    for i in range(len(ids)):
+        L, S = len(ids[i]), steps[i]
+        _, p, a, _ = to.inference(ids[i], r, S)
+        M = S * r
+        err = float(np.abs(post[i, :M] - p).max())
+        worst = max(worst, err)
+        assert err <= MEL_TOL, (i, L, S, err)
+        assert (align[i, :S, :L].argmax(1) == a.argmax(1)).all(), i
+        if i == short:
+            ref = vo.inference(p.T, pad=0).reshape(-1)
+            assert wav.size == ref.size and np.abs(wav.reshape(-1) - ref).max() <= WAV_TOL
+    print(f"32 utterances, worst mel error {worst:.2e}")
