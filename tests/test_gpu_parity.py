@@ -859,3 +859,43 @@ def test_bench_workload_full_size_vs_oracle():
             ref = vo.inference(p.T, pad=0).reshape(-1)
             assert wav.size == ref.size and np.abs(wav.reshape(-1) - ref).max() <= WAV_TOL
     print(f"32 utterances, worst mel error {worst:.2e}")
+
+
+def test_glow_lj_batch_full_size_vs_oracle():
+    """Glow-TTS on tools/glow_bench.py's workload at full size (32 LJ-profile utterances, 3346
+    tokens, ~19 k frames, seed-3 weights), every utterance against the oracle at B = 1: y_lengths and
+    the path exact, mel <= 1e-4. length_scale is taken near the bench's calibrated value where every
+    token's ceil((exp(logw) - 1) * ls) argument is >= 2e-5 away from an integer, so the ~1e-6
+    differences in logw cannot flip a duration (the reference itself is only defined up to that)."""
+    from oracle.glow_np import GlowOracle
+    from tts_amd import GlowTts
+    from tts_amd.spec import GlowConfig, glow_spec
+    from tts_amd.workload import lj_profile, pad_batch, synthetic_ids
+    _dev()
+    cfg = GlowConfig()
+    sd = synth_state_dict(glow_spec(cfg), 3)
+    m = GlowTts(num_chars=cfg.num_chars)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    T, M = lj_profile()
+    ids = synthetic_ids(T)
+    orc = GlowOracle(sd)
+    w = [np.exp(orc.encode(x)[1].astype(np.float64)).reshape(-1) - 1 for x in ids]
+    base = sum(M) / float(sum(np.ceil(np.maximum(v, 0)).sum() for v in w))
+    ls = next(s for s in base * (1 + 0.01 * np.arange(20))
+              if min(np.abs(v * s - np.round(v * s)).min() for v in w) > 2e-5)
+    outs = [orc.inference(x, None, 0.0, ls) for x in ids]
+    batch, lens = pad_batch(ids)
+    m.length_scale, m.noise_scale = float(ls), 0.0
+    Ty = max(o[4] for o in outs)
+    y, _, _, _, attn, _, _ = m.inference(torch.from_numpy(batch).cuda(), lens,
+                                         noise=torch.zeros(len(ids), 80, Ty).cuda())
+    y, attn = y.cpu().numpy(), attn.cpu().numpy()
+    worst = 0.0
+    for i, (yr, _, ar, _, ty) in enumerate(outs):
+        assert int(m.last_y_lengths[i]) == ty, i
+        assert np.array_equal(attn[i, :ty, :len(ids[i])], ar), i
+        err = float(np.abs(y[i, :, :yr.shape[1]] - yr).max())
+        worst = max(worst, err)
+        assert err <= 1e-4, (i, err)
+    print(f"32 utterances, {int(m.last_y_lengths.sum())} frames, length_scale {ls:.4f}, worst mel error {worst:.2e}")
