@@ -819,8 +819,9 @@ def test_bench_workload_full_size_vs_oracle():
     """The headline workload at its full size (bench.py: 32 LJ-profile utterances in one batch,
     r = 2, forced lengths of up to 429 decoder steps, the bench's own weights), every utterance
     checked against the oracle run at B = 1, like the reference CPU path: mel L-inf within 1e-4
-    (north_star), alignment argmax indices identical; and the MB-MelGAN waveform of the shortest
-    utterance within WAV_TOL. Measured: mel error ~1e-6 at 429 steps."""
+    (north_star), alignment argmax indices identical; the MB-MelGAN waveform of the shortest
+    utterance within WAV_TOL, and the batched vocoder call's rows (per-row lengths) bit-identical to
+    B = 1 calls. Measured: mel error ~1e-6 at 429 steps."""
     import bench
     from oracle.melgan_np import MelganOracle
     from oracle.taco_np import TacoOracle
@@ -843,6 +844,13 @@ def test_bench_workload_full_size_vs_oracle():
         short = int(np.argmin(steps))  # vocoder on the shortest row alone (a padded batch would convolve the zeros)
         mel = post[short:short + 1, :steps[short] * r].transpose(1, 2).contiguous()
         wav = voc.inference(mel).cpu().numpy()
+        # the bench's batched vocoder call (per-row lengths): every row equals its own B = 1 call
+        mlens = [S * r for S in steps]
+        wavb = voc.inference(post.transpose(1, 2).contiguous(), lengths=mlens).cpu().numpy()
+        for i in (short, int(np.argmax(steps)), len(steps) // 2):
+            one = voc.inference(post[i:i + 1, :mlens[i]].transpose(1, 2).contiguous()).cpu().numpy()
+            assert np.array_equal(wavb[i, 0, :one.shape[-1]], one[0, 0]), i
+            assert not wavb[i, 0, one.shape[-1]:].any(), i
     post, align = post.cpu().numpy(), align.cpu().numpy()
     to = TacoOracle(tsd, tcfg.attn_norm, tcfg.r)
     vo = MelganOracle(vsd, melgan_layers(vcfg), pqmf_filters()[1])
