@@ -907,3 +907,33 @@ def test_glow_lj_batch_full_size_vs_oracle():
         worst = max(worst, err)
         assert err <= 1e-4, (i, err)
     print(f"32 utterances, {int(m.last_y_lengths.sum())} frames, length_scale {ls:.4f}, worst mel error {worst:.2e}")
+
+
+def test_pwgan_lj_batch_full_size_batched_equals_single():
+    """ParallelWaveGAN at tools/pwgan_bench.py's size (32 LJ-profile mel lengths, 4.9 M samples in
+    one call, explicit noise): the shortest, median and longest rows of the batched call are
+    bit-identical to B = 1 calls on the same mel and noise, and zero past their length. (The oracle
+    runs ~2.6 k samples/s, too slow at this size; parity vs the oracle is the small-size tests.)"""
+    from tts_amd import ParallelWaveganGenerator
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    from tts_amd.workload import lj_profile
+    _dev()
+    sd = synth_state_dict(pwgan_spec(PwganConfig()), 5)
+    g = ParallelWaveganGenerator(inference_padding=0)
+    g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    g = g.cuda().eval()
+    _, M = lj_profile()
+    rs = np.random.RandomState(8)
+    mel = np.zeros((len(M), 80, max(M)), np.float32)
+    for i, m in enumerate(M):
+        mel[i, :, :m] = rs.normal(0, 1, (80, m))
+    noise = torch.randn(len(M), 1, max(M) * 256, generator=torch.Generator().manual_seed(2)).cuda()
+    melt = torch.from_numpy(mel).cuda()
+    with torch.no_grad():
+        yb = g.inference(melt, lengths=list(M), noise=noise).cpu().numpy()
+        for i in (int(np.argmin(M)), len(M) // 2, int(np.argmax(M))):
+            n = M[i] * 256
+            y1 = g.inference(melt[i:i + 1, :, :M[i]], noise=noise[i:i + 1, :, :n].contiguous()).cpu().numpy()
+            assert y1.shape[-1] == n
+            assert np.array_equal(yb[i, 0, :n], y1[0, 0]), i
+            assert not yb[i, 0, n:].any(), i
