@@ -24,6 +24,17 @@
  * owned by the caller; h_ are host memory. `stream` is a hipStream_t (NULL = default stream);
  * work is ordered after prior work on `stream` and later work on `stream` is ordered after it.
  * Tensors are fp32, C-contiguous, in the layouts documented per function.
+ *
+ * Threads: a context may be shared by host threads. Every entry point that takes a context holds
+ * that context's (recursive) mutex for the whole call, so calls on one context run one at a time;
+ * sequences that must not interleave (load a model then infer with it, glow_encode then
+ * glow_decode) need a caller-side lock around them (the Python layer's Engine.lock). Different
+ * contexts (one per device) run concurrently. The reference model is not re-entrant at all
+ * (per-call state on self: TTS/tts/layers/tacotron2.py:221-233).
+ *
+ * Grid barriers: the persistent decoder / BiLSTM / GE2E kernels give up a barrier wait after
+ * TTS_BARRIER_TIMEOUT_MS (environment, default 2000) and the call returns an error; nothing is
+ * left half-written that a retry depends on, so retrying the call is safe.
  */
 #ifndef TTSHIP_H
 #define TTSHIP_H

@@ -389,6 +389,93 @@ def test_tacotron2_batch_tiles_shrink_vs_oracle():
         assert not dec[i, M:].any() and not post[i, M:].any()
 
 
+def test_tacotron2_multichunk_ragged_steps_vs_oracle():
+    """B = 70 (two library calls of 64 and 6 rows) with the longest row in the second chunk:
+    the joined outputs keep every row's frames and zero padding, and sampled rows of both
+    chunks equal their B = 1 oracle runs."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=17, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    r = 2
+    m.decoder.set_r(r)
+    m.decoder.verbose = False
+    rs = np.random.RandomState(21)
+    B = 70
+    lens = [int(x) for x in rs.randint(1, 20, B)]
+    steps = [int(x) for x in rs.randint(2, 7, B)]
+    steps[66] = 15
+    batch = np.zeros((B, max(lens)), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, L)
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=lens, max_decoder_steps=steps)
+    assert list(m.last_steps) == steps
+    S = max(steps)
+    assert dec.shape == (B, S * r, 80) and align.shape == (B, S, max(lens)) and stop.shape == (B, S, 1)
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    post, align = post.cpu().numpy(), align.cpu().numpy()
+    for i in (0, 31, 63, 64, 66, 69):
+        L = lens[i]
+        _, p, a, _ = orc.inference(batch[i, :L], r, steps[i])
+        M = steps[i] * r
+        assert np.abs(post[i, :M] - p).max() <= MEL_TOL, i
+        assert np.abs(align[i, :steps[i], :L] - a).max() <= 1e-5, i
+    for i in range(B):
+        assert not post[i, steps[i] * r:].any() and not align[i, steps[i]:].any()
+
+
+def test_engine_concurrent_threads_match_sequential():
+    """Two host threads share one device context (two Tacotron2 models, so every call re-checks
+    and reloads the packed weights, plus the vocoder) on their own streams: every result equals
+    the same call made alone."""
+    import threading
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    models = []
+    for seed in (31, 32):
+        _, sd = taco_state_dict(None, seed=seed, overrides={}, stop_bias=-1e4, cfg=cfg)
+        m = build_taco(cfg, sd)
+        m.decoder.set_r(2)
+        m.decoder.verbose = False
+        models.append(m)
+    vcfg, vsd = melgan_state_dict(3)
+    voc = build_melgan(vcfg, vsd)
+    voc.inference_padding = 0
+    rs = np.random.RandomState(3)
+    ids = [torch.from_numpy(rs.randint(1, 129, (3, 15))).cuda() for _ in models]
+
+    def run(k):
+        _, post, _, _ = models[k].inference(ids[k], max_decoder_steps=[6, 9, 4])
+        wav = voc.inference(post.transpose(1, 2).contiguous(), lengths=models[k].last_mel_lengths)
+        torch.cuda.current_stream().synchronize()
+        return post.cpu(), wav.cpu()
+
+    want = [run(k) for k in (0, 1)]
+    got = {0: [], 1: []}
+    errs = []
+
+    def worker(k):
+        try:
+            with torch.cuda.stream(torch.cuda.Stream()):
+                for _ in range(4):
+                    got[k].append(run(k))
+        except Exception as e:  # pragma: no cover - reported below
+            errs.append(e)
+
+    th = [threading.Thread(target=worker, args=(k,)) for k in (0, 1)]
+    for t in th:
+        t.start()
+    for t in th:
+        t.join()
+    assert not errs, errs
+    for k in (0, 1):
+        for post, wav in got[k]:
+            assert torch.equal(post, want[k][0]) and torch.equal(wav, want[k][1])
+
+
 def test_tacotron2_deterministic():
     _dev()
     fx = load_fixture("taco_sigmoid")

@@ -223,3 +223,81 @@ def test_bidirectional_decoder_keys():
     bwd = [k for k in keys if k.startswith("decoder_backward.")]
     assert bwd == ["decoder_backward." + k[len("decoder."):] for k in dec]
     assert keys.index(bwd[-1]) < keys.index("coarse_decoder.prenet.linear_layers.0.linear_layer.weight")
+
+
+class _FakeTacoEngine:
+    """Stands in for the library context: records the chunks the host logic hands it and fills
+    each row's outputs with recognisable values up to that row's own step count."""
+
+    def __init__(self):
+        import threading
+        self.lock = threading.RLock()
+        self.taco_key = None
+        self.calls = []
+
+    def load_tacotron(self, *a, **k):
+        pass
+
+    def taco_infer(self, ids, lens, r, ms, S_cap, thr, dec, post, align, stop, speaker_ids=None,
+                   speaker_embeddings=None):
+        assert self.lock._is_owned()  # the model holds the engine lock across the call
+        nb = ids.shape[0]
+        self.calls.append((nb, S_cap, ids.shape[1]))
+        steps = np.asarray(ms, np.int32).copy()
+        dec.zero_(), post.zero_(), align.zero_(), stop.zero_()
+        for i in range(nb):
+            tag = float(ids[i, 0])
+            dec[i, :steps[i] * r] = tag
+            post[i, :steps[i] * r] = tag + 0.5
+            align[i, :steps[i], :int(lens[i])] = tag
+            stop[i, :steps[i]] = tag
+        return steps, np.full(nb, 2, np.int32)
+
+
+def test_tacotron2_multichunk_join_ragged_steps(monkeypatch):
+    """B = 70 splits into chunks of 64 and 6 that decode to different S_cap (the second chunk
+    longer than the first, then shorter): every row keeps its own frames and zero padding, in
+    the caller's order (the join used to assume equal chunk lengths)."""
+    import tts_amd.tacotron2 as tmod
+    eng = _FakeTacoEngine()
+    monkeypatch.setattr(tmod, "get_engine", lambda dev: eng)
+    m = Tacotron2(num_chars=129, r=7, attn_norm="sigmoid")
+    m.decoder.set_r(2)
+    m.decoder.verbose = False
+    B = 70
+    rs = np.random.RandomState(0)
+    for long_chunk in (0, 1):
+        lens = rs.randint(1, 30, B)
+        steps = rs.randint(1, 6, B)
+        steps[64 + 2 if long_chunk else 5] = 17  # the longest row sits in one chunk only
+        ids = np.zeros((B, lens.max()), np.int64)
+        for i in range(B):
+            ids[i, :lens[i]] = i + 1
+        eng.calls.clear()
+        dec, post, align, stop = m.inference(torch.from_numpy(ids), text_lengths=lens, max_decoder_steps=steps)
+        assert [c[0] for c in eng.calls] == [64, 6]
+        S = int(steps.max())
+        assert dec.shape == (B, 2 * S, 80) and post.shape == (B, 2 * S, 80)
+        assert align.shape == (B, S, lens.max()) and stop.shape == (B, S, 1)
+        for i in range(B):
+            M = 2 * steps[i]
+            assert (dec[i, :M] == i + 1).all() and not dec[i, M:].any()
+            assert (post[i, :M] == i + 1.5).all() and not post[i, M:].any()
+            assert (align[i, :steps[i], :lens[i]] == i + 1).all() and not align[i, :, lens[i]:].any()
+            assert not align[i, steps[i]:].any() and not stop[i, steps[i]:].any()
+        assert list(m.last_steps) == list(steps)
+
+
+def test_single_speaker_model_ignores_speaker_arguments(monkeypatch):
+    """models/tacotron2.py:152: speaker_ids / speaker_embeddings are ignored when num_speakers <= 1."""
+    import tts_amd.tacotron2 as tmod
+    eng = _FakeTacoEngine()
+    monkeypatch.setattr(tmod, "get_engine", lambda dev: eng)
+    m = Tacotron2(num_chars=129, r=2, attn_norm="sigmoid")
+    m.decoder.verbose = False
+    ids = torch.ones(1, 5, dtype=torch.long)
+    a = m.inference(ids, max_decoder_steps=3)
+    b = m.inference(ids, speaker_ids=torch.tensor([3]), speaker_embeddings=torch.ones(1, 256),
+                    max_decoder_steps=3)
+    for x, y in zip(a, b):
+        assert torch.equal(x, y)

@@ -111,6 +111,11 @@ class Engine:
     def __init__(self, device_index: int):
         self.lib = load_library()
         self.device = device_index
+        # Held by every model across its weight check-and-upload (``_sync``) and its whole compute
+        # sequence: the context's workspace, graphs and packed weights are shared by all models on
+        # this device, and ctypes releases the GIL inside each call. (Each C entry point also locks
+        # the context; this lock makes multi-call sequences such as Glow encode + decode atomic.)
+        self.lock = threading.RLock()
         h = ctypes.c_void_p()
         _check(self.lib.tts_ctx_create(device_index, ctypes.byref(h)))
         self.h = h

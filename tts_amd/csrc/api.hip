@@ -11,6 +11,7 @@
 #include <cstring>
 #include <map>
 #include <memory>
+#include <mutex>
 #include <stdexcept>
 #include <string>
 #include <vector>
@@ -367,6 +368,7 @@ struct PwganWS {
 };
 
 struct tts_ctx {
+  std::recursive_mutex mu;  // held by every entry point (guarded_ctx)
   int device = 0;
   hipStream_t s = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_chunk[2] = {nullptr, nullptr};
@@ -1021,7 +1023,7 @@ void check_encoder_barrier(tts_ctx* c) {
   unsigned err2 = 0;
   HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(c->tws.lc.p) + 16, 4, hipMemcpyDeviceToHost));
   HIP_OK(hipMemcpy(&err2, reinterpret_cast<unsigned*>(c->tws.lc.p) + 512 + 16, 4, hipMemcpyDeviceToHost));
-  TTS_CHECK(err == 0 && err2 == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident)");
+  TTS_CHECK(err == 0 && err2 == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
 }
 
 void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int B, int Mmax_alloc, int max_q,
@@ -1411,7 +1413,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   if (persist) {
     unsigned err = 0;
     HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(W.pbar.p) + 16, 4, hipMemcpyDeviceToHost));
-    TTS_CHECK(err == 0, "persistent decoder: grid barrier timed out (workgroups not co-resident)");
+    TTS_CHECK(err == 0, "persistent decoder: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
   }
   std::vector<int> res(3 * BMAX);
   HIP_OK(hipMemcpy(res.data(), W.ctl.i() + 4, 3 * BMAX * 4, hipMemcpyDeviceToHost));
@@ -1684,6 +1686,19 @@ int guarded(F&& f) {
   }
 }
 
+// Entry points that take a context hold its mutex for the whole call: a context owns one
+// workspace, one internal stream, cached graphs and pinned polling words, so two host threads
+// (ctypes releases the GIL) must not interleave inside it. Recursive so that helpers may re-enter.
+template <class F>
+int guarded_ctx(tts_ctx* c, F&& f) {
+  if (!c) {
+    tts_set_error("null ctx");
+    return 1;
+  }
+  std::lock_guard<std::recursive_mutex> lk(c->mu);
+  return guarded(std::forward<F>(f));
+}
+
 // (B, T, D) -> (B, T, Dp) with zero channels D..Dp-1 (the conv staging reads 16-channel chunks)
 __global__ void pad_channels_kernel(const float* __restrict__ x, int D, int Dp, long n_rows, float* __restrict__ y) {
   for (long i = (long)blockIdx.x * blockDim.x + threadIdx.x; i < n_rows * Dp; i += (long)gridDim.x * blockDim.x) {
@@ -1832,7 +1847,7 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
   HIP_OK(hipStreamSynchronize(s));
   unsigned err = 0;
   HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(W.bar.p) + 16, 4, hipMemcpyDeviceToHost));
-  TTS_CHECK(err == 0, "speaker encoder: grid barrier timed out (workgroups not co-resident)");
+  TTS_CHECK(err == 0, "speaker encoder: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
 }
 
 // ------------------------------------------------------------------------------------ Glow-TTS
@@ -2412,6 +2427,7 @@ int tts_ctx_create(int device, tts_ctx** out) {
 int tts_ctx_destroy(tts_ctx* c) {
   return guarded([&] {
     if (!c) return;
+    { std::lock_guard<std::recursive_mutex> lk(c->mu); }  // a call still inside the context ends first
     {
       DeviceGuard g(c->device);
       (void)hipStreamSynchronize(c->s);
@@ -2436,7 +2452,7 @@ int tts_ctx_destroy(tts_ctx* c) {
 }
 
 int tts_taco_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     set_tensor(c->taco_host, name, h, shape, ndim);
   });
@@ -2449,7 +2465,7 @@ struct HostMapConsumer {
 };
 
 int tts_taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     TTS_CHECK(attn_norm == 0 || attn_norm == 1, "attn_norm must be 0 (sigmoid) or 1 (softmax)");
     TTS_CHECK(r_init >= 1 && r_init <= 16, "r_init out of range");
@@ -2462,7 +2478,7 @@ int tts_taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
 int tts_taco_infer(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
                    const int32_t* h_max_steps, int S_cap, float thr, float* d_dec, float* d_post, float* d_align,
                    float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && h_steps && h_status,
               "null argument");
     DeviceGuard g(c->device);
@@ -2475,7 +2491,7 @@ int tts_taco_infer_spk(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, 
                        const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
                        const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
                        int32_t* h_steps, int32_t* h_status, void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && h_steps && h_status,
               "null argument");
     DeviceGuard g(c->device);
@@ -2485,7 +2501,7 @@ int tts_taco_infer_spk(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, 
 }
 
 int tts_taco_set_options(tts_ctx* c, int windowing, int forward_attn, int forward_attn_mask) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     c->taco.windowing = windowing != 0;
     c->taco.forward_attn = forward_attn != 0;
@@ -2494,7 +2510,7 @@ int tts_taco_set_options(tts_ctx* c, int windowing, int forward_attn, int forwar
 }
 
 int tts_taco_speaker_dim(tts_ctx* c, int* spk_dim, int* num_speakers) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && spk_dim && num_speakers, "null argument");
     TTS_CHECK(c->taco.ready, "tacotron2 weights not finalized");
     *spk_dim = c->taco.spk_dim;
@@ -2504,7 +2520,7 @@ int tts_taco_speaker_dim(tts_ctx* c, int* spk_dim, int* num_speakers) {
 
 int tts_taco_encoder(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, float* d_out,
                      void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_ids && h_lens && d_out, "null argument");
     TTS_CHECK(c->taco.ready, "tacotron2 weights not finalized");
     TTS_CHECK(B >= 1 && B <= BMAX && T_max >= 1, "bad sizes");
@@ -2523,7 +2539,7 @@ int tts_taco_encoder(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, in
 
 int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int B, int M_max, float* d_out,
                      void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_dec && h_lens && d_out, "null argument");
     TTS_CHECK(c->taco.ready, "tacotron2 weights not finalized");
     TTS_CHECK(B >= 1 && B <= BMAX && M_max >= 1, "bad sizes");
@@ -2550,14 +2566,14 @@ int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int 
 }
 
 int tts_pwgan_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     set_tensor(c->pw_host, name, h, shape, ndim);
   });
 }
 
 int tts_pwgan_finalize(tts_ctx* c, int num_res_blocks, int stacks, const int32_t* upsample_factors, int n_up) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && upsample_factors, "null argument");
     DeviceGuard g(c->device);
     HostMapConsumer consume{c->pw_host};
@@ -2567,7 +2583,7 @@ int tts_pwgan_finalize(tts_ctx* c, int num_res_blocks, int stacks, const int32_t
 
 int tts_pwgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
                     const float* d_noise, float* d_out, void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_mel && h_lens && d_noise && d_out, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
@@ -2577,14 +2593,14 @@ int tts_pwgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B
 }
 
 int tts_glow_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     set_tensor(c->glow_host, name, h, shape, ndim);
   });
 }
 
 int tts_glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int num_flow_blocks, int num_block_layers) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     DeviceGuard g(c->device);
     HostMapConsumer consume{c->glow_host};
@@ -2594,7 +2610,7 @@ int tts_glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int num_flow_bl
 
 int tts_glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, float length_scale,
                     int32_t* h_ylens, void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_ids && h_lens && h_ylens, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
@@ -2605,7 +2621,7 @@ int tts_glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int
 
 int tts_glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, float* d_y, float* d_ymean,
                     float* d_attn, float* d_logw, void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_y && d_ymean && d_attn && d_logw, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
@@ -2615,7 +2631,7 @@ int tts_glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty,
 }
 
 int tts_ge2e_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     set_tensor(c->ge2e_host, name, h, shape, ndim);
   });
@@ -2623,7 +2639,7 @@ int tts_ge2e_set_tensor(tts_ctx* c, const char* name, const float* h, const int6
 
 int tts_ge2e_finalize(tts_ctx* c, int input_dim, int proj_dim, int lstm_dim, int num_lstm_layers,
                       int use_lstm_with_projection) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     DeviceGuard g(c->device);
     HostMapConsumer consume{c->ge2e_host};
@@ -2633,7 +2649,7 @@ int tts_ge2e_finalize(tts_ctx* c, int input_dim, int proj_dim, int lstm_dim, int
 
 int tts_ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int T_max, float* d_out,
                    void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_x && h_lens && d_out, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
@@ -2643,7 +2659,7 @@ int tts_ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, i
 }
 
 int tts_melgan_set_tensor(tts_ctx* c, const char* name, const float* h, const int64_t* shape, int ndim) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     set_tensor(c->mg_host, name, h, shape, ndim);
   });
@@ -2651,7 +2667,7 @@ int tts_melgan_set_tensor(tts_ctx* c, const char* name, const float* h, const in
 
 int tts_melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t* ups, int n_up, int nres,
                         int use_pqmf) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && ups && n_up >= 1 && n_up <= 6, "bad arguments");
     DeviceGuard g(c->device);
     HostMapConsumer consume{c->mg_host};
@@ -2661,7 +2677,7 @@ int tts_melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32
 
 int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
                          float* d_out, void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_mel && h_lens && d_out, "null argument");
     TTS_CHECK(pad >= 0, "pad >= 0");
     DeviceGuard g(c->device);
@@ -2673,7 +2689,7 @@ int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, 
 
 int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
                      float* d_wav, void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_mel && h_lens && d_wav, "null argument");
     TTS_CHECK(pad >= 0, "pad >= 0");
     auto& G = c->mg;
@@ -2704,7 +2720,7 @@ int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int 
 
 int tts_pqmf_synthesis(tts_ctx* c, const float* d_x, int B, int N, int L, const float* d_G, int taps, float* d_y,
                        void* stream) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_x && d_G && d_y, "null argument");
     TTS_CHECK(B >= 1 && N >= 1 && N <= 8 && L >= 1 && taps >= 0, "bad sizes");
     DeviceGuard g(c->device);
@@ -2719,7 +2735,7 @@ int tts_pqmf_synthesis(tts_ctx* c, const float* d_x, int B, int N, int L, const 
 }
 
 int tts_decoder_stats(tts_ctx* c, int* path, int* nlaunch, float* ms, int* steps) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && path && nlaunch && ms && steps, "bad arguments");
     TTS_CHECK(c->last_B > 0, "run tts_taco_infer first");
     *path = c->dec_path;
@@ -2734,7 +2750,7 @@ int tts_decoder_stats(tts_ctx* c, int* path, int* nlaunch, float* ms, int* steps
 }
 
 int tts_time_decoder_kernel(tts_ctx* c, int which, int iters, float* ms_out) {
-  return guarded([&] {
+  return guarded_ctx(c, [&] {
     TTS_CHECK(c && ms_out && iters >= 1, "bad arguments");
     TTS_CHECK(c->last_B > 0 && c->tws.graphs[c->tws.MT], "run tts_taco_infer first");
     TTS_CHECK(c->tws.S_cap >= CHUNK + 2, "S_cap too small for timing");

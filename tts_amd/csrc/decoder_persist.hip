@@ -26,8 +26,8 @@
 // Memory model: cross-workgroup data is written with agent-scope relaxed atomic stores (sc1:
 // write-through past the non-coherent per-XCD L2) and read with agent-scope loads (sc1), every
 // wave drains its stores (vmcnt(0)) before the barrier arrival; no L2 invalidation is needed.
-// Barrier waits give up after 0.2 s (error word set, every workgroup exits): a launch that was
-// not fully co-resident fails loudly instead of hanging.
+// Barrier waits give up after TTS_BARRIER_TIMEOUT_MS (default 2 s; error word set, every
+// workgroup exits): a launch that was not fully co-resident fails loudly instead of hanging.
 #include "common.h"
 #include "decoder.h"
 #include "gsync.h"
@@ -1124,8 +1124,8 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
     attr[MT - 1][var] = true;
   }
-  HIP_OK(hipMemsetAsync(a.bar, 0, 512 * 4, s));
+  arm_barrier(a.bar, 1, s);
   PArgs copy = a;
   void* kargs[] = {&copy};
-  HIP_OK(hipLaunchCooperativeKernel(f, dim3(PW), dim3(PT), kargs, P_LDS, s));
+  launch_resident(f, dim3(PW), dim3(PT), kargs, P_LDS, s);
 }

@@ -201,11 +201,11 @@ static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const int*
   if (!coop) return false;
   const int MT = (B + 15) / 16, Bp = MT * 16;
   HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * NDIR * Bp * H * 4, s));
-  HIP_OK(hipMemsetAsync(bar, 0, (size_t)NDIR * 512 * 4, s));
+  arm_barrier(bar, NDIR, s);
   void* args[] = {(void*)&Whh, (void*)&Gin, (void*)&lens, (void*)&T_max, (void*)&B, (void*)&hbuf, (void*)&out, (void*)&bar};
   const void* f = MT == 1 ? (const void*)lstm_persist_kernel<1, H, NDIR> : MT == 2 ? (const void*)lstm_persist_kernel<2, H, NDIR>
                 : MT == 3 ? (const void*)lstm_persist_kernel<3, H, NDIR> : (const void*)lstm_persist_kernel<4, H, NDIR>;
-  HIP_OK(hipLaunchCooperativeKernel(f, dim3(NDIR * H / 4), dim3(256), args, 0, s));
+  launch_resident(f, dim3(NDIR * H / 4), dim3(256), args, 0, s);
   return true;
 }
 

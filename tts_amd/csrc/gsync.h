@@ -3,12 +3,64 @@
 //
 // Memory model: cross-workgroup data is written with agent-scope relaxed atomic stores (sc1:
 // write-through past the per-XCD L2) and read with agent-scope loads (sc1, L1 bypass); every wave
-// drains its stores (vmcnt(0)) before the barrier arrival. Barrier waits give up after 0.2 s
+// drains its stores (vmcnt(0)) before the barrier arrival. Barrier waits give up after a limit
 // (error word set, every workgroup exits): a launch that is not co-resident fails loudly.
+// The wait limit sits in word BAR_TMO of each 512-word barrier block, written by arm_barrier at
+// launch: TTS_BARRIER_TIMEOUT_MS (default 2000 ms). The cooperative launch itself guarantees
+// co-residency; the limit only turns an over-admitted grid (occupancy API one workgroup per CU
+// too high) into an error instead of a hang, so it is generous enough that a workgroup preempted
+// by another queue on the same GPU does not trip it.
 #pragma once
 #include "common.h"
 
-constexpr unsigned long long BAR_TIMEOUT = 20000000ull;  // s_memrealtime ticks (100 MHz): 0.2 s
+#include <cstdlib>
+#include <map>
+#include <mutex>
+
+constexpr int BAR_TMO = 48;  // word of the barrier block holding the wait limit (s_memrealtime ticks)
+
+// zero `nblk` 512-word barrier blocks and write their wait limit (stream-ordered before the launch)
+inline void arm_barrier(unsigned* bar, int nblk, hipStream_t s) {
+  static const unsigned ticks = [] {
+    double ms = 2000.0;
+    if (const char* e = std::getenv("TTS_BARRIER_TIMEOUT_MS")) ms = std::atof(e);
+    ms = ms < 1.0 ? 1.0 : (ms > 40000.0 ? 40000.0 : ms);
+    return (unsigned)(ms * 1e5);  // 100 MHz ticks
+  }();
+  HIP_OK(hipMemsetAsync(bar, 0, (size_t)nblk * 512 * 4, s));
+  for (int i = 0; i < nblk; ++i) HIP_OK(hipMemsetD32Async((hipDeviceptr_t)(bar + i * 512 + BAR_TMO), (int)ticks, 1, s));
+}
+
+// Launch a kernel whose workgroups meet at grid barriers. Every workgroup must be resident at
+// once: that is checked here against the occupancy query, which is all a cooperative launch adds
+// (MI355X_MICROARCH.md "coop-launch": same residency as a plain launch, +15-19 us of host time).
+// hipLaunchCooperativeKernel also sets up HIP's cooperative queue, whose teardown at process exit
+// collides with the HSA runtime rocprofv3 preloads (SIGSEGV in exit() after the profile is
+// written), so the plain launch is the default. TTS_COOP_LAUNCH=1 restores it.
+inline void launch_resident(const void* f, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
+  static std::mutex mu;
+  static std::map<const void*, int> fits;  // kernel -> workgroups the device holds at once
+  static const bool coop = [] {
+    const char* e = std::getenv("TTS_COOP_LAUNCH");
+    return e && std::atoi(e) != 0;
+  }();
+  int cap = 0;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = fits.find(f);
+    if (it == fits.end()) {
+      int dev = 0, cus = 0, nb = 0;
+      HIP_OK(hipGetDevice(&dev));
+      HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, (int)(block.x * block.y * block.z), lds));
+      it = fits.emplace(f, nb * cus).first;
+    }
+    cap = it->second;
+  }
+  TTS_CHECK((long)grid.x * grid.y * grid.z <= cap, "grid-barrier kernel: grid larger than the device holds at once");
+  if (coop) HIP_OK(hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)lds, s));
+  else HIP_OK(hipLaunchKernel(f, grid, block, args, lds, s));
+}
 
 // ------------------------------------------------------------------ coherent access helpers
 __device__ __forceinline__ float ldc(const float* p) {
@@ -57,8 +109,9 @@ __device__ __forceinline__ bool gsync_wait(unsigned* bar, unsigned gen, int* fla
   if (threadIdx.x == 0) {
     int good = 1;
     const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    const unsigned long long tmo = bar[BAR_TMO];
     while (__hip_atomic_load(bar + 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
-      if (__builtin_amdgcn_s_memrealtime() - t0 > BAR_TIMEOUT) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
         __hip_atomic_fetch_or(bar + 16, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         good = 0;
         break;

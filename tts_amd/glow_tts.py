@@ -95,29 +95,30 @@ class GlowTts(nn.Module):
             raise NotImplementedError("speaker conditioning (g) is not implemented")
         dev = self.encoder.emb.weight.device
         eng = get_engine(dev)
-        self._sync(eng)
-        x = torch.as_tensor(x).to(dev, torch.int64)
-        if x.dim() == 1:
-            x = x[None]
-        x = x.contiguous()
-        B, T = x.shape
-        lens = np.asarray(torch.as_tensor(x_lengths).cpu(), np.int64).reshape(-1)
-        if len(lens) != B or lens.min() < 1 or lens.max() > T:
-            raise ValueError("x_lengths must have B entries in [1, T]")
-        if B > 64:
-            raise ValueError("at most 64 utterances per call")
-        ylens = eng.glow_encode(x, lens, float(self.length_scale))
-        Ty = int(ylens.max())
-        if noise is None:
-            noise = torch.randn(B, 80, Ty, device=dev)
-        noise = torch.as_tensor(noise).to(dev, torch.float32)[:, :, :Ty].contiguous()
-        if noise.shape != (B, 80, Ty):
-            raise ValueError(f"noise must be (B, 80, >= {Ty})")
-        y = torch.empty(B, 80, 2 * (Ty // 2), device=dev)
-        y_mean = torch.empty(B, 80, Ty, device=dev)
-        attn = torch.empty(B, Ty, T, device=dev)
-        logw = torch.empty(B, 1, T, device=dev)
-        eng.glow_decode(noise, float(self.noise_scale), Ty, y, y_mean, attn, logw)
+        with eng.lock:  # encode and decode share the context's Glow workspace
+            self._sync(eng)
+            x = torch.as_tensor(x).to(dev, torch.int64)
+            if x.dim() == 1:
+                x = x[None]
+            x = x.contiguous()
+            B, T = x.shape
+            lens = np.asarray(torch.as_tensor(x_lengths).cpu(), np.int64).reshape(-1)
+            if len(lens) != B or lens.min() < 1 or lens.max() > T:
+                raise ValueError("x_lengths must have B entries in [1, T]")
+            if B > 64:
+                raise ValueError("at most 64 utterances per call")
+            ylens = eng.glow_encode(x, lens, float(self.length_scale))
+            Ty = int(ylens.max())
+            if noise is None:
+                noise = torch.randn(B, 80, Ty, device=dev)
+            noise = torch.as_tensor(noise).to(dev, torch.float32)[:, :, :Ty].contiguous()
+            if noise.shape != (B, 80, Ty):
+                raise ValueError(f"noise must be (B, 80, >= {Ty})")
+            y = torch.empty(B, 80, 2 * (Ty // 2), device=dev)
+            y_mean = torch.empty(B, 80, Ty, device=dev)
+            attn = torch.empty(B, Ty, T, device=dev)
+            logw = torch.empty(B, 1, T, device=dev)
+            eng.glow_decode(noise, float(self.noise_scale), Ty, y, y_mean, attn, logw)
         x_mask = (torch.arange(T, device=dev)[None] < torch.as_tensor(lens, device=dev)[:, None]).float()[:, None]
         o_attn_dur = torch.log(1 + attn.sum(1, keepdim=True)) * x_mask
         self.last_y_lengths = ylens

@@ -67,7 +67,6 @@ class SpeakerEncoder(nn.Module):
     def inference(self, x, lengths: Optional[Sequence[int]] = None):
         dev = self._device()
         eng = get_engine(dev)
-        self._sync(eng)
         x = torch.as_tensor(x).to(dev, torch.float32)
         if x.dim() == 2:
             x = x[None]
@@ -79,10 +78,12 @@ class SpeakerEncoder(nn.Module):
         if len(lens) != B or lens.min() < 1 or lens.max() > T:
             raise ValueError("lengths must have B entries in [1, T]")
         out = torch.empty(B, self.cfg.proj_dim, device=dev)
-        for b0 in range(0, B, MAX_SEQS):
-            b1 = min(B, b0 + MAX_SEQS)
-            Tn = int(lens[b0:b1].max())
-            eng.ge2e_infer(x[b0:b1, :Tn].contiguous(), lens[b0:b1], out[b0:b1])
+        with eng.lock:
+            self._sync(eng)
+            for b0 in range(0, B, MAX_SEQS):
+                b1 = min(B, b0 + MAX_SEQS)
+                Tn = int(lens[b0:b1].max())
+                eng.ge2e_infer(x[b0:b1, :Tn].contiguous(), lens[b0:b1], out[b0:b1])
         return out
 
     @torch.no_grad()

@@ -105,9 +105,7 @@ class Tacotron2(nn.Module):
     def _speaker_args(self, speaker_ids, speaker_embeddings, B, dev):
         """Speaker conditioning as the reference takes it (models/tacotron2.py:152-155): ids into
         the learned table, or per-sample embeddings (B, speaker_embedding_dim) / (B, 1, dim)."""
-        if self.num_speakers <= 1:
-            if speaker_ids is not None or speaker_embeddings is not None:
-                raise ValueError("single-speaker model: speaker_ids / speaker_embeddings must be None")
+        if self.num_speakers <= 1:  # the reference ignores both arguments here (models/tacotron2.py:152)
             return None, None
         if self.embeddings_per_sample:
             if speaker_embeddings is None:
@@ -162,7 +160,6 @@ class Tacotron2(nn.Module):
             raise NotImplementedError("GST style conditioning is not implemented (SURVEY.md §8f)")
         dev = self.embedding.weight.device
         eng = get_engine(dev)
-        self._sync(eng)
         text = torch.as_tensor(text).to(dev, torch.int64)
         if text.dim() == 1:
             text = text[None]
@@ -182,22 +179,23 @@ class Tacotron2(nn.Module):
             self.cfg.attn_type == "graves"
         limit = BATCH_LIMIT if self.num_speakers <= 1 and not variant else SPEAKER_BATCH_LIMIT
         outs = []
-        for b0 in range(0, B, limit):
-            b1 = min(B, b0 + limit)
-            sub = text[b0:b1]
-            Tn = int(lens[b0:b1].max())
-            sub = sub[:, :Tn].contiguous()
-            S_cap = int(ms[b0:b1].max())
-            nb = b1 - b0
-            dec = torch.empty(nb, S_cap * r, 80, device=dev, dtype=torch.float32)
-            post = torch.empty_like(dec)
-            align = torch.empty(nb, S_cap, Tn, device=dev, dtype=torch.float32)
-            stop = torch.empty(nb, S_cap, device=dev, dtype=torch.float32)
-            steps, status = eng.taco_infer(
-                sub, lens[b0:b1], r, ms[b0:b1], S_cap, self.decoder.stop_threshold, dec, post, align, stop,
-                speaker_ids=None if spk_ids is None else spk_ids[b0:b1].contiguous(),
-                speaker_embeddings=None if spk_emb is None else spk_emb[b0:b1].contiguous())
-            outs.append((dec, post, align, stop, steps, status, Tn))
+        with eng.lock:
+            self._sync(eng)
+            for b0 in range(0, B, limit):
+                b1 = min(B, b0 + limit)
+                Tn = int(lens[b0:b1].max())
+                sub = text[b0:b1, :Tn].contiguous()
+                S_cap = int(ms[b0:b1].max())
+                nb = b1 - b0
+                dec = torch.empty(nb, S_cap * r, 80, device=dev, dtype=torch.float32)
+                post = torch.empty_like(dec)
+                align = torch.empty(nb, S_cap, Tn, device=dev, dtype=torch.float32)
+                stop = torch.empty(nb, S_cap, device=dev, dtype=torch.float32)
+                steps, status = eng.taco_infer(
+                    sub, lens[b0:b1], r, ms[b0:b1], S_cap, self.decoder.stop_threshold, dec, post, align, stop,
+                    speaker_ids=None if spk_ids is None else spk_ids[b0:b1].contiguous(),
+                    speaker_embeddings=None if spk_emb is None else spk_emb[b0:b1].contiguous())
+                outs.append((dec, post, align, stop, steps, status))
         steps = np.concatenate([o[4] for o in outs])
         status = np.concatenate([o[5] for o in outs])
         if getattr(self.decoder, "verbose", True):  # reference behaviour (tacotron2.py:365); bench.py mutes it
@@ -206,20 +204,26 @@ class Tacotron2(nn.Module):
                     print("   | > Decoder stopped with 'max_decoder_steps")
         S = int(steps.max())
         M = S * r
-        dec = torch.cat([o[0][:, :M] for o in outs]) if len(outs) > 1 else outs[0][0][:, :M]
-        post = torch.cat([o[1][:, :M] for o in outs]) if len(outs) > 1 else outs[0][1][:, :M]
-        if len(outs) > 1:
-            align = torch.zeros(B, S, T, device=dev)
-            b0 = 0
-            for o in outs:
-                n = o[2].shape[0]
-                align[b0:b0 + n, :, :o[6]] = o[2][:, :S]
-                b0 += n
-        else:
-            align = outs[0][2][:, :S]
+        if len(outs) == 1:
+            dec, post, align, stop = outs[0][0][:, :M], outs[0][1][:, :M], outs[0][2][:, :S], outs[0][3][:, :S]
             if align.shape[2] != T:
                 align = torch.nn.functional.pad(align, (0, T - align.shape[2]))
-        stop = torch.cat([o[3][:, :S] for o in outs]) if len(outs) > 1 else outs[0][3][:, :S]
+        else:
+            # chunks of a split batch decode to their own S_cap; each is cut or zero-padded to the
+            # batch's S steps (M frames) before joining (a chunk's rows are zero past their own steps)
+            dec = torch.zeros(B, M, 80, device=dev)
+            post = torch.zeros(B, M, 80, device=dev)
+            align = torch.zeros(B, S, T, device=dev)
+            stop = torch.zeros(B, S, device=dev)
+            b0 = 0
+            for o in outs:
+                n, Sc, Tn = o[2].shape
+                s_ = min(S, Sc)
+                dec[b0:b0 + n, :s_ * r] = o[0][:, :s_ * r]
+                post[b0:b0 + n, :s_ * r] = o[1][:, :s_ * r]
+                align[b0:b0 + n, :s_, :Tn] = o[2][:, :s_]
+                stop[b0:b0 + n, :s_] = o[3][:, :s_]
+                b0 += n
         self.last_steps = steps
         self.last_mel_lengths = steps * r
         self.last_status = status

@@ -40,7 +40,8 @@ class PQMF(Container):
             raise ValueError(f"expected {self.N} subbands, got {N}")
         y = torch.empty(B, 1, N * L, device=x.device, dtype=torch.float32)
         G = self.G.to(x.device, torch.float32).reshape(N, -1).contiguous()
-        eng.pqmf_synthesis(x, G, y)
+        with eng.lock:
+            eng.pqmf_synthesis(x, G, y)
         return y
 
     def analysis(self, x):  # training-only path in the reference (pqmf.py:48-49)
@@ -116,7 +117,6 @@ class MelganGenerator(nn.Module):
     def _prep(self, c, lengths):
         dev = self.layers._modules["1"].bias.device
         eng = get_engine(dev)
-        self._sync(eng)
         c = torch.as_tensor(c).to(dev, torch.float32)
         if c.dim() == 2:
             c = c[None]
@@ -137,7 +137,9 @@ class MelganGenerator(nn.Module):
         B, _, M = c.shape
         up = int(np.prod(self.cfg.upsample_factors))
         out = torch.empty(B, self.cfg.out_channels, up * (M + 2 * pad), device=c.device)
-        eng.melgan_generator(c, lens, pad, out)
+        with eng.lock:
+            self._sync(eng)
+            eng.melgan_generator(c, lens, pad, out)
         return out
 
     @torch.no_grad()
@@ -168,7 +170,9 @@ class MultibandMelganGenerator(MelganGenerator):
         eng, c, lens, pad = self._prep(cond_features, lengths)
         B, _, M = c.shape
         wav = torch.empty(B, 1, self.hop * (M + 2 * pad), device=c.device)
-        eng.melgan_infer(c, lens, pad, wav)
+        with eng.lock:
+            self._sync(eng)
+            eng.melgan_infer(c, lens, pad, wav)
         return wav
 
 
@@ -261,7 +265,6 @@ class ParallelWaveganGenerator(nn.Module):
     def inference(self, c, lengths: Optional[Sequence[int]] = None, noise: Optional[torch.Tensor] = None):
         dev = self.first_conv.bias.device
         eng = get_engine(dev)
-        self._sync(eng)
         c = torch.as_tensor(c).to(dev, torch.float32)
         if c.dim() == 2:
             c = c[None]
@@ -278,5 +281,7 @@ class ParallelWaveganGenerator(nn.Module):
         if tuple(noise.shape) != (B, 1, T):
             raise ValueError(f"noise must be (B, 1, {T})")
         out = torch.empty(B, 1, T, device=dev)
-        eng.pwgan_infer(c, lens, pad, noise, out)
+        with eng.lock:
+            self._sync(eng)
+            eng.pwgan_infer(c, lens, pad, noise, out)
         return out
