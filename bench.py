@@ -98,6 +98,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=15.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
+    ap.add_argument("--f32-steps", type=int, default=3, help="steps re-timed with fp32-MFMA GEMMs only (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -170,9 +171,23 @@ def main():
     taco_ms, voc_ms = float(np.median(tt)), float(np.median(tv))
     my_frames = int(sum(s * r for s in steps))
 
-    # dominant decoder kernel, timed live with HIP events on the library's stream
     from tts_amd._lib import get_engine
     eng = get_engine(dev)
+    gemm_mode, fallbacks = eng.gemm_mode()
+    # the same step with every GEMM on the fp32 MFMA (no split-f16 kernels), for comparison
+    f32_ms = None
+    if gemm_mode == "x3" and args.f32_steps > 0:
+        eng.set_gemm_mode("f32")
+        one_step(False)
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.f32_steps):
+            one_step(False)
+        torch.cuda.synchronize()
+        f32_ms = (time.perf_counter() - t1) / args.f32_steps * 1000.0
+        eng.set_gemm_mode("x3")
+
+    # dominant decoder kernel, timed live with HIP events on the library's stream
     path, launches = eng.decoder_stats()
     if path == 1:
         # persistent decoder: the MT = 2 launch (32-row batch tile) carries most steps. Algorithmic
@@ -233,6 +248,10 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": "f32",
+        "gemm": ("split-f16 MFMA, fp32-accurate (split16.h: 3 f16 products per fp32 product, fp32 accumulate)"
+                 if gemm_mode == "x3" else "fp32 MFMA"),
+        "f32_gemm_ms_per_step": None if f32_ms is None else round(f32_ms, 3),
+        "x3_range_fallbacks": fallbacks,
         "data": "synthetic (LJ-profile lengths, RandomState(0) ids, seeded random weights, forced length)",
         "config": {"workload": f"C{2 if world == 1 else 3}: Tacotron2-DDC (r_init=7, r={r}, sigmoid attn) + "
                                f"MB-MelGAN [8,4,2]x4, {args.per_gpu_batch} LJ-length utterances per GPU",

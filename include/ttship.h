@@ -172,6 +172,15 @@ int tts_time_decoder_kernel(tts_ctx* ctx, int which, int iters, float* ms_out);
    decoder steps it completed), path 0 = step graphs (nlaunch = 0). */
 int tts_decoder_stats(tts_ctx* ctx, int* path, int* nlaunch, float* ms, int* steps);
 
+/* GEMM arithmetic of the context's kernels. mode 1 (default) = split-f16 MFMA where a kernel has
+   it: every fp32 operand as hi + 2^-11 lo f16 halves, three f16 MFMAs per product accumulated in
+   fp32, error equal to the fp32 MFMA GEMM's; a call whose operands leave the f16
+   range (|v| >= 65504) is re-run on the fp32 kernels. mode 0 = fp32 MFMA everywhere. The
+   environment variable TTS_GEMM=f32 starts contexts in mode 0. tts_gemm_mode reports the mode and
+   how many calls fell back to fp32. */
+int tts_set_gemm_mode(tts_ctx* ctx, int mode);
+int tts_gemm_mode(tts_ctx* ctx, int* mode, int64_t* fallbacks);
+
 #ifdef __cplusplus
 }
 #endif

@@ -105,6 +105,63 @@ def test_mbmelgan_random_vs_oracle(melgan):
         assert np.abs(wav[i, 0, :len(ref)] - ref).max() <= WAV_TOL
 
 
+def _gemm(mode):
+    from tts_amd._lib import get_engine
+    eng = get_engine(torch.device("cuda:0"))
+    eng.set_gemm_mode(mode)
+    return eng
+
+
+def test_mbmelgan_split_f16_equals_fp32_path_and_oracle(melgan):
+    """The split-f16 ResidualStack kernels (default) against the fp32-MFMA kernels and the oracle
+    on ragged utterances long enough for every dilation: both paths within WAV_TOL of the oracle,
+    and the split path's error no more than twice the fp32 path's (the same error class)."""
+    fx, cfg, sd, v = melgan
+    orc = melgan_oracle(cfg, sd)
+    rs = np.random.RandomState(8)
+    lens = [61, 7, 40]
+    batch = np.zeros((3, 80, max(lens)), np.float32)
+    for i, L in enumerate(lens):
+        batch[i, :, :L] = rs.normal(0, 1.5, (80, L))
+    v.inference_padding = 0
+    x = torch.from_numpy(batch).cuda()
+    eng = _gemm("f32")
+    try:
+        w32 = v.inference(x, lengths=lens).cpu().numpy()
+    finally:
+        eng = _gemm("x3")
+    n0 = eng.gemm_mode()[1]
+    w16 = v.inference(x, lengths=lens).cpu().numpy()
+    assert eng.gemm_mode() == ("x3", n0)  # no range fallback on this input
+    e16 = e32 = 0.0
+    for i, L in enumerate(lens):
+        ref = orc.inference(batch[i, :, :L], pad=0)[0]
+        e16 = max(e16, float(np.abs(w16[i, 0, :len(ref)] - ref).max()))
+        e32 = max(e32, float(np.abs(w32[i, 0, :len(ref)] - ref).max()))
+        assert not w16[i, 0, len(ref):].any()
+    print(f"waveform error vs oracle: split-f16 {e16:.2e}, fp32 {e32:.2e}, between {np.abs(w16 - w32).max():.2e}")
+    assert e16 <= WAV_TOL and e32 <= WAV_TOL
+    assert e16 <= 2 * e32 + 2e-6  # same error class as the fp32 GEMM
+
+
+def test_mbmelgan_f16_range_fallback_reruns_in_fp32(melgan):
+    """An input that drives the ResidualStack operands past the f16 range (|v| >= 65504) raises the
+    range flag and the call is re-run on the fp32 kernels: the result is bit-identical to the
+    fp32-mode call and the fallback counter moves."""
+    fx, cfg, sd, v = melgan
+    v.inference_padding = 0
+    mel = torch.from_numpy(fx["M64_p0_mel"] * np.float32(1e5)).cuda()
+    eng = _gemm("f32")
+    try:
+        w32 = v.inference(mel).cpu().numpy()
+    finally:
+        eng = _gemm("x3")
+    n0 = eng.gemm_mode()[1]
+    w16 = v.inference(mel).cpu().numpy()
+    assert eng.gemm_mode()[1] == n0 + 1
+    assert np.array_equal(w16, w32)
+
+
 def test_mbmelgan_too_short_raises(melgan):
     fx, cfg, sd, v = melgan
     v.inference_padding = 0

@@ -65,6 +65,8 @@ SIGNATURES = [
     ("tts_glow_decode", ctypes.c_int, [_vp, _vp, ctypes.c_float, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("tts_time_decoder_kernel", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_f_p]),
     ("tts_decoder_stats", ctypes.c_int, [_vp, _c_i_p, _c_i_p, _c_f_p, _c_i_p]),
+    ("tts_set_gemm_mode", ctypes.c_int, [_vp, ctypes.c_int]),
+    ("tts_gemm_mode", ctypes.c_int, [_vp, _c_i_p, _c_i64_p]),
 ]
 
 
@@ -251,6 +253,19 @@ class Engine:
         st = (ctypes.c_int * 2)()
         _check(self.lib.tts_decoder_stats(self.h, ctypes.byref(path), ctypes.byref(n), ms, st))
         return int(path.value), [(float(ms[i]), int(st[i])) for i in range(n.value)]
+
+    def set_gemm_mode(self, mode: str):
+        """'x3' = split-f16 MFMA GEMMs where built (fp32-accurate, the default), 'f32' = fp32 MFMA."""
+        if mode not in ("x3", "f32"):
+            raise ValueError("gemm mode must be 'x3' or 'f32'")
+        with self.lock:
+            _check(self.lib.tts_set_gemm_mode(self.h, 1 if mode == "x3" else 0))
+
+    def gemm_mode(self):
+        """(mode, calls re-run in fp32 because an operand left the f16 range)."""
+        m, n = ctypes.c_int(0), ctypes.c_int64(0)
+        _check(self.lib.tts_gemm_mode(self.h, ctypes.byref(m), ctypes.byref(n)))
+        return ("x3" if m.value else "f32"), int(n.value)
 
     def time_decoder_kernel(self, which: int, iters: int) -> float:
         ms = ctypes.c_float(0.0)

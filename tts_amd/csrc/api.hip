@@ -281,6 +281,7 @@ struct MelganModel {
   ConvLayer conv_in, conv_out;
   std::vector<ConvLayer> convT;
   std::vector<ConvLayer> dconv, fused;  // [stage*nres + block]
+  std::vector<DevBuf> rb_wd16, rb_wf16;  // split-f16 block weights (resblock_x3.hip), empty if C unsupported
   DevBuf G;
   DevBuf out_w, out_b;  // conv_out as [c][k][o] for the fused output + PQMF kernel
   int C_last = 0;
@@ -295,7 +296,7 @@ struct GenTail {
 };
 
 struct MelganWS {
-  DevBuf lens, xa, xb, bands;
+  DevBuf lens, xa, xb, bands, oflow;
 };
 
 }  // namespace
@@ -375,6 +376,10 @@ struct tts_ctx {
   hipEvent_t ev_dec[3] = {nullptr, nullptr, nullptr};  // around the persistent decoder launches
   int* pinned = nullptr;  // [16]: [0:4) chunk polling, [8:10) step index after each persistent launch
   int dec_path = 0;       // last decode: 0 = step graphs, 1 = persistent kernel
+  // GEMM arithmetic: true = split-f16 MFMA kernels where built (fp32-accurate, split16.h), false =
+  // fp32 MFMA everywhere (tts_set_gemm_mode; TTS_GEMM=f32 in the environment starts a context so)
+  bool gemm_x3 = true;
+  long x3_fallbacks = 0;  // calls re-run in fp32 because an operand left the f16 range
   int dec_nlaunch = 0;
   HostMap taco_host, mg_host;
   TacoModel taco;
@@ -1482,6 +1487,10 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
   G.convT.resize(n_up);
   G.dconv.resize((size_t)n_up * nres);
   G.fused.resize((size_t)n_up * nres);
+  G.rb_wd16.clear();
+  G.rb_wf16.clear();
+  G.rb_wd16.resize((size_t)n_up * nres);
+  G.rb_wf16.resize((size_t)n_up * nres);
   int pl3[8] = {3}, pl0[8] = {0};
   {
     auto w = wn_weight(m, "layers.1", {base, in_ch, 7});
@@ -1531,6 +1540,12 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
         bf[co] = b1[co] + bs[co];
       }
       pack_conv(G.fused[(size_t)i * nres + bk], Wf, bf, 2 * C, C, 1, 1, 1, pl0);
+      if (resblock_x3_supported(C)) {
+        std::vector<uint16_t> wd16, wf16;
+        pack_resblock_x3(wd, Wf, C, wd16, wf16);
+        G.rb_wd16[(size_t)i * nres + bk].upload(wd16);
+        G.rb_wf16[(size_t)i * nres + bk].upload(wf16);
+      }
     }
     idx += 3;
   }
@@ -1584,6 +1599,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     }
   }
   W.lens.ensure(B * 4);
+  W.oflow.ensure(4);
   W.xa.ensure((size_t)B * maxelems * 4);
   W.xb.ensure((size_t)B * maxelems * 4);
   std::vector<int> lens(h_lens, h_lens + B);
@@ -1646,7 +1662,15 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
       ra.bf = fl.bias.f();
       ra.max_q = Lb * mul;
       ra.B = B;
-      launch_resblock(ra, C, s);
+      const DevBuf& w16 = G.rb_wd16[i * G.nres + bk];
+      if (c->gemm_x3 && w16.p) {
+        ra.Wd16 = w16.p;
+        ra.Wf16 = G.rb_wf16[i * G.nres + bk].p;
+        ra.oflow = reinterpret_cast<unsigned*>(W.oflow.p);
+        launch_resblock_x3(ra, C, s);
+      } else {
+        launch_resblock(ra, C, s);
+      }
       std::swap(x, xo);
     }
   }
@@ -1670,6 +1694,36 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   HIP_OK(hipMemsetAsync(out, 0, (size_t)B * G.out_ch * Ls * 4, s));
   run_conv(G.conv_out, o, s);
   return up;
+}
+
+// Runs fn, which enqueues vocoder kernels on c->s; split-f16 kernels among them raise the
+// workspace's range flag when an operand falls outside the f16 range (split16.h). If it was
+// raised, fn runs again on the fp32 kernels, so results are always fp32-accurate. Costs one
+// stream synchronisation per call while split-f16 is on. fn must be re-runnable (it rewrites
+// all of its outputs).
+template <class F>
+void with_x3_fallback(tts_ctx* c, F&& fn) {
+  auto& W = c->mws;
+  W.oflow.ensure(4);
+  if (!c->gemm_x3) {
+    fn();
+    return;
+  }
+  HIP_OK(hipMemsetAsync(W.oflow.p, 0, 4, c->s));
+  fn();
+  HIP_OK(hipMemcpyAsync(&c->pinned[12], W.oflow.p, 4, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  if (c->pinned[12]) {
+    c->x3_fallbacks++;
+    c->gemm_x3 = false;
+    try {
+      fn();
+    } catch (...) {
+      c->gemm_x3 = true;
+      throw;
+    }
+    c->gemm_x3 = true;
+  }
 }
 
 template <class F>
@@ -2411,6 +2465,7 @@ int tts_ctx_create(int device, tts_ctx** out) {
     TTS_CHECK(device >= 0 && device < n, "invalid device");
     auto c = std::make_unique<tts_ctx>();
     c->device = device;
+    if (const char* e = std::getenv("TTS_GEMM")) c->gemm_x3 = std::string(e) != "f32";
     DeviceGuard g(device);
     HIP_OK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
     HIP_OK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
@@ -2682,7 +2737,7 @@ int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, 
     TTS_CHECK(pad >= 0, "pad >= 0");
     DeviceGuard g(c->device);
     enter(c, stream);
-    run_generator(c, d_mel, h_lens, B, M_max, pad, d_out, c->s);
+    with_x3_fallback(c, [&] { run_generator(c, d_mel, h_lens, B, M_max, pad, d_out, c->s); });
     leave(c, stream);
   });
 }
@@ -2696,24 +2751,26 @@ int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int 
     TTS_CHECK(G.ready && G.pqmf, "melgan (with PQMF) not finalized");
     DeviceGuard g(c->device);
     enter(c, stream);
-    int up = 1;
-    for (int u : G.ups) up *= u;
-    const long Ls = (long)(M_max + 2 * pad) * up;
-    HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
-    const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
-    if (fused) {
-      GenTail t;
-      run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t);
-      TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
-      TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
-                                G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
-                "fused output/PQMF shape not covered");
-    } else {
-      c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
-      run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s);
-      launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
-                            2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
-    }
+    with_x3_fallback(c, [&] {
+      int up = 1;
+      for (int u : G.ups) up *= u;
+      const long Ls = (long)(M_max + 2 * pad) * up;
+      HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
+      const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
+      if (fused) {
+        GenTail t;
+        run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t);
+        TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
+        TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
+                                  G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
+                  "fused output/PQMF shape not covered");
+      } else {
+        c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
+        run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s);
+        launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
+                              2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
+      }
+    });
     leave(c, stream);
   });
 }
@@ -2731,6 +2788,21 @@ int tts_pqmf_synthesis(tts_ctx* c, const float* d_x, int B, int N, int L, const 
     launch_pqmf_synthesis(d_x, (long)N * L, L, d_G, N, taps, c->mws.lens.i(), 0, 1, L, B, d_y, (long)N * L, c->s);
     HIP_OK(hipStreamSynchronize(c->s));
     leave(c, stream);
+  });
+}
+
+int tts_set_gemm_mode(tts_ctx* c, int mode) {
+  return guarded_ctx(c, [&] {
+    TTS_CHECK(mode == 0 || mode == 1, "gemm mode must be 0 (fp32) or 1 (split-f16)");
+    c->gemm_x3 = mode == 1;
+  });
+}
+
+int tts_gemm_mode(tts_ctx* c, int* mode, int64_t* fallbacks) {
+  return guarded_ctx(c, [&] {
+    TTS_CHECK(mode && fallbacks, "null argument");
+    *mode = c->gemm_x3 ? 1 : 0;
+    *fallbacks = c->x3_fallbacks;
   });
 }
 

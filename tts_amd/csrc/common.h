@@ -3,6 +3,7 @@
 #include <hip/hip_runtime.h>
 #include <cstdint>
 #include <string>
+#include <vector>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
 
@@ -107,8 +108,16 @@ struct ResArgs {
   const float* Wf;  // [W_1x1 | W_sc], swizzled rows C, K = 2C
   const float* bf;
   int max_q, B;
+  // split-f16 variant (resblock_x3.hip): pre-split A fragments of Wd / Wf and the range flag
+  const void* Wd16 = nullptr;
+  const void* Wf16 = nullptr;
+  unsigned* oflow = nullptr;
 };
 void launch_resblock(const ResArgs& a, int C, hipStream_t s);
+bool resblock_x3_supported(int C);
+void launch_resblock_x3(const ResArgs& a, int C, hipStream_t s);
+void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf, int C,
+                      std::vector<uint16_t>& wd16, std::vector<uint16_t>& wf16);
 
 // fused MB-MelGAN output conv (C -> 4, k7, LReLU + reflect pad 3 + tanh) and PQMF synthesis
 // (melgan_out.hip); returns false when the shape is not covered (N != 4, 63 taps, C not 32/48)
