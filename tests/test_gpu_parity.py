@@ -374,6 +374,75 @@ def test_tacotron2_random_batch_vs_oracle():
         assert not align[i, :, L:].any()
 
 
+def _taco_random_batch(seed, scale_embedding=1.0):
+    from tts_amd.spec import TacotronConfig
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=seed, overrides={}, stop_bias=-1e4, cfg=cfg)
+    if scale_embedding != 1.0:
+        sd["embedding.weight"] = sd["embedding.weight"] * scale_embedding
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(2)
+    rs = np.random.RandomState(5)
+    lens = [23, 4, 37, 11]
+    steps = [8, 5, 12, 6]
+    batch = np.zeros((len(lens), max(lens)), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, L)
+    return cfg, sd, m, batch, lens, steps
+
+
+def test_tacotron2_split_f16_equals_fp32_path_and_oracle():
+    """Encoder convs, BiLSTM input projection, processed inputs and postnet on the split-f16 conv
+    kernel (conv_x3.hip, the default) against the fp32-MFMA kernels and the oracle: both within
+    MEL_TOL, the split path's error no more than twice the fp32 path's plus 2e-6 (the same error
+    class), stop steps identical, no range fallback."""
+    from oracle.taco_np import TacoOracle
+    _dev()
+    cfg, sd, m, batch, lens, steps = _taco_random_batch(13)
+    x = torch.from_numpy(batch).cuda()
+    eng = _gemm("f32")
+    try:
+        _, p32, a32, _ = m.inference(x, text_lengths=lens, max_decoder_steps=steps)
+    finally:
+        eng = _gemm("x3")
+    n0 = eng.gemm_mode()[1]
+    _, p16, a16, _ = m.inference(x, text_lengths=lens, max_decoder_steps=steps)
+    assert eng.gemm_mode() == ("x3", n0)
+    assert list(m.last_steps) == steps
+    p32, p16, a16 = p32.cpu().numpy(), p16.cpu().numpy(), a16.cpu().numpy()
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    e16 = e32 = 0.0
+    for i, L in enumerate(lens):
+        _, p, a, _ = orc.inference(batch[i, :L], 2, steps[i])
+        M = steps[i] * 2
+        e16 = max(e16, float(np.abs(p16[i, :M] - p).max()))
+        e32 = max(e32, float(np.abs(p32[i, :M] - p).max()))
+        assert (a16[i, :steps[i], :L].argmax(1) == a.argmax(1)).all()
+        assert not p16[i, M:].any()
+    print(f"postnet error vs oracle: split-f16 {e16:.2e}, fp32 {e32:.2e}")
+    assert e16 <= MEL_TOL and e32 <= MEL_TOL
+    assert e16 <= 2 * e32 + 2e-6
+
+
+def test_tacotron2_f16_range_fallback_reruns_in_fp32():
+    """An embedding table scaled far past the f16 range drives the encoder conv operands over 65504:
+    the split-f16 call raises its range flag and re-runs on the fp32 kernels, bit-identical to the
+    fp32-mode call, and the fallback counter moves."""
+    _dev()
+    cfg, sd, m, batch, lens, steps = _taco_random_batch(13, scale_embedding=1e8)
+    x = torch.from_numpy(batch).cuda()
+    eng = _gemm("f32")
+    try:
+        out32 = [t.cpu().numpy() for t in m.inference(x, text_lengths=lens, max_decoder_steps=steps)]
+    finally:
+        eng = _gemm("x3")
+    n0 = eng.gemm_mode()[1]
+    out16 = [t.cpu().numpy() for t in m.inference(x, text_lengths=lens, max_decoder_steps=steps)]
+    assert eng.gemm_mode()[1] == n0 + 1
+    for u, v in zip(out16, out32):
+        assert np.array_equal(u, v, equal_nan=True)
+
+
 @pytest.mark.parametrize("variant", ["graves", "fwdmask", "window_softmax"])
 def test_tacotron2_variant_random_batch_vs_oracle(variant):
     """Decoder variants on 6 ragged utterances (1 to 40 tokens, forced lengths) against the oracle:

@@ -2,6 +2,7 @@
 // graph-captured autoregressive decode loop, and the vocoder pipeline.
 #include "common.h"
 #include "decoder.h"
+#include "split16.h"
 #include "../../include/ttship.h"
 
 #include <algorithm>
@@ -84,6 +85,11 @@ struct DevBuf {
     ensure(v.size() * sizeof(T));
     HIP_OK(hipMemcpy(p, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice));
   }
+  void reset() {
+    if (p) HIP_OK(hipFree(p));
+    p = nullptr;
+    bytes = 0;
+  }
   float* f() const { return static_cast<float*>(p); }
   int* i() const { return static_cast<int*>(p); }
 };
@@ -115,6 +121,8 @@ struct ConvLayer {
   int Cin = 0, Cout = 0, Cout_pad = 0, K = 1, dil = 1, tile = 0, nphase = 1;
   int pad_left[8] = {0};
   long phase_stride = 0;
+  DevBuf W16;             // split-f16 A fragments (conv_x3.hip); empty when the shape is not covered
+  long w16_stride = 0;    // bytes per phase
 };
 
 // Wm: nphase blocks of [Cout][Cin*K] row-major
@@ -146,6 +154,16 @@ void pack_conv(ConvLayer& L, const std::vector<float>& Wm, const std::vector<flo
   L.W.upload(sw);
   L.bias.upload(bias);
   for (int ph = 0; ph < nphase; ++ph) L.pad_left[ph] = pad_left[ph];
+  // split-f16 weights when the shape is covered and every weight is inside the f16 range
+  bool in_range = true;
+  for (float v : Wm) in_range &= std::fabs(v) < F16_RANGE;
+  if (conv_x3_supported(Cin, Cout, K, dil) && in_range) {
+    const std::vector<uint16_t> w16 = pack_conv_x3(Wm, Cin, Cout, K, nphase, &L.w16_stride);
+    L.W16.ensure(w16.size() * 2);
+    HIP_OK(hipMemcpy(L.W16.p, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
+  } else {
+    L.W16.reset();
+  }
 }
 
 struct ConvCall {
@@ -163,6 +181,7 @@ struct ConvCall {
   int rc = 0, rt = 0, resid_rows = 0;
   const float* aux = nullptr;
   int max_q = 0, B = 0;
+  unsigned* oflow = nullptr;  // set: run the split-f16 kernel where the layer has split weights
 };
 
 void run_conv(const ConvLayer& L, const ConvCall& c, hipStream_t st) {
@@ -201,6 +220,13 @@ void run_conv(const ConvLayer& L, const ConvCall& c, hipStream_t st) {
   a.aux = c.aux;
   a.max_q = c.max_q;
   a.B = c.B;
+  if (c.oflow && L.W16.p) {
+    a.W16 = L.W16.p;
+    a.w16_phase_stride = L.w16_stride;
+    a.oflow = c.oflow;
+    launch_conv_x3(a, st);
+    return;
+  }
   launch_conv(a, L.tile, st);
 }
 
@@ -296,7 +322,7 @@ struct GenTail {
 };
 
 struct MelganWS {
-  DevBuf lens, xa, xb, bands, oflow;
+  DevBuf lens, xa, xb, bands;
 };
 
 }  // namespace
@@ -380,6 +406,7 @@ struct tts_ctx {
   // fp32 MFMA everywhere (tts_set_gemm_mode; TTS_GEMM=f32 in the environment starts a context so)
   bool gemm_x3 = true;
   long x3_fallbacks = 0;  // calls re-run in fp32 because an operand left the f16 range
+  DevBuf x3flag;          // range flag raised by split-f16 kernels during one call (with_x3_fallback)
   int dec_nlaunch = 0;
   HostMap taco_host, mg_host;
   TacoModel taco;
@@ -398,6 +425,13 @@ struct tts_ctx {
   // last decode configuration (for tts_time_decoder_kernel)
   int last_B = 0, last_T = 0, last_S = 0, last_r = 0;
 };
+
+// range flag for the split-f16 kernels of the current call, or null (fp32 kernels)
+unsigned* x3_flag(tts_ctx* c) {
+  if (!c->gemm_x3) return nullptr;
+  c->x3flag.ensure(4);
+  return reinterpret_cast<unsigned*>(c->x3flag.p);
+}
 
 namespace {
 
@@ -989,6 +1023,7 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
   ConvCall cc;
   cc.lens = lens;
   cc.B = B;
+  cc.oflow = x3_flag(c);
   cc.max_q = T_max;
   cc.pad_mode = 0;
   cc.epi = 1;
@@ -1038,6 +1073,7 @@ void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int
   ConvCall cc;
   cc.lens = mlens;
   cc.B = B;
+  cc.oflow = x3_flag(c);
   cc.max_q = max_q;
   cc.pad_mode = 0;
   cc.epi = 2;
@@ -1350,6 +1386,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     ConvCall cc;
     cc.lens = W.lens.i();
     cc.B = B;
+    cc.oflow = x3_flag(c);
     cc.max_q = T_max;
     cc.s[0] = src_of(W.enc.f(), (long)T_max * 512, 1, 512, 512, 0);
     cc.out = W.penc.f();
@@ -1599,7 +1636,6 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     }
   }
   W.lens.ensure(B * 4);
-  W.oflow.ensure(4);
   W.xa.ensure((size_t)B * maxelems * 4);
   W.xb.ensure((size_t)B * maxelems * 4);
   std::vector<int> lens(h_lens, h_lens + B);
@@ -1607,6 +1643,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   ConvCall cc;
   cc.lens = W.lens.i();
   cc.B = B;
+  cc.oflow = x3_flag(c);
   cc.len_add = 2 * pad;
   // layers[0..1]: replicate pad (inference_padding) + ReflectionPad1d(3) + Conv1d(k7)
   cc.s[0] = src_of(mel, (long)G.in_ch * M_max, M_max, 1, G.in_ch, 0);
@@ -1663,10 +1700,10 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
       ra.max_q = Lb * mul;
       ra.B = B;
       const DevBuf& w16 = G.rb_wd16[i * G.nres + bk];
-      if (c->gemm_x3 && w16.p) {
+      if (cc.oflow && w16.p) {
         ra.Wd16 = w16.p;
         ra.Wf16 = G.rb_wf16[i * G.nres + bk].p;
-        ra.oflow = reinterpret_cast<unsigned*>(W.oflow.p);
+        ra.oflow = cc.oflow;
         launch_resblock_x3(ra, C, s);
       } else {
         launch_resblock(ra, C, s);
@@ -1703,15 +1740,14 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
 // all of its outputs).
 template <class F>
 void with_x3_fallback(tts_ctx* c, F&& fn) {
-  auto& W = c->mws;
-  W.oflow.ensure(4);
   if (!c->gemm_x3) {
     fn();
     return;
   }
-  HIP_OK(hipMemsetAsync(W.oflow.p, 0, 4, c->s));
+  unsigned* flag = x3_flag(c);
+  HIP_OK(hipMemsetAsync(flag, 0, 4, c->s));
   fn();
-  HIP_OK(hipMemcpyAsync(&c->pinned[12], W.oflow.p, 4, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(&c->pinned[12], flag, 4, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
   if (c->pinned[12]) {
     c->x3_fallbacks++;
@@ -2537,8 +2573,10 @@ int tts_taco_infer(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int 
     TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && h_steps && h_status,
               "null argument");
     DeviceGuard g(c->device);
-    taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
-               h_status, stream);
+    with_x3_fallback(c, [&] {
+      taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+                 h_status, stream);
+    });
   });
 }
 
@@ -2550,8 +2588,10 @@ int tts_taco_infer_spk(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, 
     TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && h_steps && h_status,
               "null argument");
     DeviceGuard g(c->device);
-    taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
-               h_status, stream, d_spk_ids, d_spk_emb);
+    with_x3_fallback(c, [&] {
+      taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+                 h_status, stream, d_spk_ids, d_spk_emb);
+    });
   });
 }
 
@@ -2585,8 +2625,7 @@ int tts_taco_encoder(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, in
     enter(c, stream);
     std::vector<int> lens(h_lens, h_lens + B);
     HIP_OK(hipMemcpyAsync(c->tws.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, c->s));
-    run_encoder(c, d_ids, B, T_max, d_out, c->s);
-    HIP_OK(hipStreamSynchronize(c->s));
+    with_x3_fallback(c, [&] { run_encoder(c, d_ids, B, T_max, d_out, c->s); });
     check_encoder_barrier(c);
     leave(c, stream);
   });
@@ -2614,7 +2653,9 @@ int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int 
     std::vector<int> lens(h_lens, h_lens + B);
     HIP_OK(hipMemcpyAsync(W.mlens.p, lens.data(), B * 4, hipMemcpyHostToDevice, c->s));
     HIP_OK(hipMemsetAsync(d_out, 0, (size_t)B * M_max * 80 * 4, c->s));
-    run_postnet(c, d_dec, (long)M_max * 80, W.mlens.i(), B, M_max, maxM, d_out, (long)M_max * 80, c->s);
+    with_x3_fallback(c, [&] {
+      run_postnet(c, d_dec, (long)M_max * 80, W.mlens.i(), B, M_max, maxM, d_out, (long)M_max * 80, c->s);
+    });
     HIP_OK(hipStreamSynchronize(c->s));
     leave(c, stream);
   });

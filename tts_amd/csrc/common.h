@@ -76,6 +76,11 @@ struct ConvArgs {
   const float* aux;   // epi 5: per output channel {w[4], actnorm bias, exp(-logs)}
   int max_q;          // max over batch of output positions per phase (grid x extent)
   int B;
+  // split-f16 variant (conv_x3.hip): pre-split A fragments [co16][k-step][64][hi 8 | lo 8] per
+  // phase (k-step = 32 input channels of one tap), and the range flag
+  const void* W16 = nullptr;
+  long w16_phase_stride = 0;  // bytes
+  unsigned* oflow = nullptr;
 };
 
 // tile configs: TC = output channels per workgroup, TQ = output positions per workgroup
@@ -83,6 +88,12 @@ enum ConvTile { TILE_128x64 = 0, TILE_64x64, TILE_192x64, TILE_96x64, TILE_48x12
 int conv_tile_tc(int tile);
 int conv_tile_for_cout(int cout);
 void launch_conv(const ConvArgs& a, int tile, hipStream_t s);
+// split-f16 form of the same conv (conv_x3.hip); false when the shape is not covered
+bool conv_x3_supported(int Cin, int Cout, int K, int dil);
+void launch_conv_x3(const ConvArgs& a, hipStream_t s);
+// host packing of the split weights: Wm = nphase blocks of [Cout][Cin*K] row-major
+std::vector<uint16_t> pack_conv_x3(const std::vector<float>& Wm, int Cin, int Cout, int K, int nphase,
+                                   long* phase_stride_bytes);
 
 // host-side swizzle of a row-major weight matrix Wm[Cout][Kdim] (Kdim % 16 == 0) into the
 // MFMA fragment order: dst[((m*nkc + kc)*64 + l)*4 + s] = Wm[m*16 + (l&15)][kc*16 + 4*(l>>4) + s]
