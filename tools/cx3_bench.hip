@@ -65,6 +65,7 @@ struct Built {
   size_t out_elems;
   int tile;
   double flop;
+  ConvArgs am;  // nph > 1: the phase-merged form (merged_u)
 };
 
 static Built build(const Case& c, uint32_t seed, float xscale) {
@@ -127,7 +128,23 @@ static Built build(const Case& c, uint32_t seed, float xscale) {
   }
   a.max_q = Lmax + 2 * c.rep_pad;
   a.B = B;
-  Built r{a, out, oe, tile, 2.0 * c.Cout * c.Cin * c.K * sumL * c.nph};
+  Built r{a, out, oe, tile, 2.0 * c.Cout * c.Cin * c.K * sumL * c.nph, a};
+  if (c.nph > 1) {
+    ConvArgs& m = r.am;
+    long st;
+    m.W16 = dup(pack_conv_x3(merge_convT_phases(Wm, c.nph, c.Cin, c.Cout), c.Cin, c.nph * c.Cout, 2, 1, &st));
+    m.w16_phase_stride = st;
+    std::vector<float> hb(c.Cout), bm((size_t)c.nph * c.Cout);
+    HIP_OK(hipMemcpy(hb.data(), a.bias, c.Cout * 4, hipMemcpyDeviceToHost));
+    for (size_t i = 0; i < bm.size(); ++i) bm[i] = hb[i / c.nph];
+    m.bias = dup(bm);
+    m.Cout = m.Cout_pad = c.nph * c.Cout;
+    m.nphase = 1;
+    m.pad_left[0] = 1;
+    m.out_mul = 1;
+    m.max_q = Lmax + 1;
+    m.merged_u = c.nph;
+  }
   return r;
 }
 
@@ -164,8 +181,19 @@ static int check(const Case& c, float xscale = 1.f) {
     mag = std::max(mag, (double)std::fabs(ref[i]));
   }
   const bool want_of = xscale > 1e4f;
-  const bool ok = (want_of || err <= 4e-6 * std::max(1.0, mag)) && (of != 0) == want_of;
+  bool ok = (want_of || err <= 4e-6 * std::max(1.0, mag)) && (of != 0) == want_of;
   printf("check %-28s max|err| %.3e (max|y| %.3e) oflow %u  %s\n", c.name.c_str(), err, mag, of, ok ? "OK" : "FAIL");
+  if (c.nph > 1) {
+    HIP_OK(hipMemset(r.out, 0, r.out_elems * 4));
+    launch_conv_x3(r.am, S);
+    HIP_OK(hipStreamSynchronize(S));
+    HIP_OK(hipMemcpy(got.data(), r.out, r.out_elems * 4, hipMemcpyDeviceToHost));
+    double e2 = 0;
+    for (size_t i = 0; i < r.out_elems; ++i) e2 = std::max(e2, (double)std::fabs(got[i] - ref[i]));
+    const bool ok2 = e2 <= 4e-6 * std::max(1.0, mag);
+    printf("check %-28s max|err| %.3e (phase-merged)  %s\n", c.name.c_str(), e2, ok2 ? "OK" : "FAIL");
+    ok = ok && ok2;
+  }
   return ok ? 0 : 1;
 }
 
@@ -179,6 +207,7 @@ int main(int argc, char** argv) {
     // name, Cin, Cout, K, nph, B, lens, in_mul, pad_mode, rep_pad, act, epi, two_src, time_major, resid
     fails += check({"k5 512->512 relu tmajor", 512, 512, 5, 1, 3, small, 1, 0, 0, 0, 1, 0, 1, 0});
     fails += check({"k5 80->512 tanh", 80, 512, 5, 1, 3, small, 1, 0, 0, 0, 2, 0, 0, 0});
+    fails += check({"k5 80->512 tanh tmajor", 80, 512, 5, 1, 3, small, 1, 0, 0, 0, 2, 0, 1, 0});
     fails += check({"k5 512->80 resid", 512, 80, 5, 1, 3, small, 1, 0, 0, 0, 0, 0, 0, 1});
     fails += check({"k1 512->2048", 512, 2048, 1, 1, 3, small, 1, 0, 0, 0, 0, 0, 0, 0});
     fails += check({"k1 512->128 tmajor", 512, 128, 1, 1, 3, small, 1, 0, 0, 0, 0, 0, 1, 0});
@@ -187,7 +216,7 @@ int main(int argc, char** argv) {
     fails += check({"convT 384->192 x8 lrelu", 384, 192, 2, 8, 3, small, 1, 0, 0, 1, 0, 0, 0, 0});
     fails += check({"convT 192->96 x4 lrelu", 192, 96, 2, 4, 3, small, 8, 0, 0, 1, 0, 0, 0, 0});
     fails += check({"convT 96->48 x2 lrelu", 96, 48, 2, 2, 3, small, 32, 0, 0, 1, 0, 0, 0, 0});
-    fails += check({"k3 two-src 256->64 clamp", 256, 64, 3, 1, 3, small, 2, 2, 0, 1, 1, 1, 0, 0});
+    fails += check({"k3 256->64 clamp lrelu", 256, 64, 3, 1, 3, small, 2, 2, 0, 1, 1, 0, 0, 0});
     fails += check({"k5 192->384 gate pair", 192, 384, 5, 1, 3, small, 1, 0, 0, 0, 3, 0, 0, 0});
     fails += check({"k5 512->512 range", 512, 512, 5, 1, 3, small, 1, 0, 0, 0, 1, 0, 0, 0}, 1e5f);
   }
@@ -210,7 +239,7 @@ int main(int argc, char** argv) {
   for (auto& sh : shapes) {
     Built r = build(sh.c, 99, 1.f);
     if (prof) {
-      for (int i = 0; i < 3; ++i) launch_conv_x3(r.a, S);
+      for (int i = 0; i < 3; ++i) launch_conv_x3(sh.c.nph > 1 ? r.am : r.a, S);
       HIP_OK(hipStreamSynchronize(S));
       continue;
     }
@@ -218,6 +247,11 @@ int main(int argc, char** argv) {
     const float tx3 = time_it([&] { launch_conv_x3(r.a, S); });
     printf("%-24s fp32 %8.1f us (%6.1f TF/s)   x3 %8.1f us (%6.1f TF/s fp32-equiv)  %s\n", sh.c.name.c_str(), t32,
            r.flop / (t32 * 1e-6) / 1e12, tx3, r.flop / (tx3 * 1e-6) / 1e12, sh.what);
+    if (sh.c.nph > 1) {
+      const float tm = time_it([&] { launch_conv_x3(r.am, S); });
+      printf("%-24s                              x3 %8.1f us (%6.1f TF/s fp32-equiv)  phase-merged\n", sh.c.name.c_str(),
+             tm, r.flop / (tm * 1e-6) / 1e12);
+    }
   }
   printf(fails ? "FAILED\n" : "all checks passed\n");
   return fails ? 1 : 0;

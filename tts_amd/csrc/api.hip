@@ -166,6 +166,23 @@ void pack_conv(ConvLayer& L, const std::vector<float>& Wm, const std::vector<flo
   }
 }
 
+// split-f16 weights only (a layer that has no fp32 form: the phase-merged ConvTranspose)
+void pack_conv_x3_only(ConvLayer& L, const std::vector<float>& Wm, const std::vector<float>& bias, int Cin, int Cout,
+                       int K) {
+  TTS_CHECK(conv_x3_supported(Cin, Cout, K, 1), "conv_x3: shape not covered");
+  L.Cin = Cin;
+  L.Cout = L.Cout_pad = Cout;
+  L.K = K;
+  L.dil = 1;
+  L.nphase = 1;
+  L.pad_left[0] = (K - 1) / 2 + (K == 2 ? 1 : 0);
+  for (float v : Wm) TTS_CHECK(std::fabs(v) < F16_RANGE, "conv_x3: weight outside the f16 range");
+  const std::vector<uint16_t> w16 = pack_conv_x3(Wm, Cin, Cout, K, 1, &L.w16_stride);
+  L.W16.ensure(w16.size() * 2);
+  HIP_OK(hipMemcpy(L.W16.p, w16.data(), w16.size() * 2, hipMemcpyHostToDevice));
+  L.bias.upload(bias);
+}
+
 struct ConvCall {
   ConvSrc s[2];
   int nsrc = 1;
@@ -182,6 +199,7 @@ struct ConvCall {
   const float* aux = nullptr;
   int max_q = 0, B = 0;
   unsigned* oflow = nullptr;  // set: run the split-f16 kernel where the layer has split weights
+  int merged_u = 0;           // phase-merged ConvTranspose (layer from pack_conv_x3_only)
 };
 
 void run_conv(const ConvLayer& L, const ConvCall& c, hipStream_t st) {
@@ -220,7 +238,9 @@ void run_conv(const ConvLayer& L, const ConvCall& c, hipStream_t st) {
   a.aux = c.aux;
   a.max_q = c.max_q;
   a.B = c.B;
-  if (c.oflow && L.W16.p) {
+  a.merged_u = c.merged_u;
+  TTS_CHECK(!c.merged_u || (c.oflow && L.W16.p), "phase-merged ConvTranspose runs on split-f16 weights only");
+  if (c.oflow && L.W16.p && c.nsrc == 1 && (c.s[0].sc != 1 || c.s[0].st % 4 == 0)) {
     a.W16 = L.W16.p;
     a.w16_phase_stride = L.w16_stride;
     a.oflow = c.oflow;
@@ -306,6 +326,7 @@ struct MelganModel {
   std::vector<int> ups;
   ConvLayer conv_in, conv_out;
   std::vector<ConvLayer> convT;
+  std::vector<ConvLayer> convTm;  // phase-merged split-f16 form (conv_x3.hip merged_u), W16 only
   std::vector<ConvLayer> dconv, fused;  // [stage*nres + block]
   std::vector<DevBuf> rb_wd16, rb_wf16;  // split-f16 block weights (resblock_x3.hip), empty if C unsupported
   DevBuf G;
@@ -1522,6 +1543,8 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
   G.dconv.clear();
   G.fused.clear();
   G.convT.resize(n_up);
+  G.convTm.clear();
+  G.convTm.resize(n_up);
   G.dconv.resize((size_t)n_up * nres);
   G.fused.resize((size_t)n_up * nres);
   G.rb_wd16.clear();
@@ -1555,6 +1578,12 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
           }
     }
     pack_conv(G.convT[i], Wm, need(m, nm + ".bias", {cout}).d, cin, cout, 2, 1, u, pls);
+    if (G.convT[i].W16.p && conv_x3_supported(cin, u * cout, 2, 1)) {
+      const auto& bias = need(m, nm + ".bias", {cout}).d;
+      std::vector<float> bm((size_t)u * cout);
+      for (size_t r = 0; r < bm.size(); ++r) bm[r] = bias[r / u];
+      pack_conv_x3_only(G.convTm[i], merge_convT_phases(Wm, u, cin, cout), bm, cin, u * cout, 2);
+    }
     C = cout;
     for (int bk = 0; bk < nres; ++bk) {
       const int d = 1;
@@ -1676,7 +1705,14 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     t.ob = (long)Cn * Ln;
     t.oc = Ln;
     t.ot = 1;
-    run_conv(G.convT[i], t, s);
+    if (t.oflow && G.convTm[i].W16.p) {  // all u phases as one GEMM over input positions 0 .. L
+      t.out_mul = 1;
+      t.max_q = Lb * mul + 1;
+      t.merged_u = u;
+      run_conv(G.convTm[i], t, s);
+    } else {
+      run_conv(G.convT[i], t, s);
+    }
     std::swap(x, xo);
     C = Cn;
     Ls = Ln;

@@ -81,6 +81,11 @@ struct ConvArgs {
   const void* W16 = nullptr;
   long w16_phase_stride = 0;  // bytes
   unsigned* oflow = nullptr;
+  // > 0: phase-merged ConvTranspose1d of stride merged_u (conv_x3.hip only): GEMM row
+  // m = co * merged_u + phase, 2 taps at input q - 1 and q for q in [0, L] (nphase = 1,
+  // pad_left 1, zero padding), bias per row; phases >= merged_u / 2 write output position
+  // (q - 1) * merged_u + phase, the others q * merged_u + phase
+  int merged_u = 0;
 };
 
 // tile configs: TC = output channels per workgroup, TQ = output positions per workgroup
@@ -94,6 +99,8 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t s);
 // host packing of the split weights: Wm = nphase blocks of [Cout][Cin*K] row-major
 std::vector<uint16_t> pack_conv_x3(const std::vector<float>& Wm, int Cin, int Cout, int K, int nphase,
                                    long* phase_stride_bytes);
+// merged ConvTranspose weights from the polyphase form Wm [u][Cout][Cin][2] (merged_u above)
+std::vector<float> merge_convT_phases(const std::vector<float>& Wm, int u, int Cin, int Cout);
 
 // host-side swizzle of a row-major weight matrix Wm[Cout][Kdim] (Kdim % 16 == 0) into the
 // MFMA fragment order: dst[((m*nkc + kc)*64 + l)*4 + s] = Wm[m*16 + (l&15)][kc*16 + 4*(l>>4) + s]

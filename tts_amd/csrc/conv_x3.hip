@@ -7,15 +7,19 @@
 //   k-step     32 input channels of one tap (the fp32 kernel's k-chunk is 4 channels);
 //              Cin is zero-padded to a multiple of 32 in the packed weights and at staging.
 //   weights    pre-split on the host into A fragments [co16][k-step][lane][hi 8 | lo 8]
-//              (32 B per lane per 16 x 32 block), streamed from L2 through an RS-slot register
-//              ring over the flattened (chunk, tap) sequence, reloaded in place after use.
-//   staging    per 32-channel chunk, TQ + span rows of the (padded, activated) input, split
+//              (32 B per lane per 16 x 32 block), streamed from L2 through a register ring of
+//              one (k >= 5) or two (k <= 3) chunks of taps, each slot reloaded in place after use.
+//   staging    per 32-channel chunk (one source), TQ + span rows of the (padded, activated) input, split
 //              into hi / lo and stored position-major [pos][32 hi | 32 lo | 16 pad] (160 B):
 //              a lane's B operand (8 consecutive channels at one position) is one ds_read_b128
-//              and a tap is a row offset. Double-buffered: chunk c+1's global loads are in
-//              flight during chunk c's MFMAs, one barrier per chunk.
+//              and a tap is a row offset. Two LDS buffers and two register sets: chunk c+2's
+//              global loads are in flight during chunk c's MFMAs, one barrier per chunk.
 //   range      staged activations outside the f16 range set *oflow (split16.h); the host then
 //              re-runs the call on the fp32 kernels. Weights are range-checked at pack time.
+//   ConvT      merged_u > 0: the u phases of a ConvTranspose1d(k = 2u, stride u, padding u/2) as
+//              ONE GEMM (rows co * u + phase, both tap pairs expressed as input q - 1, q): the
+//              input is staged once instead of u times and a workgroup writes whole runs of
+//              consecutive output samples instead of every u-th one.
 //   placement  a 1-D grid dealt so that the workgroups of one XCD (blockIdx % 8) take a
 //              contiguous run of the output-channel-major tile list: each XCD's L2 holds the
 //              weights of ~1/8 of the output channels instead of all of them.
@@ -31,11 +35,12 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t cx_rsrc(const void* p) {
 }
 }  // namespace
 
-template <int MI, int NI, int WM, int WN, int KT, int RS>
+template <int MI, int NI, int WM, int WN, int KT, int RS, int SD>
 __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int nq, int nco, int nz) {
   constexpr int NTHR = 64 * WM * WN;
   constexpr int TC = 16 * MI * WM, TQ = 16 * NI * WN;
   constexpr int SPT = (4 * (TQ + CONV_MAX_SPAN) + NTHR - 1) / NTHR;  // staging items per thread
+  static_assert(RS == KT || RS == 2 * KT, "weight ring: one or two chunks of taps");
   extern __shared__ __attribute__((aligned(16))) _Float16 shx[];
 
   // XCD-aware deal: physical block p runs logical tile (p % 8) * per + p / 8 of the
@@ -52,7 +57,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
   const int ph = z % a.nphase;
   const int b = z / a.nphase;
   const int base = a.lens[b] + a.len_add;
-  const int Lq = base * a.q_mul;
+  const int Lq = base * a.q_mul + (a.merged_u ? 1 : 0);
   const int q0 = qt * TQ;
   if (q0 >= Lq) return;
   const int co0 = cot * TC;
@@ -64,7 +69,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
   _Float16* X1 = shx + ROWS * CX_XR;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int nb = wn * 16 * NI + (lane & 15);  // this lane's B column (position) for ni = 0
   const int kg = 8 * (lane >> 4);             // this lane's channel offset inside a k-step
@@ -73,65 +78,65 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
   const int mtiles = (a.Cout + 15) / 16;
   bool bad = false;
 
-  // ---- staging: item e = (channel octet g, row), rows fastest (coalesced along time) ----
+  // ---- staging: item e = (channel octet g, row), rows fastest (coalesced along time). An item's
+  //      position (and its padding) is fixed for the whole kernel: one VGPR byte offset per item;
+  //      the chunk and the channel inside the octet are SGPR offsets of raw buffer loads whose
+  //      range is this utterance's source (channels past Cin are zeroed at the store) ----
+  const ConvSrc& S = a.src[0];
   const int i0 = q0 - a.pad_left[ph];
   const bool interior = (a.rep_pad == 0) && i0 >= 0 && i0 + ROWS <= Lin;
   const int rawL = a.lens[b];
   const int Lsrc = a.rep_pad ? rawL : Lin;
-  int srow[SPT], sg[SPT];
+  const bool tmajor = S.sc == 1;  // 8 channels of a position are contiguous: two 16-byte loads
+  const __amdgpu_buffer_rsrc_t xr = __builtin_amdgcn_make_buffer_rsrc(
+      const_cast<float*>(S.ptr + (long)b * S.sb), 0,
+      (int)min((long)0x7fffffff, ((long)(S.C - 1) * S.sc + (long)(Lsrc - 1) * S.st + 1) * 4), 0x00020000);
+  int voff[SPT], sgv[SPT], srow[SPT];
+  bool sval[SPT];
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int e = tid + NTHR * j;
-    sg[j] = e / ROWS;
-    srow[j] = e - sg[j] * ROWS;
+    const int g = e / ROWS;
+    srow[j] = e - g * ROWS;
+    sgv[j] = g;
+    int i = i0 + srow[j];
+    bool valid = true;
+    if (!interior) {
+      i = map_pad_index(i, Lin, a.pad_mode, valid);
+      if (a.rep_pad) i -= a.rep_pad;
+    }
+    i = i < 0 ? 0 : (i >= Lsrc ? Lsrc - 1 : i);
+    sval[j] = valid && g < 4;
+    voff[j] = (min(g, 3) * 8 * S.sc + i * S.st) * 4;
   }
-  float st[SPT][8];
-  auto stage_load = [&](int ch) {
+  const int act = S.act;
+  float st[SD][SPT][8];
+  auto stage_load = [&](float (&sr)[SPT][8], int ch) {
+    const int cb = 32 * ch * S.sc * 4;  // uniform
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
-      const int g = min(sg[j], 3);
-      int c0 = 32 * ch + 8 * g;
-      c0 = min(c0, a.Cin - 8);  // past Cin: loaded (clamped) but stored as zero
-      const bool first = c0 < a.src[0].C;
-      const ConvSrc& S = first ? a.src[0] : a.src[1];
-      const int cs = first ? c0 : c0 - a.src[0].C;
-      int i = i0 + srow[j];
-      bool valid = true;
-      if (!interior) {
-        i = map_pad_index(i, Lin, a.pad_mode, valid);
-        if (a.rep_pad) i -= a.rep_pad;
-      }
-      i = i < 0 ? 0 : (i >= Lsrc ? Lsrc - 1 : i);
-      const float* p = S.ptr + (long)b * S.sb + (long)cs * S.sc + (long)i * S.st;
-      if (S.sc == 1 && ((S.st & 3) == 0) && ((reinterpret_cast<uintptr_t>(S.ptr) & 15) == 0)) {
-        const float4 u = *reinterpret_cast<const float4*>(p);
-        const float4 v = *reinterpret_cast<const float4*>(p + 4);
-        st[j][0] = u.x, st[j][1] = u.y, st[j][2] = u.z, st[j][3] = u.w;
-        st[j][4] = v.x, st[j][5] = v.y, st[j][6] = v.z, st[j][7] = v.w;
+      if (tmajor) {
+        const f32x4 u = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, voff[j], cb, 0));
+        const f32x4 v = __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(xr, voff[j] + 16, cb, 0));
+#pragma unroll
+        for (int c = 0; c < 4; ++c) sr[j][c] = u[c], sr[j][4 + c] = v[c];
       } else {
 #pragma unroll
-        for (int c = 0; c < 8; ++c) st[j][c] = p[(long)c * S.sc];
-      }
-      if (!valid) {
-#pragma unroll
-        for (int c = 0; c < 8; ++c) st[j][c] = 0.f;
+        for (int c = 0; c < 8; ++c)
+          sr[j][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, voff[j], cb + c * S.sc * 4, 0));
       }
     }
   };
-  auto stage_store = [&](_Float16* X, int ch) {
+  auto stage_store = [&](_Float16* X, const float (&sr)[SPT][8], int ch) {
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
-      const int g = sg[j], row = srow[j];
-      if (g < 4) {
-        const int c0 = 32 * ch + 8 * g;
-        const bool real = c0 < a.Cin;
-        const bool first = min(c0, a.Cin - 8) < a.src[0].C;
-        const int act = first ? a.src[0].act : a.src[1].act;
+      if (sgv[j] < 4) {
+        const bool keep = sval[j] && 32 * ch + 8 * sgv[j] < a.Cin;  // zero padding; channels past Cin
         float mx = 0.f;
         h8 hi, lo;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          float v = real ? st[j][c] : 0.f;
+          float v = keep ? sr[j][c] : 0.f;
           mx = fmaxf(mx, __builtin_fabsf(v));
           if (act) v = lrelu02(v);
           _Float16 h, l;
@@ -140,8 +145,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
           lo[c] = l;
         }
         bad |= !(mx < F16_RANGE);  // |lrelu(v)| <= |v|
-        *reinterpret_cast<h8*>(X + row * CX_XR + 8 * g) = hi;
-        *reinterpret_cast<h8*>(X + row * CX_XR + 32 + 8 * g) = lo;
+        *reinterpret_cast<h8*>(X + srow[j] * CX_XR + 8 * sgv[j]) = hi;
+        *reinterpret_cast<h8*>(X + srow[j] * CX_XR + 32 + 8 * sgv[j]) = lo;
       }
     }
   };
@@ -167,39 +172,55 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
   for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
     for (int ni = 0; ni < NI; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-  stage_load(0);
+  // SD = 2: staging runs two chunks ahead (chunk c's global loads are issued after chunk c - 3's
+  // MFMAs into register set c & 1 and stored to LDS buffer c & 1 after chunk c - 1's);
+  // SD = 1: one chunk ahead (loads issued before chunk c - 1's MFMAs), one register set
+  stage_load(st[0], 0);
 #pragma unroll
   for (int u = 0; u < RS; ++u) wload(ring[u], u);
-  stage_store(X0, 0);
+  stage_store(X0, st[0], 0);
+  if constexpr (SD == 2) {
+    if (NCH > 1) stage_load(st[1], 1);
+    if (NCH > 2) stage_load(st[0], 2);
+  }
   __syncthreads();
-  for (int s0 = 0; s0 < NKS; s0 += RS) {
+  for (int ch0 = 0; ch0 < NCH; ch0 += 2) {
 #pragma unroll
-    for (int u = 0; u < RS; ++u) {
-      const int seq = s0 + u;
-      if (seq < NKS) {
-        const int ch = seq / KT;
-        const int kq = seq - ch * KT;
-        const _Float16* X = (ch & 1) ? X1 : X0;
-        if (kq == 0 && ch + 1 < NCH) stage_load(ch + 1);  // in flight during this chunk's MFMAs
-        __builtin_amdgcn_sched_barrier(0);
-        h8 bh[NI], bl[NI];
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const _Float16* p = X + (nb + ni * 16 + kq * dil) * CX_XR + kg;
-          bh[ni] = *reinterpret_cast<const h8*>(p);
-          bl[ni] = *reinterpret_cast<const h8*>(p + 32);
+    for (int p = 0; p < 2; ++p) {
+      const int ch = ch0 + p;
+      if (ch < NCH) {
+        const _Float16* X = p ? X1 : X0;
+        if constexpr (SD == 1) {
+          if (ch + 1 < NCH) stage_load(st[0], ch + 1);
+          __builtin_amdgcn_sched_barrier(0);
         }
-        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
+        for (int kq = 0; kq < KT; ++kq) {
+          constexpr bool TWO = RS == 2 * KT;
+          const int slot = TWO ? p * KT + kq : kq;
+          h8 bh[NI], bl[NI];
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            mfma_x3(ring[u][mi][0], ring[u][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-        wload(ring[u], seq + RS);  // reload the slot in place after its MFMAs
-        if (kq == KT - 1) {
-          if (ch + 1 < NCH) stage_store((ch & 1) ? X0 : X1, ch + 1);
-          __syncthreads();
+          for (int ni = 0; ni < NI; ++ni) {
+            const _Float16* q = X + (nb + ni * 16 + kq * dil) * CX_XR + kg;
+            bh[ni] = *reinterpret_cast<const h8*>(q);
+            bl[ni] = *reinterpret_cast<const h8*>(q + 32);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+          for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+            for (int ni = 0; ni < NI; ++ni)
+              mfma_x3(ring[slot][mi][0], ring[slot][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
+          wload(ring[slot], ch * KT + kq + RS);  // reload the slot in place after its MFMAs
+          __builtin_amdgcn_sched_barrier(0);
         }
+        if constexpr (SD == 2) {
+          if (ch + 1 < NCH) stage_store(p ? X0 : X1, st[p ^ 1], ch + 1);
+          if (ch + 3 < NCH) stage_load(st[p ^ 1], ch + 3);
+        } else {
+          if (ch + 1 < NCH) stage_store(p ? X0 : X1, st[0], ch + 1);
+        }
+        __syncthreads();
       }
     }
   }
@@ -210,7 +231,27 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[mi][ni][j] = x3_value(am[mi][ni][j], ac[mi][ni][j]);
-  conv_epilogue<MI, NI, WN>(a, acc, b, ph, q0, co0, wm, wn, lane);
+  if (a.merged_u) {  // phase-merged ConvTranspose: row m = co * u + phase
+    const int u = a.merged_u, L = Lin;
+    float* ob = a.out + (long)b * a.ob;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int m = co0 + wm * 16 * MI + mi * 16 + 4 * (lane >> 4) + j;
+        if (m >= a.Cout) continue;
+        const int co = m / u, phs = m - co * u;
+        const int hi = 2 * phs >= u;  // taps (q, q + 1) of the polyphase form, i.e. this q - 1
+        const float bias = a.bias[m];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const int qq = q0 + nb + ni * 16 - hi;
+          if (qq >= 0 && qq < L) ob[(long)co * a.oc + (long)(qq * u + phs) * a.ot] = acc[mi][ni][j] + bias;
+        }
+      }
+  } else {
+    conv_epilogue<MI, NI, WN>(a, acc, b, ph, q0, co0, wm, wn, lane);
+  }
   if (bad) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -236,12 +277,15 @@ bool conv_x3_supported(int Cin, int Cout, int K, int dil) {
          (K - 1) * dil <= CONV_MAX_SPAN;
 }
 
-template <int MI, int NI, int WM, int WN, int KT>
+// RS weight-ring slots (one or two chunks of taps), SD staging depth in chunks: per shape from
+// tools/cx3_bench.hip (two chunks ahead wins where a chunk's MFMAs are long enough to keep two
+// register sets without losing occupancy)
+template <int MI, int NI, int WM, int WN, int KT, int RS, int SD>
 static void cx_launch(const ConvArgs& a, hipStream_t s) {
-  constexpr int TC = 16 * MI * WM, TQ = 16 * NI * WN, RS = 3;
+  constexpr int TC = 16 * MI * WM, TQ = 16 * NI * WN;
   static bool attr = false;
   if (!attr) {
-    HIP_OK(hipFuncSetAttribute((const void*)conv_x3_kernel<MI, NI, WM, WN, KT, RS>,
+    HIP_OK(hipFuncSetAttribute((const void*)conv_x3_kernel<MI, NI, WM, WN, KT, RS, SD>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
     attr = true;
   }
@@ -250,17 +294,17 @@ static void cx_launch(const ConvArgs& a, hipStream_t s) {
   TTS_CHECK(ntile < (1L << 30), "conv_x3: grid too large");
   const int per = (int)((ntile + 7) / 8);
   const size_t lds = (size_t)2 * (TQ + (KT - 1) * a.dil) * CX_XR * 2;
-  conv_x3_kernel<MI, NI, WM, WN, KT, RS><<<dim3(8 * per), 64 * WM * WN, lds, s>>>(a, nq, nco, nz);
+  conv_x3_kernel<MI, NI, WM, WN, KT, RS, SD><<<dim3(8 * per), 64 * WM * WN, lds, s>>>(a, nq, nco, nz);
 }
 
-template <int MI, int NI, int WM, int WN>
+template <int MI, int NI, int WM, int WN, int SD12>
 static void cx_taps(const ConvArgs& a, hipStream_t s) {
   switch (a.K) {
-    case 1: cx_launch<MI, NI, WM, WN, 1>(a, s); break;
-    case 2: cx_launch<MI, NI, WM, WN, 2>(a, s); break;
-    case 3: cx_launch<MI, NI, WM, WN, 3>(a, s); break;
-    case 5: cx_launch<MI, NI, WM, WN, 5>(a, s); break;
-    case 7: cx_launch<MI, NI, WM, WN, 7>(a, s); break;
+    case 1: cx_launch<MI, NI, WM, WN, 1, 2, SD12>(a, s); break;
+    case 2: cx_launch<MI, NI, WM, WN, 2, 2 * SD12, SD12>(a, s); break;
+    case 3: cx_launch<MI, NI, WM, WN, 3, 3, 1>(a, s); break;
+    case 5: cx_launch<MI, NI, WM, WN, 5, 5, 2>(a, s); break;
+    case 7: cx_launch<MI, NI, WM, WN, 7, 7, 1>(a, s); break;
     default: TTS_CHECK(false, "conv_x3: unsupported tap count");
   }
 }
@@ -269,15 +313,20 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t s) {
   TTS_CHECK(conv_x3_supported(a.Cin, a.Cout, a.K, a.dil), "conv_x3: unsupported shape");
   TTS_CHECK(a.W16 && a.oflow, "conv_x3: split weights / overflow flag missing");
   TTS_CHECK(a.nphase >= 1 && a.nphase <= 8, "conv: nphase");
-  TTS_CHECK(a.nsrc == 1 || a.src[0].C % 8 == 0, "conv_x3: first source's channels must be a multiple of 8");
+  TTS_CHECK(a.nsrc == 1 && a.src[0].C == a.Cin, "conv_x3: one source");
+  TTS_CHECK(!a.merged_u || (a.nphase == 1 && a.K == 2 && a.pad_left[0] == 1 && a.pad_mode == 0 && a.epi_act == 0 &&
+                            a.rep_pad == 0 && a.Cout % a.merged_u == 0 && a.merged_u % 2 == 0),
+            "conv_x3: phase-merged ConvTranspose arguments");
+  TTS_CHECK(a.src[0].sc != 1 || (a.src[0].st % 4 == 0 && (reinterpret_cast<uintptr_t>(a.src[0].ptr) & 15) == 0),
+            "conv_x3: time-major source rows must be 16-byte aligned");
   if (a.max_q <= 0 || a.B <= 0) return;
   switch (cx_tile(a.Cout)) {
-    case CX_T128: cx_taps<2, 4, 4, 1>(a, s); break;
-    case CX_T192: cx_taps<3, 4, 4, 1>(a, s); break;
-    case CX_T96: cx_taps<3, 4, 2, 2>(a, s); break;
-    case CX_T64: cx_taps<2, 4, 2, 2>(a, s); break;
-    case CX_T80: cx_taps<5, 2, 1, 4>(a, s); break;
-    case CX_T48: cx_taps<3, 2, 1, 4>(a, s); break;
+    case CX_T128: cx_taps<2, 4, 4, 1, 2>(a, s); break;
+    case CX_T192: cx_taps<3, 4, 4, 1, 2>(a, s); break;
+    case CX_T96: cx_taps<3, 4, 2, 2, 1>(a, s); break;
+    case CX_T64: cx_taps<2, 4, 2, 2, 1>(a, s); break;
+    case CX_T80: cx_taps<5, 2, 1, 4, 2>(a, s); break;
+    case CX_T48: cx_taps<3, 2, 1, 4, 1>(a, s); break;
     default: TTS_CHECK(false, "conv_x3: unsupported output channel count");
   }
   HIP_OK(hipGetLastError());
@@ -298,5 +347,13 @@ std::vector<uint16_t> pack_conv_x3(const std::vector<float>& Wm, int Cin, int Co
     std::copy(blk.begin(), blk.end(), out.begin() + per * ph);
   }
   *phase_stride_bytes = (long)(per * 2);
+  return out;
+}
+
+std::vector<float> merge_convT_phases(const std::vector<float>& Wm, int u, int Cin, int Cout) {
+  std::vector<float> out((size_t)u * Cout * Cin * 2);
+  for (int ph = 0; ph < u; ++ph)
+    for (int co = 0; co < Cout; ++co)
+      std::copy_n(&Wm[(((size_t)ph * Cout + co) * Cin) * 2], (size_t)Cin * 2, &out[(((size_t)co * u + ph) * Cin) * 2]);
   return out;
 }
