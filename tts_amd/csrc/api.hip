@@ -421,7 +421,8 @@ struct tts_ctx {
   hipStream_t s = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_chunk[2] = {nullptr, nullptr};
   hipEvent_t ev_dec[3] = {nullptr, nullptr, nullptr};  // around the persistent decoder launches
-  int* pinned = nullptr;  // [16]: [0:4) chunk polling, [8:10) step index after each persistent launch
+  int* pinned = nullptr;  // [256]: [0:4) chunk polling, [8:10) step index after each persistent launch,
+                          // [12] range flag, [16:20) barrier error words, [20:20+3*BMAX) decoder results
   int dec_path = 0;       // last decode: 0 = step graphs, 1 = persistent kernel
   // GEMM arithmetic: true = split-f16 MFMA kernels where built (fp32-accurate, split16.h), false =
   // fp32 MFMA everywhere (tts_set_gemm_mode; TTS_GEMM=f32 in the environment starts a context so)
@@ -1418,19 +1419,24 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   }
   // decoder state
   const int Bp = W.MT * 16;
-  HIP_OK(hipMemsetAsync(W.catt.p, 0, (size_t)Bp * 1024 * 4, s));
-  HIP_OK(hipMemsetAsync(W.hatt.p, 0, (size_t)Bp * 1024 * 4, s));
-  HIP_OK(hipMemsetAsync(W.hdec0.p, 0, (size_t)Bp * 1024 * 4, s));
-  HIP_OK(hipMemsetAsync(W.hdec1.p, 0, (size_t)Bp * 1024 * 4, s));
-  HIP_OK(hipMemsetAsync(W.cdec.p, 0, (size_t)Bp * 1024 * 4, s));
-  HIP_OK(hipMemsetAsync(W.ctx.p, 0, (size_t)Bp * 512 * 4, s));
-  HIP_OK(hipMemsetAsync(W.y.p, 0, (size_t)Bp * 80 * M.r_init * 4, s));
-  HIP_OK(hipMemsetAsync(W.alpha.p, 0, (size_t)B * T_max * 4, s));
-  HIP_OK(hipMemsetAsync(W.acum.p, 0, (size_t)B * T_max * 4, s));
-  HIP_OK(hipMemsetAsync(W.dec.p, 0, (size_t)B * S_cap * r * 80 * 4, s));
-  HIP_OK(hipMemsetAsync(W.align.p, 0, (size_t)B * S_cap * T_max * 4, s));
-  HIP_OK(hipMemsetAsync(W.stop.p, 0, (size_t)B * S_cap * 4, s));
-  HIP_OK(hipMemsetAsync(W.acnt.p, 0, BMAX * sizeof(unsigned), s));
+  {
+    FillList f;  // decoder state and outputs zeroed in one launch (the postnet output too)
+    f.add(W.catt.p, (size_t)Bp * 1024 * 4);
+    f.add(W.hatt.p, (size_t)Bp * 1024 * 4);
+    f.add(W.hdec0.p, (size_t)Bp * 1024 * 4);
+    f.add(W.hdec1.p, (size_t)Bp * 1024 * 4);
+    f.add(W.cdec.p, (size_t)Bp * 1024 * 4);
+    f.add(W.ctx.p, (size_t)Bp * 512 * 4);
+    f.add(W.y.p, (size_t)Bp * 80 * M.r_init * 4);
+    f.add(W.alpha.p, (size_t)B * T_max * 4);
+    f.add(W.acum.p, (size_t)B * T_max * 4);
+    f.add(W.dec.p, (size_t)B * S_cap * r * 80 * 4);
+    f.add(W.align.p, (size_t)B * S_cap * T_max * 4);
+    f.add(W.stop.p, (size_t)B * S_cap * 4);
+    f.add(W.acnt.p, BMAX * sizeof(unsigned));
+    f.add(W.post.p, (size_t)B * S_cap * r * 80 * 4);
+    launch_fills(f, s);
+  }
   bcast_rows_kernel<<<256, 256, 0, s>>>(M.att_bias.f(), 4096, W.gatt.f(), Bp);
   HIP_OK(hipGetLastError());
   const bool persist = use_persistent(c);
@@ -1471,15 +1477,26 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     }
   }
   }
-  HIP_OK(hipStreamSynchronize(s));
-  check_encoder_barrier(c);
-  if (persist) {
-    unsigned err = 0;
-    HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(W.pbar.p) + 16, 4, hipMemcpyDeviceToHost));
-    TTS_CHECK(err == 0, "persistent decoder: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
+  // one host round trip after the decode: barrier error words and the per-row results
+  {
+    int* pin = c->pinned;
+    pin[16] = pin[17] = pin[18] = 0;  // before the copies are enqueued
+    const unsigned* lc = reinterpret_cast<const unsigned*>(W.lc.p);
+    if (W.enc_persist) {
+      HIP_OK(hipMemcpyAsync(&pin[16], lc + 16, 4, hipMemcpyDeviceToHost, s));
+      HIP_OK(hipMemcpyAsync(&pin[17], lc + 512 + 16, 4, hipMemcpyDeviceToHost, s));
+    }
+    if (persist) HIP_OK(hipMemcpyAsync(&pin[18], reinterpret_cast<unsigned*>(W.pbar.p) + 16, 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipMemcpyAsync(&pin[20], W.ctl.i() + 4, 3 * BMAX * 4, hipMemcpyDeviceToHost, s));
+    HIP_OK(hipStreamSynchronize(s));
+    TTS_CHECK(!W.enc_persist || (pin[16] == 0 && pin[17] == 0),
+              "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past "
+              "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
+    TTS_CHECK(!persist || pin[18] == 0,
+              "persistent decoder: grid barrier timed out (workgroups not co-resident) or preempted past "
+              "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
   }
-  std::vector<int> res(3 * BMAX);
-  HIP_OK(hipMemcpy(res.data(), W.ctl.i() + 4, 3 * BMAX * 4, hipMemcpyDeviceToHost));
+  std::vector<int> res(c->pinned + 20, c->pinned + 20 + 3 * BMAX);
   int maxM = 0;
   std::vector<int> mlens(B);
   for (int i = 0; i < B; ++i) {
@@ -1491,8 +1508,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     maxM = std::max(maxM, mlens[i]);
   }
   HIP_OK(hipMemcpyAsync(W.mlens.p, mlens.data(), B * 4, hipMemcpyHostToDevice, s));
-  const long fb = (long)S_cap * r * 80;
-  HIP_OK(hipMemsetAsync(W.post.p, 0, (size_t)B * fb * 4, s));
+  const long fb = (long)S_cap * r * 80;  // W.post was zeroed with the decoder state
   run_postnet(c, W.dec.f(), fb, W.mlens.i(), B, S_cap * r, maxM, W.post.f(), fb, s);
   // scatter back to the caller's row order: output row b <- decode row inv[b]
   HIP_OK(hipMemcpyAsync(d_map, inv.data(), B * 4, hipMemcpyHostToDevice, s));
@@ -2545,8 +2561,8 @@ int tts_ctx_create(int device, tts_ctx** out) {
     HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[0], hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[1], hipEventDisableTiming));
     for (auto& e : c->ev_dec) HIP_OK(hipEventCreate(&e));
-    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), 64, hipHostMallocDefault));
-    std::memset(c->pinned, 0, 64);
+    HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), 1024, hipHostMallocDefault));
+    std::memset(c->pinned, 0, 1024);
     *out = c.release();
   });
 }

@@ -106,6 +106,25 @@ std::vector<float> merge_convT_phases(const std::vector<float>& Wm, int u, int C
 // MFMA fragment order: dst[((m*nkc + kc)*64 + l)*4 + s] = Wm[m*16 + (l&15)][kc*16 + 4*(l>>4) + s]
 void swizzle_rows16(const float* Wm, int rows, int rows_pad, int Kdim, float* dst);
 
+// Several buffer fills as ONE launch (each hipMemsetAsync is a ~5 us kernel of its own): entries
+// are (pointer, bytes, 32-bit fill word); bytes a multiple of 4, entries must not overlap.
+struct FillList {
+  static constexpr int N = 24;
+  int n = 0;
+  void* p[N];
+  long words[N];
+  unsigned val[N];
+  void add(void* ptr, size_t bytes, unsigned v = 0) {
+    TTS_CHECK(n < N && bytes % 4 == 0, "FillList: too many entries or unaligned size");
+    if (!bytes) return;
+    p[n] = ptr;
+    words[n] = (long)(bytes / 4);
+    val[n] = v;
+    ++n;
+  }
+};
+void launch_fills(const FillList& f, hipStream_t s);
+
 // PQMF synthesis (pqmf.py:51-56): x (B, N, L) -> y (B, 1, N*L)
 void launch_pqmf_synthesis(const float* x, long xb, long xc, const float* G, int N, int taps,
                            const int* lens, int len_add, int L_mul, int maxL, int B, float* y, long yb,

@@ -16,6 +16,7 @@
 // A wave owns MI x NI 16x16 tiles so each LDS read feeds MI MFMAs and each weight fragment NI.
 #include "common.h"
 #include "conv_epi.h"
+#include <algorithm>
 #include <stdexcept>
 
 
@@ -316,5 +317,32 @@ void launch_pqmf_synthesis(const float* x, long xb, long xc, const float* G, int
   if (maxL <= 0 || B <= 0) return;
   dim3 grid((N * maxL + 255) / 256, B);
   pqmf_synth_kernel<<<grid, 256, 0, s>>>(x, xb, xc, G, N, taps, lens, len_add, L_mul, y, yb);
+  HIP_OK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------- FillList
+__global__ __launch_bounds__(256) void fill_list_kernel(FillList f) {
+  const int e = blockIdx.y;
+  unsigned* p = static_cast<unsigned*>(f.p[e]);
+  const long n = f.words[e];
+  const unsigned v = f.val[e];
+  const long stride = (long)gridDim.x * blockDim.x;
+  const long i0 = (long)blockIdx.x * blockDim.x + threadIdx.x;
+  if ((reinterpret_cast<uintptr_t>(p) & 15) == 0) {  // 16-byte stores for the aligned bulk
+    uint4* q = reinterpret_cast<uint4*>(p);
+    const uint4 v4 = make_uint4(v, v, v, v);
+    for (long i = i0; i < n / 4; i += stride) q[i] = v4;
+    for (long i = (n / 4) * 4 + i0; i < n; i += stride) p[i] = v;
+  } else {
+    for (long i = i0; i < n; i += stride) p[i] = v;
+  }
+}
+
+void launch_fills(const FillList& f, hipStream_t s) {
+  if (!f.n) return;
+  long mx = 0;
+  for (int i = 0; i < f.n; ++i) mx = std::max(mx, f.words[i]);
+  const int gx = (int)std::min<long>(512, std::max<long>(1, (mx / 4 + 255) / 256));
+  fill_list_kernel<<<dim3(gx, f.n), 256, 0, s>>>(f);
   HIP_OK(hipGetLastError());
 }

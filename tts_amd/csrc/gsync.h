@@ -27,8 +27,13 @@ inline void arm_barrier(unsigned* bar, int nblk, hipStream_t s) {
     ms = ms < 1.0 ? 1.0 : (ms > 40000.0 ? 40000.0 : ms);
     return (unsigned)(ms * 1e5);  // 100 MHz ticks
   }();
-  HIP_OK(hipMemsetAsync(bar, 0, (size_t)nblk * 512 * 4, s));
-  for (int i = 0; i < nblk; ++i) HIP_OK(hipMemsetD32Async((hipDeviceptr_t)(bar + i * 512 + BAR_TMO), (int)ticks, 1, s));
+  FillList f;
+  for (int i = 0; i < nblk; ++i) {
+    f.add(bar + i * 512, BAR_TMO * 4);
+    f.add(bar + i * 512 + BAR_TMO, 4, ticks);
+    f.add(bar + i * 512 + BAR_TMO + 1, (512 - BAR_TMO - 1) * 4);
+  }
+  launch_fills(f, s);
 }
 
 // Launch a kernel whose workgroups meet at grid barriers. Every workgroup must be resident at
