@@ -102,7 +102,7 @@ static int check(int C, int d, float xscale) {
   a.oflow = dup(std::vector<unsigned>(1, 0));
   a.max_q = 301;
   a.B = B;
-  launch_resblock_x3(a, C, S);
+  launch_resblock_x3(a, lens, C, S);
   HIP_OK(hipStreamSynchronize(S));
   std::vector<float> y((size_t)B * C * Ls);
   HIP_OK(hipMemcpy(y.data(), a.y, y.size() * 4, hipMemcpyDeviceToHost));
@@ -187,25 +187,33 @@ int main(int argc, char** argv) {
     };
     if (prof_C) {
       a.dil = 9;
-      for (int i = 0; i < 5; ++i) launch_resblock_x3(a, C, S);
+      for (int i = 0; i < 5; ++i) launch_resblock_x3(a, kM, C, S);
       HIP_OK(hipStreamSynchronize(S));
       continue;
     }
     timeit("fp32", [&] { launch_resblock(a, C, S); });
-    timeit("split-f16 (library tile)", [&] { launch_resblock_x3(a, C, S); });
+    timeit("split-f16 (library tile)", [&] { launch_resblock_x3(a, kM, C, S); });
     if (C == 192) {
-      timeit("x3 TQ64 12x1", [&] { launch_rbx3<192, 64, 12, 1>(a, S); });
-      timeit("x3 TQ32 12x1", [&] { launch_rbx3<192, 32, 12, 1>(a, S); });
-      timeit("x3 TQ64 6x2", [&] { launch_rbx3<192, 64, 6, 2>(a, S); });
-      timeit("x3 TQ32 4x1", [&] { launch_rbx3<192, 32, 4, 1>(a, S); });
+      timeit("x3 TQ64 12x1", [&] { launch_rbx3<192, 64, 12, 1>(a, kM, S); });
+      timeit("x3 TQ64 4x1 (MI3 NI4)", [&] { launch_rbx3<192, 64, 4, 1>(a, kM, S); });
+      timeit("x3 TQ64 6x1 (MI2 NI4)", [&] { launch_rbx3<192, 64, 6, 1>(a, kM, S); });
+      timeit("x3 TQ64 4x2 (MI3 NI2)", [&] { launch_rbx3<192, 64, 4, 2>(a, kM, S); });
+      timeit("x3 TQ64 6x2 (MI2 NI2)", [&] { launch_rbx3<192, 64, 6, 2>(a, kM, S); });
+      timeit("x3 TQ32 4x1 (MI3 NI2)", [&] { launch_rbx3<192, 32, 4, 1>(a, kM, S); });
     } else if (C == 96) {
-      timeit("x3 TQ128 6x2", [&] { launch_rbx3<96, 128, 6, 2>(a, S); });
-      timeit("x3 TQ64 6x1", [&] { launch_rbx3<96, 64, 6, 1>(a, S); });
-      timeit("x3 TQ64 3x2", [&] { launch_rbx3<96, 64, 3, 2>(a, S); });
+      timeit("x3 TQ128 6x2", [&] { launch_rbx3<96, 128, 6, 2>(a, kM, S); });
+      timeit("x3 TQ128 2x2 (MI3 NI4)", [&] { launch_rbx3<96, 128, 2, 2>(a, kM, S); });
+      timeit("x3 TQ128 2x4 (MI3 NI2)", [&] { launch_rbx3<96, 128, 2, 4>(a, kM, S); });
+      timeit("x3 TQ128 3x2 (MI2 NI4)", [&] { launch_rbx3<96, 128, 3, 2>(a, kM, S); });
+      timeit("x3 TQ128 3x4 (MI2 NI2)", [&] { launch_rbx3<96, 128, 3, 4>(a, kM, S); });
+      timeit("x3 TQ64 2x2 (MI3 NI2)", [&] { launch_rbx3<96, 64, 2, 2>(a, kM, S); });
     } else {
-      timeit("x3 TQ128 3x4", [&] { launch_rbx3<48, 128, 3, 4>(a, S); });
-      timeit("x3 TQ64 3x2", [&] { launch_rbx3<48, 64, 3, 2>(a, S); });
-      timeit("x3 TQ64 3x4", [&] { launch_rbx3<48, 64, 3, 4>(a, S); });
+      timeit("x3 TQ128 3x4", [&] { launch_rbx3<48, 128, 3, 4>(a, kM, S); });
+      timeit("x3 TQ128 1x4 (MI3 NI2)", [&] { launch_rbx3<48, 128, 1, 4>(a, kM, S); });
+      timeit("x3 TQ128 1x8 (MI3 NI1)", [&] { launch_rbx3<48, 128, 1, 8>(a, kM, S); });
+      timeit("x3 TQ128 1x2 (MI3 NI4)", [&] { launch_rbx3<48, 128, 1, 2>(a, kM, S); });
+      timeit("x3 TQ256 1x4 (MI3 NI4)", [&] { launch_rbx3<48, 256, 1, 4>(a, kM, S); });
+      timeit("x3 TQ256 1x8 (MI3 NI2)", [&] { launch_rbx3<48, 256, 1, 8>(a, kM, S); });
     }
   }
   printf(fails ? "FAILED\n" : "all checks passed\n");

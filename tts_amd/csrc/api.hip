@@ -1756,7 +1756,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
         ra.Wd16 = w16.p;
         ra.Wf16 = G.rb_wf16[i * G.nres + bk].p;
         ra.oflow = cc.oflow;
-        launch_resblock_x3(ra, C, s);
+        launch_resblock_x3(ra, lens.data(), C, s);
       } else {
         launch_resblock(ra, C, s);
       }

@@ -152,7 +152,9 @@ struct ResArgs {
 };
 void launch_resblock(const ResArgs& a, int C, hipStream_t s);
 bool resblock_x3_supported(int C);
-void launch_resblock_x3(const ResArgs& a, int C, hipStream_t s);
+// persistent: one workgroup per CU loops over the (utterance, position) tiles; h_lens = the
+// host copy of lens (tile count)
+void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t s);
 void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf, int C,
                       std::vector<uint16_t>& wd16, std::vector<uint16_t>& wf16);
 

@@ -132,19 +132,16 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
     for (int j = 0; j < SPT; ++j) {
       if (sgv[j] < 4) {
         const bool keep = sval[j] && 32 * ch + 8 * sgv[j] < a.Cin;  // zero padding; channels past Cin
-        float mx = 0.f;
-        h8 hi, lo;
+        float mx = 0.f, v[8];
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          float v = keep ? sr[j][c] : 0.f;
-          mx = fmaxf(mx, __builtin_fabsf(v));
-          if (act) v = lrelu02(v);
-          _Float16 h, l;
-          split_fast(v, h, l);
-          hi[c] = h;
-          lo[c] = l;
+          v[c] = keep ? sr[j][c] : 0.f;
+          mx = fmaxf(mx, __builtin_fabsf(v[c]));
+          if (act) v[c] = lrelu02(v[c]);
         }
         bad |= !(mx < F16_RANGE);  // |lrelu(v)| <= |v|
+        h8 hi, lo;
+        split8(v, hi, lo);
         *reinterpret_cast<h8*>(X + srow[j] * CX_XR + 8 * sgv[j]) = hi;
         *reinterpret_cast<h8*>(X + srow[j] * CX_XR + 32 + 8 * sgv[j]) = lo;
       }

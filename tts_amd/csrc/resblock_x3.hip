@@ -3,19 +3,25 @@
 //   h = conv_k3_dil_d(ReflectionPad(d)(LeakyReLU(x))) + b_d
 //   y = [W_1x1 | W_sc] . [lrelu(h); x] + (b_1x1 + b_sc)
 // Same structure as the fp32 kernel (resblock.hip): one workgroup owns all C output channels of
-// TQ positions, so h never leaves the CU.
+// TQ positions, so h never leaves the CU. Persistent: one workgroup per CU (the LDS tile allows no
+// more) loops over the (utterance, position) tiles; the next tile's first two staging chunks and
+// phase-1 weights load during this tile's phase 2, so neither the staging latency of a tile's
+// start nor its output stores sit on the critical path (a launch-per-tile grid spent ~2 us of a
+// 7-21 us tile in its prologue, tools/rbx3_bench.hip).
 //   staging   32 input channels x (TQ + 2d) positions of lrelu(x), reflect-padded per utterance,
 //             split into hi / lo f16 and stored position-major ([pos][32 hi | 32 lo | 16 pad]):
 //             one lane's B operand (8 consecutive channels of one position) is one ds_read_b128,
 //             and the 160-byte row stride keeps those reads bank-conflict free for any tap offset.
-//             The centre positions' raw x (shortcut input) go split into HX. Double-buffered:
-//             chunk c+1's global loads are in flight during chunk c's MFMAs.
+//             The centre positions' raw x (shortcut input) go split into HX. Two LDS buffers and
+//             two register sets: chunk c+2's global loads are in flight during chunk c's MFMAs.
 //   phase 1   h = Wd . X over K = 3 taps x C channels (3 MFMAs per product), weights (A operand,
 //             pre-split on the host) streamed from L2 through a 3-slot register ring.
 //   phase 2   lrelu(h + b_d) split into HX ([pos][2C hi | 2C lo]), then y = Wf . HX, K = 2C.
 // Any operand outside the f16 range sets *oflow; the host then re-runs the call in fp32.
 #include "common.h"
 #include "split16.h"
+
+#include <algorithm>
 
 namespace {
 constexpr int X3_DMAX = 27;   // largest dilation (3^3, num_res_blocks <= 4)
@@ -27,8 +33,13 @@ __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
 __device__ __forceinline__ float lrelu_x3(float v) { return fmaxf(v, 0.2f * v); }  // == lrelu02
 }  // namespace
 
+// Tile of the persistent loop: utterance b, positions [q0, q0 + TQ) of its L = (lens + len_add) * mul
+struct RbTile {
+  int b, q0, L;
+};
+
 template <int C, int TQ, int WM, int WN>
-__global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a) {
+__global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, int ntiles) {
   constexpr int NTHR = 64 * WM * WN;
   constexpr int MI = C / 16 / WM;
   constexpr int NI = TQ / 16 / WN;
@@ -36,15 +47,13 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a) {
   constexpr int NCH = (C + 31) / 32;     // staging chunks of 32 input channels (C = 48: 16 zero channels)
   constexpr int NK1 = 3 * NCH;           // phase-1 k-steps: (chunk, tap)
   constexpr int NK2 = 2 * C / 32;        // phase-2 k-steps
+  constexpr int NTOT = NK1 + NK2;        // weight sequence of one tile (the ring runs on across tiles)
   static_assert(NK2 * 32 == 2 * C && NK2 % 3 == 0, "phase-2 k-steps: multiple of the 3-slot ring");
   constexpr int HR = 4 * C + 16;         // HX row, halves: 2C hi | 2C lo | 16 pad (8C + 32 bytes)
   constexpr int SPT = (4 * (TQ + 2 * X3_DMAX) + NTHR - 1) / NTHR;  // staging items (8 channels x 1 pos) per thread
   extern __shared__ __attribute__((aligned(16))) _Float16 sh[];
 
-  const int b = blockIdx.y;
-  const int L = (a.lens[b] + a.len_add) * a.mul;
-  const int q0 = blockIdx.x * TQ;
-  if (q0 >= L) return;
+  int t = blockIdx.x;
   const int d = a.dil;
   const int ROWS = TQ + 2 * d;
   _Float16* X0 = sh;
@@ -52,18 +61,43 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a) {
   _Float16* HX = sh + 2 * ROWS * XR;
 
   const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = tid >> 6;
+  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = wave / WN, wn = wave % WN;
   const int nb = wn * 16 * NI + (lane & 15);  // this lane's position (B column) for ni = 0
   const int kg = 8 * (lane >> 4);             // this lane's k offset inside a k-step
   const int mt0 = wm * MI;
   bool bad = false;
 
+  // tile index -> (utterance, first position): per-utterance tile offsets (exclusive scan over the
+  // <= 64 lengths, once per workgroup, in LDS); a lookup is one LDS read per lane and a ballot
+  __shared__ int tcum[65], tlen[64];
+  if (wave == 0) {
+    const int L = lane < a.B ? (a.lens[lane] + a.len_add) * a.mul : 0;
+    const int n = (L + TQ - 1) / TQ;
+    int v = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (lane >= o) v += y;
+    }
+    tcum[lane] = v - n;
+    tlen[lane] = L;
+    if (lane == 63) tcum[64] = v;
+  }
+  __syncthreads();
+  auto tile_of = [&](int i) {
+    const bool hit = lane < a.B && tcum[lane] <= i && i < tcum[lane + 1];
+    const unsigned long long m = __ballot(hit);
+    const int b = __builtin_amdgcn_readfirstlane(m ? __ffsll((long long)m) - 1 : 0);
+    RbTile r;
+    r.b = b;
+    r.q0 = __builtin_amdgcn_readfirstlane((i - tcum[b]) * TQ);
+    r.L = __builtin_amdgcn_readfirstlane(tlen[b]);
+    return r;
+  };
+
   // ---- staging: item e = (channel octet g, row); rows fastest so that lanes read consecutive
   //      positions of one channel (coalesced); clamped addresses, no per-element guard
-  const __amdgpu_buffer_rsrc_t xr = rsrc(a.x + (long)b * a.sb);  // one utterance: < 2^31 bytes
-  const int i0 = q0 - d;
-  const bool interior = i0 >= 0 && i0 + ROWS <= L;
   int srow[SPT], sg[SPT];
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
@@ -71,24 +105,27 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a) {
     sg[j] = e / ROWS;
     srow[j] = e - sg[j] * ROWS;
   }
-  float st[SPT][8];
-  auto stage_load = [&](int ch) {
+  float st[2][SPT][8];
+  auto stage_load = [&](const RbTile& T, float (&sr)[SPT][8], int ch) {
+    const __amdgpu_buffer_rsrc_t xr = rsrc(a.x + (long)T.b * a.sb);  // one utterance: < 2^31 bytes
+    const int i0 = T.q0 - d;
+    const bool interior = i0 >= 0 && i0 + ROWS <= T.L;
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
       int i = i0 + srow[j];
       if (!interior) {  // reflection (torch ReflectionPad1d), then clamp
         if (i < 0) i = -i;
-        if (i >= L) i = 2 * (L - 1) - i;
-        i = i < 0 ? 0 : (i >= L ? L - 1 : i);
+        if (i >= T.L) i = 2 * (T.L - 1) - i;
+        i = i < 0 ? 0 : (i >= T.L ? T.L - 1 : i);
       }
       const int c0 = min(32 * ch + 8 * min(sg[j], 3), C - 8);
       const int vo = (c0 * a.Ls + i) * 4;  // per-lane offset; the 8 channel rows are SGPR offsets
 #pragma unroll
       for (int c = 0; c < 8; ++c)
-        st[j][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, c * a.Ls * 4, 0));
+        sr[j][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, c * a.Ls * 4, 0));
     }
   };
-  auto stage_store = [&](_Float16* X, int ch) {
+  auto stage_store = [&](_Float16* X, const float (&sr)[SPT][8], int ch) {
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
       const int g = sg[j], row = srow[j];
@@ -97,29 +134,20 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a) {
         float v[8], mx = 0.f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
-          v[c] = real ? st[j][c] : 0.f;
+          v[c] = real ? sr[j][c] : 0.f;
           mx = fmaxf(mx, __builtin_fabsf(v[c]));
         }
         bad |= !(mx < F16_RANGE);  // |lrelu(v)| <= |v|: one check covers both splits
-        h8 hi, lo;
+        float lv[8];
 #pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          _Float16 h, l;
-          split_fast(lrelu_x3(v[c]), h, l);
-          hi[c] = h;
-          lo[c] = l;
-        }
+        for (int c = 0; c < 8; ++c) lv[c] = lrelu_x3(v[c]);
+        h8 hi, lo;
+        split8(lv, hi, lo);
         *reinterpret_cast<h8*>(X + row * XR + 8 * g) = hi;
         *reinterpret_cast<h8*>(X + row * XR + 32 + 8 * g) = lo;
         const int p = row - d;
         if (real && p >= 0 && p < TQ) {  // raw x of the centre positions: the shortcut's operand
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            _Float16 h, l;
-            split_fast(v[c], h, l);
-            hi[c] = h;
-            lo[c] = l;
-          }
+          split8(v, hi, lo);
           *reinterpret_cast<h8*>(HX + p * HR + C + 32 * ch + 8 * g) = hi;
           *reinterpret_cast<h8*>(HX + p * HR + 3 * C + 32 * ch + 8 * g) = lo;
         }
@@ -127,17 +155,19 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a) {
     }
   };
 
-  // ---- weights: A fragments [mt][k-step][lane][hi 8 | lo 8], phase 1 then phase 2 as one
-  //      sequence through a 3-slot ring, so phase 2's first slots load during phase 1's last
+  // ---- weights: A fragments [mt][k-step][lane][hi 8 | lo 8]; phase 1 then phase 2 as one
+  //      sequence through a 3-slot ring that wraps into the next tile's phase 1, so every slot
+  //      is reloaded in place right after its MFMAs and never waits at a tile boundary
   // buffer loads: the lane's 32 bytes are a VGPR offset, the (m-tile, k-step) block an SGPR one
   const __amdgpu_buffer_rsrc_t wdr = rsrc(a.Wd16), wfr = rsrc(a.Wf16);
   const int wlo = lane * 32;
   h8 ring[3][MI][2];
   auto wload = [&](h8 (&r)[MI][2], int seq) {
+    if (seq >= NTOT) seq -= NTOT;
     const bool p1 = seq < NK1;
     const __amdgpu_buffer_rsrc_t wr = p1 ? wdr : wfr;
     const int nk = p1 ? NK1 : NK2;
-    const int ks = p1 ? seq : min(seq - NK1, NK2 - 1);
+    const int ks = p1 ? seq : seq - NK1;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       const int so = ((mt0 + mi) * nk + ks) * 2048;
@@ -146,114 +176,149 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a) {
     }
   };
 
-  // ---------------- phase 1: h = Wd . lrelu(x) ----------------
-  f32x4 am[MI][NI], ac[MI][NI];
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-    for (int ni = 0; ni < NI; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-  stage_load(0);
+  if (t >= ntiles) return;
+  // first tile's prologue; later tiles stage chunks 0 and 1 during the previous tile's phase 2.
+  // Staging runs two chunks ahead: chunk c is loaded into register set c & 1 after chunk c - 3's
+  // MFMAs and stored to LDS buffer c & 1 after chunk c - 1's.
+  RbTile cur = tile_of(t);
+  stage_load(cur, st[0], 0);
 #pragma unroll
   for (int u = 0; u < 3; ++u) wload(ring[u], u);
-  stage_store(X0, 0);
+  if (NCH > 1) stage_load(cur, st[1], 1);
+  stage_store(X0, st[0], 0);
+  if (NCH > 2) stage_load(cur, st[0], 2);
   __syncthreads();
-  for (int ch = 0; ch < NCH; ++ch) {
-    const _Float16* X = (ch & 1) ? X1 : X0;
-    if (ch + 1 < NCH) stage_load(ch + 1);
-    __builtin_amdgcn_sched_barrier(0);
+  f32x4 am[MI][NI], ac[MI][NI];
+  for (;;) {
+    // ---------------- phase 1: h = Wd . lrelu(x) ----------------
 #pragma unroll
-    for (int kq = 0; kq < 3; ++kq) {
-      h8 bh[NI], bl[NI];
+    for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ch = 0; ch < NCH; ++ch) {
+      const _Float16* X = (ch & 1) ? X1 : X0;
+#pragma unroll
+      for (int kq = 0; kq < 3; ++kq) {
+        h8 bh[NI], bl[NI];
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const _Float16* p = X + (nb + ni * 16 + kq * d) * XR + kg;
+          bh[ni] = *reinterpret_cast<const h8*>(p);
+          bl[ni] = *reinterpret_cast<const h8*>(p + 32);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[kq][mi][0], ring[kq][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
+        wload(ring[kq], (ch + 1) * 3 + kq);
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (ch + 1 < NCH) stage_store((ch & 1) ? X0 : X1, st[(ch + 1) & 1], ch + 1);
+      if (ch + 3 < NCH) stage_load(cur, st[(ch + 1) & 1], ch + 3);
+      __syncthreads();
+    }
+    // lrelu(h + b_d), split, into HX[pos][0:C) (hi) and HX[pos][2C:3C) (lo)
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int co = (mt0 + mi) * 16 + 4 * (lane >> 4);
+      float bd[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) bd[j] = a.bd[co + j];
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
-        const _Float16* p = X + (nb + ni * 16 + kq * d) * XR + kg;
-        bh[ni] = *reinterpret_cast<const h8*>(p);
-        bl[ni] = *reinterpret_cast<const h8*>(p + 32);
+        h4 hi, lo;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          _Float16 h, l;
+          split_dev(lrelu_x3(x3_value(am[mi][ni][j], ac[mi][ni][j]) + bd[j]), h, l, bad);
+          hi[j] = h;
+          lo[j] = l;
+        }
+        const int p = nb + ni * 16;
+        *reinterpret_cast<h4*>(HX + p * HR + co) = hi;
+        *reinterpret_cast<h4*>(HX + p * HR + 2 * C + co) = lo;
+        am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[kq][mi][0], ring[kq][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-      wload(ring[kq], (ch + 1) * 3 + kq);
     }
-    if (ch + 1 < NCH) stage_store((ch & 1) ? X0 : X1, ch + 1);
     __syncthreads();
-  }
-  // lrelu(h + b_d), split, into HX[pos][0:C) (hi) and HX[pos][2C:3C) (lo)
+    // the next tile's first two chunks: global loads in flight during phase 2
+    const int tn = t + gridDim.x;
+    const bool more = tn < ntiles;
+    RbTile nxt = cur;
+    if (more) {
+      nxt = tile_of(tn);
+      stage_load(nxt, st[0], 0);
+      if (NCH > 1) stage_load(nxt, st[1], 1);
+    }
+    // ---------------- phase 2: y = [W1 | Wsc] . [lrelu(h); x] ----------------
+    for (int k0 = 0; k0 < NK2; k0 += 3) {
 #pragma unroll
-  for (int mi = 0; mi < MI; ++mi) {
-    const int co = (mt0 + mi) * 16 + 4 * (lane >> 4);
-    float bd[4];
+      for (int u = 0; u < 3; ++u) {
+        const int kc = k0 + u;
+        h8 bh[NI], bl[NI];
 #pragma unroll
-    for (int j = 0; j < 4; ++j) bd[j] = a.bd[co + j];
+        for (int ni = 0; ni < NI; ++ni) {
+          const _Float16* p = HX + (nb + ni * 16) * HR + kc * 32 + kg;
+          bh[ni] = *reinterpret_cast<const h8*>(p);
+          bl[ni] = *reinterpret_cast<const h8*>(p + 2 * C);
+        }
+        __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int ni = 0; ni < NI; ++ni) {
-      h4 hi, lo;
+        for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+          for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[u][mi][0], ring[u][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
+        wload(ring[u], NK1 + kc + 3);  // past NK2: the next tile's phase-1 weights
+      }
+    }
+    float* yb = a.y + (long)cur.b * a.sb;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        _Float16 h, l;
-        split_dev(lrelu_x3(x3_value(am[mi][ni][j], ac[mi][ni][j]) + bd[j]), h, l, bad);
-        hi[j] = h;
-        lo[j] = l;
-      }
-      const int p = nb + ni * 16;
-      *reinterpret_cast<h4*>(HX + p * HR + co) = hi;
-      *reinterpret_cast<h4*>(HX + p * HR + 2 * C + co) = lo;
-      am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-    }
-  }
-  __syncthreads();
-  // ---------------- phase 2: y = [W1 | Wsc] . [lrelu(h); x] ----------------
-  for (int k0 = 0; k0 < NK2; k0 += 3) {
+        const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
+        const float bf = a.bf[co];
 #pragma unroll
-    for (int u = 0; u < 3; ++u) {
-      const int kc = k0 + u;
-      h8 bh[NI], bl[NI];
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        const _Float16* p = HX + (nb + ni * 16) * HR + kc * 32 + kg;
-        bh[ni] = *reinterpret_cast<const h8*>(p);
-        bl[ni] = *reinterpret_cast<const h8*>(p + 2 * C);
-      }
-      __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[u][mi][0], ring[u][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-      wload(ring[u], NK1 + kc + 3);
-    }
-  }
-  float* yb = a.y + (long)b * a.sb;
-#pragma unroll
-  for (int mi = 0; mi < MI; ++mi) {
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
-      const float bf = a.bf[co];
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni) {
-        const int q = q0 + nb + ni * 16;
-        if (q < L) yb[(long)co * a.Ls + q] = x3_value(am[mi][ni][j], ac[mi][ni][j]) + bf;
+        for (int ni = 0; ni < NI; ++ni) {
+          const int q = cur.q0 + nb + ni * 16;
+          if (q < cur.L) yb[(long)co * a.Ls + q] = x3_value(am[mi][ni][j], ac[mi][ni][j]) + bf;
+        }
       }
     }
+    if (!more) break;
+    __syncthreads();  // every wave is done with this tile's X / HX
+    cur = nxt;
+    t = tn;
+    stage_store(X0, st[0], 0);
+    if (NCH > 2) stage_load(cur, st[0], 2);
+    __syncthreads();
   }
   if (bad) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// one resident workgroup per CU (the LDS tile allows no more), each looping over tiles; the
+// dynamic LDS leaves 1 KiB of the CU's 160 KiB for the kernel's static tile tables
+constexpr int RB_DYN_LDS = 159 * 1024;
 template <int C, int TQ, int WM, int WN>
-static void launch_rbx3(const ResArgs& a, hipStream_t s) {
+static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   const int ROWS = TQ + 2 * a.dil;
   const size_t lds = ((size_t)2 * ROWS * XR + (size_t)TQ * (4 * C + 16)) * 2;
-  static bool attr = false;
-  if (!attr) {
+  static int ncu = 0;
+  if (!ncu) {
     HIP_OK(hipFuncSetAttribute((const void*)resblock_x3_kernel<C, TQ, WM, WN>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
+                               hipFuncAttributeMaxDynamicSharedMemorySize, RB_DYN_LDS));
+    int dev = 0;
+    HIP_OK(hipGetDevice(&dev));
+    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
   }
-  TTS_CHECK(lds <= 160 * 1024, "resblock_x3: LDS tile too large");
-  dim3 grid((a.max_q + TQ - 1) / TQ, a.B);
-  resblock_x3_kernel<C, TQ, WM, WN><<<grid, 64 * WM * WN, lds, s>>>(a);
+  TTS_CHECK(lds <= RB_DYN_LDS, "resblock_x3: LDS tile too large");
+  long ntiles = 0;
+  for (int b = 0; b < a.B; ++b) ntiles += ((long)(h_lens[b] + a.len_add) * a.mul + TQ - 1) / TQ;
+  TTS_CHECK(ntiles < (1L << 30), "resblock_x3: too many tiles");
+  if (ntiles == 0) return;
+  const int grid = (int)std::min<long>(ntiles, ncu);
+  resblock_x3_kernel<C, TQ, WM, WN><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles);
 }
 
 bool resblock_x3_supported(int C) { return C == 192 || C == 96 || C == 48; }
@@ -269,15 +334,16 @@ void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf
   wf16 = pack_split_a(C / 16, 2 * C / 32, [&](int m, int k) -> float { return wf[(size_t)m * 2 * C + k]; });
 }
 
-void launch_resblock_x3(const ResArgs& a, int C, hipStream_t s) {
+void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t s) {
   TTS_CHECK(a.dil >= 1 && a.dil <= X3_DMAX, "resblock: dilation must be in [1, 27] (num_res_blocks <= 4)");
   TTS_CHECK(a.Wd16 && a.Wf16 && a.oflow, "resblock_x3: split weights / overflow flag missing");
+  TTS_CHECK(a.B <= 64, "resblock_x3: at most 64 utterances per call");
   if (a.max_q <= 0 || a.B <= 0) return;
   switch (C) {
     // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave
-    case 192: launch_rbx3<192, 64, 12, 1>(a, s); break;
-    case 96: launch_rbx3<96, 128, 6, 2>(a, s); break;
-    case 48: launch_rbx3<48, 128, 3, 4>(a, s); break;
+    case 192: launch_rbx3<192, 64, 12, 1>(a, h_lens, s); break;
+    case 96: launch_rbx3<96, 128, 6, 2>(a, h_lens, s); break;
+    case 48: launch_rbx3<48, 128, 3, 4>(a, h_lens, s); break;
     default: TTS_CHECK(false, "resblock_x3: unsupported channel count");
   }
   HIP_OK(hipGetLastError());
