@@ -877,6 +877,52 @@ def test_pwgan_inference_padding_zero_vs_oracle():
     assert np.abs(y - ref).max() <= 1e-4
 
 
+def test_pwgan_split_f16_equals_fp32_path_and_oracle():
+    """The split-f16 residual-block kernel (pw_layer_x3_kernel, the default) against the fp32-MFMA
+    kernel and the oracle on a ragged 2-row batch long enough for every dilation (up to 512): both
+    within 1e-4 of the oracle, the split path's error at most twice the fp32 path's plus 2e-6, no
+    range fallback; an input scaled past the f16 range re-runs in fp32, bit-identical."""
+    from oracle.pwgan_np import PwganOracle
+    from tts_amd import ParallelWaveganGenerator
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    _dev()
+    fx = load_fixture("pwgan")
+    cfg = PwganConfig(inference_padding=0)
+    sd = synth_state_dict(pwgan_spec(PwganConfig()), int(fx["seed"]))
+    g = ParallelWaveganGenerator(inference_padding=0)
+    g.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    g = g.cuda().eval()
+    rs = np.random.RandomState(21)
+    lens = [9, 4]
+    mel = np.zeros((2, 80, 9), np.float32)
+    for i, L in enumerate(lens):
+        mel[i, :, :L] = rs.uniform(-1, 1, (80, L))
+    noise = rs.randn(2, 1, 9 * 256).astype(np.float32)
+    m, n = torch.from_numpy(mel).cuda(), torch.from_numpy(noise).cuda()
+    eng = _gemm("f32")
+    try:
+        y32 = g.inference(m, lengths=lens, noise=n).cpu().numpy()
+        big32 = g.inference(m * 1e6, lengths=lens, noise=n).cpu().numpy()
+    finally:
+        eng = _gemm("x3")
+    n0 = eng.gemm_mode()[1]
+    y16 = g.inference(m, lengths=lens, noise=n).cpu().numpy()
+    assert eng.gemm_mode() == ("x3", n0)
+    orc = PwganOracle(sd, cfg)
+    e16 = e32 = 0.0
+    for i, L in enumerate(lens):
+        ref = orc.inference(mel[i, :, :L], noise[i, 0, :L * 256])
+        e16 = max(e16, float(np.abs(y16[i, 0, :L * 256] - ref).max()))
+        e32 = max(e32, float(np.abs(y32[i, 0, :L * 256] - ref).max()))
+        assert not y16[i, 0, L * 256:].any()
+    print(f"PWGAN waveform error vs oracle: split-f16 {e16:.2e}, fp32 {e32:.2e}")
+    assert e16 <= 1e-4 and e32 <= 1e-4
+    assert e16 <= 2 * e32 + 2e-6
+    big16 = g.inference(m * 1e6, lengths=lens, noise=n).cpu().numpy()
+    assert eng.gemm_mode()[1] == n0 + 1
+    assert np.array_equal(big16, big32, equal_nan=True)
+
+
 def test_glow_length_and_noise_scale_vs_oracle():
     """GlowTts.length_scale / noise_scale (glow_tts.py:172-186) away from their defaults, against the
     oracle: y_lengths and the path exact, mel <= 1e-4."""

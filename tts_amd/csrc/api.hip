@@ -42,6 +42,11 @@ void launch_pw_first(const float* noise, long nb, const float* w, const float* b
 void launch_pw_layer(const float* x, const float* c, float* xn, float* skip, const float* W1, const float* b1,
                      const float* W2, const float* b2, const int* lens, const float* zeros, int len_add, int hop,
                      int Tmax, int dil, int first, int B, int variant, hipStream_t st);
+void launch_pw_layer_x3(const float* x, const float* c, float* xn, float* skip, const void* W1x, const float* b1,
+                        const void* W2x, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
+                        int first, int B, unsigned* oflow, hipStream_t st);
+void pack_pw_layer_x3(const std::vector<float>& m1, const std::vector<float>& m2, std::vector<uint16_t>& w1x,
+                      std::vector<uint16_t>& w2x);
 void launch_pw_out(const float* skip, float scale, const float* W3, const float* b3, const float* w4,
                    const float* b4, const int* lens, int len_add, int hop, int Tmax, float* out, int B,
                    hipStream_t st);
@@ -408,6 +413,7 @@ struct PwganModel {
   ConvLayer conv_in;                 // 80 -> 80, k1, no bias
   std::vector<DevBuf> up_h;          // per factor s: 2s + 1 taps
   std::vector<DevBuf> W1, b1, W2, b2;  // per residual block (pw_layer_kernel layouts)
+  std::vector<DevBuf> W1x, W2x;        // split-f16 forms (pw_layer_x3_kernel); empty if out of range
   DevBuf W3, b3, w4, b4;
 };
 
@@ -2410,6 +2416,10 @@ void pwgan_finalize(tts_ctx* c, int layers, int stacks, const int32_t* ups, int 
   P.W2.resize(layers);
   P.b2.clear();
   P.b2.resize(layers);
+  P.W1x.clear();
+  P.W1x.resize(layers);
+  P.W2x.clear();
+  P.W2x.resize(layers);
   for (int l = 0; l < layers; ++l) {
     const std::string q = "conv_layers." + std::to_string(l) + ".";
     const auto wd = wn_weight(h, q + "conv", {G, R, 3});
@@ -2442,6 +2452,15 @@ void pwgan_finalize(tts_ctx* c, int layers, int stacks, const int32_t* ups, int 
     swizzle_rows16(m2.data(), R + S, R + S, G / 2, sw2.data());
     P.W2[l].upload(sw2);
     P.b2[l].upload(bb2);
+    bool in_range = true;
+    for (float v : m1) in_range &= std::fabs(v) < F16_RANGE;
+    for (float v : m2) in_range &= std::fabs(v) < F16_RANGE;
+    if (in_range) {
+      std::vector<uint16_t> w1x, w2x;
+      pack_pw_layer_x3(m1, m2, w1x, w2x);
+      P.W1x[l].upload(w1x);
+      P.W2x[l].upload(w2x);
+    }
   }
   P.W3.upload(wn_weight(h, "last_conv_layers.1", {S, S, 1}));
   P.b3.upload(need(h, "last_conv_layers.1.bias", {S}).d);
@@ -2515,9 +2534,14 @@ void pwgan_infer(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int
     return 1;
   }();
   const int per_stack = P.layers / P.stacks;
+  unsigned* flag = x3_flag(c);
   for (int l = 0; l < P.layers; ++l) {
-    launch_pw_layer(x, cfeat, xn, W.skip.f(), P.W1[l].f(), P.b1[l].f(), P.W2[l].f(), P.b2[l].f(), dl, W.zeros.f(),
-                    2 * pad, hop, Tmax, 1 << (l % per_stack), l == 0, B, variant, s);
+    if (flag && P.W1x[l].p)
+      launch_pw_layer_x3(x, cfeat, xn, W.skip.f(), P.W1x[l].p, P.b1[l].f(), P.W2x[l].p, P.b2[l].f(), dl, 2 * pad,
+                         hop, Tmax, 1 << (l % per_stack), l == 0, B, flag, s);
+    else
+      launch_pw_layer(x, cfeat, xn, W.skip.f(), P.W1[l].f(), P.b1[l].f(), P.W2[l].f(), P.b2[l].f(), dl, W.zeros.f(),
+                      2 * pad, hop, Tmax, 1 << (l % per_stack), l == 0, B, variant, s);
     std::swap(x, xn);
   }
   launch_pw_out(W.skip.f(), std::sqrt(1.0f / P.layers), P.W3.f(), P.b3.f(), P.w4.f(), P.b4.f(), dl, 2 * pad, hop,
@@ -2735,7 +2759,7 @@ int tts_pwgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B
     TTS_CHECK(c && d_mel && h_lens && d_noise && d_out, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
-    pwgan_infer(c, d_mel, h_lens, B, M_max, pad, d_noise, d_out);
+    with_x3_fallback(c, [&] { pwgan_infer(c, d_mel, h_lens, B, M_max, pad, d_noise, d_out); });
     leave(c, stream);
   });
 }

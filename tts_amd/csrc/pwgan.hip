@@ -13,6 +13,7 @@
 //   epilogue  x' = (out + b + x) / 4  -> ping-pong buffer;  skip (+)= s + b  (in place)
 // HBM per sample per block: x (+halo, L2) 256 B, c 320 B, skip r/w 512 B, x' 256 B.
 #include "common.h"
+#include "split16.h"
 
 namespace {
 constexpr int PW_TQ = 128;          // time columns per workgroup
@@ -432,4 +433,220 @@ void launch_pw_out(const float* skip, float scale, const float* W3, const float*
   pw_out_kernel<<<dim3((Tmax + 255) / 256, B), 256, 0, st>>>(skip, scale, W3, b3, w4, b4, lens, len_add, hop, Tmax,
                                                              out);
   HIP_OK(hipGetLastError());
+}
+
+// ------------------------------------------------------------------------------------------
+// The residual block on the f16 MFMA with split-f16 operands (split16.h), the
+// same arithmetic as pw_layer_kernel at ~2x its speed:
+//   GEMM1  9 k-steps of 32: the 3 dilated taps x 2 x-channel halves, then the 80 aux channels
+//          padded to 96; each k-step staged as [pos][32 hi | 32 lo | 16 pad] (conflict-free
+//          ds_read_b128 B operands), two steps ahead through two register sets
+//   gate   z = tanh * sigmoid of the interleaved row pairs, split, into two [pos][32 | 32] planes
+//   GEMM2  2 k-steps over the z planes; rows 0..63 conv1x1_out, 64..127 conv1x1_skip
+// 4 waves (4 x 1): 32 gate rows x 64 positions each; weights (pre-split A fragments, L2-resident)
+// through a 3-slot register ring that runs from GEMM1 straight into GEMM2.
+namespace {
+constexpr int PX_XR = 80;                 // staging row, halves
+constexpr int PX_NK1 = 9, PX_NK2 = 2;     // k-steps
+}  // namespace
+
+// WN column groups of 64 positions: TQ = 64 WN positions, 4 WN waves (4 x WN)
+template <int WN>
+__global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, const void* W1x, const void* W2x,
+                                                               unsigned* oflow) {
+  constexpr int TQ = 64 * WN;
+  constexpr int PX_PLANE = TQ * PX_XR;  // one staged k-step / one z plane (halves)
+  __shared__ __attribute__((aligned(16))) _Float16 Xs[2 * PX_PLANE];
+  __shared__ __attribute__((aligned(16))) _Float16 Zs[2 * PX_PLANE];
+  const int b = blockIdx.y;
+  const int T = (a.lens[b] + a.len_add) * a.hop;
+  const int t0 = blockIdx.x * TQ;
+  if (t0 >= T) return;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave / WN, wn = wave % WN;  // 4 x WN waves: 32 rows x 64 positions
+  const int nb = wn * 64 + (lane & 15), kg = 8 * (lane >> 4);
+  const float* xb = a.x + (long)b * PW_R * a.Tmax;
+  const float* cb = a.c + (long)b * PW_A * a.Tmax;
+  bool bad = false;
+
+  // staging item of this thread: channel octet g (0..3) of the k-step, position q (0..127)
+  const int sg = tid / TQ, sq = tid % TQ;
+  float st[2][8];
+  auto stage_load = [&](float (&r8)[8], int ks) {
+    const float* src;
+    int off, c0, cmax;
+    if (ks < 6) {
+      src = xb;
+      c0 = 32 * (ks & 1) + 8 * sg;
+      off = (ks / 2 - 1) * a.dil;
+      cmax = PW_R;
+    } else {
+      src = cb;
+      c0 = 32 * (ks - 6) + 8 * sg;
+      off = 0;
+      cmax = PW_A;
+    }
+    const int t = t0 + sq + off;
+    const bool ok = t >= 0 && t < T && c0 < cmax;
+    const float* p = src + (long)min(c0, cmax - 8) * a.Tmax + (ok ? t : 0);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      const float v = p[(long)c * a.Tmax];
+      r8[c] = ok ? v : 0.f;
+    }
+  };
+  auto stage_store = [&](_Float16* X, const float (&r8)[8]) {
+    float mx = 0.f;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) mx = fmaxf(mx, __builtin_fabsf(r8[c]));
+    bad |= !(mx < F16_RANGE);
+    h8 hi, lo;
+    split8(r8, hi, lo);
+    *reinterpret_cast<h8*>(X + sq * PX_XR + 8 * sg) = hi;
+    *reinterpret_cast<h8*>(X + sq * PX_XR + 32 + 8 * sg) = lo;
+  };
+
+  // weights: A fragments [m16 (8)][k-step][lane][hi 8 | lo 8]; sequence 0..8 = GEMM1, 9..10 = GEMM2
+  const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W1x), 0, 0x7fffffff, 0x00020000);
+  const __amdgpu_buffer_rsrc_t w2r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W2x), 0, 0x7fffffff, 0x00020000);
+  const int mt0 = wm * 2;
+  h8 ring[3][2][2];
+  auto wload = [&](h8 (&r)[2][2], int seq) {
+    seq = min(seq, PX_NK1 + PX_NK2 - 1);
+    const bool g1 = seq < PX_NK1;
+    const __amdgpu_buffer_rsrc_t wr = g1 ? w1r : w2r;
+    const int nk = g1 ? PX_NK1 : PX_NK2, ks = g1 ? seq : seq - PX_NK1;
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int so = ((mt0 + mi) * nk + ks) * 2048;
+      r[mi][0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, lane * 32, so, 0));
+      r[mi][1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, lane * 32 + 16, so, 0));
+    }
+  };
+
+  // the epilogue's residual operands (x for the conv1x1_out rows, the running skip sum for the
+  // skip rows), loaded now so their latency hides under the GEMMs
+  float res[2][4][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int R = wm * 32 + mi * 16 + 4 * (lane >> 4) + j;
+      const bool out_row = R < PW_R;
+      const float* src = out_row ? a.x : a.skip;
+      const long rowb = ((long)b * 64 + (out_row ? R : R - PW_R)) * a.Tmax;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int t = min(t0 + nb + ni * 16, T - 1);
+        res[mi][j][ni] = (out_row || !a.first) ? src[rowb + t] : 0.f;
+      }
+    }
+  f32x4 am[2][4], ac[2][4];
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+  auto kstep = [&](const _Float16* X, const h8 (&w)[2][2]) {
+    h8 bh[4], bl[4];
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const _Float16* q = X + (nb + ni * 16) * PX_XR + kg;
+      bh[ni] = *reinterpret_cast<const h8*>(q);
+      bl[ni] = *reinterpret_cast<const h8*>(q + 32);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) mfma_x3(w[mi][0], w[mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
+  };
+
+  // GEMM1: staging two k-steps ahead (step s loaded into set s & 1 after step s - 3's MFMAs,
+  // stored to LDS buffer s & 1 after step s - 1's)
+  stage_load(st[0], 0);
+#pragma unroll
+  for (int u = 0; u < 3; ++u) wload(ring[u], u);
+  stage_load(st[1], 1);
+  stage_store(Xs, st[0]);
+  stage_load(st[0], 2);
+  __syncthreads();
+#pragma unroll
+  for (int ks = 0; ks < PX_NK1; ++ks) {
+    kstep(Xs + (ks & 1) * PX_PLANE, ring[ks % 3]);
+    wload(ring[ks % 3], ks + 3);
+    __builtin_amdgcn_sched_barrier(0);
+    if (ks + 1 < PX_NK1) stage_store(Xs + ((ks + 1) & 1) * PX_PLANE, st[(ks + 1) & 1]);
+    if (ks + 3 < PX_NK1) stage_load(st[(ks + 1) & 1], ks + 3);
+    __syncthreads();
+  }
+  // gate: rows R = wm * 32 + mi * 16 + 4 (lane >> 4) + j, pairs (R, R + 1) -> z[R / 2]
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+    const int R = wm * 32 + mi * 16 + 4 * (lane >> 4);
+    const float b0 = a.b1[R], b1 = a.b1[R + 1], b2 = a.b1[R + 2], b3 = a.b1[R + 3];
+    const int zc = R >> 1;  // z channels zc, zc + 1
+    _Float16* Z = Zs + (zc >> 5) * PX_PLANE + (zc & 31);
+#pragma unroll
+    for (int ni = 0; ni < 4; ++ni) {
+      const int q = nb + ni * 16;
+      f32x4 v;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) v[j] = x3_value(am[mi][ni][j], ac[mi][ni][j]);
+      h2_ zh, zl;
+      split2(f32x2_{pw_gate(v[0] + b0, v[1] + b1), pw_gate(v[2] + b2, v[3] + b3)}, zh, zl);
+      *reinterpret_cast<h2_*>(Z + q * PX_XR) = zh;
+      *reinterpret_cast<h2_*>(Z + q * PX_XR + 32) = zl;
+      am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
+  __syncthreads();
+  // GEMM2 (weights 9, 10 already in ring slots 0, 1)
+#pragma unroll
+  for (int ks = 0; ks < PX_NK2; ++ks) kstep(Zs + ks * PX_PLANE, ring[ks]);
+  // x' = (out + b + x) * 0.25 (parallel_wavegan.py:85); skip (+)= s + b
+#pragma unroll
+  for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int R = wm * 32 + mi * 16 + 4 * (lane >> 4) + j;
+      const float bias = a.b2[R];
+      const bool out_row = R < PW_R;
+      const int ch = out_row ? R : R - PW_R;
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int t = t0 + nb + ni * 16;
+        if (t >= T) continue;
+        const float v = x3_value(am[mi][ni][j], ac[mi][ni][j]) + bias;
+        const long i = ((long)b * 64 + ch) * a.Tmax + t;
+        if (out_row) a.xn[i] = (v + res[mi][j][ni]) * 0.25f;
+        else a.skip[i] = a.first ? v : res[mi][j][ni] + v;
+      }
+    }
+  }
+  if (bad) __hip_atomic_fetch_or(oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+void launch_pw_layer_x3(const float* x, const float* c, float* xn, float* skip, const void* W1x, const float* b1,
+                        const void* W2x, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
+                        int first, int B, unsigned* oflow, hipStream_t st) {
+  TTS_CHECK(W1x && W2x && oflow, "pwgan split-f16: weights / range flag missing");
+  PwLayerArgs a{x, c, xn, skip, nullptr, b1, nullptr, b2, lens, nullptr, len_add, hop, Tmax, dil, first};
+  // two 4-wave workgroups per CU (64 positions each) overlap one another's staging and epilogue
+  constexpr int WN = 1;
+  const dim3 grid((Tmax + 64 * WN - 1) / (64 * WN), B);
+  pw_layer_x3_kernel<WN><<<grid, 256 * WN, 0, st>>>(a, W1x, W2x, oflow);
+  HIP_OK(hipGetLastError());
+}
+
+// host packing: m1 (128 x 272: 3 taps x 64 x-channels, then 80 aux) and m2 (128 x 64)
+void pack_pw_layer_x3(const std::vector<float>& m1, const std::vector<float>& m2, std::vector<uint16_t>& w1x,
+                      std::vector<uint16_t>& w2x) {
+  const int K1 = 3 * PW_R + PW_A;
+  w1x = pack_split_a(8, PX_NK1, [&](int m, int k) -> float {
+    const int ks = k / 32, kk = k % 32;
+    if (ks < 6) return m1[(size_t)m * K1 + (ks / 2) * PW_R + 32 * (ks & 1) + kk];
+    const int ch = 32 * (ks - 6) + kk;
+    return ch < PW_A ? m1[(size_t)m * K1 + 3 * PW_R + ch] : 0.f;
+  });
+  w2x = pack_split_a(8, PX_NK2, [&](int m, int k) -> float { return m2[(size_t)m * (PW_G / 2) + k]; });
 }
