@@ -2249,6 +2249,7 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
     ConvCall cc;
     cc.lens = dl;
     cc.B = B;
+    cc.oflow = x3_flag(c);
     cc.max_q = T;
     cc.s[0] = src_of(in, (long)cin * T, T, 1, cin, 0);
     cc.out = out;
@@ -2349,6 +2350,7 @@ void glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, fl
     ConvCall cc;
     cc.lens = kl;
     cc.B = B;
+    cc.oflow = x3_flag(c);
     cc.max_q = K;
     cc.s[0] = src_of(in, (long)in_rows * K, K, 1, L.Cin, 0);
     cc.out = out;
@@ -2786,7 +2788,7 @@ int tts_glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int
     TTS_CHECK(c && d_ids && h_lens && h_ylens, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
-    glow_encode(c, d_ids, h_lens, B, T_max, length_scale, h_ylens);
+    with_x3_fallback(c, [&] { glow_encode(c, d_ids, h_lens, B, T_max, length_scale, h_ylens); });
     leave(c, stream);
   });
 }
@@ -2797,7 +2799,7 @@ int tts_glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty,
     TTS_CHECK(c && d_y && d_ymean && d_attn && d_logw, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
-    glow_decode(c, d_noise, noise_scale, Ty, d_y, d_ymean, d_attn, d_logw);
+    with_x3_fallback(c, [&] { glow_decode(c, d_noise, noise_scale, Ty, d_y, d_ymean, d_attn, d_logw); });
     leave(c, stream);
   });
 }
