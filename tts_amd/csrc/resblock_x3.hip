@@ -342,7 +342,7 @@ void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t 
   switch (C) {
     // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave
     case 192: launch_rbx3<192, 64, 12, 1>(a, h_lens, s); break;
-    case 96: launch_rbx3<96, 128, 6, 2>(a, h_lens, s); break;
+    case 96: launch_rbx3<96, 96, 6, 2>(a, h_lens, s); break;
     case 48: launch_rbx3<48, 128, 3, 4>(a, h_lens, s); break;
     default: TTS_CHECK(false, "resblock_x3: unsupported channel count");
   }
