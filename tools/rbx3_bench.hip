@@ -3,6 +3,9 @@
 // MB-MelGAN stage shapes of the C2 workload. Not part of the library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/rbx3_bench.hip -o tools/rbx3_bench
 #include "../tts_amd/csrc/resblock.hip"
+#ifdef RB_TRACE
+__device__ unsigned long long* rb_trace;
+#endif
 #include "../tts_amd/csrc/resblock_x3.hip"
 
 #include <cmath>
@@ -144,7 +147,7 @@ int main(int argc, char** argv) {
   int Mmax = 0;
   for (int b = 0; b < 32; ++b) Mmax = std::max(Mmax, kM[b]);
   for (int stage = 0; stage < 3; ++stage) {
-    if (prof_C && (192 >> stage) != prof_C) continue;
+    if (prof_C && (192 >> stage) != std::abs(prof_C)) continue;
     const int C = 192 >> stage, mul = stage == 0 ? 8 : stage == 1 ? 32 : 64;
     const int Ls = Mmax * mul;
     // random operands (DVFS: constant or zero data clocks higher, MI355X_MICROARCH.md)
@@ -185,6 +188,35 @@ int main(int argc, char** argv) {
       }
       printf("C=%3d  4 blocks %-26s %8.1f us (%6.1f TF/s fp32-equivalent)\n", C, name, t, 4 * flop / (t * 1e-6) / 1e12);
     };
+#ifdef RB_TRACE
+    if (prof_C < 0) {  // phase stamps of the first 4 tiles of every workgroup, dilation 9
+      if (C != -prof_C) continue;
+      a.dil = 9;
+      std::vector<unsigned long long> h((size_t)256 * 4 * 8, 0);
+      unsigned long long* dtr = dup(h);
+      HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(rb_trace), &dtr, sizeof(dtr)));
+      launch_resblock_x3(a, kM, C, S);
+      HIP_OK(hipStreamSynchronize(S));
+      HIP_OK(hipMemcpy(h.data(), dtr, h.size() * 8, hipMemcpyDeviceToHost));
+      double seg[5] = {0};
+      int n = 0;
+      for (int w = 0; w < 256; ++w)
+        for (int i = 1; i < 3; ++i) {  // tiles 1, 2: steady state
+          const unsigned long long* r = &h[((size_t)w * 4 + i) * 8];
+          const unsigned long long* rn = &h[((size_t)w * 4 + i + 1) * 8];
+          if (!r[0] || !r[5] || !rn[0]) continue;
+          seg[0] += (r[1] - r[0]) * 0.01;
+          seg[1] += (r[2] - r[1]) * 0.01;
+          seg[2] += (r[3] - r[2]) * 0.01;
+          seg[3] += (r[5] - r[3]) * 0.01;
+          seg[4] += (rn[0] - r[5]) * 0.01;
+          ++n;
+        }
+      printf("C=%d trace (us per tile, mean of %d): phase 1 %.2f, h split %.2f, phase 2 %.2f, stores+sync %.2f, "
+             "next-tile store+sync %.2f\n", C, n, seg[0] / n, seg[1] / n, seg[2] / n, seg[3] / n, seg[4] / n);
+      continue;
+    }
+#endif
     if (prof_C) {
       a.dil = 9;
       for (int i = 0; i < 5; ++i) launch_resblock_x3(a, kM, C, S);
@@ -195,18 +227,14 @@ int main(int argc, char** argv) {
     timeit("split-f16 (library tile)", [&] { launch_resblock_x3(a, kM, C, S); });
     if (C == 192) {
       timeit("x3 TQ64 12x1", [&] { launch_rbx3<192, 64, 12, 1>(a, kM, S); });
-      timeit("x3 TQ64 6x2 (MI2 NI2)", [&] { launch_rbx3<192, 64, 6, 2>(a, kM, S); });
-      timeit("x3 TQ32 12x1 (NI2)", [&] { launch_rbx3<192, 32, 12, 1>(a, kM, S); });
+      timeit("x3 TQ48 12x1 (NI3)", [&] { launch_rbx3<192, 48, 12, 1>(a, kM, S); });
     } else if (C == 96) {
       timeit("x3 TQ128 6x2", [&] { launch_rbx3<96, 128, 6, 2>(a, kM, S); });
-      timeit("x3 TQ64 6x1 (NI4)", [&] { launch_rbx3<96, 64, 6, 1>(a, kM, S); });
-      timeit("x3 TQ64 6x2 (NI2)", [&] { launch_rbx3<96, 64, 6, 2>(a, kM, S); });
       timeit("x3 TQ96 6x2 (NI3)", [&] { launch_rbx3<96, 96, 6, 2>(a, kM, S); });
     } else {
       timeit("x3 TQ128 3x4", [&] { launch_rbx3<48, 128, 3, 4>(a, kM, S); });
       timeit("x3 TQ192 3x4 (NI3)", [&] { launch_rbx3<48, 192, 3, 4>(a, kM, S); });
-      timeit("x3 TQ64 3x4 (NI1)", [&] { launch_rbx3<48, 64, 3, 4>(a, kM, S); });
-      timeit("x3 TQ128 3x2 (NI4)", [&] { launch_rbx3<48, 128, 3, 2>(a, kM, S); });
+      timeit("x3 TQ256 3x4 (NI4)", [&] { launch_rbx3<48, 256, 3, 4>(a, kM, S); });
     }
   }
   printf(fails ? "FAILED\n" : "all checks passed\n");

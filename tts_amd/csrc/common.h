@@ -29,6 +29,11 @@ void tts_set_error(const std::string& msg);
     if (!(cond)) throw std::runtime_error(std::string(msg));                           \
   } while (0)
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
+// global loads and stores (__syncthreads also drains vmcnt, which would complete every prefetch
+// issued before it and stall on every store)
+__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
+
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float lrelu02(float x) { return x >= 0.f ? x : 0.2f * x; }
 

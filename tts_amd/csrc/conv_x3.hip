@@ -180,7 +180,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
     if (NCH > 1) stage_load(st[1], 1);
     if (NCH > 2) stage_load(st[0], 2);
   }
-  __syncthreads();
+  lds_barrier();
   for (int ch0 = 0; ch0 < NCH; ch0 += 2) {
 #pragma unroll
     for (int p = 0; p < 2; ++p) {
@@ -217,7 +217,7 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
         } else {
           if (ch + 1 < NCH) stage_store(p ? X0 : X1, st[0], ch + 1);
         }
-        __syncthreads();
+        lds_barrier();
       }
     }
   }

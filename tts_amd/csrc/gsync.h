@@ -90,7 +90,6 @@ __device__ __forceinline__ f32x4 ldc4(const float* base, int off) {
 
 // LDS-only workgroup barrier: unlike __syncthreads() (whose workgroup-scope fences wait for every
 // outstanding global load, vmcnt(0)), global loads already in flight stay in flight
-__device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory"); }
 
 // Hierarchical grid barrier, split so that loads for the next phase can be issued between the
 // arrival and the wait. arrive: every wave drains its stores (sc1 write-through), then thread 0

@@ -472,7 +472,8 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
   // staging item of this thread: channel octet g (0..3) of the k-step, position q (0..127)
   const int sg = tid / TQ, sq = tid % TQ;
   float st[2][8];
-  auto stage_load = [&](float (&r8)[8], int ks) {
+  bool sok[2];  // validity applied at the LDS store, so no load is waited for where it is issued
+  auto stage_load = [&](float (&r8)[8], bool& okr, int ks) {
     const float* src;
     int off, c0, cmax;
     if (ks < 6) {
@@ -487,21 +488,21 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
       cmax = PW_A;
     }
     const int t = t0 + sq + off;
-    const bool ok = t >= 0 && t < T && c0 < cmax;
-    const float* p = src + (long)min(c0, cmax - 8) * a.Tmax + (ok ? t : 0);
+    okr = t >= 0 && t < T && c0 < cmax;
+    const float* p = src + (long)min(c0, cmax - 8) * a.Tmax + (okr ? t : 0);
+#pragma unroll
+    for (int c = 0; c < 8; ++c) r8[c] = p[(long)c * a.Tmax];
+  };
+  auto stage_store = [&](_Float16* X, const float (&r8)[8], bool okr) {
+    float mx = 0.f, v[8];
 #pragma unroll
     for (int c = 0; c < 8; ++c) {
-      const float v = p[(long)c * a.Tmax];
-      r8[c] = ok ? v : 0.f;
+      v[c] = okr ? r8[c] : 0.f;
+      mx = fmaxf(mx, __builtin_fabsf(v[c]));
     }
-  };
-  auto stage_store = [&](_Float16* X, const float (&r8)[8]) {
-    float mx = 0.f;
-#pragma unroll
-    for (int c = 0; c < 8; ++c) mx = fmaxf(mx, __builtin_fabsf(r8[c]));
     bad |= !(mx < F16_RANGE);
     h8 hi, lo;
-    split8(r8, hi, lo);
+    split8(v, hi, lo);
     *reinterpret_cast<h8*>(X + sq * PX_XR + 8 * sg) = hi;
     *reinterpret_cast<h8*>(X + sq * PX_XR + 32 + 8 * sg) = lo;
   };
@@ -538,7 +539,7 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) {
         const int t = min(t0 + nb + ni * 16, T - 1);
-        res[mi][j][ni] = (out_row || !a.first) ? src[rowb + t] : 0.f;
+        res[mi][j][ni] = src[rowb + t];  // the skip rows' value is unused on the first block
       }
     }
   f32x4 am[2][4], ac[2][4];
@@ -563,21 +564,21 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
 
   // GEMM1: staging two k-steps ahead (step s loaded into set s & 1 after step s - 3's MFMAs,
   // stored to LDS buffer s & 1 after step s - 1's)
-  stage_load(st[0], 0);
+  stage_load(st[0], sok[0], 0);
 #pragma unroll
   for (int u = 0; u < 3; ++u) wload(ring[u], u);
-  stage_load(st[1], 1);
-  stage_store(Xs, st[0]);
-  stage_load(st[0], 2);
-  __syncthreads();
+  stage_load(st[1], sok[1], 1);
+  stage_store(Xs, st[0], sok[0]);
+  stage_load(st[0], sok[0], 2);
+  lds_barrier();
 #pragma unroll
   for (int ks = 0; ks < PX_NK1; ++ks) {
     kstep(Xs + (ks & 1) * PX_PLANE, ring[ks % 3]);
     wload(ring[ks % 3], ks + 3);
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + 1 < PX_NK1) stage_store(Xs + ((ks + 1) & 1) * PX_PLANE, st[(ks + 1) & 1]);
-    if (ks + 3 < PX_NK1) stage_load(st[(ks + 1) & 1], ks + 3);
-    __syncthreads();
+    if (ks + 1 < PX_NK1) stage_store(Xs + ((ks + 1) & 1) * PX_PLANE, st[(ks + 1) & 1], sok[(ks + 1) & 1]);
+    if (ks + 3 < PX_NK1) stage_load(st[(ks + 1) & 1], sok[(ks + 1) & 1], ks + 3);
+    lds_barrier();
   }
   // gate: rows R = wm * 32 + mi * 16 + 4 (lane >> 4) + j, pairs (R, R + 1) -> z[R / 2]
 #pragma unroll
@@ -599,7 +600,7 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
       am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   }
-  __syncthreads();
+  lds_barrier();
   // GEMM2 (weights 9, 10 already in ring slots 0, 1)
 #pragma unroll
   for (int ks = 0; ks < PX_NK2; ++ks) kstep(Zs + ks * PX_PLANE, ring[ks]);

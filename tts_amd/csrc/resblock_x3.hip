@@ -84,7 +84,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     tlen[lane] = L;
     if (lane == 63) tcum[64] = v;
   }
-  __syncthreads();
+  lds_barrier();
   auto tile_of = [&](int i) {
     const bool hit = lane < a.B && tcum[lane] <= i && i < tcum[lane + 1];
     const unsigned long long m = __ballot(hit);
@@ -187,9 +187,38 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   if (NCH > 1) stage_load(cur, st[1], 1);
   stage_store(X0, st[0], 0);
   if (NCH > 2) stage_load(cur, st[0], 2);
-  __syncthreads();
+  lds_barrier();
   f32x4 am[MI][NI], ac[MI][NI];
+  // EARLY (an even chunk count): the next tile's chunk k loads into the register set this tile's
+  // chunk NCH - 2 + k vacates, i.e. during phase 1, a whole tile ahead of its use; with an odd
+  // count the set parity would flip every tile, so those loads wait for phase 2
+  constexpr bool EARLY = NCH % 2 == 0;
+  // per-channel biases, loaded once (a load inside the tile loop would be the youngest in the
+  // vmcnt order and make its wait drain every prefetch)
+  float bdv[MI][4], bfv[MI][4];
+#pragma unroll
+  for (int mi = 0; mi < MI; ++mi)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
+      bdv[mi][j] = a.bd[co];
+      bfv[mi][j] = a.bf[co];
+    }
+#ifdef RB_TRACE  // tools/rbx3_bench.hip trace mode: s_memrealtime per phase, first 4 tiles of a workgroup
+  int it = 0;
+#define RB_STAMP(k)                                                                             \
+  if (threadIdx.x == 0 && it < 4) rb_trace[((long)blockIdx.x * 4 + it) * 8 + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define RB_STAMP(k)
+#endif
   for (;;) {
+    RB_STAMP(0);
+    const int tn = t + gridDim.x;
+    const bool more = tn < ntiles;
+    const RbTile nxt = more ? tile_of(tn) : cur;
+    // the prefetch loads are issued unconditionally (a last tile re-loads itself): vmcnt is an
+    // in-order counter, and a conditional load makes the compiler wait for everything (vmcnt(0))
+    if (EARLY && NCH == 2) stage_load(nxt, st[0], 0);
     // ---------------- phase 1: h = Wd . lrelu(x) ----------------
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
@@ -217,15 +246,15 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
       }
       if (ch + 1 < NCH) stage_store((ch & 1) ? X0 : X1, st[(ch + 1) & 1], ch + 1);
       if (ch + 3 < NCH) stage_load(cur, st[(ch + 1) & 1], ch + 3);
-      __syncthreads();
+      else if (EARLY && ch + 3 - NCH < 2) stage_load(nxt, st[(ch + 1) & 1], ch + 3 - NCH);
+      lds_barrier();
     }
+    RB_STAMP(1);
     // lrelu(h + b_d), split, into HX[pos][0:C) (hi) and HX[pos][2C:3C) (lo)
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       const int co = (mt0 + mi) * 16 + 4 * (lane >> 4);
-      float bd[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) bd[j] = a.bd[co + j];
+      const float(&bd)[4] = bdv[mi];
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         h4 hi, lo;
@@ -242,16 +271,13 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
       }
     }
-    __syncthreads();
-    // the next tile's first two chunks: global loads in flight during phase 2
-    const int tn = t + gridDim.x;
-    const bool more = tn < ntiles;
-    RbTile nxt = cur;
-    if (more) {
-      nxt = tile_of(tn);
+    lds_barrier();
+    // odd chunk count: the next tile's first two chunks load during phase 2
+    if (!EARLY) {
       stage_load(nxt, st[0], 0);
       if (NCH > 1) stage_load(nxt, st[1], 1);
     }
+    RB_STAMP(2);
     // ---------------- phase 2: y = [W1 | Wsc] . [lrelu(h); x] ----------------
     for (int k0 = 0; k0 < NK2; k0 += 3) {
 #pragma unroll
@@ -272,13 +298,14 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         wload(ring[u], NK1 + kc + 3);  // past NK2: the next tile's phase-1 weights
       }
     }
+    RB_STAMP(3);
     float* yb = a.y + (long)cur.b * a.sb;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
         const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
-        const float bf = a.bf[co];
+        const float bf = bfv[mi][j];
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
           const int q = cur.q0 + nb + ni * 16;
@@ -286,14 +313,20 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         }
       }
     }
+    RB_STAMP(4);
     if (!more) break;
-    __syncthreads();  // every wave is done with this tile's X / HX
+    lds_barrier();  // every wave is done with this tile's X / HX
+    RB_STAMP(5);
     cur = nxt;
     t = tn;
     stage_store(X0, st[0], 0);
     if (NCH > 2) stage_load(cur, st[0], 2);
-    __syncthreads();
+    lds_barrier();
+#ifdef RB_TRACE
+    ++it;
+#endif
   }
+#undef RB_STAMP
   if (bad) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
@@ -343,7 +376,7 @@ void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t 
     // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave
     case 192: launch_rbx3<192, 64, 12, 1>(a, h_lens, s); break;
     case 96: launch_rbx3<96, 96, 6, 2>(a, h_lens, s); break;
-    case 48: launch_rbx3<48, 128, 3, 4>(a, h_lens, s); break;
+    case 48: launch_rbx3<48, 192, 3, 4>(a, h_lens, s); break;
     default: TTS_CHECK(false, "resblock_x3: unsupported channel count");
   }
   HIP_OK(hipGetLastError());
