@@ -1,109 +1,147 @@
 // MB-MelGAN output stage fused with PQMF synthesis (gfx950):
 //   bands = tanh(Conv1d(C -> 4, k7)(ReflectionPad1d(3)(LeakyReLU(x))))   melgan_generator.py:75-81
 //   wav   = conv1d(conv_transpose1d(bands, 4 I, stride 4), G, pad = taps/2)  pqmf.py:51-56
-// One workgroup produces TOUT = 960 waveform samples of one utterance. It stages the C input
-// channels it needs (240 band positions + 8 each side for the 63-tap synthesis filter + 3 each
-// side for the k7 conv) once in LDS, computes the 256 band positions x 4 bands on the VALU (4
-// outputs per thread: M = 4 would waste 3/4 of a 16-wide MFMA tile), keeps them in LDS, and
-// runs the polyphase synthesis from there. Versus the generic conv + a separate PQMF launch this
-// removes the band tensor round trip and the padded-to-16 output tile.
+// One workgroup (256 threads) produces OP_TB = 1008 band positions (4032 waveform samples) of
+// one utterance. The k7 conv computes OP_NB = 1024 band positions (8 of halo each side for the
+// 63-tap synthesis filter), four consecutive positions x four bands per thread in packed fp32
+// FMAs (v_pk_fma_f32: band pairs x a broadcast input), so one thread's 12-value input window
+// serves 112 FMAs per channel. Channels stream through LDS in chunks of OP_CC: chunk c+1 is
+// loaded into registers (coalesced, clamped, unguarded) while chunk c is computed. The 4 x 1024
+// band tile then reuses the chunk buffer and the polyphase synthesis reads it from there: output
+// samples 4m..4m+3 share their 16 band values per band (taps 3-r+4jj), so a thread does four
+// samples per band read with the taps as one broadcast 16-byte LDS read. Weights and biases are
+// wave-uniform (scalar loads). The band tensor never reaches HBM.
 #include "common.h"
 
 namespace {
-constexpr int OP_N = 4;                 // bands
-constexpr int OP_NB = 256;              // band positions per workgroup (one per thread)
-constexpr int OP_HB = 8;                // band halo each side (31 filter taps / 4, rounded up)
-constexpr int OP_TB = OP_NB - 2 * OP_HB;  // 240 band positions of output
-constexpr int OP_TOUT = OP_N * OP_TB;     // 960 waveform samples
-constexpr int OP_NX = OP_NB + 6;          // input positions incl. the k7 halo
-constexpr int OP_XLD = OP_NX + 1;         // LDS row stride
+constexpr int OP_N = 4;                  // bands
+constexpr int OP_NB = 1024;              // band positions computed per workgroup (4 per thread)
+constexpr int OP_HB = 8;                 // band halo on the left (7 used) and right (8 used)
+constexpr int OP_TB = OP_NB - 2 * OP_HB;  // 1008 band positions of output
+constexpr int OP_XW = OP_NB + 8;          // staged input positions [p0 - 12, p0 + 1020)
+constexpr int OP_CC = 8;                  // channels per staged chunk
 constexpr int OP_TAPS = 63;
+constexpr int OP_PER = (OP_CC * OP_XW + 255) / 256;  // staged floats per thread per chunk
+typedef float f32x2 __attribute__((ext_vector_type(2)));
 }  // namespace
 
 template <int C>
 __global__ __launch_bounds__(256) void out_pqmf_kernel(const float* __restrict__ x, long xb, long xc,
                                                        const float* __restrict__ Wo, const float* __restrict__ bo,
-                                                       const float* __restrict__ G, const int* lens, int len_add,
-                                                       int L_mul, float* __restrict__ y, long yb) {
-  __shared__ float Xs[C * OP_XLD];
-  __shared__ __attribute__((aligned(16))) float Ws[C * 7 * 4];  // [c][k][o]
-  __shared__ float Bs[OP_N][OP_NB];
-  __shared__ float Gs[OP_N][OP_TAPS + 1];
+                                                       const float* __restrict__ G, const int* __restrict__ lens,
+                                                       int len_add, int L_mul, float* __restrict__ y, long yb) {
+  static_assert(C % OP_CC == 0, "channel chunking");
+  constexpr int NCH = C / OP_CC;
+  // chunk buffer [OP_CC][OP_XW]; after the conv it holds the band tile [4][OP_NB]
+  __shared__ __attribute__((aligned(16))) float Xs[OP_CC * OP_XW];
+  __shared__ __attribute__((aligned(16))) float Gr[OP_N][16][4];  // Gr[k][jj][r] = G[k][4jj + 3 - r]
+  static_assert(OP_N * OP_NB <= OP_CC * OP_XW, "band tile fits the chunk buffer");
   const int b = blockIdx.y;
   const int L = (lens[b] + len_add) * L_mul;  // band length of this utterance
-  const int n0 = blockIdx.x * OP_TOUT;
-  if (n0 >= OP_N * L) return;
+  const int p0 = blockIdx.x * OP_TB;
+  if (p0 >= L) return;
   const int tid = threadIdx.x;
-  const int p0 = n0 / OP_N - OP_HB;  // first band position held in Bs
   const float* xp = x + (long)b * xb;
-  for (int i = tid; i < C * 7 * 4; i += 256) Ws[i] = Wo[i];
-  for (int i = tid; i < OP_N * OP_TAPS; i += 256) Gs[i / OP_TAPS][i % OP_TAPS] = G[i];
-  // input window [p0 - 3, p0 + NB + 3): ReflectionPad1d(3) at the utterance edges; positions a
-  // band outside [0, L) would use are clamped (those bands are forced to zero below). All loads
-  // of the window are issued before the first LDS store (clamped element index, no guards).
-  constexpr int PER = (C * OP_NX + 255) / 256;
-  float v[PER];
+  for (int i = tid; i < OP_N * 64; i += 256) {
+    const int k = i >> 6, jj = (i >> 2) & 15, r = i & 3;
+    const int j = 4 * jj + 3 - r;
+    Gr[k][jj][r] = j < OP_TAPS ? G[k * OP_TAPS + j] : 0.f;
+  }
+  // staged element e -> (channel e / XW, position p0 - 12 + e % XW), ReflectionPad1d(3) at the
+  // utterance edges, clamped beyond (positions whose bands are outside [0, L) are zeroed below)
+  int off[OP_PER];
 #pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const int e = min(tid + 256 * r, C * OP_NX - 1);
-    const int c = e / OP_NX, i = e - c * OP_NX;
-    int q = p0 - 3 + i;
+  for (int r = 0; r < OP_PER; ++r) {
+    const int e = min(tid + 256 * r, OP_CC * OP_XW - 1);
+    const int c = e / OP_XW;
+    int q = p0 - 12 + (e - c * OP_XW);
     if (q < 0) q = -q;
     if (q >= L) q = 2 * (L - 1) - q;
     q = min(max(q, 0), L - 1);
-    v[r] = xp[(long)c * xc + q];
+    off[r] = c * (int)xc + q;
   }
+  float v[OP_PER];
 #pragma unroll
-  for (int r = 0; r < PER; ++r) {
-    const int e = tid + 256 * r;
-    if (e < C * OP_NX) {
-      const int c = e / OP_NX, i = e - c * OP_NX;
-      Xs[c * OP_XLD + i] = lrelu02(v[r]);
-    }
-  }
-  __syncthreads();
+  for (int r = 0; r < OP_PER; ++r) v[r] = xp[off[r]];
+  f32x2 acc01[4], acc23[4];  // [position][band pair]
   {
-    const int j = tid;  // band position p0 + j
-    float a0 = bo[0], a1 = bo[1], a2 = bo[2], a3 = bo[3];
-#pragma unroll 4
-    for (int c = 0; c < C; ++c) {
-      const float* xr = Xs + c * OP_XLD + j;
-      const f32x4* wr = reinterpret_cast<const f32x4*>(Ws + c * 28);
+    const f32x2 b01 = {bo[0], bo[1]}, b23 = {bo[2], bo[3]};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc01[j] = b01, acc23[j] = b23;
+  }
+  for (int ch = 0; ch < NCH; ++ch) {
+    if (ch > 0) lds_barrier();  // the previous chunk's reads are done
+#pragma unroll
+    for (int r = 0; r < OP_PER; ++r) {
+      const int e = tid + 256 * r;
+      if (r < OP_PER - 1 || e < OP_CC * OP_XW) Xs[e] = lrelu02(v[r]);
+    }
+    lds_barrier();
+    {  // next chunk's loads (the last iteration re-reads its own chunk: unconditional loads)
+      const long nb = (long)min(ch + 1, NCH - 1) * OP_CC * xc;
+#pragma unroll
+      for (int r = 0; r < OP_PER; ++r) v[r] = xp[nb + off[r]];
+    }
+    const float* wc = Wo + (long)ch * OP_CC * 28;
+#pragma unroll 2
+    for (int c = 0; c < OP_CC; ++c) {
+      const f32x4* xr = reinterpret_cast<const f32x4*>(Xs + c * OP_XW + 4 * tid);
+      const f32x4 x0 = xr[0], x1 = xr[1], x2 = xr[2];
+      const float xw[12] = {x0[0], x0[1], x0[2], x0[3], x1[0], x1[1], x1[2], x1[3], x2[0], x2[1], x2[2], x2[3]};
 #pragma unroll
       for (int k = 0; k < 7; ++k) {
-        const float xv = xr[k];
-        const f32x4 w = wr[k];
-        a0 = fmaf(w[0], xv, a0);
-        a1 = fmaf(w[1], xv, a1);
-        a2 = fmaf(w[2], xv, a2);
-        a3 = fmaf(w[3], xv, a3);
+        const f32x2 w01 = {wc[c * 28 + 4 * k + 0], wc[c * 28 + 4 * k + 1]};
+        const f32x2 w23 = {wc[c * 28 + 4 * k + 2], wc[c * 28 + 4 * k + 3]};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float xv = xw[1 + j + k];  // input position (p0 - 8 + 4 tid + j) - 3 + k
+          const f32x2 xx = {xv, xv};
+          acc01[j] = w01 * xx + acc01[j];
+          acc23[j] = w23 * xx + acc23[j];
+        }
       }
     }
-    const int p = p0 + j;
-    const bool valid = p >= 0 && p < L;  // the synthesis conv zero-pads outside the utterance
-    Bs[0][j] = valid ? tanhf(a0) : 0.f;
-    Bs[1][j] = valid ? tanhf(a1) : 0.f;
-    Bs[2][j] = valid ? tanhf(a2) : 0.f;
-    Bs[3][j] = valid ? tanhf(a3) : 0.f;
   }
-  __syncthreads();
-  // y[n] = sum_k sum_j G[k][j] * 4 * bands_k[(n + j - 31) / 4]   over j with n + j - 31 = 0 (mod 4)
-  constexpr int P = OP_TAPS / 2;
-  float* yp = y + (long)b * yb;
-  for (int t = tid; t < OP_TOUT; t += 256) {
-    const int n = n0 + t;
-    if (n >= OP_N * L) break;
-    const int j0 = (P - t) & (OP_N - 1);  // (P - n) mod 4; n0 is a multiple of 4
-    float acc = 0.f;
+  lds_barrier();  // all chunk reads done: Xs becomes the band tile Bs[band][OP_NB]
+  float* Bs = Xs;
+  {
+    f32x4 o[OP_N];
 #pragma unroll
-    for (int k = 0; k < OP_N; ++k) {
+    for (int j = 0; j < 4; ++j) {
+      const int p = p0 - OP_HB + 4 * tid + j;
+      const bool valid = p >= 0 && p < L;  // the synthesis conv zero-pads outside the utterance
+      o[0][j] = valid ? tanhf(acc01[j][0]) : 0.f;
+      o[1][j] = valid ? tanhf(acc01[j][1]) : 0.f;
+      o[2][j] = valid ? tanhf(acc23[j][0]) : 0.f;
+      o[3][j] = valid ? tanhf(acc23[j][1]) : 0.f;
+    }
 #pragma unroll
-      for (int jj = 0; jj < 16; ++jj) {
-        const int j = j0 + OP_N * jj;
-        if (j < OP_TAPS) acc = fmaf(Gs[k][j], Bs[k][(t + j - P) / OP_N + OP_HB], acc);
+    for (int k = 0; k < OP_N; ++k) *reinterpret_cast<f32x4*>(Bs + k * OP_NB + 4 * tid) = o[k];
+  }
+  lds_barrier();
+  // y[4m + r] = 4 sum_k sum_jj G[k][4jj + 3 - r] bands_k[m + jj - 7]   (pqmf.py:51-56 restated)
+  f32x4 out[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) out[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < OP_N; ++k) {
+#pragma unroll 4
+    for (int jj = 0; jj < 16; ++jj) {
+      const f32x4 g = *reinterpret_cast<const f32x4*>(&Gr[k][jj][0]);
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int mm = min(tid + 256 * i, OP_TB - 1);  // local band position of the output quad
+        const float bv = Bs[k * OP_NB + mm + 1 + jj];
+        out[i] = g * bv + out[i];
       }
     }
-    yp[n] = (float)OP_N * acc;
+  }
+  float* yp = y + (long)b * yb;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int mm = tid + 256 * i;
+    const int m = p0 + mm;
+    if (mm < OP_TB && m < L) *reinterpret_cast<f32x4*>(yp + 4L * m) = (float)OP_N * out[i];
   }
 }
 
@@ -112,7 +150,9 @@ bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, c
                      hipStream_t s) {
   if (N != OP_N || taps + 1 != OP_TAPS) return false;
   if (maxL <= 0 || B <= 0) return true;
-  dim3 grid((OP_N * maxL + OP_TOUT - 1) / OP_TOUT, B);
+  if (yb % 4 != 0 || (reinterpret_cast<uintptr_t>(y) & 15) != 0) return false;  // float4 output stores
+  if ((long)C * xc >= (1L << 31)) return false;                                  // 32-bit staging offsets
+  dim3 grid((maxL + OP_TB - 1) / OP_TB, B);
   switch (C) {
     case 48: out_pqmf_kernel<48><<<grid, 256, 0, s>>>(x, xb, xc, Wo, bo, G, lens, len_add, L_mul, y, yb); break;
     case 32: out_pqmf_kernel<32><<<grid, 256, 0, s>>>(x, xb, xc, Wo, bo, G, lens, len_add, L_mul, y, yb); break;
