@@ -29,9 +29,11 @@ for k in range(5):
 step = np.median([(a[s + 1][0].min() - a[s][0].min()) / 100.0 for s in range(7)])
 print(f"step {step:.2f} us")
 NATT = 64
-sub = [np.median([(a[s][k][:NATT] - a[s][2][:NATT]).astype(float) / 100.0 for s in range(7)]) for k in (10, 11, 12, 3)]
-print("P3 inside attention_rnn workgroups (median, us after release): MFMA %.2f, cell %.2f, query partials %.2f, "
-      "done %.2f" % tuple(sub))
+for agg, lab in ((np.median, "median"), (np.max, "max")):
+    sub = [np.median([agg((a[s][k][:NATT] - a[s][2][:NATT]).astype(float) / 100.0) for s in range(7)])
+           for k in (13, 10, 11, 12, 3)]
+    print(f"P3 inside attention_rnn workgroups ({lab} WG, us after release): staged %.2f, MFMA %.2f, cell %.2f, "
+          "query partials %.2f, done %.2f" % tuple(sub))
 sub = [np.median([(a[s][k][NATT:] - a[s][2][NATT:]).astype(float) / 100.0 for s in range(7)]) for k in (3,)]
 print("P3 item workgroups (h_dec part + frames) done %.2f" % tuple(sub))
 

@@ -274,6 +274,7 @@ struct TacoModel {
   ConvLayer enc[3], lstm_in, penc, post[5];
   DevBuf whhT;
   DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b;
+  DevBuf att_p_x3;  // att_p split-f16 (split16.h) for the persistent decoder's P3; empty if out of range
   DevBuf Wcomb;  // location_dense . location_conv folded, [64 taps (62 used)][128 dims]
   float bv = 0.f;
   // persistent decoder: projection rows [stop tile | W_p] (+ bias) and prenet layer 1 on the host,
@@ -680,7 +681,14 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     auto wp = slice_cols(wih, 4 * Q, P + ES, 0, P);
     auto wc = slice_cols(wih, 4 * Q, P + ES, P, P + E);
     M.spk_att_h = S ? lstm_tile_rows(slice_cols(wih, 4 * Q, P + ES, P + E, P + ES), Q, S) : std::vector<float>();
-    M.att_p.upload(swz(lstm_tile_rows(wp, Q, P), 4 * Q, P));
+    const auto wpt = lstm_tile_rows(wp, Q, P);
+    M.att_p.upload(swz(wpt, 4 * Q, P));
+    bool in_range = P % 32 == 0;
+    for (float v : wpt) in_range &= std::fabs(v) < F16_RANGE;
+    if (in_range)
+      M.att_p_x3.upload(pack_split_a(4 * Q / 16, P / 32, [&](int m, int k) { return wpt[(size_t)m * P + k]; }));
+    else
+      M.att_p_x3.reset();
     auto pre = hcat({{wc.data(), E}, {whh.data(), Q}}, 4 * Q);
     M.att_pre.upload(swz(lstm_tile_rows(pre, Q, E + Q), 4 * Q, E + Q));
     std::vector<float> bsum(4 * Q);
@@ -1238,6 +1246,8 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.apre_w = M.att_pre.f();
   a.apre_b = M.att_bias.f();
   a.attp_w = M.att_p.f();
+  a.x3flag = x3_flag(c);  // null in fp32 mode
+  a.attp_x3 = a.x3flag && M.att_p_x3.p && !std::getenv("TTS_DECODER_F32") ? static_cast<const uint16_t*>(M.att_p_x3.p) : nullptr;
   a.pj_w = M.pj_w.f();
   a.pj_b = M.pj_b.f();
   {  // per-row biases: projection (always), speaker columns when the model has them

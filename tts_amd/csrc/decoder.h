@@ -109,6 +109,8 @@ struct PArgs {
   const float* apre_w;  // [256][96][64][4] attention_rnn [W_ih,ctx | W_hh]
   const float* apre_b;  // [4096] b_ih + b_hh
   const float* attp_w;  // [256][16][64][4] attention_rnn W_ih,prenet
+  const uint16_t* attp_x3;  // the same weights split-f16 (split16.h pack_split_a [256][8][64][16]) or null
+  unsigned* x3flag;         // raised when a split-f16 operand is outside the f16 range
   const float* pj_w;    // [ntj][96][64][4] stop tile, 5r frame tiles, 16 folded prenet-1 tiles
   const float* pj_b;    // [ntj * 16]
   // per-row biases (api.hip spk_bias_kernel), row stride spk_ld: projection bias per row (always),

@@ -31,6 +31,7 @@
 #include "common.h"
 #include "decoder.h"
 #include "gsync.h"
+#include "split16.h"
 
 #include <type_traits>
 
@@ -82,6 +83,23 @@ __device__ __forceinline__ float lds_sum(const float* part, int m, int n) {
 }
 
 __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); }
+// Short forms for the LSTM cells and the attention energies (on the step's critical path):
+// v_exp_f32 / v_rcp_f32 (1 ulp each) instead of the libm sequences. Absolute error below 2e-7
+// over the whole range (tools/fast_math_err.py); tanh takes an odd Taylor polynomial below 0.25,
+// where 1 - e^-2x would cancel.
+__device__ __forceinline__ float sigm_f(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float tanh_f(float x) {
+  const float ax = __builtin_fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * ax);  // exp(-2|x|)
+  const float big = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
+  const float x2 = ax * ax;
+  const float small =
+      __builtin_fmaf(ax * x2, __builtin_fmaf(x2, __builtin_fmaf(x2, __builtin_fmaf(x2, 0.021869488f, -0.053968254f),
+                                                               0.13333334f), -0.33333334f), ax);
+  return __builtin_copysignf(ax < 0.25f ? small : big, x);
+}
 
 // sum over the 16 lanes of a DPP row (every lane of the row gets the row sum)
 __device__ __forceinline__ float row16_sum(float v) {
@@ -235,7 +253,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   {
     float z[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) z[i] = row16_sum(tanhf(pqa + L[i]) * va);
+    for (int i = 0; i < 8; ++i) z[i] = row16_sum(tanh_f(pqa + L[i]) * va);
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) esum[wave * TC + 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3)] = z[i];
@@ -287,7 +305,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   };
   if (tid < TC) {
     const float e = sv[tid];
-    float x = P.softmax ? (m_c == -INFINITY ? 0.f : expf(e - m_c)) : 1.f / (1.f + expf(-e));
+    float x = P.softmax ? (m_c == -INFINITY ? 0.f : expf(e - m_c)) : sigm_f(e);
     if (tid >= nvalid) x = 0.f;
     sw[tid] = x;
     if ((FWD && P.fwd)) {
@@ -665,7 +683,7 @@ __device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], 
 // LDS: [att-pre weights 96 x 1 KiB][Wcomb 64 x 128][scratch: GEMM reduction + hs | attention]
 constexpr size_t P_LDS_APRE = 96 * 64 * 16;
 constexpr size_t P_LDS_WC = 64 * 128 * 4;
-constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 16 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
+constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 17 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
 constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
 
 // phase timestamps of every workgroup for 8 steps (P.trace, optional): [step][16][256]
@@ -677,6 +695,7 @@ constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
 template <int MT, int VAR>
 __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   constexpr bool GRAVES = (VAR & 4) != 0;  // Graves attention replaces the location-sensitive one
+  constexpr bool X3P = (VAR & 8) != 0;     // P3's attention_rnn prenet part on the split-f16 MFMA
   extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
   __shared__ int sflag, is_last, dflag[64];
   constexpr int Bp = MT * 16;
@@ -685,7 +704,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   float* wcomb = reinterpret_cast<float*>(smem4) + 96 * 64 * 4;    // [64][128]
   float* scr = wcomb + 64 * 128;
   float* red0 = scr;                   // [8][Bp][17]
-  float* hs = red0 + 8 * Bp * 17;      // [Bp][16]
+  float* hs = red0 + 8 * Bp * 17;      // [Bp][17]
   const int g = blockIdx.x, tid0 = threadIdx.x, lane0 = tid0 & 63;
   const int wave0 = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   const int YP = P.ntj * 16;
@@ -852,7 +871,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     gsync_arrive(P.bar, gen);
     // P3 operands that are already final: its epilogue's gate addends (written by P5 of the
     // previous step), c_att, the query-projection weights
-    float ga[4], ca, wq[16];
+    float ga[4], ca, wq[4];
     {
       const int idx = min(tid, 4 * Bp * 4 - 1);
       const int gl = idx / (Bp * 4), rem = idx % (Bp * 4);
@@ -862,12 +881,20 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       for (int q = 0; q < 4; ++q) ga[q] = ldc(P.gatt + (long)m * 4096 + tile * 16 + q * 4 + u);
       ca = P.catt[(long)m * 1024 + tile * 4 + u];
 #pragma unroll
-      for (int u2 = 0; u2 < 16; ++u2) wq[u2] = P.WqT[(long)(16 * min(g, NATT - 1) + u2) * 128 + (tid & 127)];
+      // query-projection B operand: Wq^T rows 16 g + 4 q + (lane >> 4), attention dim 16 wave + (lane & 15)
+      for (int q = 0; q < 4; ++q)
+        wq[q] = P.WqT[(long)(16 * min(g, NATT - 1) + 4 * q + (lane >> 4)) * 128 + 16 * wave + (lane & 15)];
     }
     // attention_rnn prenet-part weights for P3: 4 tiles per workgroup, waves 2j, 2j+1 = tile j
     // K halves (8 k-chunks each)
     f32x4 wa[ATTP_NC];
-    {
+    h8 wx[ATTP_NC / 2][2];  // split-f16: k-steps 4 (wave & 1) .. +3 of tile tl, [hi | lo]
+    if constexpr (X3P) {
+      const int tl = 4 * min(g, NATT - 1) + (wave >> 1);
+      const h8* src = reinterpret_cast<const h8*>(P.attp_x3) + (((long)tl * 8 + 4 * (wave & 1)) * 64 + lane) * 2;
+#pragma unroll
+      for (int i = 0; i < ATTP_NC / 2; ++i) wx[i][0] = src[(long)i * 128], wx[i][1] = src[(long)i * 128 + 1];
+    } else {
       const int tl = 4 * min(g, NATT - 1) + (wave >> 1);
       const f32x4* src = reinterpret_cast<const f32x4*>(P.attp_w) + ((long)tl * 16 + 8 * (wave & 1)) * 64 + lane;
 #pragma unroll
@@ -891,31 +918,82 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     if (g < NATT) {
       // relu(prenet output) staged once per workgroup in LDS (the Wcomb area: attention_rnn
       // workgroups have no attention item); wave w loads k-chunks 2w, 2w+1
-      f32x4* xs = reinterpret_cast<f32x4*>(wcomb);  // [MT * 16 chunks][64 lanes]
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int c = mt * 16 + 2 * wave + i;
-          f32x4 x = ldc4(P.pb, (c * 64 + lane) * 16) + ldc4(P.pb, (c * 64 + lane) * 16 + PB_HALF * 4);
-#pragma unroll
-          for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
-          xs[c * 64 + lane] = x;
-        }
-      lds_barrier();
-      // waves 2j, 2j+1: tile 4g + j, K halves (8 chunks each)
       f32x4 acc[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+      if constexpr (X3P) {
+        // split-f16 A fragments [MT][8 k-steps][64 lanes][hi | lo]; wave w stages k-step w: lane L
+        // holds row L & 15, k = 32 w + 8 (L >> 4) + 0..7, i.e. two fp32 fragments of pb's
+        // 16-column chunk 2 w + (L >> 5), lanes l1 and l1 + 16 (frag_idx order)
+        h8* xs = reinterpret_cast<h8*>(wcomb);
+        const int l1 = 32 * ((lane >> 4) & 1) + (lane & 15);
+        bool bad = false;
 #pragma unroll
-      for (int i = 0; i < ATTP_NC; ++i) {
-        f32x4 x[MT];
+        for (int mt = 0; mt < MT; ++mt) {
+          const int c = mt * 16 + 2 * wave + (lane >> 5);
+          const f32x4 x0 = ldc4(P.pb, (c * 64 + l1) * 16) + ldc4(P.pb, (c * 64 + l1) * 16 + PB_HALF * 4);
+          const f32x4 x1 = ldc4(P.pb, (c * 64 + l1 + 16) * 16) + ldc4(P.pb, (c * 64 + l1 + 16) * 16 + PB_HALF * 4);
+          float v[8];
+          float mx = 0.f;
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) x[mt] = xs[(mt * 16 + 8 * (wave & 1) + i) * 64 + lane];
+          for (int q = 0; q < 4; ++q) {
+            v[q] = fmaxf(x0[q], 0.f), v[4 + q] = fmaxf(x1[q], 0.f);
+            mx = fmaxf(mx, fmaxf(v[q], v[4 + q]));
+          }
+          bad |= !(mx < F16_RANGE);
+          h8 hi, lo;
+          split8(v, hi, lo);
+          xs[((mt * 8 + wave) * 64 + lane) * 2] = hi;
+          xs[((mt * 8 + wave) * 64 + lane) * 2 + 1] = lo;
+        }
+        if (bad) __hip_atomic_fetch_or(P.x3flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        lds_barrier();
+        PTRACE(13);
+        // waves 2j, 2j+1: tile 4g + j, K halves (4 k-steps each)
+        f32x4 am[MT], ac[MT];
 #pragma unroll
-        for (int q = 0; q < 4; ++q)
+        for (int mt = 0; mt < MT; ++mt) am[mt] = ac[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[mt][q], wa[i][q], acc[mt]);
+        for (int i = 0; i < ATTP_NC / 2; ++i) {
+          h8 xh[MT], xl[MT];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const int ks = 4 * (wave & 1) + i;
+            xh[mt] = xs[((mt * 8 + ks) * 64 + lane) * 2];
+            xl[mt] = xs[((mt * 8 + ks) * 64 + lane) * 2 + 1];
+          }
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) mfma_x3(xh[mt], xl[mt], wx[i][0], wx[i][1], am[mt], ac[mt]);
+        }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc[mt][j] = x3_value(am[mt][j], ac[mt][j]);
+      } else {
+        f32x4* xs = reinterpret_cast<f32x4*>(wcomb);  // [MT * 16 chunks][64 lanes]
+#pragma unroll
+        for (int i = 0; i < 2; ++i)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            const int c = mt * 16 + 2 * wave + i;
+            f32x4 x = ldc4(P.pb, (c * 64 + lane) * 16) + ldc4(P.pb, (c * 64 + lane) * 16 + PB_HALF * 4);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
+            xs[c * 64 + lane] = x;
+          }
+        lds_barrier();
+        PTRACE(13);
+        // waves 2j, 2j+1: tile 4g + j, K halves (8 chunks each)
+#pragma unroll
+        for (int i = 0; i < ATTP_NC; ++i) {
+          f32x4 x[MT];
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) x[mt] = xs[(mt * 16 + 8 * (wave & 1) + i) * 64 + lane];
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[mt][q], wa[i][q], acc[mt]);
+        }
       }
       PTRACE(10);
       acc_to_lds<MT>(red0 + (wave >> 1) * 2 * Bp * 17, wave & 1, lane, acc);
@@ -929,22 +1007,29 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) pre[q] = lds_sum<2, Bp>(pg, m, q * 4 + u) + ga[q];
         const long ci = (long)m * 1024 + tile * 4 + u;
-        const float c = sigm(pre[1]) * ca + sigm(pre[0]) * tanhf(pre[2]);
-        const float h = sigm(pre[3]) * tanhf(c);
+        const float c = sigm_f(pre[1]) * ca + sigm_f(pre[0]) * tanh_f(pre[2]);
+        const float h = sigm_f(pre[3]) * tanh_f(c);
         P.catt[ci] = c;
         stc(P.hatt + frag_idx(m, tile * 4 + u, 1024), h);
-        hs[m * 16 + gl * 4 + u] = h;
+        hs[m * 17 + gl * 4 + u] = h;
       }
       lds_barrier();
       PTRACE(11);
       if (!GRAVES) {  // partial query projection over this workgroup's 16 units
-        const int a = tid & 127;
-        for (int m = tid >> 7; m < Bp; m += PT / 128) {
-          float s = 0.f;
+        // on the MFMA: wave w owns attention dims 16 w .. 16 w + 15, K = this workgroup's 16 units
+        f32x4 qa[MT];
 #pragma unroll
-          for (int u = 0; u < 16; ++u) s = fmaf(wq[u], hs[m * 16 + u], s);
-          stc(P.pq + ((long)g * Bp + m) * 128 + a, s);
-        }
+        for (int mt = 0; mt < MT; ++mt) qa[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int q = 0; q < 4; ++q)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt)
+            qa[mt] = MFMA16(hs[(mt * 16 + (lane & 15)) * 17 + 4 * q + (lane >> 4)], wq[q], qa[mt]);
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            stc(P.pq + ((long)g * Bp + mt * 16 + 4 * (lane >> 4) + j) * 128 + 16 * wave + (lane & 15), qa[mt][j]);
       }
       PTRACE(12);
     } else {
@@ -1027,8 +1112,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
         for (int q = 0; q < 4; ++q) pre[q] = lds_sum<NWV, Bp>(red0, m, q * 4 + u) + db[q];
         const long ci = (long)m * 1024 + g * 4 + u;
-        const float c = sigm(pre[1]) * cd + sigm(pre[0]) * tanhf(pre[2]);
-        const float h = sigm(pre[3]) * tanhf(c);
+        const float c = sigm_f(pre[1]) * cd + sigm_f(pre[0]) * tanh_f(pre[2]);
+        const float h = sigm_f(pre[3]) * tanh_f(c);
         P.cdec[ci] = c;
         stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
       }
@@ -1109,17 +1194,19 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
   TTS_CHECK(a.nchmax * PTC >= a.D.T_max, "persistent decoder: attention partial buffers too small");
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
   // decoder variants are compiled in only where used: VAR bit 0 windowing, bit 1 forward attention
-  // (bit 2: Graves attention, exclusive of the others)
-  const int var = a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0);
-  static const void* const fns[2][5] = {
-      {(const void*)persist_decoder_kernel<1, 0>, (const void*)persist_decoder_kernel<1, 1>,
-       (const void*)persist_decoder_kernel<1, 2>, (const void*)persist_decoder_kernel<1, 3>,
-       (const void*)persist_decoder_kernel<1, 4>},
-      {(const void*)persist_decoder_kernel<2, 0>, (const void*)persist_decoder_kernel<2, 1>,
-       (const void*)persist_decoder_kernel<2, 2>, (const void*)persist_decoder_kernel<2, 3>,
-       (const void*)persist_decoder_kernel<2, 4>}};
+  // (bit 2: Graves attention, exclusive of the others); bit 3: split-f16 P3 (attp_x3 given)
+  TTS_CHECK(!a.attp_x3 || a.x3flag, "persistent decoder: split-f16 weights without a range flag");
+  const int var = (a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0)) | (a.attp_x3 ? 8 : 0);
+#define PDK(mt, v) (const void*)persist_decoder_kernel<mt, v>
+  static const void* const fns[2][13] = {
+      {PDK(1, 0), PDK(1, 1), PDK(1, 2), PDK(1, 3), PDK(1, 4), nullptr, nullptr, nullptr, PDK(1, 8), PDK(1, 9),
+       PDK(1, 10), PDK(1, 11), PDK(1, 12)},
+      {PDK(2, 0), PDK(2, 1), PDK(2, 2), PDK(2, 3), PDK(2, 4), nullptr, nullptr, nullptr, PDK(2, 8), PDK(2, 9),
+       PDK(2, 10), PDK(2, 11), PDK(2, 12)}};
+#undef PDK
   const void* f = fns[MT - 1][var];
-  static bool attr[2][5] = {};
+  TTS_CHECK(f != nullptr, "persistent decoder: variant");
+  static bool attr[2][13] = {};
   if (!attr[MT - 1][var]) {
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
     attr[MT - 1][var] = true;
