@@ -19,8 +19,8 @@
 
 void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int num_rows, int D,
                          const int* lens, int B, float* out, hipStream_t s);
-bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
-                           unsigned* bar, float* out, hipStream_t s);
+bool launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                           int B, float* hbuf, unsigned* bar, float* out, hipStream_t s);
 void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, const float* beta, const float* res,
                        long rb, float* out, long ob, const int* lens, int B, int T, hipStream_t s);
 void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, const int* lens, int B, int T,
@@ -52,8 +52,8 @@ void launch_pw_out(const float* skip, float scale, const float* W3, const float*
                    hipStream_t st);
 void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
                        int B, hipStream_t s);
-bool launch_lstm768_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
-                            unsigned* bar, float* out, hipStream_t s);
+bool launch_lstm768_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                            int B, float* hbuf, unsigned* bar, float* out, hipStream_t s);
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
                    float* out,
                        hipStream_t s);
@@ -97,7 +97,21 @@ struct DevBuf {
   }
   float* f() const { return static_cast<float*>(p); }
   int* i() const { return static_cast<int*>(p); }
+  const uint16_t* h() const { return static_cast<const uint16_t*>(p); }
 };
+
+// split-f16 A fragments (split16.h pack_split_a) of a row-major (rows x K) matrix, rows and K
+// multiples of 16 and 32; the buffer stays empty when a weight is outside the f16 range (the
+// kernels then take their fp32 path)
+void upload_split_rows(DevBuf& d, const std::vector<float>& w, int rows, int K) {
+  bool ok = rows % 16 == 0 && K % 32 == 0 && w.size() == (size_t)rows * K;
+  for (float v : w) ok &= std::fabs(v) < F16_RANGE;
+  if (!ok) {
+    d.reset();
+    return;
+  }
+  d.upload(pack_split_a(rows / 16, K / 32, [&](int m, int k) { return w[(size_t)m * K + k]; }));
+}
 
 struct HostT {
   std::vector<float> d;
@@ -273,6 +287,7 @@ struct TacoModel {
   DevBuf emb;
   ConvLayer enc[3], lstm_in, penc, post[5];
   DevBuf whhT;
+  DevBuf whhT16;  // W_hh split-f16 for the persistent BiLSTM (empty if out of the f16 range)
   DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b;
   DevBuf att_p_x3;  // att_p split-f16 (split16.h) for the persistent decoder's P3; empty if out of range
   DevBuf Wcomb;  // location_dense . location_conv folded, [64 taps (62 used)][128 dims]
@@ -362,6 +377,7 @@ struct Ge2eModel {
   int in_dim = 40, in_pad = 48, proj = 256, H = 768, nl = 3, with_proj = 1;
   ConvLayer gin[4];      // input projections (K = 1, Cout = 4H gate-interleaved tiles, b_ih + b_hh)
   DevBuf whh[4];         // W_hh, swizzled tiles
+  DevBuf whh16[4];       // W_hh split-f16 (empty if out of the f16 range)
   ConvLayer proj_l[4];   // with_proj: Linear(768 -> proj) per layer as a K = 1 conv
   DevBuf lin_w, lin_b;   // without projection: final Linear (proj x H) + bias
 };
@@ -612,7 +628,7 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     // gate rows of both the input projection and W_hh in gate-interleaved tile order:
     // column dir*1024 + tile*16 + gate*4 + unit  (unit = 4*tile + u)
     std::vector<float> Wm((size_t)2048 * E), b(2048);
-    std::vector<float> whh_all;
+    std::vector<float> whh_all, whh_rows;
     for (int dir = 0; dir < 2; ++dir) {
       const std::string sfx = dir ? "_reverse" : "";
       const auto& wih = need(h, "encoder.lstm.weight_ih_l0" + sfx, {4 * H, E}).d;
@@ -625,11 +641,14 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
       for (int i = 0; i < 4 * H; ++i) bs[i] = bih[i] + bhh[i];
       const auto bt = lstm_tile_rows(bs, H, 1);
       std::copy(bt.begin(), bt.end(), b.begin() + dir * 1024);
-      const auto hs = swz(lstm_tile_rows(whh, H, H), 4 * H, H);
+      const auto rows = lstm_tile_rows(whh, H, H);
+      const auto hs = swz(rows, 4 * H, H);
       whh_all.insert(whh_all.end(), hs.begin(), hs.end());
+      whh_rows.insert(whh_rows.end(), rows.begin(), rows.end());
     }
     pack_conv(M.lstm_in, Wm, b, E, 2048, 1, 1, 1, pl0);
     M.whhT.upload(whh_all);
+    upload_split_rows(M.whhT16, whh_rows, 2 * 4 * H, H);
   }
   {  // processed_inputs = inputs_layer(enc)  (common_layers.py:262-263), K=1 conv, no bias
     const auto& win_all = need(h, "decoder.attention.inputs_layer.linear_layer.weight", {A, ES}).d;
@@ -1087,7 +1106,8 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
   // per-step launches when cooperative launch is unavailable or TTS_ENCODER=steps
   const char* e = std::getenv("TTS_ENCODER");
   W.enc_persist = !(e && std::string(e) == "steps") &&
-                  launch_bilstm_persist(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(),
+                  launch_bilstm_persist(W.gin.f(), M.whhT.f(), c->gemm_x3 ? M.whhT16.h() : nullptr, lens, T_max, B,
+                                        W.lh.f(),
                                         reinterpret_cast<unsigned*>(W.lc.p), enc_out, s);
   if (!W.enc_persist) launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
 }
@@ -1927,6 +1947,7 @@ void ge2e_finalize(tts_ctx* c, int in_dim, int proj, int lstm, int nl, int with_
     for (int i = 0; i < 4 * H; ++i) bs[i] = bih[i] + bhh[i];
     pack_conv(G.gin[l], w2, lstm_tile_rows(bs, H, 1), dpad, 4 * H, 1, 1, 1, pl0);
     G.whh[l].upload(swz(lstm_tile_rows(whh, H, H), 4 * H, H));
+    upload_split_rows(G.whh16[l], lstm_tile_rows(whh, H, H), 4 * H, H);
     if (with_proj) {
       const auto& wl = need(h, "layers." + std::to_string(l) + ".linear.weight", {proj, H}).d;
       pack_conv(G.proj_l[l], wl, std::vector<float>(proj, 0.f), H, proj, 1, 1, 1, pl0);
@@ -1974,7 +1995,8 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
     cc.oc = 1;
     cc.ot = 4 * H;
     run_conv(G.gin[l], cc, s);
-    const bool ok = launch_lstm768_persist(W.g.f(), G.whh[l].f(), W.lens.i(), T_max, B, W.hbuf.f(),
+    const bool ok = launch_lstm768_persist(W.g.f(), G.whh[l].f(), c->gemm_x3 ? G.whh16[l].h() : nullptr, W.lens.i(),
+                                           T_max, B, W.hbuf.f(),
                                            reinterpret_cast<unsigned*>(W.bar.p), W.o.f(), s);
     TTS_CHECK(ok, "speaker encoder: cooperative launch unavailable");
     if (G.with_proj) {

@@ -36,6 +36,23 @@ __device__ __forceinline__ void lds_barrier() { asm volatile("s_waitcnt lgkmcnt(
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + __expf(-x)); }
 __device__ __forceinline__ float lrelu02(float x) { return x >= 0.f ? x : 0.2f * x; }
+// Short forms for the recurrent cells and the attention energies (on the steps' critical paths):
+// v_exp_f32 / v_rcp_f32 (1 ulp each) instead of the libm sequences. Absolute error below 2e-7
+// over the whole range (tools/fast_math_err.py); tanh takes an odd Taylor polynomial below 0.25,
+// where 1 - e^-2x would cancel.
+__device__ __forceinline__ float sigm_f(float x) {
+  return __builtin_amdgcn_rcpf(1.f + __builtin_amdgcn_exp2f(-1.4426950408889634f * x));
+}
+__device__ __forceinline__ float tanh_f(float x) {
+  const float ax = __builtin_fabsf(x);
+  const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * ax);  // exp(-2|x|)
+  const float big = (1.f - e) * __builtin_amdgcn_rcpf(1.f + e);
+  const float x2 = ax * ax;
+  const float small =
+      __builtin_fmaf(ax * x2, __builtin_fmaf(x2, __builtin_fmaf(x2, __builtin_fmaf(x2, 0.021869488f, -0.053968254f),
+                                                               0.13333334f), -0.33333334f), ax);
+  return __builtin_copysignf(ax < 0.25f ? small : big, x);
+}
 
 // ---------------------------------------------------------------------------------------
 // Generic fp32 MFMA Conv1d (implicit GEMM): out[b][co][q*out_mul+ph] =

@@ -8,6 +8,7 @@
 #include "common.h"
 #include "decoder.h"  // frag_idx
 #include "gsync.h"
+#include "split16.h"
 
 __global__ __launch_bounds__(256) void embed_gather_kernel(const int64_t* __restrict__ ids, int T_max,
                                                            const float* __restrict__ table, int num_rows,
@@ -111,8 +112,11 @@ __global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restric
 // directions) and the GE2E speaker encoder LSTMs (H = 768, 1 direction).
 //   Whh : [dir][H/4 tiles][H/16 k-chunks][64 lanes][4]   Gin : (B, T_max, NDIR*4H) incl. biases
 //   hbuf: [2 ping-pong][dir][Bp x H] fragment order      out : (B, T_max, NDIR*H)
-template <int MT, int H, int NDIR>
+//   Whh16 (X3): the same tiles split-f16 (split16.h pack_split_a, [dir * H/4 + tile][H/32][64][16]);
+//   h is loaded from the fp32 fragment buffer and split in registers (|h| <= 1: always in range)
+template <int MT, int H, int NDIR, bool X3>
 __global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restrict__ Whh,
+                                                           const uint16_t* __restrict__ Whh16,
                                                            const float* __restrict__ Gin, const int* lens,
                                                            int T_max, int B, float* hbuf, float* __restrict__ out,
                                                            unsigned* bar) {
@@ -125,8 +129,14 @@ __global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restri
   __shared__ int sflag;
   const int dir = blockIdx.x / NT, tl = blockIdx.x % NT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  f32x4 w[KPW];
-  {
+  constexpr int KSW = KPW / 2;  // split-f16 k-steps (32) per wave
+  f32x4 w[X3 ? 1 : KPW];
+  h8 wx[X3 ? KSW : 1][2];
+  if constexpr (X3) {
+    const h8* Wv = reinterpret_cast<const h8*>(Whh16) + (((long)(dir * NT + tl) * (H / 32) + wave * KSW) * 64 + lane) * 2;
+#pragma unroll
+    for (int k = 0; k < KSW; ++k) wx[k][0] = Wv[(long)k * 128], wx[k][1] = Wv[(long)k * 128 + 1];
+  } else {
     const f32x4* Wv = reinterpret_cast<const f32x4*>(Whh) + ((long)(dir * NT + tl) * NKC + wave * KPW) * 64 + lane;
 #pragma unroll
     for (int k = 0; k < KPW; ++k) w[k] = Wv[(long)k * 64];
@@ -146,20 +156,52 @@ __global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restri
     const float* hi = hbuf + (size_t)(step & 1) * NDIR * Bp * H + (long)dir * Bp * H;
     float* ho = hbuf + (size_t)((step + 1) & 1) * NDIR * Bp * H + (long)dir * Bp * H;
     const int t = tpos(step);
-    f32x4 x[KPW][MT];
-#pragma unroll
-    for (int k = 0; k < KPW; ++k)
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) x[k][mt] = ldc4(hi, ((mt * NKC + wave * KPW + k) * 64 + lane) * 16);
     f32x4 acc[MT];
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (X3) {
+      // k-step ks: lane L holds row L & 15, k = 32 ks + 8 (L >> 4) + 0..7 = fp32 fragment chunk
+      // 2 ks + (L >> 5), lanes l1 and l1 + 16 (frag_idx order)
+      const int l1 = 32 * ((lane >> 4) & 1) + (lane & 15);
+      f32x4 x[KSW][MT][2];
 #pragma unroll
-    for (int k = 0; k < KPW; ++k)
+      for (int k = 0; k < KSW; ++k)
 #pragma unroll
-      for (int s4 = 0; s4 < 4; ++s4)
+        for (int mt = 0; mt < MT; ++mt) {
+          const int c = mt * NKC + 2 * (wave * KSW + k) + (lane >> 5);
+          x[k][mt][0] = ldc4(hi, (c * 64 + l1) * 16);
+          x[k][mt][1] = ldc4(hi, (c * 64 + l1 + 16) * 16);
+        }
+      f32x4 am[MT], ac[MT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[k][mt][s4], w[k][s4], acc[mt]);
+      for (int mt = 0; mt < MT; ++mt) am[mt] = ac[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int k = 0; k < KSW; ++k)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) {
+          const float v[8] = {x[k][mt][0][0], x[k][mt][0][1], x[k][mt][0][2], x[k][mt][0][3],
+                              x[k][mt][1][0], x[k][mt][1][1], x[k][mt][1][2], x[k][mt][1][3]};
+          h8 xh, xl;
+          split8(v, xh, xl);
+          mfma_x3(xh, xl, wx[k][0], wx[k][1], am[mt], ac[mt]);
+        }
+#pragma unroll
+      for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+        for (int j = 0; j < 4; ++j) acc[mt][j] = x3_value(am[mt][j], ac[mt][j]);
+    } else {
+      f32x4 x[KPW][MT];
+#pragma unroll
+      for (int k = 0; k < KPW; ++k)
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt) x[k][mt] = ldc4(hi, ((mt * NKC + wave * KPW + k) * 64 + lane) * 16);
+#pragma unroll
+      for (int k = 0; k < KPW; ++k)
+#pragma unroll
+        for (int s4 = 0; s4 < 4; ++s4)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[k][mt][s4], w[k][s4], acc[mt]);
+    }
     float* p = part + wave * Bp * 17;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
@@ -174,12 +216,8 @@ __global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restri
         pre[q] = part[m * 17 + n] + part[(Bp + m) * 17 + n] + part[(2 * Bp + m) * 17 + n] +
                  part[(3 * Bp + m) * 17 + n] + gin[q];
       }
-      const float ig = 1.f / (1.f + expf(-pre[0]));
-      const float fg = 1.f / (1.f + expf(-pre[1]));
-      const float gg = tanhf(pre[2]);
-      const float og = 1.f / (1.f + expf(-pre[3]));
-      cst = fg * cst + ig * gg;
-      const float hn = og * tanhf(cst);
+      cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
+      const float hn = sigm_f(pre[3]) * tanh_f(cst);
       stc(ho + frag_idx(m, tl * 4 + u, H), hn);
       out[((long)m * T_max + t) * O + dir * H + tl * 4 + u] = hn;
     }
@@ -193,8 +231,8 @@ __global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restri
 }
 
 template <int H, int NDIR>
-static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
-                                  unsigned* bar, float* out, hipStream_t s) {
+static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                                  int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
   int dev = 0, coop = 0;
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
@@ -202,24 +240,28 @@ static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const int*
   const int MT = (B + 15) / 16, Bp = MT * 16;
   HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * NDIR * Bp * H * 4, s));
   arm_barrier(bar, NDIR, s);
-  void* args[] = {(void*)&Whh, (void*)&Gin, (void*)&lens, (void*)&T_max, (void*)&B, (void*)&hbuf, (void*)&out, (void*)&bar};
-  const void* f = MT == 1 ? (const void*)lstm_persist_kernel<1, H, NDIR> : MT == 2 ? (const void*)lstm_persist_kernel<2, H, NDIR>
-                : MT == 3 ? (const void*)lstm_persist_kernel<3, H, NDIR> : (const void*)lstm_persist_kernel<4, H, NDIR>;
+  void* args[] = {(void*)&Whh, (void*)&Whh16, (void*)&Gin, (void*)&lens, (void*)&T_max,
+                  (void*)&B,   (void*)&hbuf,  (void*)&out, (void*)&bar};
+#define LPK(mt, x) (const void*)lstm_persist_kernel<mt, H, NDIR, x>
+  static const void* const fns[2][4] = {{LPK(1, false), LPK(2, false), LPK(3, false), LPK(4, false)},
+                                        {LPK(1, true), LPK(2, true), LPK(3, true), LPK(4, true)}};
+#undef LPK
+  const void* f = fns[Whh16 ? 1 : 0][MT - 1];
   launch_resident(f, dim3(NDIR * H / 4), dim3(256), args, 0, s);
   return true;
 }
 
 // encoder BiLSTM (H = 256, both directions); false = cooperative launch unavailable
-bool launch_bilstm_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
-                           unsigned* bar, float* out, hipStream_t s) {
-  return launch_lstm_persist_t<256, 2>(Gin, Whh, lens, T_max, B, hbuf, bar, out, s);
+bool launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                           int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
+  return launch_lstm_persist_t<256, 2>(Gin, Whh, Whh16, lens, T_max, B, hbuf, bar, out, s);
 }
 
 // GE2E speaker-encoder LSTM layer (H = 768, forward only); hbuf >= 2 x 64 x 768 floats, bar >= 512 words
-bool launch_lstm768_persist(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf,
-                            unsigned* bar, float* out, hipStream_t s) {
+bool launch_lstm768_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                            int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
   TTS_CHECK(B >= 1 && B <= 64, "speaker encoder: 1..64 sequences per launch");
-  return launch_lstm_persist_t<768, 1>(Gin, Whh, lens, T_max, B, hbuf, bar, out, s);
+  return launch_lstm_persist_t<768, 1>(Gin, Whh, Whh16, lens, T_max, B, hbuf, bar, out, s);
 }
 
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
