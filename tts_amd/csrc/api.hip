@@ -289,7 +289,8 @@ struct TacoModel {
   DevBuf whhT;
   DevBuf whhT16;  // W_hh split-f16 for the persistent BiLSTM (empty if out of the f16 range)
   DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b;
-  DevBuf att_p_x3;  // att_p split-f16 (split16.h) for the persistent decoder's P3; empty if out of range
+  // split-f16 forms for the persistent decoder (P3 prenet part, P5 ctx parts); empty if out of range
+  DevBuf att_p_x3, dec_ctx_x3, apre_ctx_x3;
   DevBuf Wcomb;  // location_dense . location_conv folded, [64 taps (62 used)][128 dims]
   float bv = 0.f;
   // persistent decoder: projection rows [stop tile | W_p] (+ bias) and prenet layer 1 on the host,
@@ -702,14 +703,11 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     M.spk_att_h = S ? lstm_tile_rows(slice_cols(wih, 4 * Q, P + ES, P + E, P + ES), Q, S) : std::vector<float>();
     const auto wpt = lstm_tile_rows(wp, Q, P);
     M.att_p.upload(swz(wpt, 4 * Q, P));
-    bool in_range = P % 32 == 0;
-    for (float v : wpt) in_range &= std::fabs(v) < F16_RANGE;
-    if (in_range)
-      M.att_p_x3.upload(pack_split_a(4 * Q / 16, P / 32, [&](int m, int k) { return wpt[(size_t)m * P + k]; }));
-    else
-      M.att_p_x3.reset();
+    upload_split_rows(M.att_p_x3, wpt, 4 * Q, P);
     auto pre = hcat({{wc.data(), E}, {whh.data(), Q}}, 4 * Q);
-    M.att_pre.upload(swz(lstm_tile_rows(pre, Q, E + Q), 4 * Q, E + Q));
+    const auto pret = lstm_tile_rows(pre, Q, E + Q);
+    M.att_pre.upload(swz(pret, 4 * Q, E + Q));
+    upload_split_rows(M.apre_ctx_x3, slice_cols(pret, 4 * Q, E + Q, 0, E), 4 * Q, E);
     std::vector<float> bsum(4 * Q);
     for (int i = 0; i < 4 * Q; ++i) bsum[i] = bih[i] + bhh[i];
     M.att_bias.upload(lstm_tile_rows(bsum, Q, 1));
@@ -749,7 +747,9 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     const auto wih = slice_cols(wih_all, 4 * D, Q + ES, 0, Q + E);
     M.spk_dec_h = S ? lstm_tile_rows(slice_cols(wih_all, 4 * D, Q + ES, Q + E, Q + ES), D, S) : std::vector<float>();
     auto w = hcat({{wih.data(), Q + E}, {whh.data(), D}}, 4 * D);
-    M.dec_w.upload(swz(lstm_tile_rows(w, D, Q + E + D), 4 * D, Q + E + D));
+    const auto wt = lstm_tile_rows(w, D, Q + E + D);
+    M.dec_w.upload(swz(wt, 4 * D, Q + E + D));
+    upload_split_rows(M.dec_ctx_x3, slice_cols(wt, 4 * D, Q + E + D, Q, Q + E), 4 * D, E);
     std::vector<float> bsum(4 * D);
     for (int i = 0; i < 4 * D; ++i) bsum[i] = bih[i] + bhh[i];
     M.dec_bias.upload(lstm_tile_rows(bsum, D, 1));
@@ -1267,7 +1267,12 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.apre_b = M.att_bias.f();
   a.attp_w = M.att_p.f();
   a.x3flag = x3_flag(c);  // null in fp32 mode
-  a.attp_x3 = a.x3flag && M.att_p_x3.p && !std::getenv("TTS_DECODER_F32") ? static_cast<const uint16_t*>(M.att_p_x3.p) : nullptr;
+  // split-f16 decoder GEMM parts: only with every split weight set in range, and Q = 1024,
+  // E = 512, prenet 256 (the kernel's fixed geometry, checked by build_pj's callers)
+  const bool dx3 = a.x3flag && M.att_p_x3.p && M.dec_ctx_x3.p && M.apre_ctx_x3.p && !std::getenv("TTS_DECODER_F32");
+  a.attp_x3 = dx3 ? M.att_p_x3.h() : nullptr;
+  a.dec_ctx_x3 = dx3 ? M.dec_ctx_x3.h() : nullptr;
+  a.apre_ctx_x3 = dx3 ? M.apre_ctx_x3.h() : nullptr;
   a.pj_w = M.pj_w.f();
   a.pj_b = M.pj_b.f();
   {  // per-row biases: projection (always), speaker columns when the model has them

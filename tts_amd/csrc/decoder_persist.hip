@@ -625,6 +625,49 @@ __device__ __forceinline__ void gemm_seg(f32x4 (&acc)[MT], const float* base, in
   }
 }
 
+// split-f16 form of gemm_seg2 over k-steps ks0 .. ks0 + NKS - 1 (32 columns each) of an fp32
+// fragment-order activation with nk 16-column chunks per 16-row block: the activation is split in
+// registers (lane L of k-step ks: row L & 15, k = 32 ks + 8 (L >> 4) + 0..7, i.e. chunk
+// 2 ks + (L >> 5), fragment lanes l1 and l1 + 16); w1 in registers, w2 in LDS as
+// [k-step][lane][hi | lo]. Adds to acc1 / acc2.
+template <int MT, int NKS>
+__device__ __forceinline__ void gemm_x3_pair(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* base, int nk, int ks0,
+                                             int lane, const h8 (&w1)[NKS][2], const h8* w2) {
+  const int l1 = 32 * ((lane >> 4) & 1) + (lane & 15);
+  f32x4 x[NKS][MT][2];
+#pragma unroll
+  for (int k = 0; k < NKS; ++k)
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const int c = mt * nk + 2 * (ks0 + k) + (lane >> 5);
+      x[k][mt][0] = ldc4<ACT_AUX>(base, (c * 64 + l1) * 16);
+      x[k][mt][1] = ldc4<ACT_AUX>(base, (c * 64 + l1 + 16) * 16);
+    }
+  f32x4 am1[MT], ac1[MT], am2[MT], ac2[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) am1[mt] = ac1[mt] = am2[mt] = ac2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < NKS; ++k) {
+    const h8 bh = w2[((ks0 + k) * 64 + lane) * 2], bl = w2[((ks0 + k) * 64 + lane) * 2 + 1];
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      const float v[8] = {x[k][mt][0][0], x[k][mt][0][1], x[k][mt][0][2], x[k][mt][0][3],
+                          x[k][mt][1][0], x[k][mt][1][1], x[k][mt][1][2], x[k][mt][1][3]};
+      h8 xh, xl;
+      split8(v, xh, xl);
+      mfma_x3(xh, xl, w1[k][0], w1[k][1], am1[mt], ac1[mt]);
+      mfma_x3(xh, xl, bh, bl, am2[mt], ac2[mt]);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc1[mt][j] += x3_value(am1[mt][j], ac1[mt][j]);
+      acc2[mt][j] += x3_value(am2[mt][j], ac2[mt][j]);
+    }
+}
+
 // gemm_seg for two accumulator sets over the SAME activation chunks (one load per chunk feeds both)
 template <int MT, int NC, int G, class WF1, class WF2>
 __device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* base, int nk, int kc0,
@@ -696,7 +739,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   int tid = tid0, lane = lane0, wave = wave0;
   {
     const f32x4* src = reinterpret_cast<const f32x4*>(P.apre_w) + (long)g * 96 * 64;
-    for (int i = tid; i < 96 * 64; i += PT) Wap[i] = src[i];
+    // split-f16 variant: chunks 0-31 (the ctx columns) hold the same bytes as split A fragments
+    // [16 k-steps][64 lanes][hi | lo] (P5)
+    const f32x4* srcx = reinterpret_cast<const f32x4*>(P.apre_ctx_x3) + (long)g * 32 * 64;
+    for (int i = tid; i < 96 * 64; i += PT) Wap[i] = (X3P && i < 32 * 64) ? srcx[i] : src[i];
     if (g >= IW0)  // attention_rnn workgroups use this area as P3 staging instead
       for (int i = tid; i < 64 * 128; i += PT) wcomb[i] = P.Wcomb[i];
   }
@@ -709,9 +755,16 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
     for (int i = 0; i < 8; ++i) wd[i] = src[(long)(8 * wave + i) * 64];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wd[8 + i] = src[(long)(64 + 4 * wave + i) * 64];
+    for (int i = 0; i < 4; ++i) wd[8 + i] = X3P ? f32x4{0.f, 0.f, 0.f, 0.f} : src[(long)(64 + 4 * wave + i) * 64];
 #pragma unroll
     for (int i = 0; i < 8; ++i) wd[12 + i] = src[(long)(96 + 8 * wave + i) * 64];
+  }
+  // split-f16 variant: the ctx columns of this wave (k-steps 2 wave, 2 wave + 1) as B fragments
+  h8 wdx[2][2];
+  if constexpr (X3P) {
+    const h8* src = reinterpret_cast<const h8*>(P.dec_ctx_x3) + (((long)g * 16 + 2 * wave) * 64 + lane) * 2;
+#pragma unroll
+    for (int i = 0; i < 2; ++i) wdx[i][0] = src[(long)i * 128], wdx[i][1] = src[(long)i * 128 + 1];
   }
   // epilogue constants: decoder_rnn biases of this thread's (row, unit) item, attention_rnn
   // ctx/h-part bias of its column
@@ -1084,8 +1137,11 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
     {
-      gemm_seg<MT, 4, 4>(accd, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; });
-      gemm_seg<MT, 4, 4>(acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return Wap[(4 * wave + i) * 64 + lane]; });
+      if constexpr (X3P)
+        gemm_x3_pair<MT, 2>(accd, acca, P.ctx, 32, 2 * wave, lane, wdx, reinterpret_cast<const h8*>(Wap));
+      else
+        gemm_seg2<MT, 4, 4>(accd, acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; },
+                            [&](int i) { return Wap[(4 * wave + i) * 64 + lane]; });
       float* red1 = red0;  // two reductions back to back: [2][8][Bp][17] would not fit; reuse
       acc_to_lds<MT>(red0, wave, lane, accd);
       lds_barrier();
@@ -1178,7 +1234,8 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
   // decoder variants are compiled in only where used: VAR bit 0 windowing, bit 1 forward attention
   // (bit 2: Graves attention, exclusive of the others); bit 3: split-f16 P3 (attp_x3 given)
-  TTS_CHECK(!a.attp_x3 || a.x3flag, "persistent decoder: split-f16 weights without a range flag");
+  TTS_CHECK(!a.attp_x3 || (a.x3flag && a.dec_ctx_x3 && a.apre_ctx_x3),
+            "persistent decoder: split-f16 weights incomplete or without a range flag");
   const int var = (a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0)) | (a.attp_x3 ? 8 : 0);
 #define PDK(mt, v) (const void*)persist_decoder_kernel<mt, v>
   static const void* const fns[2][13] = {
