@@ -31,6 +31,8 @@ from tts_amd.workload import (HOP, SAMPLE_RATE, forced_steps, lj_profile, pad_ba
 
 HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F32_PEAK_TFLOPS = 157.3     # dense fp32 (vector == f32 MFMA rate)
+F16_PEAK_TFLOPS = 2500.0    # dense f16 MFMA (v_mfma_f32_16x16x32_f16)
+X3_PEAK_TFLOPS = F16_PEAK_TFLOPS / 3  # fp32-equivalent rate of the split-f16 form (3 f16 MFMAs per product)
 
 
 def build_models(device, seed=0):
@@ -174,6 +176,8 @@ def main():
     from tts_amd._lib import get_engine
     eng = get_engine(dev)
     gemm_mode, fallbacks = eng.gemm_mode()
+    # decoder launch stats of the last step above (the headline GEMM mode), before the fp32 pass
+    path, launches = eng.decoder_stats()
     # the same step with every GEMM on the fp32 MFMA (no split-f16 kernels), for comparison
     f32_ms = None
     if gemm_mode == "x3" and args.f32_steps > 0:
@@ -187,8 +191,7 @@ def main():
         f32_ms = (time.perf_counter() - t1) / args.f32_steps * 1000.0
         eng.set_gemm_mode("x3")
 
-    # dominant decoder kernel, timed live with HIP events on the library's stream
-    path, launches = eng.decoder_stats()
+    # dominant decoder kernel, timed live with HIP events on the library's stream (stats above)
     if path == 1:
         # persistent decoder: the MT = 2 launch (32-row batch tile) carries most steps. Algorithmic
         # work = useful row-steps (rows still decoding) x the per-row GEMM flops of one step
@@ -210,9 +213,14 @@ def main():
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
             except Exception:
                 traffic = None
-        roof = {"kernel": "persist_decoder_kernel<2> (whole decoder loop, weights resident on chip)",
-                "bound": "mfma", "achieved": round(achieved, 2), "peak": F32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                "frac": round(achieved / F32_PEAK_TFLOPS, 4), "traffic": traffic,
+        # split-f16 mode: the decoder's GEMM parts run 3 f16 MFMAs per fp32 product, so the
+        # ceiling is the f16 MFMA peak / 3 in fp32-equivalent FLOP/s; fp32 mode: the fp32 MFMA peak
+        peak = X3_PEAK_TFLOPS if gemm_mode == "x3" else F32_PEAK_TFLOPS
+        roof = {"kernel": "persist_decoder_kernel<2%s> (whole decoder loop, weights resident on chip)"
+                          % (", split-f16" if gemm_mode == "x3" else ""),
+                "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "frac": round(achieved / peak, 4), "frac_vs_fp32_mfma_peak": round(achieved / F32_PEAK_TFLOPS, 4),
+                "traffic": traffic,
                 "avg_launch_us": round(ms0 * 1000.0, 1), "algorithmic_flops": flops,
                 "launch_steps": st0, "launches": [[round(m_, 3), s_] for m_, s_ in launches]}
     else:

@@ -290,7 +290,7 @@ struct TacoModel {
   DevBuf whhT16;  // W_hh split-f16 for the persistent BiLSTM (empty if out of the f16 range)
   DevBuf pre1, pre2, att_p, att_pre, att_bias, dec_w, dec_bias, WqT, Wloc, Wdense, v, proj_w, proj_b;
   // split-f16 forms for the persistent decoder (P3 prenet part, P5 ctx parts); empty if out of range
-  DevBuf att_p_x3, dec_ctx_x3, apre_ctx_x3;
+  DevBuf att_p_x3, dec_x3, apre_x3, pj_x3;
   DevBuf Wcomb;  // location_dense . location_conv folded, [64 taps (62 used)][128 dims]
   float bv = 0.f;
   // persistent decoder: projection rows [stop tile | W_p] (+ bias) and prenet layer 1 on the host,
@@ -707,7 +707,7 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     auto pre = hcat({{wc.data(), E}, {whh.data(), Q}}, 4 * Q);
     const auto pret = lstm_tile_rows(pre, Q, E + Q);
     M.att_pre.upload(swz(pret, 4 * Q, E + Q));
-    upload_split_rows(M.apre_ctx_x3, slice_cols(pret, 4 * Q, E + Q, 0, E), 4 * Q, E);
+    upload_split_rows(M.apre_x3, pret, 4 * Q, E + Q);
     std::vector<float> bsum(4 * Q);
     for (int i = 0; i < 4 * Q; ++i) bsum[i] = bih[i] + bhh[i];
     M.att_bias.upload(lstm_tile_rows(bsum, Q, 1));
@@ -749,7 +749,7 @@ void taco_finalize(tts_ctx* c, int num_chars, int r_init, int attn_norm) {
     auto w = hcat({{wih.data(), Q + E}, {whh.data(), D}}, 4 * D);
     const auto wt = lstm_tile_rows(w, D, Q + E + D);
     M.dec_w.upload(swz(wt, 4 * D, Q + E + D));
-    upload_split_rows(M.dec_ctx_x3, slice_cols(wt, 4 * D, Q + E + D, Q, Q + E), 4 * D, E);
+    upload_split_rows(M.dec_x3, wt, 4 * D, Q + E + D);
     std::vector<float> bsum(4 * D);
     for (int i = 0; i < 4 * D; ++i) bsum[i] = bih[i] + bhh[i];
     M.dec_bias.upload(lstm_tile_rows(bsum, D, 1));
@@ -1224,6 +1224,7 @@ void build_pj(tts_ctx* c, int r) {
     bias[rows_p + k] = (float)(bs + (M.pre1_bias.empty() ? 0.0 : (double)M.pre1_bias[k]));
   }
   M.pj_w.upload(swz(rows, rows_p + P, K));
+  upload_split_rows(M.pj_x3, rows, rows_p + P, K);
   M.pj_b.upload(bias);
   if (M.spk_dim) {
     // speaker columns, transposed [Es][att 4096 | dec 4096 | penc 128 | pj rows_p + P]
@@ -1269,10 +1270,11 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.x3flag = x3_flag(c);  // null in fp32 mode
   // split-f16 decoder GEMM parts: only with every split weight set in range, and Q = 1024,
   // E = 512, prenet 256 (the kernel's fixed geometry, checked by build_pj's callers)
-  const bool dx3 = a.x3flag && M.att_p_x3.p && M.dec_ctx_x3.p && M.apre_ctx_x3.p && !std::getenv("TTS_DECODER_F32");
+  const bool dx3 = a.x3flag && M.att_p_x3.p && M.dec_x3.p && M.apre_x3.p && M.pj_x3.p && !std::getenv("TTS_DECODER_F32");
   a.attp_x3 = dx3 ? M.att_p_x3.h() : nullptr;
-  a.dec_ctx_x3 = dx3 ? M.dec_ctx_x3.h() : nullptr;
-  a.apre_ctx_x3 = dx3 ? M.apre_ctx_x3.h() : nullptr;
+  a.dec_x3 = dx3 ? M.dec_x3.h() : nullptr;
+  a.apre_x3 = dx3 ? M.apre_x3.h() : nullptr;
+  a.pj_x3 = dx3 ? M.pj_x3.h() : nullptr;
   a.pj_w = M.pj_w.f();
   a.pj_b = M.pj_b.f();
   {  // per-row biases: projection (always), speaker columns when the model has them

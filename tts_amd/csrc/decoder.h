@@ -111,8 +111,9 @@ struct PArgs {
   const float* attp_w;  // [256][16][64][4] attention_rnn W_ih,prenet
   const uint16_t* attp_x3;  // the same weights split-f16 (split16.h pack_split_a [256][8][64][16]) or null
   unsigned* x3flag;         // raised when a split-f16 operand is outside the f16 range
-  const uint16_t* dec_ctx_x3;   // decoder_rnn ctx columns split-f16 [256 tiles][16][64][16] (with attp_x3)
-  const uint16_t* apre_ctx_x3;  // attention_rnn ctx columns split-f16 [256 tiles][16][64][16] (with attp_x3)
+  const uint16_t* dec_x3;   // dec_w split-f16 [256 tiles][80 k-steps][64][16] (with attp_x3)
+  const uint16_t* apre_x3;  // apre_w split-f16 [256 tiles][48][64][16] (with attp_x3)
+  const uint16_t* pj_x3;    // pj_w split-f16 [ntj tiles][48][64][16] (with attp_x3)
   const float* pj_w;    // [ntj][96][64][4] stop tile, 5r frame tiles, 16 folded prenet-1 tiles
   const float* pj_b;    // [ntj * 16]
   // per-row biases (api.hip spk_bias_kernel), row stride spk_ld: projection bias per row (always),

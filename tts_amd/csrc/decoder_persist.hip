@@ -625,38 +625,69 @@ __device__ __forceinline__ void gemm_seg(f32x4 (&acc)[MT], const float* base, in
   }
 }
 
-// split-f16 form of gemm_seg2 over k-steps ks0 .. ks0 + NKS - 1 (32 columns each) of an fp32
-// fragment-order activation with nk 16-column chunks per 16-row block: the activation is split in
-// registers (lane L of k-step ks: row L & 15, k = 32 ks + 8 (L >> 4) + 0..7, i.e. chunk
-// 2 ks + (L >> 5), fragment lanes l1 and l1 + 16); w1 in registers, w2 in LDS as
-// [k-step][lane][hi | lo]. Adds to acc1 / acc2.
-template <int MT, int NKS>
-__device__ __forceinline__ void gemm_x3_pair(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* base, int nk, int ks0,
-                                             int lane, const h8 (&w1)[NKS][2], const h8* w2) {
+// Split-f16 forms of gemm_seg / gemm_seg2 over k-steps ks0 .. ks0 + NKS - 1 (32 columns each) of
+// an fp32 fragment-order activation with nk 16-column chunks per 16-row block. The activation is
+// split in registers: lane L of k-step ks holds row L & 15, k = 32 ks + 8 (L >> 4) + 0..7, i.e.
+// chunk 2 ks + (L >> 5) at fragment lanes l1 and l1 + 16. wf(k, hi, lo) yields the B fragment
+// (split weights) of the k-th step. Adds to the accumulators; one k-step of loads in flight.
+template <int MT>
+__device__ __forceinline__ void ld_x3_step(f32x4 (&x)[MT][2], const float* base, int nk, int ks, int lane) {
   const int l1 = 32 * ((lane >> 4) & 1) + (lane & 15);
-  f32x4 x[NKS][MT][2];
 #pragma unroll
-  for (int k = 0; k < NKS; ++k)
+  for (int mt = 0; mt < MT; ++mt) {
+    const int c = mt * nk + 2 * ks + (lane >> 5);
+    x[mt][0] = ldc4<ACT_AUX>(base, (c * 64 + l1) * 16);
+    x[mt][1] = ldc4<ACT_AUX>(base, (c * 64 + l1 + 16) * 16);
+  }
+}
+__device__ __forceinline__ void split_x3_step(const f32x4 (&x)[2], h8& xh, h8& xl) {
+  const float v[8] = {x[0][0], x[0][1], x[0][2], x[0][3], x[1][0], x[1][1], x[1][2], x[1][3]};
+  split8(v, xh, xl);
+}
+template <int MT, int NKS, class WF>
+__device__ __forceinline__ void gemm_x3(f32x4 (&acc)[MT], const float* base, int nk, int ks0, int lane, WF wf) {
+  f32x4 x[2][MT][2];
+  ld_x3_step<MT>(x[0], base, nk, ks0, lane);
+  f32x4 am[MT], ac[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) am[mt] = ac[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < NKS; ++k) {
+    if (k + 1 < NKS) ld_x3_step<MT>(x[(k + 1) & 1], base, nk, ks0 + k + 1, lane);
+    h8 bh, bl;
+    wf(k, bh, bl);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const int c = mt * nk + 2 * (ks0 + k) + (lane >> 5);
-      x[k][mt][0] = ldc4<ACT_AUX>(base, (c * 64 + l1) * 16);
-      x[k][mt][1] = ldc4<ACT_AUX>(base, (c * 64 + l1 + 16) * 16);
+      h8 xh, xl;
+      split_x3_step(x[k & 1][mt], xh, xl);
+      mfma_x3(xh, xl, bh, bl, am[mt], ac[mt]);
     }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[mt][j] += x3_value(am[mt][j], ac[mt][j]);
+}
+template <int MT, int NKS, class WF1, class WF2>
+__device__ __forceinline__ void gemm_x3_pair(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* base, int nk, int ks0,
+                                             int lane, WF1 wf1, WF2 wf2) {
+  f32x4 x[2][MT][2];
+  ld_x3_step<MT>(x[0], base, nk, ks0, lane);
   f32x4 am1[MT], ac1[MT], am2[MT], ac2[MT];
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) am1[mt] = ac1[mt] = am2[mt] = ac2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
   for (int k = 0; k < NKS; ++k) {
-    const h8 bh = w2[((ks0 + k) * 64 + lane) * 2], bl = w2[((ks0 + k) * 64 + lane) * 2 + 1];
+    if (k + 1 < NKS) ld_x3_step<MT>(x[(k + 1) & 1], base, nk, ks0 + k + 1, lane);
+    h8 b1h, b1l, b2h, b2l;
+    wf1(k, b1h, b1l);
+    wf2(k, b2h, b2l);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
-      const float v[8] = {x[k][mt][0][0], x[k][mt][0][1], x[k][mt][0][2], x[k][mt][0][3],
-                          x[k][mt][1][0], x[k][mt][1][1], x[k][mt][1][2], x[k][mt][1][3]};
       h8 xh, xl;
-      split8(v, xh, xl);
-      mfma_x3(xh, xl, w1[k][0], w1[k][1], am1[mt], ac1[mt]);
-      mfma_x3(xh, xl, bh, bl, am2[mt], ac2[mt]);
+      split_x3_step(x[k & 1][mt], xh, xl);
+      mfma_x3(xh, xl, b1h, b1l, am1[mt], ac1[mt]);
+      mfma_x3(xh, xl, b2h, b2l, am2[mt], ac2[mt]);
     }
   }
 #pragma unroll
@@ -739,33 +770,44 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   int tid = tid0, lane = lane0, wave = wave0;
   {
     const f32x4* src = reinterpret_cast<const f32x4*>(P.apre_w) + (long)g * 96 * 64;
-    // split-f16 variant: chunks 0-31 (the ctx columns) hold the same bytes as split A fragments
-    // [16 k-steps][64 lanes][hi | lo] (P5)
-    const f32x4* srcx = reinterpret_cast<const f32x4*>(P.apre_ctx_x3) + (long)g * 32 * 64;
-    for (int i = tid; i < 96 * 64; i += PT) Wap[i] = (X3P && i < 32 * 64) ? srcx[i] : src[i];
+    // split-f16 variant: the same bytes hold split B fragments [48 k-steps][64 lanes][hi | lo]
+    const f32x4* srcx = reinterpret_cast<const f32x4*>(P.apre_x3) + (long)g * 96 * 64;
+    for (int i = tid; i < 96 * 64; i += PT) Wap[i] = X3P ? srcx[i] : src[i];
     if (g >= IW0)  // attention_rnn workgroups use this area as P3 staging instead
       for (int i = tid; i < 64 * 128; i += PT) wcomb[i] = P.Wcomb[i];
   }
   // decoder_rnn weights of this wave: K = [h_att 64 chunks | ctx 32 | h_dec 64]; wave w keeps
   // h_att chunks 8w..8w+7 (wd[0..7]), ctx chunks 4w..4w+3 (wd[8..11]), h_dec chunks 8w..8w+7
   // (wd[12..19]), so that each part can run in the phase where its input becomes final
-  f32x4 wd[DEC_NC];
-  {
+  f32x4 wd[X3P ? 1 : DEC_NC];
+  // split-f16 variant: slots 0-3 h_att k-steps 4w..4w+3, 4-5 ctx k-steps 32+2w, +1, 6-9 h_dec
+  // k-steps 48+4w..+3 (the same K ranges as the fp32 chunks, 32 columns per k-step)
+  h8 wdx[X3P ? 10 : 1][2];
+  if constexpr (X3P) {
+    const h8* src = reinterpret_cast<const h8*>(P.dec_x3) + ((long)g * 80 * 64 + lane) * 2;
+#pragma unroll
+    for (int i = 0; i < 10; ++i) {
+      const int ks = i < 4 ? 4 * wave + i : (i < 6 ? 32 + 2 * wave + (i - 4) : 48 + 4 * wave + (i - 6));
+      wdx[i][0] = src[(long)ks * 128];
+      wdx[i][1] = src[(long)ks * 128 + 1];
+    }
+  } else {
     const f32x4* src = reinterpret_cast<const f32x4*>(P.dec_w) + (long)g * 160 * 64 + lane;
 #pragma unroll
     for (int i = 0; i < 8; ++i) wd[i] = src[(long)(8 * wave + i) * 64];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) wd[8 + i] = X3P ? f32x4{0.f, 0.f, 0.f, 0.f} : src[(long)(64 + 4 * wave + i) * 64];
+    for (int i = 0; i < 4; ++i) wd[8 + i] = src[(long)(64 + 4 * wave + i) * 64];
 #pragma unroll
     for (int i = 0; i < 8; ++i) wd[12 + i] = src[(long)(96 + 8 * wave + i) * 64];
   }
-  // split-f16 variant: the ctx columns of this wave (k-steps 2 wave, 2 wave + 1) as B fragments
-  h8 wdx[2][2];
-  if constexpr (X3P) {
-    const h8* src = reinterpret_cast<const h8*>(P.dec_ctx_x3) + (((long)g * 16 + 2 * wave) * 64 + lane) * 2;
-#pragma unroll
-    for (int i = 0; i < 2; ++i) wdx[i][0] = src[(long)i * 128], wdx[i][1] = src[(long)i * 128 + 1];
-  }
+  const h8* Wapx = reinterpret_cast<const h8*>(Wap);
+  auto wdx_f = [&](int base) { return [&, base](int k, h8& hi, h8& lo) { hi = wdx[base + k][0], lo = wdx[base + k][1]; }; };
+  auto wap_f = [&](int ks0) {
+    return [&, ks0](int k, h8& hi, h8& lo) {
+      hi = Wapx[((ks0 + k) * 64 + lane) * 2];
+      lo = Wapx[((ks0 + k) * 64 + lane) * 2 + 1];
+    };
+  };
   // epilogue constants: decoder_rnn biases of this thread's (row, unit) item, attention_rnn
   // ctx/h-part bias of its column
   float db[4];
@@ -795,7 +837,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) accd[mt] = acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto dec_hdec_part = [&](const float* hd) {
-    gemm_seg<MT, 8, 4>(accd, hd, 64, 8 * wave, lane, [&](int i) { return wd[12 + i]; });
+    if constexpr (X3P) gemm_x3<MT, 4>(accd, hd, 64, 4 * wave, lane, wdx_f(6));
+    else gemm_seg<MT, 8, 4>(accd, hd, 64, 8 * wave, lane, [&](int i) { return wd[12 + i]; });
   };
   // attention_rnn ctx/h tile g complete: reduce over the waves, add the biases, publish the next
   // step's gate addends, reset the accumulator
@@ -1118,10 +1161,14 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
           lds_barrier();
         }
-        gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
+        if constexpr (X3P) gemm_x3<MT, 4>(accd, P.hatt, 64, 4 * wave, lane, wdx_f(0));
+        else gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
       } else {  // no item: both h_att parts and the decoder_rnn h_dec part
-        gemm_seg2<MT, 8, 2>(accd, acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; },
-                            [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
+        if constexpr (X3P)
+          gemm_x3_pair<MT, 4>(accd, acca, P.hatt, 64, 4 * wave, lane, wdx_f(0), wap_f(16 + 4 * wave));
+        else
+          gemm_seg2<MT, 8, 2>(accd, acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; },
+                              [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
         dec_hdec_part(hd_cur);
       }
     }
@@ -1138,7 +1185,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     wave = opaque_s(wave0);
     {
       if constexpr (X3P)
-        gemm_x3_pair<MT, 2>(accd, acca, P.ctx, 32, 2 * wave, lane, wdx, reinterpret_cast<const h8*>(Wap));
+        gemm_x3_pair<MT, 2>(accd, acca, P.ctx, 32, 2 * wave, lane, wdx_f(4), wap_f(2 * wave));
       else
         gemm_seg2<MT, 4, 4>(accd, acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; },
                             [&](int i) { return Wap[(4 * wave + i) * 64 + lane]; });
@@ -1164,12 +1211,19 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     PTRACE(7);
     gsync_arrive(P.bar, gen);
     // projection weights for P6 (half pj & 1 of job tile pj >> 1, 6 k-chunks per wave)
-    f32x4 wp[PJ_NC];
+    f32x4 wp[X3P ? 1 : PJ_NC];
+    h8 wpx[X3P ? PJ_NC / 2 : 1][2];  // split-f16: k-steps 24 half + 3 wave .. + 2
     {
       const int q = min(max(pj, 0) >> 1, P.ntj - 1), half = pj & 1;
-      const f32x4* src = reinterpret_cast<const f32x4*>(P.pj_w) + ((long)q * 96 + 48 * half + wave * PJ_NC) * 64 + lane;
+      if constexpr (X3P) {
+        const h8* src = reinterpret_cast<const h8*>(P.pj_x3) + (((long)q * 48 + 24 * half + 3 * wave) * 64 + lane) * 2;
 #pragma unroll
-      for (int i = 0; i < PJ_NC; ++i) wp[i] = src[(long)i * 64];
+        for (int i = 0; i < PJ_NC / 2; ++i) wpx[i][0] = src[(long)i * 128], wpx[i][1] = src[(long)i * 128 + 1];
+      } else {
+        const f32x4* src = reinterpret_cast<const f32x4*>(P.pj_w) + ((long)q * 96 + 48 * half + wave * PJ_NC) * 64 + lane;
+#pragma unroll
+        for (int i = 0; i < PJ_NC; ++i) wp[i] = src[(long)i * 64];
+      }
     }
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(8);
@@ -1182,22 +1236,48 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int kb = 48 * (pj & 1) + wave * PJ_NC;  // K = [h_dec 1024 | ctx 512]
-      f32x4 y[PJ_NC][MT];
+      if constexpr (X3P) {
+        // k-step kb / 2 + i: 32 columns of one source (the h_dec / ctx boundary is k-step 32)
+        f32x4 y[PJ_NC / 2][MT][2];
 #pragma unroll
-      for (int i = 0; i < PJ_NC; ++i) {
-        const int kc = kb + i;
-        const float* base = kc < 64 ? hd_nxt : P.ctx;
-        const int kl = kc < 64 ? kc : kc - 64;
-        const int nk = kc < 64 ? 64 : 32;
+        for (int i = 0; i < PJ_NC / 2; ++i) {
+          const int ks = kb / 2 + i;
+          if (ks < 32) ld_x3_step<MT>(y[i], hd_nxt, 64, ks, lane);
+          else ld_x3_step<MT>(y[i], P.ctx, 32, ks - 32, lane);
+        }
+        f32x4 am[MT], ac[MT];
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) y[i][mt] = ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
+        for (int mt = 0; mt < MT; ++mt) am[mt] = ac[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int i = 0; i < PJ_NC / 2; ++i)
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) {
+            h8 xh, xl;
+            split_x3_step(y[i][mt], xh, xl);
+            mfma_x3(xh, xl, wpx[i][0], wpx[i][1], am[mt], ac[mt]);
+          }
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) acc2[mt][j] = x3_value(am[mt][j], ac[mt][j]);
+      } else {
+        f32x4 y[PJ_NC][MT];
+#pragma unroll
+        for (int i = 0; i < PJ_NC; ++i) {
+          const int kc = kb + i;
+          const float* base = kc < 64 ? hd_nxt : P.ctx;
+          const int kl = kc < 64 ? kc : kc - 64;
+          const int nk = kc < 64 ? 64 : 32;
+#pragma unroll
+          for (int mt = 0; mt < MT; ++mt) y[i][mt] = ldc4<ACT_AUX>(base, ((mt * nk + kl) * 64 + lane) * 16);
+        }
+#pragma unroll
+        for (int i = 0; i < PJ_NC; ++i)
+#pragma unroll
+          for (int q = 0; q < 4; ++q)
+#pragma unroll
+            for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
       }
-#pragma unroll
-      for (int i = 0; i < PJ_NC; ++i)
-#pragma unroll
-        for (int q = 0; q < 4; ++q)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
       acc_to_lds<MT>(red0, wave, lane, acc2);
       lds_barrier();
       for (int idx = tid; idx < Bp * 16; idx += PT) {
@@ -1207,7 +1287,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       lds_barrier();
     }
     if (g >= IW0) {  // item workgroups: attention_rnn h_att part (h_att of step t is still in place)
-      gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
+      if constexpr (X3P) gemm_x3<MT, 4>(acca, P.hatt, 64, 4 * wave, lane, wap_f(16 + 4 * wave));
+      else gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
       att_epilogue(red0);
     }
     PTRACE(9);
@@ -1234,7 +1315,7 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
   // decoder variants are compiled in only where used: VAR bit 0 windowing, bit 1 forward attention
   // (bit 2: Graves attention, exclusive of the others); bit 3: split-f16 P3 (attp_x3 given)
-  TTS_CHECK(!a.attp_x3 || (a.x3flag && a.dec_ctx_x3 && a.apre_ctx_x3),
+  TTS_CHECK(!a.attp_x3 || (a.x3flag && a.dec_x3 && a.apre_x3 && a.pj_x3),
             "persistent decoder: split-f16 weights incomplete or without a range flag");
   const int var = (a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0)) | (a.attp_x3 ? 8 : 0);
 #define PDK(mt, v) (const void*)persist_decoder_kernel<mt, v>
