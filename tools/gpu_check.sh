@@ -5,7 +5,8 @@ set -o pipefail
 mkdir -p gpurun_out
 cd "$(dirname "$0")/.."
 export TMPDIR=/tmp
-step() { local name=$1; shift; echo "== $name"; "$@"; local rc=$?; echo "== $name rc=$rc"; return $rc; }
+exec 3>&1  # step markers go to the script's stdout, not into the per-step logs
+step() { local name=$1; shift; echo "== $name" >&3; "$@"; local rc=$?; echo "== $name rc=$rc" >&3; return $rc; }
 step tests timeout -k 10 400 python -u -m pytest tests -x -v -m gpu --timeout 120 --timeout-method thread > gpurun_out/gpu_tests.log 2>&1 &&
 step smoke timeout -k 10 200 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 &&
 step bench timeout -k 10 400 python bench.py > gpurun_out/bench.log 2>&1 &&

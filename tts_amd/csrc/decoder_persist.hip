@@ -322,6 +322,12 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   lds_barrier();
   ATRACE(6);
   if (!*is_last) return;
+  // the alignment pass's first loads (position tid), issued ahead of the combine's: they do not
+  // depend on it, and vmcnt is in order, so they land while the partials are summed
+  const long ab = (long)b * D.T_max;
+  const int tt0 = min(tid, Tm1);
+  const float e_first = ldc(P.energy + ab + tt0);
+  const float acum_first = ldc(P.acum + ab + tt0);
   // combine: chunk partials in batches of 8, all loads of a batch in flight (clamped)
   const long pb0 = (long)b * P.nchmax;
   constexpr int CB = 8;
@@ -363,7 +369,6 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   float ctx_v = cx / ((FWD && P.fwd) ? Fz : S);
   stc(P.ctx + frag_idx(b, tid, 512), ctx_v);
   ATRACE(7);
-  const long ab = (long)b * D.T_max;
   float bestv = -INFINITY;
   int besti = 0x7fffffff;
   // forward_attn_mask (common_layers.py:309-318): argmax of the shifted previous alignment
@@ -371,14 +376,14 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   float prv_m = 0.f, vmax = 0.f;
   int prv_i = 0x7fffffff;
   for (int tt = tid; tt < T; tt += NT) {
-    const float e = ldc(P.energy + ab + tt);
+    const float e = tt == tid ? e_first : ldc(P.energy + ab + tt);
     if ((WIN && P.win) && (e > bestv || (e == bestv && tt < besti))) {
       bestv = e;
       besti = tt;
     }
     const float raw = P.softmax ? (e == -INFINITY ? 0.f : expf(e - m)) : 1.f / (1.f + expf(-e));
     const float al = raw / S;
-    stc(P.acum + ab + tt, ldc(P.acum + ab + tt) + al);  // location state accumulates the raw alignment
+    stc(P.acum + ab + tt, (tt == tid ? acum_first : ldc(P.acum + ab + tt)) + al);  // location state: raw alignment
     if ((FWD && P.fwd)) {  // forward alignment into the energy slot (alpha is still read as a[t-1] here)
       const float ap = fwd_prev(tt);
       const float fa = ((1.f - fu) * ap + fu * fwd_prev(tt - 1) + 1e-8f) * raw / Fz;
@@ -682,6 +687,47 @@ __device__ __forceinline__ void gemm_x3_pair(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT
     h8 b1h, b1l, b2h, b2l;
     wf1(k, b1h, b1l);
     wf2(k, b2h, b2l);
+#pragma unroll
+    for (int mt = 0; mt < MT; ++mt) {
+      h8 xh, xl;
+      split_x3_step(x[k & 1][mt], xh, xl);
+      mfma_x3(xh, xl, b1h, b1l, am1[mt], ac1[mt]);
+      mfma_x3(xh, xl, b2h, b2l, am2[mt], ac2[mt]);
+    }
+  }
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc1[mt][j] += x3_value(am1[mt][j], ac1[mt][j]);
+      acc2[mt][j] += x3_value(am2[mt][j], ac2[mt][j]);
+    }
+}
+
+// P5 of the attention-item workgroups (split-f16): the h_att parts (NKA k-steps from `a`, weights
+// wa1 / wa2) then the ctx parts (NKC k-steps from `c`, weights wc1 / wc2) of both LSTMs, one
+// pipeline: every activation chunk is read once and the first ctx k-step's loads are in flight
+// under the last h_att k-step
+template <int MT, int NKA, int NKC, class WA1, class WA2, class WC1, class WC2>
+__device__ __forceinline__ void gemm_x3_hatt_ctx(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* a, int nka,
+                                                 int ksa, const float* c, int nkc, int ksc, int lane, WA1 wa1,
+                                                 WA2 wa2, WC1 wc1, WC2 wc2) {
+  constexpr int NS = NKA + NKC;
+  auto ld = [&](f32x4 (&x)[MT][2], int k) {
+    if (k < NKA) ld_x3_step<MT>(x, a, nka, ksa + k, lane);
+    else ld_x3_step<MT>(x, c, nkc, ksc + k - NKA, lane);
+  };
+  f32x4 x[2][MT][2];
+  ld(x[0], 0);
+  f32x4 am1[MT], ac1[MT], am2[MT], ac2[MT];
+#pragma unroll
+  for (int mt = 0; mt < MT; ++mt) am1[mt] = ac1[mt] = am2[mt] = ac2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+  for (int k = 0; k < NS; ++k) {
+    if (k + 1 < NS) ld(x[(k + 1) & 1], k + 1);
+    h8 b1h, b1l, b2h, b2l;
+    if (k < NKA) wa1(k, b1h, b1l), wa2(k, b2h, b2l);
+    else wc1(k - NKA, b1h, b1l), wc2(k - NKA, b2h, b2l);
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       h8 xh, xl;
@@ -1161,8 +1207,9 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
           lds_barrier();
         }
-        if constexpr (X3P) gemm_x3<MT, 4>(accd, P.hatt, 64, 4 * wave, lane, wdx_f(0));
-        else gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
+        // split-f16: the h_att part runs at the start of P5 instead (h_att is still in place), off
+        // the chain of the utterances' last arrivers, whose combine and alignment pass end P4
+        if constexpr (!X3P) gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
       } else {  // no item: both h_att parts and the decoder_rnn h_dec part
         if constexpr (X3P)
           gemm_x3_pair<MT, 4>(accd, acca, P.hatt, 64, 4 * wave, lane, wdx_f(0), wap_f(16 + 4 * wave));
@@ -1184,8 +1231,13 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
     {
-      if constexpr (X3P)
-        gemm_x3_pair<MT, 2>(accd, acca, P.ctx, 32, 2 * wave, lane, wdx_f(4), wap_f(2 * wave));
+      if constexpr (X3P) {
+        if (g >= IW0)  // + both h_att parts (moved here from P4 / P6: h_att read once per step)
+          gemm_x3_hatt_ctx<MT, 4, 2>(accd, acca, P.hatt, 64, 4 * wave, P.ctx, 32, 2 * wave, lane, wdx_f(0),
+                                     wap_f(16 + 4 * wave), wdx_f(4), wap_f(2 * wave));
+        else
+          gemm_x3_pair<MT, 2>(accd, acca, P.ctx, 32, 2 * wave, lane, wdx_f(4), wap_f(2 * wave));
+      }
       else
         gemm_seg2<MT, 4, 4>(accd, acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; },
                             [&](int i) { return Wap[(4 * wave + i) * 64 + lane]; });
@@ -1287,8 +1339,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       lds_barrier();
     }
     if (g >= IW0) {  // item workgroups: attention_rnn h_att part (h_att of step t is still in place)
-      if constexpr (X3P) gemm_x3<MT, 4>(acca, P.hatt, 64, 4 * wave, lane, wap_f(16 + 4 * wave));
-      else gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
+      if constexpr (!X3P)  // split-f16: done in P5 beside the decoder_rnn h_att part
+        gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
       att_epilogue(red0);
     }
     PTRACE(9);
