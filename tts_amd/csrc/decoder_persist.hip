@@ -40,7 +40,6 @@ constexpr int PW = 256, PT = 512, NWV = 8;
 constexpr int DEC_NC = 20;   // 160 k-chunks / 8 waves
 constexpr int ATTP_NC = 8;   // 4 tiles x 16 chunks / 8 waves
 constexpr int PJ_NC = 6;     // 48 / 8
-constexpr int PB_HALF = 64 * 256;  // prenet-2 K halves (fragment order, 64 rows each)
 constexpr int NATT = 64;           // attention_rnn workgroups (P3): 4 gate tiles = 16 units each
 constexpr int PJ_WG0 = 0;          // first projection workgroup (P6); jobs sit on the attention_rnn
                                    // workgroups, which have no attention item
@@ -872,8 +871,11 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   const int pj_jobs = 2 * P.ntj;
   const int pj = g - PJ_WG0;  // projection job of this workgroup (P6), if 0 <= pj < pj_jobs
   const bool is_pj = pj >= 0 && pj < pj_jobs;
-  // prenet layer-2 weight chunk of this wave (workgroups 0-31: tile g & 15, k-chunk 8 (g >> 4) + wave)
-  const f32x4 w2 = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + 8 * ((g >> 4) & 1) + wave) * 64 + lane];
+  // prenet layer-2 weight chunks of this wave
+  // (workgroups 0-31: tile g & 15, k-chunks wave and 8 + wave: the whole K for 16 batch rows,
+  // so P3 reads one pb copy)
+  const f32x4 w2 = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + wave) * 64 + lane];
+  const f32x4 w2b = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + 8 + wave) * 64 + lane];
   // partial sums of this workgroup's decoder_rnn tile (accd) and attention_rnn ctx/h tile (acca),
   // accumulated across phases. Attention-item workgroups (g >= IW0): accd h_dec part in P3, h_att
   // part in P4 after the item, ctx part in P5; acca ctx part in P5, h_att part + epilogue in P6.
@@ -921,41 +923,47 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     PTRACE(0);
     float* hd_cur = (t & 1) ? P.hdec1 : P.hdec0;
     float* hd_nxt = (t & 1) ? P.hdec0 : P.hdec1;
-    // ======== P1: prenet layer 2 halves (workgroups 0-31) || stop(t-1) (workgroup 255) ========
+    // ======== P1: prenet layer 2 (workgroups 0-31) || stop(t-1) (workgroup IW0 - 1) ========
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (g < 32) {  // prenet layer 2, tile g & 15, K half g >> 4 (one k-chunk per wave)
-      f32x4 acc[MT];
-#pragma unroll
-      for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (g < 32 && (g >> 4) < MT) {  // prenet layer 2: tile g & 15, batch rows 16 (g >> 4) .. + 15, whole K
+      const int tl2 = g & 15, mt = g >> 4;
+      f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
       // t = 0: the prenet input is the zero go-frame: layer 1 gives relu(b1') (BN prenet) or 0
       if (t > 0 || P.pre1_b0) {
-        const int kc = 8 * (g >> 4) + wave;
-        const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
+        f32x4 x[2];
+        const int m = mt * 16 + (lane & 15);
 #pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int m = mt * 16 + (lane & 15);
-          f32x4 x;
+        for (int h = 0; h < 2; ++h) {
+          const int kc = 8 * h + wave;
+          const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
           if (t > 0) {
             const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pjb_rows + (long)m * P.spk_ld + col);
-            x = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
+            x[h] = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
           } else {
-            x = *reinterpret_cast<const f32x4*>(P.pre1_b0 + kc * 16 + 4 * (lane >> 4));
+            x[h] = *reinterpret_cast<const f32x4*>(P.pre1_b0 + kc * 16 + 4 * (lane >> 4));
           }
+        }
 #pragma unroll
-          for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
+        for (int h = 0; h < 2; ++h) {
 #pragma unroll
-          for (int q = 0; q < 4; ++q) acc[mt] = MFMA16(x[q], w2[q], acc[mt]);
+          for (int q = 0; q < 4; ++q) x[h][q] = fmaxf(x[h][q], 0.f);
+#pragma unroll
+          for (int q = 0; q < 4; ++q) acc = MFMA16(x[h][q], h ? w2b[q] : w2[q], acc);
         }
       }
-      acc_to_lds<MT>(red0, wave, lane, acc);
+      float* p = red0 + wave * 16 * 17;  // [wave][16 rows][17]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[(4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[j];
       lds_barrier();
-      for (int idx = tid; idx < Bp * 16; idx += PT) {
-        const int m = idx >> 4, n = idx & 15;
-        float v = lds_sum<NWV, Bp>(red0, m, n);
-        if (P.pre2_b && (g >> 4) == 0) v += P.pre2_b[(g & 15) * 16 + n];  // BN prenet layer-2 bias, once
-        stc(P.pb + (g >> 4) * PB_HALF + frag_idx(m, (g & 15) * 16 + n, 256), v);
+      if (tid < 256) {
+        const int mm = tid >> 4, n = tid & 15;
+        float v = red0[mm * 17 + n];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * 17 + n];
+        if (P.pre2_b) v += P.pre2_b[tl2 * 16 + n];  // BN prenet layer-2 bias
+        stc(P.pb + frag_idx(mt * 16 + mm, tl2 * 16 + n, 256), v);
       }
       lds_barrier();
     }
@@ -1056,8 +1064,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
           const int c = mt * 16 + 2 * wave + (lane >> 5);
-          const f32x4 x0 = ldc4(P.pb, (c * 64 + l1) * 16) + ldc4(P.pb, (c * 64 + l1) * 16 + PB_HALF * 4);
-          const f32x4 x1 = ldc4(P.pb, (c * 64 + l1 + 16) * 16) + ldc4(P.pb, (c * 64 + l1 + 16) * 16 + PB_HALF * 4);
+          const f32x4 x0 = ldc4(P.pb, (c * 64 + l1) * 16);
+          const f32x4 x1 = ldc4(P.pb, (c * 64 + l1 + 16) * 16);
           float v[8];
           float mx = 0.f;
 #pragma unroll
@@ -1101,7 +1109,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) {
             const int c = mt * 16 + 2 * wave + i;
-            f32x4 x = ldc4(P.pb, (c * 64 + lane) * 16) + ldc4(P.pb, (c * 64 + lane) * 16 + PB_HALF * 4);
+            f32x4 x = ldc4(P.pb, (c * 64 + lane) * 16);
 #pragma unroll
             for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
             xs[c * 64 + lane] = x;
