@@ -912,7 +912,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     for (int idx = (g - wg0) * PT + tid; idx < n; idx += nwg * PT) {
       const int m = idx / FR, c = idx - m * FR;
       if (!ldci(D.done + m) || ldci(D.steps + m) > s) {
-        const float v = ldc(P.ypart + (long)m * YP + 16 + c) + ldc(P.ypart + (long)(YROWS + m) * YP + 16 + c) +
+        const float v = ldc(P.ypart + (long)m * YP + 16 + c) + (X3P ? 0.f : ldc(P.ypart + (long)(YROWS + m) * YP + 16 + c)) +
                         P.pjb_rows[(long)m * P.spk_ld + 16 + c];
         D.dec_out[((long)m * D.S_cap + s) * FR + c] = v;
       }
@@ -940,7 +940,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
           if (t > 0) {
             const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pjb_rows + (long)m * P.spk_ld + col);
-            x[h] = ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
+            x[h] = X3P ? ldc4(P.ypart, (m * YP + col) * 4) + bb
+                       : ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
           } else {
             x[h] = *reinterpret_cast<const f32x4*>(P.pre1_b0 + kc * 16 + 4 * (lane >> 4));
           }
@@ -977,7 +978,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         const int m = tid;
         int dn = ldci(D.done + m);
         if (t >= 1 && !dn) {
-          const float logit = ldc(P.ypart + (long)m * YP) + ldc(P.ypart + (long)(YROWS + m) * YP) +
+          const float logit = ldc(P.ypart + (long)m * YP) + (X3P ? 0.f : ldc(P.ypart + (long)(YROWS + m) * YP)) +
                               P.pjb_rows[(long)m * P.spk_ld];
           const float sg = sigm(logit);
           if (t - 1 < D.S_cap) D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
@@ -1272,13 +1273,14 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     gsync_arrive(P.bar, gen);
     // projection weights for P6 (half pj & 1 of job tile pj >> 1, 6 k-chunks per wave)
     f32x4 wp[X3P ? 1 : PJ_NC];
-    h8 wpx[X3P ? PJ_NC / 2 : 1][2];  // split-f16: k-steps 24 half + 3 wave .. + 2
+    h8 wpx[X3P ? PJ_NC : 1][2];  // split-f16: the whole K for 16 rows, k-steps 6 wave .. + 5
     {
       const int q = min(max(pj, 0) >> 1, P.ntj - 1), half = pj & 1;
       if constexpr (X3P) {
-        const h8* src = reinterpret_cast<const h8*>(P.pj_x3) + (((long)q * 48 + 24 * half + 3 * wave) * 64 + lane) * 2;
+        (void)half;
+        const h8* src = reinterpret_cast<const h8*>(P.pj_x3) + (((long)q * 48 + 6 * wave) * 64 + lane) * 2;
 #pragma unroll
-        for (int i = 0; i < PJ_NC / 2; ++i) wpx[i][0] = src[(long)i * 128], wpx[i][1] = src[(long)i * 128 + 1];
+        for (int i = 0; i < PJ_NC; ++i) wpx[i][0] = src[(long)i * 128], wpx[i][1] = src[(long)i * 128 + 1];
       } else {
         const f32x4* src = reinterpret_cast<const f32x4*>(P.pj_w) + ((long)q * 96 + 48 * half + wave * PJ_NC) * 64 + lane;
 #pragma unroll
@@ -1291,36 +1293,42 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (is_pj) {
+    if (X3P && is_pj && (pj & 1) < MT) {
+      // split-f16: job pj = (tile pj >> 1, batch rows 16 (pj & 1) .. + 15), the whole K, so ypart
+      // holds one copy (P1, the stop decision and the frame writes read it once)
+      const int mtb = pj & 1;
+      f32x4 y[PJ_NC][1][2];
+#pragma unroll
+      for (int i = 0; i < PJ_NC; ++i) {
+        const int ks = 6 * wave + i;
+        if (ks < 32) ld_x3_step<1>(y[i], hd_nxt + (long)mtb * 64 * 256, 64, ks, lane);
+        else ld_x3_step<1>(y[i], P.ctx + (long)mtb * 32 * 256, 32, ks - 32, lane);
+      }
+      f32x4 am = f32x4{0.f, 0.f, 0.f, 0.f}, ac = am;
+#pragma unroll
+      for (int i = 0; i < PJ_NC; ++i) {
+        h8 xh, xl;
+        split_x3_step(y[i][0], xh, xl);
+        mfma_x3(xh, xl, wpx[i][0], wpx[i][1], am, ac);
+      }
+      float* p = red0 + wave * 16 * 17;  // [wave][16 rows][17]
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[(4 * (lane >> 4) + j) * 17 + (lane & 15)] = x3_value(am[j], ac[j]);
+      lds_barrier();
+      if (tid < 256) {
+        const int mm = tid >> 4, n = tid & 15;
+        float v = red0[mm * 17 + n];
+#pragma unroll
+        for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * 17 + n];
+        stc(P.ypart + (long)(mtb * 16 + mm) * YP + (pj >> 1) * 16 + n, v);
+      }
+      lds_barrier();
+    } else if (!X3P && is_pj) {
       f32x4 acc2[MT];
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc2[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
       const int kb = 48 * (pj & 1) + wave * PJ_NC;  // K = [h_dec 1024 | ctx 512]
-      if constexpr (X3P) {
-        // k-step kb / 2 + i: 32 columns of one source (the h_dec / ctx boundary is k-step 32)
-        f32x4 y[PJ_NC / 2][MT][2];
-#pragma unroll
-        for (int i = 0; i < PJ_NC / 2; ++i) {
-          const int ks = kb / 2 + i;
-          if (ks < 32) ld_x3_step<MT>(y[i], hd_nxt, 64, ks, lane);
-          else ld_x3_step<MT>(y[i], P.ctx, 32, ks - 32, lane);
-        }
-        f32x4 am[MT], ac[MT];
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) am[mt] = ac[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-        for (int i = 0; i < PJ_NC / 2; ++i)
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            h8 xh, xl;
-            split_x3_step(y[i][mt], xh, xl);
-            mfma_x3(xh, xl, wpx[i][0], wpx[i][1], am[mt], ac[mt]);
-          }
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt)
-#pragma unroll
-          for (int j = 0; j < 4; ++j) acc2[mt][j] = x3_value(am[mt][j], ac[mt][j]);
-      } else {
+      {
         f32x4 y[PJ_NC][MT];
 #pragma unroll
         for (int i = 0; i < PJ_NC; ++i) {
