@@ -1,0 +1,26 @@
+"""Timeline of the last headline step in a rocprofv3 kernel trace: per-kernel start, gap to the
+previous kernel's end and duration, then span vs busy time.
+  python tools/step_gaps.py gpurun_out/prof/run_kernel_trace.csv [--all]"""
+import csv
+import sys
+
+rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+idx = [i for i, r in enumerate(rows) if "persist_decoder_kernel<2, 8>" in r["Kernel_Name"]]
+i0 = idx[-1]
+j = i0
+while "embed_gather" not in rows[j]["Kernel_Name"]:
+    j -= 1
+k = i0
+while k + 1 < len(rows) and "out_pqmf" not in rows[k]["Kernel_Name"]:
+    k += 1
+t0 = int(rows[j]["Start_Timestamp"])
+prev = t0
+busy = 0
+show = "--all" in sys.argv
+for r in rows[j:k + 1]:
+    s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+    busy += e - s
+    if show or s - prev > 2000 or e - s < 20000:
+        print(f"{(s - t0) / 1e3:9.1f} gap={(s - prev) / 1e3:7.1f} dur={(e - s) / 1e3:8.1f}  {r['Kernel_Name'][:70]}")
+    prev = max(prev, e)
+print(f"span {(prev - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, idle {(prev - t0 - busy) / 1e3:.1f} us")

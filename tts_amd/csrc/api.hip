@@ -2,6 +2,7 @@
 // graph-captured autoregressive decode loop, and the vocoder pipeline.
 #include "common.h"
 #include "decoder.h"
+#include "gsync.h"
 #include "split16.h"
 #include "../../include/ttship.h"
 
@@ -320,6 +321,13 @@ struct TacoModel {
   DevBuf spk_wT;
 };
 
+// Tacotron2 status words (TacoWS::stat on the device, tts_ctx::pinned on the host; one copy after
+// the call): BiLSTM barrier errors (2), persistent-decoder barrier errors (one per launch), the
+// decoder results (done, steps, status per decode row), the range flag, the launches' end steps
+constexpr int TS_ENC = 16, TS_DEC = 18, TS_RES = 20, TS_FLAG = TS_RES + 3 * BMAX, TS_END = TS_FLAG + 1,
+              TS_N = TS_END + 2;
+static_assert(TS_N <= 256, "status words fit the pinned block");
+
 struct TacoWS {
   int B = 0, T_max = 0, S_cap = 0, r = 0, MT = 0;
   long gen = 0;
@@ -328,7 +336,8 @@ struct TacoWS {
   DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, spart, alpha, acum, energy, ctl;
   DevBuf dec, align, stop, pa, pbb;
   DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
-  DevBuf ids, post, map;       // rows in decode order (longest first), output scatter map
+  DevBuf ids, post, map;       // rows in decode order (longest first); map = [perm | inverse]
+  DevBuf stat;                 // status words for the host, laid out as tts_ctx::pinned (TS_*)
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
   DevBuf spk, spkid, spkb;     // speaker vectors (decode order), per-row biases [Bp][NSPK]
   DevBuf win_idx, fwd_u, apf;  // windowing argmax, transition probability, forward chunk sums
@@ -445,8 +454,10 @@ struct tts_ctx {
   hipStream_t s = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_chunk[2] = {nullptr, nullptr};
   hipEvent_t ev_dec[3] = {nullptr, nullptr, nullptr};  // around the persistent decoder launches
-  int* pinned = nullptr;  // [256]: [0:4) chunk polling, [8:10) step index after each persistent launch,
-                          // [12] range flag, [16:20) barrier error words, [20:20+3*BMAX) decoder results
+  int* pinned = nullptr;  // [256]: [0:4) chunk polling, [12] range flag, [TS_*]: status words of the last
+                          // Tacotron2 call (one copy of TacoWS::stat)
+  bool flag_read = false; // the entry point already fetched the range flag into pinned[12]
+  int dec_end[2] = {0, 0};  // step index after each persistent launch of the last decode
   int dec_path = 0;       // last decode: 0 = step graphs, 1 = persistent kernel
   // GEMM arithmetic: true = split-f16 MFMA kernels where built (fp32-accurate, split16.h), false =
   // fp32 MFMA everywhere (tts_set_gemm_mode; TTS_GEMM=f32 in the environment starts a context so)
@@ -858,9 +869,10 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.pbb, (size_t)B * 512 * S_cap * r, g);
   grow<int64_t>(W.ids, (size_t)B * T_max, g);
   grow<float>(W.post, (size_t)B * S_cap * r * 80, g);
-  grow<int>(W.map, BMAX, g);
+  grow<int>(W.map, 2 * BMAX, g);
+  grow<int>(W.stat, 256, g);
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
-  grow<unsigned>(W.pbar, 512, g);
+  grow<unsigned>(W.pbar, 2 * 512, g);  // one barrier block per persistent launch (MT = 2, 1)
   grow<float>(W.spk, (size_t)64 * 1024, g);
   grow<int>(W.win_idx, 64, g);
   grow<float>(W.gh, 32 * 1024, g);
@@ -1176,6 +1188,44 @@ void gather_rows(const T* src, T* dst, const int* d_map, long row, int B, hipStr
   HIP_OK(hipGetLastError());
 }
 
+// Per-call host arguments as kernel arguments (one launch instead of three pageable uploads):
+// decode order and its inverse, lengths in decode order, and the decoder control block
+// [base, all_done, active_tiles, pad | done | steps | status | max_steps] (DecCtl + BMAX each)
+struct TacoSetup {
+  int B, MT;
+  int perm[BMAX], inv[BMAX], lens[BMAX], max_steps[BMAX];
+};
+__global__ void taco_setup_kernel(TacoSetup a, int* map, int* lens, int* ctl) {
+  for (int e = threadIdx.x; e < 4 + 4 * BMAX; e += blockDim.x) {
+    const int ms = e - 4 - 3 * BMAX;
+    ctl[e] = e == 2 ? a.MT : (ms >= 0 && ms < a.B ? a.max_steps[ms] : 0);
+  }
+  const int i = threadIdx.x;
+  if (i < a.B) {
+    map[i] = a.perm[i];
+    map[BMAX + i] = a.inv[i];
+    lens[i] = a.lens[i];
+  }
+}
+
+// decode-order mel lengths for the postnet (steps * r), from the decoder results on the device
+__global__ void taco_mlens_kernel(const int* ctl, int B, int r, int* mlens) {
+  const int i = threadIdx.x;
+  if (i < B) mlens[i] = ctl[4 + BMAX + i] * r;
+}
+
+// gather every status word the host checks after a Tacotron2 call into one block (TS_* layout)
+__global__ void taco_status_kernel(const unsigned* enc_bar, const unsigned* dec_bar, int ndec, const int* ctl,
+                                   const unsigned* flag, int* st) {
+  const int i = threadIdx.x;
+  if (i < 3 * BMAX) st[TS_RES + i] = ctl[4 + i];
+  if (i < 2) {
+    st[TS_ENC + i] = enc_bar ? (int)enc_bar[i * 512 + 16] : 0;
+    st[TS_DEC + i] = dec_bar && i < ndec ? (int)dec_bar[i * 512 + 16] : 0;
+  }
+  if (i == 0) st[TS_FLAG] = flag ? (int)*flag : 0;
+}
+
 // CHUNK-step graph for batch tile count MT (captured once per configuration)
 hipGraphExec_t step_graph(tts_ctx* c, int MT, hipStream_t s) {
   auto& W = c->tws;
@@ -1364,8 +1414,11 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   HIP_OK(hipEventRecord(c->ev_dec[0], s));
   c->dec_nlaunch = 0;
   for (int mt = W.MT; mt >= 1; --mt) {
+    const int li = W.MT - mt;  // launch index: its barrier block (armed in taco_infer's state fill)
+    a.bar = reinterpret_cast<unsigned*>(W.pbar.p) + 512 * li;
+    a.base_out = W.stat.i() + TS_END + li;
     a.D = make_dev(c, std::min(W.B, 16 * mt));
-    launch_persist_decoder(a, mt, s);
+    launch_persist_decoder(a, mt, s, false);
     if (tr) {  // only the first launch is traced
       HIP_OK(hipStreamSynchronize(s));
       std::vector<unsigned long long> h((size_t)8 * 24 * 256);
@@ -1379,7 +1432,6 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
       tr = nullptr;
     }
     const int i = c->dec_nlaunch++;
-    HIP_OK(hipMemcpyAsync(&c->pinned[8 + i], &reinterpret_cast<DecCtl*>(W.ctl.p)->base, 4, hipMemcpyDeviceToHost, s));
     HIP_OK(hipEventRecord(c->ev_dec[i + 1], s));
   }
 }
@@ -1414,17 +1466,23 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     return h_lens[x] > h_lens[y];
   });
   for (int i = 0; i < B; ++i) inv[perm[i]] = i;
+  // decode order, its inverse, lengths and the control block (base = 0, all_done = 0,
+  // active_tiles = MT, done/steps/status = 0, max_steps) in one launch, as kernel arguments
+  {
+    TacoSetup ta{};
+    ta.B = B;
+    ta.MT = W.MT;
+    for (int i = 0; i < B; ++i) {
+      ta.perm[i] = perm[i];
+      ta.inv[i] = inv[i];
+      ta.lens[i] = h_lens[perm[i]];
+      ta.max_steps[i] = h_max_steps[perm[i]];
+    }
+    taco_setup_kernel<<<1, 256, 0, s>>>(ta, W.map.i(), W.lens.i(), W.ctl.i());
+    HIP_OK(hipGetLastError());
+  }
   int* d_map = W.map.i();
-  HIP_OK(hipMemcpyAsync(d_map, perm.data(), B * 4, hipMemcpyHostToDevice, s));
   gather_rows<int64_t>(ids, reinterpret_cast<int64_t*>(W.ids.p), d_map, T_max, B, s);
-  // control block: base = 0, all_done = 0, active_tiles = MT, done/steps/status = 0, max_steps
-  std::vector<int> ctl(4 + 4 * BMAX, 0);
-  ctl[2] = W.MT;
-  for (int i = 0; i < B; ++i) ctl[4 + 3 * BMAX + i] = h_max_steps[perm[i]];
-  HIP_OK(hipMemcpyAsync(W.ctl.p, ctl.data(), ctl.size() * 4, hipMemcpyHostToDevice, s));
-  std::vector<int> lens(B);
-  for (int i = 0; i < B; ++i) lens[i] = h_lens[perm[i]];
-  HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
   W.thr = thr;
   // speaker vectors in decode order: external embeddings, or rows of the learned table
   TTS_CHECK(!M.variant() || use_persistent(c), "BN prenet / attention windowing / forward / Graves attention run on "
@@ -1462,6 +1520,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   }
   // decoder state
   const int Bp = W.MT * 16;
+  const bool persist = use_persistent(c);
   {
     FillList f;  // decoder state and outputs zeroed in one launch (the postnet output too)
     f.add(W.catt.p, (size_t)Bp * 1024 * 4);
@@ -1478,11 +1537,11 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     f.add(W.stop.p, (size_t)B * S_cap * 4);
     f.add(W.acnt.p, BMAX * sizeof(unsigned));
     f.add(W.post.p, (size_t)B * S_cap * r * 80 * 4);
+    if (persist) add_barrier_fills(f, reinterpret_cast<unsigned*>(W.pbar.p), W.MT);
     launch_fills(f, s);
   }
   bcast_rows_kernel<<<256, 256, 0, s>>>(M.att_bias.f(), 4096, W.gatt.f(), Bp);
   HIP_OK(hipGetLastError());
-  const bool persist = use_persistent(c);
   c->dec_path = persist ? 1 : 0;
   if (persist) {
     run_persistent(c, r, thr, s);
@@ -1520,45 +1579,46 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     }
   }
   }
-  // one host round trip after the decode: barrier error words and the per-row results
+  // postnet over each row's own frames: lengths from the decoder results on the device, grid sized
+  // by S_cap (tiles past a row's length exit at entry), so the decode needs no host round trip
+  taco_mlens_kernel<<<1, 64, 0, s>>>(W.ctl.i(), B, r, W.mlens.i());
+  HIP_OK(hipGetLastError());
+  const long fb = (long)S_cap * r * 80;  // W.post was zeroed with the decoder state
+  run_postnet(c, W.dec.f(), fb, W.mlens.i(), B, S_cap * r, S_cap * r, W.post.f(), fb, s);
+  // scatter back to the caller's row order: output row b <- decode row inv[b]
+  gather_rows<float>(W.post.f(), d_post, d_map + BMAX, fb, B, s);
+  gather_rows<float>(W.dec.f(), d_dec, d_map + BMAX, fb, B, s);
+  gather_rows<float>(W.align.f(), d_align, d_map + BMAX, (long)S_cap * T_max, B, s);
+  gather_rows<float>(W.stop.f(), d_stop, d_map + BMAX, S_cap, B, s);
+  // one host round trip per call: barrier error words, per-row results, range flag, launch steps
   {
-    int* pin = c->pinned;
-    pin[16] = pin[17] = pin[18] = 0;  // before the copies are enqueued
     const unsigned* lc = reinterpret_cast<const unsigned*>(W.lc.p);
-    if (W.enc_persist) {
-      HIP_OK(hipMemcpyAsync(&pin[16], lc + 16, 4, hipMemcpyDeviceToHost, s));
-      HIP_OK(hipMemcpyAsync(&pin[17], lc + 512 + 16, 4, hipMemcpyDeviceToHost, s));
-    }
-    if (persist) HIP_OK(hipMemcpyAsync(&pin[18], reinterpret_cast<unsigned*>(W.pbar.p) + 16, 4, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipMemcpyAsync(&pin[20], W.ctl.i() + 4, 3 * BMAX * 4, hipMemcpyDeviceToHost, s));
+    taco_status_kernel<<<1, 256, 0, s>>>(W.enc_persist ? lc : nullptr,
+                                         persist ? reinterpret_cast<const unsigned*>(W.pbar.p) : nullptr,
+                                         c->dec_nlaunch, W.ctl.i(), c->gemm_x3 ? x3_flag(c) : nullptr, W.stat.i());
+    HIP_OK(hipGetLastError());
+    int* pin = c->pinned;
+    HIP_OK(hipMemcpyAsync(pin + TS_ENC, W.stat.i() + TS_ENC, (TS_N - TS_ENC) * 4, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    TTS_CHECK(!W.enc_persist || (pin[16] == 0 && pin[17] == 0),
+    TTS_CHECK(!W.enc_persist || (pin[TS_ENC] == 0 && pin[TS_ENC + 1] == 0),
               "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past "
               "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
-    TTS_CHECK(!persist || pin[18] == 0,
+    TTS_CHECK(!persist || (pin[TS_DEC] == 0 && pin[TS_DEC + 1] == 0),
               "persistent decoder: grid barrier timed out (workgroups not co-resident) or preempted past "
               "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
+    if (c->gemm_x3) {  // with_x3_fallback reads the flag from here
+      pin[12] = pin[TS_FLAG];
+      c->flag_read = true;
+    }
+    for (int i = 0; i < 2; ++i) c->dec_end[i] = persist && i < c->dec_nlaunch ? pin[TS_END + i] : 0;
   }
-  std::vector<int> res(c->pinned + 20, c->pinned + 20 + 3 * BMAX);
-  int maxM = 0;
-  std::vector<int> mlens(B);
+  const int* res = c->pinned + TS_RES;
   for (int i = 0; i < B; ++i) {
     TTS_CHECK(res[i] == 1, "decoder did not finish an utterance (internal error)");
     const int b = perm[i];
     h_steps[b] = res[BMAX + i];
     h_status[b] = res[2 * BMAX + i];
-    mlens[i] = h_steps[b] * r;
-    maxM = std::max(maxM, mlens[i]);
   }
-  HIP_OK(hipMemcpyAsync(W.mlens.p, mlens.data(), B * 4, hipMemcpyHostToDevice, s));
-  const long fb = (long)S_cap * r * 80;  // W.post was zeroed with the decoder state
-  run_postnet(c, W.dec.f(), fb, W.mlens.i(), B, S_cap * r, maxM, W.post.f(), fb, s);
-  // scatter back to the caller's row order: output row b <- decode row inv[b]
-  HIP_OK(hipMemcpyAsync(d_map, inv.data(), B * 4, hipMemcpyHostToDevice, s));
-  gather_rows<float>(W.post.f(), d_post, d_map, fb, B, s);
-  gather_rows<float>(W.dec.f(), d_dec, d_map, fb, B, s);
-  gather_rows<float>(W.align.f(), d_align, d_map, (long)S_cap * T_max, B, s);
-  gather_rows<float>(W.stop.f(), d_stop, d_map, S_cap, B, s);
   leave(c, stream);
   c->last_B = B;
   c->last_T = T_max;
@@ -1841,9 +1901,13 @@ void with_x3_fallback(tts_ctx* c, F&& fn) {
   }
   unsigned* flag = x3_flag(c);
   HIP_OK(hipMemsetAsync(flag, 0, 4, c->s));
+  c->flag_read = false;
   fn();
-  HIP_OK(hipMemcpyAsync(&c->pinned[12], flag, 4, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipStreamSynchronize(c->s));
+  if (!c->flag_read) {  // fn may have fetched it with its own status words (taco_infer)
+    HIP_OK(hipMemcpyAsync(&c->pinned[12], flag, 4, hipMemcpyDeviceToHost, c->s));
+    HIP_OK(hipStreamSynchronize(c->s));
+  }
+  c->flag_read = false;
   if (c->pinned[12]) {
     c->x3_fallbacks++;
     c->gemm_x3 = false;
@@ -2973,8 +3037,8 @@ int tts_decoder_stats(tts_ctx* c, int* path, int* nlaunch, float* ms, int* steps
     int prev = 0;
     for (int i = 0; i < *nlaunch; ++i) {
       HIP_OK(hipEventElapsedTime(&ms[i], c->ev_dec[i], c->ev_dec[i + 1]));
-      steps[i] = c->pinned[8 + i] - prev;
-      prev = c->pinned[8 + i];
+      steps[i] = c->dec_end[i] - prev;
+      prev = c->dec_end[i];
     }
   });
 }

@@ -170,6 +170,7 @@ struct PArgs {
   float thr;
   unsigned* bar;  // barrier words (zeroed before each launch): [0] global, [32] go, [64 + 32x] XCD x,
                   // [16] error
+  int* base_out;  // optional: the step index at exit (launch statistics, read back with the status words)
   unsigned long long* trace;   // optional phase timestamps [8 steps][10][256] (TTS_PTRACE)
   unsigned long long* atrace;  // optional attention-item timestamps [8 steps][256][8]
   int trace_t0;
@@ -178,7 +179,8 @@ struct PArgs {
 
 bool persist_supported(int device);
 int persist_attn_tc();  // attention positions per work item (sizes the chunk-partial buffers)
-void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s);
+// arm: zero the barrier block first (false: the caller armed it, e.g. in its state fill)
+void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm = true);
 
 void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s);
 // prenet layer 1 + layer 2 in one launch (16 workgroups) plus the stop workgroup

@@ -1040,7 +1040,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       const int all_done = ldci(&D.ctl->all_done), act = ldci(&D.ctl->active_tiles);
       if (all_done || act < MT || t > D.S_cap + 1) {
         write_frames(t - 1, 0, PW);
-        if (g == 0 && tid == 0) D.ctl->base = t;
+        if (g == 0 && tid == 0) {
+          D.ctl->base = t;
+          if (P.base_out) *P.base_out = t;
+        }
         return;
       }
     }
@@ -1375,7 +1378,7 @@ bool persist_supported(int device) {
 
 int persist_attn_tc() { return PTC; }
 
-void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
+void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
   TTS_CHECK(MT == 1 || MT == 2, "persistent decoder: MT must be 1 or 2");
   TTS_CHECK(PJ_WG0 + a.ntj * 2 <= PW && a.ntj >= 17, "persistent decoder: projection job count");
   TTS_CHECK(a.D.B <= 64 && NATT * 4 * 4 == 1024, "persistent decoder: attention_rnn layout");
@@ -1400,7 +1403,7 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s) {
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
     attr[MT - 1][var] = true;
   }
-  arm_barrier(a.bar, 1, s);
+  if (arm) arm_barrier(a.bar, 1, s);
   PArgs copy = a;
   void* kargs[] = {&copy};
   launch_resident(f, dim3(PW), dim3(PT), kargs, P_LDS, s);

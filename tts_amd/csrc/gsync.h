@@ -19,20 +19,25 @@
 
 constexpr int BAR_TMO = 48;  // word of the barrier block holding the wait limit (s_memrealtime ticks)
 
-// zero `nblk` 512-word barrier blocks and write their wait limit (stream-ordered before the launch)
-inline void arm_barrier(unsigned* bar, int nblk, hipStream_t s) {
+// entries zeroing `nblk` 512-word barrier blocks and writing their wait limit, for a caller's fill
+inline void add_barrier_fills(FillList& f, unsigned* bar, int nblk) {
   static const unsigned ticks = [] {
     double ms = 2000.0;
     if (const char* e = std::getenv("TTS_BARRIER_TIMEOUT_MS")) ms = std::atof(e);
     ms = ms < 1.0 ? 1.0 : (ms > 40000.0 ? 40000.0 : ms);
     return (unsigned)(ms * 1e5);  // 100 MHz ticks
   }();
-  FillList f;
   for (int i = 0; i < nblk; ++i) {
     f.add(bar + i * 512, BAR_TMO * 4);
     f.add(bar + i * 512 + BAR_TMO, 4, ticks);
     f.add(bar + i * 512 + BAR_TMO + 1, (512 - BAR_TMO - 1) * 4);
   }
+}
+
+// zero `nblk` 512-word barrier blocks and write their wait limit (stream-ordered before the launch)
+inline void arm_barrier(unsigned* bar, int nblk, hipStream_t s) {
+  FillList f;
+  add_barrier_fills(f, bar, nblk);
   launch_fills(f, s);
 }
 
