@@ -134,7 +134,7 @@ def main():
         if record:
             ev[1].record()
         mel_lens = taco.last_mel_lengths
-        wav = voc.inference(post.transpose(1, 2).contiguous(), lengths=mel_lens)
+        wav = voc.inference(post.transpose(1, 2), lengths=mel_lens)  # read in place (tts_melgan_infer_strided)
         if record:
             ev[2].record()
             torch.cuda.synchronize()

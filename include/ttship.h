@@ -16,6 +16,7 @@
  *   tts_melgan_set_tensor/finalize<- MultibandMelganGenerator.load_state_dict + remove_weight_norm
  *                                    (TTS/server/synthesizer.py:81-91, melgan_generator.py:91-97)
  *   tts_melgan_infer              <- MultibandMelganGenerator.inference (multiband_melgan_generator.py:32-39)
+ *   tts_melgan_infer_strided      <- the same on a (B, M, C) tensor viewed as (B, C, M) (no transposed copy)
  *   tts_melgan_generator          <- MelganGenerator.layers(c) (melgan_generator.py:28-81)
  *   tts_pqmf_synthesis            <- PQMF.synthesis (TTS/vocoder/layers/pqmf.py:51-56)
  *
@@ -113,6 +114,12 @@ int tts_melgan_finalize(tts_ctx* ctx, int in_channels, int out_channels, int bas
    samples past hop*(h_lens[b] + 2*pad) are zero. */
 int tts_melgan_infer(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
                      float* d_wav, void* stream);
+/* the same with d_mel given by element strides (batch, channel, frame), e.g. a Tacotron2 postnet
+   output (B, M, in_channels) read in place as (B, in_channels, M): strides (M*in_channels, 1,
+   in_channels), no transposed copy. Channel stride 1 needs a frame stride divisible by 4 and a
+   16-byte aligned d_mel. */
+int tts_melgan_infer_strided(tts_ctx* ctx, const float* d_mel, int64_t stride_b, int64_t stride_c, int64_t stride_t,
+                             const int32_t* h_lens, int B, int M_max, int pad, float* d_wav, void* stream);
 
 /* generator layers only: d_out (B, out_channels, up*(M_max + 2*pad)), up = prod(upsample_factors) */
 int tts_melgan_generator(tts_ctx* ctx, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,

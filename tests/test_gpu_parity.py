@@ -162,6 +162,35 @@ def test_mbmelgan_f16_range_fallback_reruns_in_fp32(melgan):
     assert np.array_equal(w16, w32)
 
 
+@pytest.mark.parametrize("mode", ["x3", "f32"])
+def test_mbmelgan_frame_major_view_equals_contiguous(melgan, mode):
+    """A (B, M, 80) postnet-style tensor passed as its (B, 80, M) transposed view is read in place
+    (tts_melgan_infer_strided, no copy): bit-identical to the contiguous call on both GEMM paths,
+    replicate padding included, and within WAV_TOL of the oracle."""
+    fx, cfg, sd, v = melgan
+    orc = melgan_oracle(cfg, sd)
+    rs = np.random.RandomState(11)
+    lens = [37, 6, 21]
+    fm = np.zeros((3, max(lens), 80), np.float32)  # frame-major
+    for i, L in enumerate(lens):
+        fm[i, :L] = rs.normal(0, 1.5, (L, 80))
+    view = torch.from_numpy(fm).cuda().transpose(1, 2)
+    assert not view.is_contiguous()
+    eng = _gemm(mode)
+    try:
+        for pad in (0, 2):
+            v.inference_padding = pad
+            w_view = v.inference(view, lengths=lens).cpu().numpy()
+            w_cont = v.inference(view.contiguous(), lengths=lens).cpu().numpy()
+            assert np.array_equal(w_view, w_cont)
+            for i, L in enumerate(lens):
+                ref = orc.inference(np.ascontiguousarray(fm[i, :L].T), pad=pad)[0]
+                assert np.abs(w_view[i, 0, :len(ref)] - ref).max() <= WAV_TOL
+    finally:
+        _gemm("x3")
+        v.inference_padding = 0
+
+
 def test_mbmelgan_too_short_raises(melgan):
     fx, cfg, sd, v = melgan
     v.inference_padding = 0

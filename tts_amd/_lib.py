@@ -46,6 +46,8 @@ SIGNATURES = [
     ("tts_melgan_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int]),
     ("tts_melgan_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    ("tts_melgan_infer_strided", ctypes.c_int, [_vp, _vp, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, _c_int_p,
+                                                ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_melgan_generator", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp,
                                             _vp]),
     ("tts_pqmf_synthesis", ctypes.c_int, [_vp, _vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _vp, ctypes.c_int,
@@ -231,9 +233,16 @@ class Engine:
         _check(self.lib.tts_ge2e_infer(self.h, _ptr(x), lens_p, B, T, _ptr(out), _stream(x.device)))
 
     def melgan_infer(self, mel, lens, pad, wav):
+        """mel (B, C, M): contiguous, or any strided view the library reads in place (e.g. a
+        (B, M, C) postnet output transposed)."""
         B, _, M = mel.shape
         lens_a, lens_p = _i32(lens)
-        _check(self.lib.tts_melgan_infer(self.h, _ptr(mel), lens_p, B, M, pad, _ptr(wav), _stream(mel.device)))
+        if mel.is_contiguous():
+            _check(self.lib.tts_melgan_infer(self.h, _ptr(mel), lens_p, B, M, pad, _ptr(wav), _stream(mel.device)))
+        else:
+            sb, sc, st = mel.stride()
+            _check(self.lib.tts_melgan_infer_strided(self.h, _ptr(mel), sb, sc, st, lens_p, B, M, pad, _ptr(wav),
+                                                     _stream(mel.device)))
 
     def melgan_generator(self, mel, lens, pad, out):
         B, _, M = mel.shape

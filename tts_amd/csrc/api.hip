@@ -1762,7 +1762,7 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
 
 // returns total upsampling factor; writes bands (B, out_ch, up*(M_max+2pad)) into `out`
 int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int M_max, int pad, float* out,
-                  hipStream_t s, GenTail* tail = nullptr) {
+                  hipStream_t s, GenTail* tail = nullptr, const int64_t* mel_strides = nullptr) {
   auto& G = c->mg;
   auto& W = c->mws;
   TTS_CHECK(G.ready, "melgan weights not finalized");
@@ -1794,7 +1794,15 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   cc.oflow = x3_flag(c);
   cc.len_add = 2 * pad;
   // layers[0..1]: replicate pad (inference_padding) + ReflectionPad1d(3) + Conv1d(k7)
-  cc.s[0] = src_of(mel, (long)G.in_ch * M_max, M_max, 1, G.in_ch, 0);
+  if (mel_strides) {
+    TTS_CHECK(mel_strides[1] >= 1 && mel_strides[2] >= 1 && mel_strides[1] < (1L << 31) && mel_strides[2] < (1L << 31),
+              "mel strides must be positive");
+    TTS_CHECK(mel_strides[1] != 1 || (mel_strides[2] % 4 == 0 && (reinterpret_cast<uintptr_t>(mel) & 15) == 0),
+              "channel stride 1 needs a frame stride divisible by 4 and a 16-byte aligned mel");
+    cc.s[0] = src_of(mel, (long)mel_strides[0], (int)mel_strides[1], (int)mel_strides[2], G.in_ch, 0);
+  } else {
+    cc.s[0] = src_of(mel, (long)G.in_ch * M_max, M_max, 1, G.in_ch, 0);
+  }
   cc.pad_mode = 1;
   cc.rep_pad = pad;
   cc.in_mul = cc.q_mul = 1;
@@ -2964,8 +2972,8 @@ int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, 
   });
 }
 
-int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
-                     float* d_wav, void* stream) {
+static int melgan_infer_impl(tts_ctx* c, const float* d_mel, const int64_t* mel_strides, const int32_t* h_lens, int B,
+                      int M_max, int pad, float* d_wav, void* stream) {
   return guarded_ctx(c, [&] {
     TTS_CHECK(c && d_mel && h_lens && d_wav, "null argument");
     TTS_CHECK(pad >= 0, "pad >= 0");
@@ -2981,20 +2989,31 @@ int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int 
       const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
       if (fused) {
         GenTail t;
-        run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t);
+        run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t, mel_strides);
         TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
         TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
                                   G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
                   "fused output/PQMF shape not covered");
       } else {
         c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
-        run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s);
+        run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s, nullptr, mel_strides);
         launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
                               2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
       }
     });
     leave(c, stream);
   });
+}
+
+int tts_melgan_infer(tts_ctx* c, const float* d_mel, const int32_t* h_lens, int B, int M_max, int pad,
+                     float* d_wav, void* stream) {
+  return melgan_infer_impl(c, d_mel, nullptr, h_lens, B, M_max, pad, d_wav, stream);
+}
+
+int tts_melgan_infer_strided(tts_ctx* c, const float* d_mel, int64_t stride_b, int64_t stride_c, int64_t stride_t,
+                             const int32_t* h_lens, int B, int M_max, int pad, float* d_wav, void* stream) {
+  const int64_t st[3] = {stride_b, stride_c, stride_t};
+  return melgan_infer_impl(c, d_mel, st, h_lens, B, M_max, pad, d_wav, stream);
 }
 
 int tts_pqmf_synthesis(tts_ctx* c, const float* d_x, int B, int N, int L, const float* d_G, int taps, float* d_y,

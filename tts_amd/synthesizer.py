@@ -112,7 +112,7 @@ class Synthesizer:
                                                          speaker_ids=spk)
                 mel_lens = [int(m) for m in self.tts_model.last_mel_lengths]
             if self.vocoder_model is not None:
-                wav = self.vocoder_model.inference(post.transpose(1, 2).contiguous(), lengths=mel_lens)
+                wav = self.vocoder_model.inference(post.transpose(1, 2), lengths=mel_lens)
                 hop = wav.shape[-1] // post.shape[1]
                 wav = wav.reshape(len(seqs), -1).cpu().numpy()
                 return [wav[i, :mel_lens[i] * hop] for i in range(len(seqs))]

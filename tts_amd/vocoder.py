@@ -114,14 +114,19 @@ class MelganGenerator(nn.Module):
                             self.cfg.upsample_factors, self.cfg.num_res_blocks, self._use_pqmf)
             eng.melgan_key = key
 
-    def _prep(self, c, lengths):
+    def _prep(self, c, lengths, frame_major_ok=False):
         dev = self.layers._modules["1"].bias.device
         eng = get_engine(dev)
         c = torch.as_tensor(c).to(dev, torch.float32)
         if c.dim() == 2:
             c = c[None]
-        c = c.contiguous()
+        # frame_major_ok: a (B, M, C) tensor viewed as (B, C, M) (e.g. postnet_out.transpose(1, 2)) is
+        # read in place by tts_melgan_infer_strided instead of being copied
         B, C, M = c.shape
+        frame_major = (frame_major_ok and c.stride(1) == 1 and c.stride(2) == C and c.stride(0) == M * C
+                       and C % 4 == 0 and c.data_ptr() % 16 == 0)
+        if not frame_major:
+            c = c.contiguous()
         if C != self.cfg.in_channels:
             raise ValueError(f"expected {self.cfg.in_channels} mel channels, got {C}")
         lens = np.full(B, M, np.int64) if lengths is None else np.asarray(torch.as_tensor(lengths).cpu(), np.int64)
@@ -167,7 +172,7 @@ class MultibandMelganGenerator(MelganGenerator):
 
     @torch.no_grad()
     def inference(self, cond_features, lengths: Optional[Sequence[int]] = None):
-        eng, c, lens, pad = self._prep(cond_features, lengths)
+        eng, c, lens, pad = self._prep(cond_features, lengths, frame_major_ok=True)
         B, _, M = c.shape
         wav = torch.empty(B, 1, self.hop * (M + 2 * pad), device=c.device)
         with eng.lock:
