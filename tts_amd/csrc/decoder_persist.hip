@@ -47,6 +47,11 @@ constexpr int PTC = 32;      // attention positions per work item
 constexpr int IW0 = NATT;    // attention items live on workgroups IW0 .. PW-1 (round-robin)
 constexpr int YROWS = 64;    // rows per projection half (independent of the batch tile: the MT = 1
                              // launch reads what the MT = 2 launch left)
+// encoder rows (of 8 per thread) an attention item keeps in registers across steps: 4 where the
+// kernel stays within 256 VGPRs without spills (split-f16 variants without forward attention), 0
+// elsewhere; pec_arr sizes the (unused) array of the latter
+constexpr int pec_of(int VAR) { return ((VAR & 8) && !(VAR & 2)) ? 4 : 0; }
+constexpr int pec_arr(int VAR) { return pec_of(VAR) > 0 ? pec_of(VAR) : 1; }
 constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = NATT;  // NPQ_: query-projection partials
 }  // namespace
 
@@ -174,7 +179,9 @@ __device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* A
 
 template <int MT, int VAR>
 __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
-                                           int* is_last, float (&L)[8], bool haveL) {
+                                           int* is_last, float (&L)[8], bool haveL,
+                                           f32x4 (&evc)[pec_arr(VAR)], bool load_ev) {
+  constexpr int PEC = pec_of(VAR);
   constexpr bool WIN = VAR & 1, FWD = (VAR & 2) != 0;  // compiled-in decoder variants
   constexpr int NT = PT, TC = PTC;
   constexpr int NPT = NPQ_ / 16;  // query partials per thread (16 groups)
@@ -215,16 +222,30 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   }
   lds_barrier();
   ATRACE(1);
-  // encoder rows for the partial context (row offsets in SGPRs, one buffer load each), issued
-  // once the first batch of loads has drained; consumed after the energies
-  float ev[TC];
+  // encoder rows for the partial context, consumed after the energies: thread (eg = tid / 128,
+  // cq = tid % 128) holds channels 4 cq .. 4 cq + 3 of positions 8 eg .. 8 eg + 7, one 16-byte
+  // buffer load each (row offsets in SGPRs: eg is wave-uniform). The encoder output is constant
+  // over the decode, so a workgroup's first item keeps its first PEC rows in registers for the
+  // whole launch (loaded on its first step; all 8 would push the kernel past 256 VGPRs); the rest
+  // load every step, once the first batch of loads has drained
+  constexpr int EPG = TC / 4;  // positions per thread group
+  const int eg = tid >> 7, cq = tid & 127;
+  f32x4 ev4[EPG];
   {
     const __amdgpu_buffer_rsrc_t er =
         __builtin_amdgcn_make_buffer_rsrc((void*)(P.enc + (long)b * D.T_max * 512), 0, 0x7fffffff, 0x00020000);
+    auto ld = [&](int i) {
+      return __builtin_bit_cast(f32x4, __builtin_amdgcn_raw_buffer_load_b128(
+          er, cq * 16, __builtin_amdgcn_readfirstlane(min(t0 + EPG * eg + i, Tm1) * 2048), 0));
+    };
+    if (load_ev) {
 #pragma unroll
-    for (int i = 0; i < TC; ++i)
-      ev[i] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(
-          er, tid * 4, __builtin_amdgcn_readfirstlane(min(t0 + i, Tm1) * 2048), 0));
+      for (int i = 0; i < PEC; ++i) evc[i] = ld(i);
+    }
+#pragma unroll
+    for (int i = PEC; i < EPG; ++i) ev4[i] = ld(i);
+#pragma unroll
+    for (int i = 0; i < PEC; ++i) ev4[i] = evc[i];
   }
   float pqa = red[a];
 #pragma unroll
@@ -297,12 +318,26 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   }
   lds_barrier();
   const float* wsel = (FWD && P.fwd) ? swf : sw;
-  float S_c = 0.f, F_c = 0.f, u = 0.f;
+  float S_c = 0.f, F_c = 0.f;
 #pragma unroll
   for (int i = 0; i < TC; ++i) {
     S_c += sw[i];
     F_c += swf[i];
-    u = fmaf(wsel[i], ev[i], u);
+  }
+  // partial context: 4 channels x 8 positions per thread, then the 4 position groups summed
+  // through LDS (the query-partial scratch `red`, [4][512], is free since the energies)
+  float u;
+  {
+    f32x4 u4 = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int i = 0; i < EPG; ++i) {
+      const float wv = wsel[EPG * eg + i];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) u4[j] = fmaf(wv, ev4[i][j], u4[j]);
+    }
+    *reinterpret_cast<f32x4*>(&red[eg * 512 + 4 * cq]) = u4;
+    lds_barrier();
+    u = (red[tid] + red[512 + tid]) + (red[1024 + tid] + red[1536 + tid]);
   }
   stc(P.part_u + pidx * 512 + tid, u);
   if (tid == 0) {
@@ -866,6 +901,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 
   unsigned gen = 0;
   float Lr[8];  // location features of the first attention item (attn_loc in P1, used in P4)
+  f32x4 evc[pec_arr(VAR)];  // encoder rows of the first attention item (loaded on its first step)
   const int t_first = D.ctl->base;
   int t = t_first;
   const int pj_jobs = 2 * P.ntj;
@@ -1216,7 +1252,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         const int nitems = D.B * P.nchmax;
         for (int it = g - IW0; it < nitems; it += PW - IW0) {
           if constexpr (GRAVES) graves_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, &is_last);
-          else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0);
+          else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0,
+                                   evc, nitems > PW - IW0 || t == t_first);
           lds_barrier();
         }
         // split-f16: the h_att part runs at the start of P5 instead (h_att is still in place), off
