@@ -91,7 +91,9 @@ __device__ __forceinline__ float sigm(float x) { return 1.f / (1.f + expf(-x)); 
 // sum over the 16 lanes of a DPP row (every lane of the row gets the row sum)
 __device__ __forceinline__ float row16_sum(float v) {
   auto dpp = [](float x, auto ctrl) {
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(x), decltype(ctrl)::value, 0xf, 0xf, false));
+    // every lane of every row is enabled and these patterns never read outside the row, so the
+    // old value is never used: mov_dpp (bound_ctrl) needs no zero-initialised destination
+    return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(x), decltype(ctrl)::value, 0xf, 0xf, true));
   };
   v += dpp(v, std::integral_constant<int, 0xB1>{});   // quad_perm(1,0,3,2)
   v += dpp(v, std::integral_constant<int, 0x4E>{});   // quad_perm(2,3,0,1)
