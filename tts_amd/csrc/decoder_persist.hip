@@ -320,11 +320,12 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   }
   lds_barrier();
   const float* wsel = (FWD && P.fwd) ? swf : sw;
+  // chunk sums of the weights: only thread 0 publishes them, so wave 0 alone sums them (one
+  // position per lane and a wave reduction instead of a 32-term loop in every thread)
   float S_c = 0.f, F_c = 0.f;
-#pragma unroll
-  for (int i = 0; i < TC; ++i) {
-    S_c += sw[i];
-    F_c += swf[i];
+  if (wave == 0) {
+    S_c = wave64_sum(lane < TC ? sw[lane] : 0.f);
+    if ((FWD && P.fwd)) F_c = wave64_sum(lane < TC ? swf[lane] : 0.f);
   }
   // partial context: 4 channels x 8 positions per thread, then the 4 position groups summed
   // through LDS (the query-partial scratch `red`, [4][512], is free since the energies)
