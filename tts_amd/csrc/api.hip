@@ -1795,7 +1795,8 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   cc.len_add = 2 * pad;
   // layers[0..1]: replicate pad (inference_padding) + ReflectionPad1d(3) + Conv1d(k7)
   if (mel_strides) {
-    TTS_CHECK(mel_strides[1] >= 1 && mel_strides[2] >= 1 && mel_strides[1] < (1L << 31) && mel_strides[2] < (1L << 31),
+    TTS_CHECK(mel_strides[1] >= 1 && mel_strides[2] >= 1 && mel_strides[1] < (1L << 31) && mel_strides[2] < (1L << 31) &&
+                  (mel_strides[0] >= 1 || B == 1) && mel_strides[0] >= 0,
               "mel strides must be positive");
     TTS_CHECK(mel_strides[1] != 1 || (mel_strides[2] % 4 == 0 && (reinterpret_cast<uintptr_t>(mel) & 15) == 0),
               "channel stride 1 needs a frame stride divisible by 4 and a 16-byte aligned mel");
