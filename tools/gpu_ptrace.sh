@@ -1,3 +1,6 @@
+#!/bin/bash
+# GPU tests, one bench line without the CPU baseline, and the persistent decoder phase trace
+# (TTS_PTRACE, tools/ptrace.py) of one bench step.
 set -o pipefail
 mkdir -p gpurun_out
 timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?; tail -2 gpurun_out/t.log; [ $rc = 0 ] || exit $rc
