@@ -191,6 +191,45 @@ def test_mbmelgan_frame_major_view_equals_contiguous(melgan, mode):
         v.inference_padding = 0
 
 
+@pytest.mark.parametrize("mode", ["x3", "f32"])
+def test_fullband_melgan_generator_vs_oracle(mode):
+    """MelganGenerator as setup_generator builds the reference's "melgan_generator" (base 512,
+    upsampling 8x8x2x2, 3 residual blocks: ResidualStacks at C = 256 / 128 / 64 / 32, the split-f16
+    block kernel's R = 4 / 4 / 2 / 1 weight rings) against the numpy oracle on a ragged batch, on
+    both GEMM paths; samples past each utterance's length are zero."""
+    from tts_amd import MelganGenerator
+    from tts_amd.spec import MelganConfig
+    _dev()
+    cfg, sd = melgan_state_dict(7, MelganConfig(out_channels=1, base_channels=512, upsample_factors=(8, 8, 2, 2),
+                                                num_res_blocks=3, pqmf=False))
+    v = MelganGenerator(in_channels=80, out_channels=1, base_channels=512, upsample_factors=(8, 8, 2, 2),
+                        num_res_blocks=3)
+    full = v.state_dict()
+    full.update({k: torch.from_numpy(t) for k, t in sd.items()})
+    v.load_state_dict(full)
+    v.remove_weight_norm()
+    v = v.cuda().eval()
+    v.inference_padding = 0
+    orc = melgan_oracle(cfg, sd)
+    rs = np.random.RandomState(4)
+    lens = [13, 5, 9]
+    batch = np.zeros((3, 80, max(lens)), np.float32)
+    for i, L in enumerate(lens):
+        batch[i, :, :L] = rs.normal(0, 1.5, (80, L))
+    eng = _gemm(mode)
+    try:
+        n0 = eng.gemm_mode()[1]
+        wav = v.inference(torch.from_numpy(batch).cuda(), lengths=lens).cpu().numpy()
+        assert eng.gemm_mode() == (mode, n0)  # no range fallback on this input
+    finally:
+        _gemm("x3")
+    for i, L in enumerate(lens):
+        ref = orc.generator(batch[i, :, :L])
+        assert wav[i, 0, :ref.shape[1]].shape == ref[0].shape
+        assert np.abs(wav[i, 0, :ref.shape[1]] - ref[0]).max() <= WAV_TOL
+        assert not wav[i, 0, ref.shape[1]:].any()
+
+
 def test_mbmelgan_too_short_raises(melgan):
     fx, cfg, sd, v = melgan
     v.inference_padding = 0

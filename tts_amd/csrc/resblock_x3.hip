@@ -38,7 +38,7 @@ struct RbTile {
   int b, q0, L;
 };
 
-template <int C, int TQ, int WM, int WN>
+template <int C, int TQ, int WM, int WN, int R>
 __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, int ntiles) {
   constexpr int NTHR = 64 * WM * WN;
   constexpr int MI = C / 16 / WM;
@@ -48,7 +48,10 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   constexpr int NK1 = 3 * NCH;           // phase-1 k-steps: (chunk, tap)
   constexpr int NK2 = 2 * C / 32;        // phase-2 k-steps
   constexpr int NTOT = NK1 + NK2;        // weight sequence of one tile (the ring runs on across tiles)
-  static_assert(NK2 * 32 == 2 * C && NK2 % 3 == 0, "phase-2 k-steps: multiple of the 3-slot ring");
+  // R-slot weight ring: k-step s of a tile's sequence uses slot s % R, so R must divide both
+  // phases' lengths for the slots to line up across phases and tiles (C = 192 / 96 / 48: R = 3;
+  // C = 256 / 128: 4; C = 64 / 32: 2 / 1)
+  static_assert(NK2 * 32 == 2 * C && NK1 % R == 0 && NK2 % R == 0, "weight ring: R must divide both phases");
   constexpr int HR = 4 * C + 16;         // HX row, halves: 2C hi | 2C lo | 16 pad (8C + 32 bytes)
   constexpr int SPT = (4 * (TQ + 2 * X3_DMAX) + NTHR - 1) / NTHR;  // staging items (8 channels x 1 pos) per thread
   extern __shared__ __attribute__((aligned(16))) _Float16 sh[];
@@ -161,7 +164,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   // buffer loads: the lane's 32 bytes are a VGPR offset, the (m-tile, k-step) block an SGPR one
   const __amdgpu_buffer_rsrc_t wdr = rsrc(a.Wd16), wfr = rsrc(a.Wf16);
   const int wlo = lane * 32;
-  h8 ring[3][MI][2];
+  h8 ring[R][MI][2];
   auto wload = [&](h8 (&r)[MI][2], int seq) {
     if (seq >= NTOT) seq -= NTOT;
     const bool p1 = seq < NK1;
@@ -183,7 +186,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   RbTile cur = tile_of(t);
   stage_load(cur, st[0], 0);
 #pragma unroll
-  for (int u = 0; u < 3; ++u) wload(ring[u], u);
+  for (int u = 0; u < R; ++u) wload(ring[u], u);
   if (NCH > 1) stage_load(cur, st[1], 1);
   stage_store(X0, st[0], 0);
   if (NCH > 2) stage_load(cur, st[0], 2);
@@ -229,6 +232,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
       const _Float16* X = (ch & 1) ? X1 : X0;
 #pragma unroll
       for (int kq = 0; kq < 3; ++kq) {
+        const int sl = (ch * 3 + kq) % R;  // compile-time after unrolling
         h8 bh[NI], bl[NI];
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
@@ -240,8 +244,8 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[kq][mi][0], ring[kq][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-        wload(ring[kq], (ch + 1) * 3 + kq);
+          for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[sl][mi][0], ring[sl][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
+        wload(ring[sl], ch * 3 + kq + R);
         __builtin_amdgcn_sched_barrier(0);
       }
       if (ch + 1 < NCH) stage_store((ch & 1) ? X0 : X1, st[(ch + 1) & 1], ch + 1);
@@ -279,10 +283,11 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     }
     RB_STAMP(2);
     // ---------------- phase 2: y = [W1 | Wsc] . [lrelu(h); x] ----------------
-    for (int k0 = 0; k0 < NK2; k0 += 3) {
 #pragma unroll
-      for (int u = 0; u < 3; ++u) {
-        const int kc = k0 + u;
+    for (int k0 = 0; k0 < NK2; k0 += R) {
+#pragma unroll
+      for (int u = 0; u < R; ++u) {
+        const int kc = k0 + u;  // slot (NK1 + kc) % R == u since R divides NK1
         h8 bh[NI], bl[NI];
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
@@ -295,7 +300,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[u][mi][0], ring[u][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-        wload(ring[u], NK1 + kc + 3);  // past NK2: the next tile's phase-1 weights
+        wload(ring[u], NK1 + kc + R);  // past NK2: the next tile's phase-1 weights
       }
     }
     RB_STAMP(3);
@@ -333,13 +338,13 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 // one resident workgroup per CU (the LDS tile allows no more), each looping over tiles; the
 // dynamic LDS leaves 1 KiB of the CU's 160 KiB for the kernel's static tile tables
 constexpr int RB_DYN_LDS = 159 * 1024;
-template <int C, int TQ, int WM, int WN>
+template <int C, int TQ, int WM, int WN, int R>
 static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   const int ROWS = TQ + 2 * a.dil;
   const size_t lds = ((size_t)2 * ROWS * XR + (size_t)TQ * (4 * C + 16)) * 2;
   static int ncu = 0;
   if (!ncu) {
-    HIP_OK(hipFuncSetAttribute((const void*)resblock_x3_kernel<C, TQ, WM, WN>,
+    HIP_OK(hipFuncSetAttribute((const void*)resblock_x3_kernel<C, TQ, WM, WN, R>,
                                hipFuncAttributeMaxDynamicSharedMemorySize, RB_DYN_LDS));
     int dev = 0;
     HIP_OK(hipGetDevice(&dev));
@@ -351,10 +356,10 @@ static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   TTS_CHECK(ntiles < (1L << 30), "resblock_x3: too many tiles");
   if (ntiles == 0) return;
   const int grid = (int)std::min<long>(ntiles, ncu);
-  resblock_x3_kernel<C, TQ, WM, WN><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles);
+  resblock_x3_kernel<C, TQ, WM, WN, R><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles);
 }
 
-bool resblock_x3_supported(int C) { return C == 192 || C == 96 || C == 48; }
+bool resblock_x3_supported(int C) { return C == 256 || C == 192 || C == 128 || C == 96 || C == 64 || C == 48 || C == 32; }
 
 // host packing of one block's split weights: Wd (C, C, 3) [co][ci][k] and Wf (C, 2C) [co][k]
 void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf, int C,
@@ -374,9 +379,14 @@ void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t 
   if (a.max_q <= 0 || a.B <= 0) return;
   switch (C) {
     // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave
-    case 192: launch_rbx3<192, 64, 12, 1>(a, h_lens, s); break;
-    case 96: launch_rbx3<96, 96, 6, 2>(a, h_lens, s); break;
-    case 48: launch_rbx3<48, 192, 3, 4>(a, h_lens, s); break;
+    case 192: launch_rbx3<192, 64, 12, 1, 3>(a, h_lens, s); break;
+    case 96: launch_rbx3<96, 96, 6, 2, 3>(a, h_lens, s); break;
+    case 48: launch_rbx3<48, 192, 3, 4, 3>(a, h_lens, s); break;
+    // full-band MelGAN stages (base 512): tiles sized to the 159 KB LDS budget, 8 waves
+    case 256: launch_rbx3<256, 32, 8, 1, 4>(a, h_lens, s); break;
+    case 128: launch_rbx3<128, 64, 8, 1, 4>(a, h_lens, s); break;
+    case 64: launch_rbx3<64, 128, 4, 2, 2>(a, h_lens, s); break;
+    case 32: launch_rbx3<32, 192, 2, 4, 1>(a, h_lens, s); break;
     default: TTS_CHECK(false, "resblock_x3: unsupported channel count");
   }
   HIP_OK(hipGetLastError());
