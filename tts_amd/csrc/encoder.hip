@@ -114,18 +114,20 @@ __global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restric
 //   hbuf: [2 ping-pong][dir][Bp x H] fragment order      out : (B, T_max, NDIR*H)
 //   Whh16 (X3): the same tiles split-f16 (split16.h pack_split_a, [dir * H/4 + tile][H/32][64][16]);
 //   h is loaded from the fp32 fragment buffer and split in registers (|h| <= 1: always in range)
+constexpr int LSTM_NW = 8;  // waves per workgroup: the K = H reduction split 8 ways
 template <int MT, int H, int NDIR, bool X3>
-__global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restrict__ Whh,
+__global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float* __restrict__ Whh,
                                                            const uint16_t* __restrict__ Whh16,
                                                            const float* __restrict__ Gin, const int* lens,
                                                            int T_max, int B, float* hbuf, float* __restrict__ out,
                                                            unsigned* bar) {
   constexpr int Bp = MT * 16;
   constexpr int NT = H / 4;                   // gate tiles per direction
-  constexpr int NKC = H / 16, KPW = NKC / 4;  // k-chunks, per wave
+  constexpr int NW = LSTM_NW;
+  constexpr int NKC = H / 16, KPW = NKC / NW;  // k-chunks, per wave
   constexpr int G = NDIR * 4 * H, O = NDIR * H;
-  static_assert(NKC % 4 == 0 && NT % 8 == 0, "LSTM geometry");
-  __shared__ float part[4 * Bp * 17];
+  static_assert(NKC % NW == 0 && KPW % 2 == 0 && NT % 8 == 0, "LSTM geometry");
+  __shared__ float part[NW * Bp * 17];
   __shared__ int sflag;
   const int dir = blockIdx.x / NT, tl = blockIdx.x % NT;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -213,8 +215,10 @@ __global__ __launch_bounds__(256) void lstm_persist_kernel(const float* __restri
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = q * 4 + u;
-        pre[q] = part[m * 17 + n] + part[(Bp + m) * 17 + n] + part[(2 * Bp + m) * 17 + n] +
-                 part[(3 * Bp + m) * 17 + n] + gin[q];
+        float sum = part[m * 17 + n];
+#pragma unroll
+        for (int w = 1; w < NW; ++w) sum += part[(w * Bp + m) * 17 + n];
+        pre[q] = sum + gin[q];
       }
       cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
       const float hn = sigm_f(pre[3]) * tanh_f(cst);
@@ -247,7 +251,7 @@ static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const uint
                                         {LPK(1, true), LPK(2, true), LPK(3, true), LPK(4, true)}};
 #undef LPK
   const void* f = fns[Whh16 ? 1 : 0][MT - 1];
-  launch_resident(f, dim3(NDIR * H / 4), dim3(256), args, 0, s);
+  launch_resident(f, dim3(NDIR * H / 4), dim3(64 * LSTM_NW), args, 0, s);
   return true;
 }
 
