@@ -1,12 +1,15 @@
 """Benchmark: Tacotron2-DDC + MultiBand-MelGAN inference, batch 32 LJ-length utterances per GPU.
 
-One "step" = Tacotron2.inference on the rank's 32-utterance batch (encoder, graph-captured
+One "step" = Tacotron2.inference on the rank's 32-utterance batch (encoder, persistent
 autoregressive decoder, postnet) followed by MultibandMelganGenerator.inference on the
 resulting mels (generator + PQMF). Forced lengths: stop bias -1e4 and
 max_decoder_steps_i = ceil(M_i / r), so every run does exactly the same work.
 
 Prints ONE JSON line (rank 0). ``value`` = mel frames produced per second by the whole
-pipeline over all ranks; Tacotron2-only frames/s and end-to-end RTF are extra fields.
+pipeline over all ranks, ids and waveforms resident in HBM (r = 2). Extra fields:
+Tacotron2-only frames/s, end-to-end RTF, ``e2e_rtf_host`` (ids on the host -> per-utterance
+waveforms on the host), the r = 1 run (``r1``), and ``roofline.pipeline_frac`` =
+SURVEY 8d's whole-pipeline bound / measured.
 Launch for N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
 """
 
@@ -33,6 +36,31 @@ HBM_PEAK_GBS = 8000.0       # MI355X_MICROARCH.md: HBM3E 8.0 TB/s spec
 F32_PEAK_TFLOPS = 157.3     # dense fp32 (vector == f32 MFMA rate)
 F16_PEAK_TFLOPS = 2500.0    # dense f16 MFMA (v_mfma_f32_16x16x32_f16)
 X3_PEAK_TFLOPS = F16_PEAK_TFLOPS / 3  # fp32-equivalent rate of the split-f16 form (3 f16 MFMAs per product)
+
+# SURVEY.md 8d algorithmic work (checked there against torch.utils.flop_counter on the reference)
+DEC_FLOP_ROW_STEP = 37_809_248     # prenet, both LSTMCells, query, projection at r_init = 7, stopnet
+ATT_FLOP_PER_T = 13_440            # loc-conv 3,968 + loc-dense 8,192 + v 256 + context 1,024 per position
+DEC_W_BYTES = 75_711_112           # 18,927,778 fp32 decoder parameters read per batched step
+ENC_FLOP_TOKEN = 11_010_048 + 131_072   # 3 convs + BiLSTM, + processed_inputs
+POST_FLOP_FRAME = 8_683_520
+VOC_FLOP_FRAME = 36_128_768        # MB-MelGAN generator + PQMF
+
+
+def pipeline_bound_ms(T, steps, r, peak_tflops=F32_PEAK_TFLOPS):
+    """SURVEY 8d lower bound for one batch: decoder sum over steps of max(bytes / HBM, flops / peak)
+    with the active set shrinking as utterances finish, plus encoder + postnet + vocoder flops / peak.
+    Returns (total_ms, decoder_ms). 10.15 ms at r=2 and 14.59 ms at r=1 for the C2 batch."""
+    T = np.asarray(T, np.float64)
+    st = np.asarray(steps)
+    dec = 0.0
+    for s_ in range(int(st.max())):
+        a = st > s_
+        fl = (DEC_FLOP_ROW_STEP + ATT_FLOP_PER_T * T[a]).sum()
+        by = DEC_W_BYTES + (2580.0 * T[a] + 320.0 * r + 37_500.0).sum()  # inputs+keys+alpha, align, frames, states
+        dec += max(by / (HBM_PEAK_GBS * 1e9), fl / (peak_tflops * 1e12))
+    frames = float((st * r).sum())
+    other = (T.sum() * ENC_FLOP_TOKEN + frames * (POST_FLOP_FRAME + VOC_FLOP_FRAME)) / (peak_tflops * 1e12)
+    return (dec + other) * 1e3, dec * 1e3
 
 
 def build_models(device, seed=0):
@@ -101,6 +129,7 @@ def main():
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--f32-steps", type=int, default=3, help="steps re-timed with fp32-MFMA GEMMs only (0: skip)")
+    ap.add_argument("--r1-steps", type=int, default=3, help="steps timed at r=1 as extra fields (0: skip)")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -113,21 +142,20 @@ def main():
         dist.init_process_group("nccl", device_id=dev)
 
     taco, tsd, voc, vsd, tcfg, vcfg = build_models(dev)
-    r = args.r
-    taco.decoder.set_r(r)
     taco.decoder.verbose = False  # forced lengths end every utterance at max_decoder_steps
     T_all, M_all, shards = replicated_workload(world, args.per_gpu_batch)
     mine = shards[rank]
     T_prof, M_prof = lj_profile()
     ids = synthetic_ids(T_prof)              # C3 replicates the same 32 utterances
     my_ids = [ids[i % len(ids)] for i in mine]
-    steps = forced_steps([M_all[i] for i in mine], r)
+    my_T = [T_all[i] for i in mine]
     batch, lens = pad_batch(my_ids)
     batch_t = torch.from_numpy(batch).to(dev)
+    batch_host = torch.from_numpy(batch).pin_memory()
     ev = [torch.cuda.Event(enable_timing=True) for _ in range(3)]
     tt, tv = [], []
 
-    def one_step(record):
+    def one_step(steps, record=False):
         if record:
             ev[0].record()
         _, post, _, _ = taco.inference(batch_t, text_lengths=lens, max_decoder_steps=steps)
@@ -142,59 +170,114 @@ def main():
             tv.append(ev[1].elapsed_time(ev[2]))
         return int(mel_lens.sum()), wav
 
-    for _ in range(args.warmup):
-        one_step(False)
-    if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    frames = 0
-    for _ in range(args.steps):
-        f, _ = one_step(False)
-        frames += f
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    el = time.perf_counter() - t0
-    per_step_frames = frames // args.steps
-    if world > 1:
-        t = torch.tensor([el], device=dev, dtype=torch.float64)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        el = float(t.item())
-        fr = torch.tensor([per_step_frames], device=dev, dtype=torch.float64)
-        dist.all_reduce(fr, op=dist.ReduceOp.SUM)
-        per_step_frames = int(fr.item())
-    ms_step = el / args.steps * 1000.0
-    value = per_step_frames / (ms_step / 1000.0)
-    audio_s = per_step_frames * HOP / SAMPLE_RATE
-    # per-stage split (separate, event-timed passes after the timed region)
-    for _ in range(2):
-        one_step(True)
-    taco_ms, voc_ms = float(np.median(tt)), float(np.median(tv))
-    my_frames = int(sum(s * r for s in steps))
+    wav_host = {}
+
+    def host_step(steps):
+        """IDs on the host -> waveforms on the host (SURVEY 8d e2e RTF; server/synthesizer.py:147,155-156):
+        H2D of the pinned id batch, both models, D2H of the waveform batch into pinned memory and the
+        per-utterance cut to its own 256 * M_i samples."""
+        x = batch_host.to(dev, non_blocking=True)
+        _, post, _, _ = taco.inference(x, text_lengths=lens, max_decoder_steps=steps)
+        mel_lens = taco.last_mel_lengths
+        wav = voc.inference(post.transpose(1, 2), lengths=mel_lens)
+        key = tuple(wav.shape)
+        if key not in wav_host:
+            wav_host[key] = torch.empty(key, dtype=wav.dtype, pin_memory=True)
+        h = wav_host[key]
+        h.copy_(wav, non_blocking=True)
+        torch.cuda.current_stream().synchronize()
+        hn = h.numpy()
+        return [hn[i, 0, :HOP * int(m)] for i, m in enumerate(mel_lens)]
+
+    def timed(fn, n):
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        frames = 0
+        for _ in range(n):
+            out = fn()
+            frames += out[0] if isinstance(out, tuple) else sum(len(w) for w in out) // HOP
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el, frames / n], device=dev, dtype=torch.float64)
+            t0_ = torch.tensor([el], device=dev, dtype=torch.float64)
+            dist.all_reduce(t0_, op=dist.ReduceOp.MAX)
+            dist.all_reduce(t, op=dist.ReduceOp.SUM)
+            el, per = float(t0_.item()), int(t[1].item())
+        else:
+            per = frames // n
+        return el / n * 1000.0, per
 
     from tts_amd._lib import get_engine
     eng = get_engine(dev)
+
+    def measure(r, steps_n, warmup, with_host):
+        """One configuration (reduction factor r): the timed device-resident step, the stage split,
+        the host-to-host step, and the decoder launch statistics."""
+        taco.decoder.set_r(r)
+        steps = forced_steps([M_all[i] for i in mine], r)
+        for _ in range(warmup):
+            one_step(steps)
+        ms, per_frames = timed(lambda: one_step(steps), steps_n)
+        tt.clear()
+        tv.clear()
+        for _ in range(2):  # per-stage split (separate, event-timed passes after the timed region)
+            one_step(steps, True)
+        path, launches = eng.decoder_stats()
+        res = {"ms": ms, "frames": per_frames, "steps": steps, "taco_ms": float(np.median(tt)),
+               "voc_ms": float(np.median(tv)), "path": path, "launches": launches}
+        if with_host:
+            host_step(steps)
+            res["host_ms"], _ = timed(lambda: host_step(steps), steps_n)
+        bound, dec_bound = pipeline_bound_ms(my_T, steps, r)
+        bound_x3, _ = pipeline_bound_ms(my_T, steps, r, X3_PEAK_TFLOPS)
+        res.update(bound_ms=bound, dec_bound_ms=dec_bound, bound_x3_ms=bound_x3)
+        return res
+
+    r = args.r
+    m2 = measure(r, args.steps, args.warmup, with_host=True)
+    ms_step, per_step_frames, steps = m2["ms"], m2["frames"], m2["steps"]
+    value = per_step_frames / (ms_step / 1000.0)
+    audio_s = per_step_frames * HOP / SAMPLE_RATE
+    taco_ms, voc_ms = m2["taco_ms"], m2["voc_ms"]
+    my_frames = int(sum(s_ * r for s_ in steps))
     gemm_mode, fallbacks = eng.gemm_mode()
-    # decoder launch stats of the last step above (the headline GEMM mode), before the fp32 pass
-    path, launches = eng.decoder_stats()
+    path, launches = m2["path"], m2["launches"]
+
     # the same step with every GEMM on the fp32 MFMA (no split-f16 kernels), for comparison
     f32_ms = None
     if gemm_mode == "x3" and args.f32_steps > 0:
         eng.set_gemm_mode("f32")
-        one_step(False)
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.f32_steps):
-            one_step(False)
-        torch.cuda.synchronize()
-        f32_ms = (time.perf_counter() - t1) / args.f32_steps * 1000.0
-        eng.set_gemm_mode("x3")
+        try:
+            one_step(steps)
+            f32_ms, _ = timed(lambda: one_step(steps), args.f32_steps)
+        finally:
+            eng.set_gemm_mode("x3")
+
+    # the other reduction factor SURVEY 8d asks for (r=1: 858 decoder steps), as extra fields
+    other = None
+    if args.r1_steps > 0 and r == 2:
+        m1 = measure(1, args.r1_steps, 1, with_host=False)
+        _, st1 = m1["launches"][0]
+        other = {"r": 1, "ms_per_step": round(m1["ms"], 3), "mel_frames_per_s": round(m1["frames"] / (m1["ms"] / 1e3), 1),
+                 "e2e_rtf": m1["ms"] / 1000.0 / (m1["frames"] * HOP / SAMPLE_RATE),
+                 "tacotron2_mel_frames_per_s": round(sum(m1["steps"]) / (m1["taco_ms"] / 1e3) * world, 1),
+                 "tacotron2_ms": round(m1["taco_ms"], 3), "vocoder_ms": round(m1["voc_ms"], 3),
+                 "decoder_steps": int(max(m1["steps"])),
+                 "decoder_step_us": round(m1["launches"][0][0] / max(st1, 1) * 1000.0, 2) if m1["path"] == 1 else None,
+                 "pipeline_bound_ms": round(m1["bound_ms"], 3), "pipeline_frac": round(m1["bound_ms"] / m1["ms"], 4),
+                 "pipeline_frac_x3_ceiling": round(m1["bound_x3_ms"] / m1["ms"], 4)}
+        taco.decoder.set_r(r)
 
     # dominant decoder kernel, timed live with HIP events on the library's stream (stats above)
     if path == 1:
         # persistent decoder: the MT = 2 launch (32-row batch tile) carries most steps. Algorithmic
-        # work = useful row-steps (rows still decoding) x the per-row GEMM flops of one step
+        # work = useful row-steps (rows still decoding) x the per-row GEMM flops of one step, plus
+        # the attention's 13,440 FLOP per (row, step, encoder position) (SURVEY 8d)
         ms0, st0 = launches[0]
         flop_row = 2 * (4096 * 2560          # decoder_rnn [W_ih | W_hh]
                         + 4096 * 1536        # attention_rnn ctx/h part
@@ -202,8 +285,10 @@ def main():
                         + (1 + 80 * r) * 1536  # projection (r frames) + stopnet
                         + 80 * 256 + 256 * 256  # prenet
                         + 1024 * 128)        # query projection
-        row_steps = sum(min(s_, st0) for s_ in steps[:16 * ((len(mine) + 15) // 16)])
-        flops = row_steps * flop_row
+        rows = range(min(len(mine), 16 * ((len(mine) + 15) // 16)))
+        row_steps = sum(min(steps[i], st0) for i in rows)
+        att_flops = sum(ATT_FLOP_PER_T * my_T[i] * min(steps[i], st0) for i in rows)
+        flops = row_steps * flop_row + att_flops
         achieved = flops / (ms0 * 1e-3) / 1e12
         step_ms = ms0 / max(st0, 1)
         traffic = None
@@ -243,7 +328,17 @@ def main():
                 "bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBS, "unit": "GB/s",
                 "frac": round(achieved / HBM_PEAK_GBS, 4), "traffic": traffic,
                 "avg_launch_us": round(k4_ms * 1000.0, 2), "algorithmic_bytes": k4_bytes}
+    # SURVEY 8d whole-pipeline bound (fp32 peaks) / measured, and the same with the compute part
+    # priced at the split-f16 ceiling the kernels actually run at
+    roof["pipeline_bound_ms"] = round(m2["bound_ms"], 3)
+    roof["pipeline_frac"] = round(m2["bound_ms"] / ms_step, 4)
+    roof["pipeline_frac_x3_ceiling"] = round(m2["bound_x3_ms"] / ms_step, 4)
+    roof["decoder_bound_ms"] = round(m2["dec_bound_ms"], 3)
+    if path == 1:
+        dec_ms = sum(m_ for m_, _ in launches)
+        roof["decoder_frac"] = round(m2["dec_bound_ms"] / dec_ms, 4)
 
+    host_audio = per_step_frames * HOP / SAMPLE_RATE
     out = {
         "metric": "mel-frames/s (Tacotron2-DDC + MB-MelGAN end-to-end)",
         "value": round(value, 1),
@@ -265,6 +360,8 @@ def main():
                                f"MB-MelGAN [8,4,2]x4, {args.per_gpu_batch} LJ-length utterances per GPU",
                    "global_batch": args.per_gpu_batch * world, "r": r, "parallelism": f"replicas x{world}"},
         "e2e_rtf": ms_step / 1000.0 / audio_s,
+        "e2e_rtf_host": m2["host_ms"] / 1000.0 / host_audio,
+        "host_ms_per_step": round(m2["host_ms"], 3),
         "tacotron2_mel_frames_per_s": round(my_frames / (taco_ms / 1000.0) * world, 1),
         "tacotron2_ms": round(taco_ms, 3),
         "vocoder_ms": round(voc_ms, 3),
@@ -272,6 +369,7 @@ def main():
         "decoder_steps": int(max(steps)),
         "decoder_path": "persistent" if path == 1 else "step-graphs",
         "roofline": roof,
+        "r1": other,
     }
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         out["cpu_baseline"] = cpu_baseline(tsd, vsd, tcfg, vcfg, ids, forced_steps(M_prof, r), r,

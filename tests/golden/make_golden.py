@@ -42,7 +42,7 @@ STOP_GAIN = {"linear_sigmoid": 100.0, "attn_v": 4.0, "linear_tanh": 3.0}
 # larger stop logits -> wider stop margins; sharper attention -> wider argmax margins
 
 
-def build_taco(cfg: TacotronConfig, seed: int, stop_bias: float, dtype=torch.float32):
+def build_taco(cfg: TacotronConfig, seed: int, stop_bias: float, dtype=torch.float32, gains=None):
     torch.set_default_dtype(dtype)
     m = Tacotron2(num_chars=cfg.num_chars, num_speakers=cfg.num_speakers, r=cfg.r, attn_norm=cfg.attn_norm,
                   prenet_dropout=False, location_attn=cfg.location_attn,
@@ -51,7 +51,7 @@ def build_taco(cfg: TacotronConfig, seed: int, stop_bias: float, dtype=torch.flo
                   prenet_type=cfg.prenet_type, attn_win=cfg.windowing, forward_attn=cfg.forward_attn,
                   trans_agent=cfg.trans_agent, forward_attn_mask=cfg.forward_attn_mask, attn_type=cfg.attn_type,
                   attn_K=cfg.attn_K)
-    sd = synth_state_dict(tacotron2_spec(cfg), seed, STOP_GAIN)
+    sd = synth_state_dict(tacotron2_spec(cfg), seed, gains or STOP_GAIN)
     sd["decoder.stopnet.1.linear_layer.bias"] = np.array([stop_bias], np.float32)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     m.eval()
@@ -111,19 +111,21 @@ def choose_stop_bias(raw_logits_list, max_steps, min_stopping, min_stop_step=4):
 
 
 def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_seed, speakers=None,
-              min_stop_step=4):
-    """speakers: per utterance a speaker id (learned table) or an embedding vector (external)."""
+              min_stop_step=4, gains=None, store64=False):
+    """speakers: per utterance a speaker id (learned table) or an embedding vector (external).
+    gains: per-kind weight scale overrides (default STOP_GAIN), recorded in the fixture."""
+    gains = gains or STOP_GAIN
     rs = np.random.RandomState(id_seed)
     utts = [rs.randint(1, cfg.num_chars, size=T).astype(np.int64) for T in utt_lens]
     spks = speakers if speakers is not None else [None] * len(utts)
     # pass 1: never stop; record bias-free logits at the largest r (same decoder state
     # trajectory for any stop bias, since the stopnet output is never fed back)
     out = {"seed": seed, "cfg": json.dumps(cfg.__dict__), "r_list": np.array(r_list),
-           "overrides": json.dumps(STOP_GAIN)}
+           "overrides": json.dumps(gains)}
     for r in r_list:
         # the first seed (from `seed` upwards) whose stop logits admit a bias with margin >= 1e-2
         for attempt in range(40):
-            m = build_taco(cfg, seed, -1e4)
+            m = build_taco(cfg, seed, -1e4, gains=gains)
             raw = []
             for ids, sp in zip(utts, spks):
                 lg = run_taco(m, ids, r, max_steps[r], spk=sp)[4]
@@ -135,10 +137,11 @@ def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_see
         else:
             raise SystemExit(f"[{name}] no seed with a usable stop margin")
         out["seed"] = seed
+        out[f"r{r}_seed"] = np.int64(seed)  # the search may move the seed between r values
         b, margin = best
         print(f"[{name}] r={r} stop bias {b:.6f} min margin {margin:.3e}")
-        m32 = build_taco(cfg, seed, b)
-        m64 = build_taco(cfg, seed, b, torch.float64)
+        m32 = build_taco(cfg, seed, b, gains=gains)
+        m64 = build_taco(cfg, seed, b, torch.float64, gains=gains)
         for i, ids in enumerate(utts):
             sp = spks[i]
             dec, post, align, stop, lg, enc = run_taco(m32, ids, r, max_steps[r], spk=sp)
@@ -158,6 +161,8 @@ def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_see
             out[f"{k}_logit"] = lg.astype(np.float32)
             out[f"{k}_top2"] = top2.astype(np.float32)
             out[f"{k}_drift64"] = np.float64(drift)
+            if store64:  # the fp64 run's postnet output: the truth both GPU GEMM modes are scored against
+                out[f"{k}_post64"] = post64
             if i == 1:
                 out[f"{k}_enc"] = enc.astype(np.float32)
             print(f"  utt{i} T={len(ids)} steps={len(stop)} frames={len(dec)} drift64={drift:.2e} "
@@ -397,6 +402,14 @@ if __name__ == "__main__":
         glow_case("glow_tdsep", "time-depth-separable", seed=27, data_seed=28)
     if "glow_tfm" in which:
         glow_case("glow_tfm", "transformer", seed=33, data_seed=30)  # seed 29: all durations 0
+    if "taco_amplified" in which:
+        # SURVEY 7 "mildly amplified" decoder regime: LSTM weights x2.1, projection x10, attention v x6
+        # (|mel| ~9). fp32-vs-fp64 drift grows to 3-5e-6 (r=2) / 1-3e-5 (r=1) over the decode, 20-200x
+        # the xavier-scale fixtures, so a reduced-precision GEMM would show here first.
+        taco_case("taco_amplified", TacotronConfig(attn_norm="sigmoid"), seed=51,
+                  utt_lens=[23, 51, 37], r_list=[2, 1], max_steps={2: 60, 1: 80}, min_stopping=2, id_seed=52,
+                  min_stop_step=40,
+                  gains={**STOP_GAIN, "lstm": 2.1, "linear": 10.0, "attn_v": 6.0}, store64=True)
     if "taco_softmax" in which:
         taco_case("taco_softmax", TacotronConfig(attn_norm="softmax"), seed=2,
                   utt_lens=[25, 9], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=8)

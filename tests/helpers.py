@@ -21,7 +21,8 @@ def taco_cfg(fx):
 
 def taco_state_dict(fx, r=None, seed=None, overrides=None, stop_bias=None, cfg=None):
     cfg = cfg or taco_cfg(fx)
-    seed = int(fx["seed"]) if seed is None else seed
+    if seed is None:  # per-r seed when the fixture's stop-margin search moved it between r values
+        seed = int(fx[f"r{r}_seed"]) if r is not None and f"r{r}_seed" in fx.files else int(fx["seed"])
     ov = json.loads(str(fx["overrides"])) if overrides is None else overrides
     sd = synth_state_dict(tacotron2_spec(cfg), seed, ov)
     if stop_bias is None and r is not None:

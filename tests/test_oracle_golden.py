@@ -67,6 +67,34 @@ def test_tacotron2_oracle_matches_reference(r):
             assert np.abs(orc.encoder(fx[k + "_ids"]) - fx[k + "_enc"]).max() <= 1e-6
 
 
+@pytest.mark.parametrize("r", [2, 1])
+def test_tacotron2_oracle_amplified_regime_matches_reference(r):
+    """SURVEY 7's mildly amplified regime: the reference's own fp32-vs-fp64 drift is 3e-6 to 3e-5
+    here, so the oracle (a different fp32 summation order) is held to the north_star 1e-4 bound;
+    stop steps and argmax above the margin stay exact."""
+    fx = load_fixture("taco_amplified")
+    cfg, sd = taco_state_dict(fx, r=r)
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for u in range(3):
+        k = f"r{r}_u{u}"
+        dec, post, align, stop = orc.inference(fx[k + "_ids"], r, int(fx[f"r{r}_max_steps"]))
+        assert len(stop) == len(fx[k + "_stop"])
+        assert np.abs(post - fx[k + "_post"]).max() <= 1e-4
+        assert np.abs(post - fx[k + "_post64"]).max() <= 1e-4
+        sel = fx[k + "_top2"] > 1e-5
+        assert np.array_equal(align.argmax(1)[sel], fx[k + "_align"].argmax(1)[sel])
+
+
+def test_amplified_fixture_is_amplified():
+    """The amplified fixture really sits where fp32 rounding grows (drift >= 1e-5 at r=1, 20x the
+    others) and still below the 1e-4 bound; every utterance decodes >= 40 steps."""
+    fx = load_fixture("taco_amplified")
+    d1 = [float(fx[f"r1_u{u}_drift64"]) for u in range(3)]
+    d2 = [float(fx[f"r2_u{u}_drift64"]) for u in range(3)]
+    assert max(d1) >= 1e-5 and max(d1 + d2) < 5e-5 and min(d2) > 1e-6
+    assert min(len(fx[f"r{r}_u{u}_stop"]) for r in (1, 2) for u in range(3)) >= 40
+
+
 def test_tacotron2_oracle_softmax_matches_reference():
     fx = load_fixture("taco_softmax")
     cfg, sd = taco_state_dict(fx, r=2)

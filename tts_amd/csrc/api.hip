@@ -1124,14 +1124,18 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
   if (!W.enc_persist) launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
 }
 
-// after a stream synchronisation: a persistent BiLSTM whose grid barrier timed out set its error word
+// a persistent BiLSTM whose grid barrier timed out set its error word. The words are read on the
+// library stream (ordered after the BiLSTM launch and its arm fill; c->s is non-blocking, so a
+// null-stream copy would not be), then the stream is drained before they are looked at.
 void check_encoder_barrier(tts_ctx* c) {
   if (!c->tws.enc_persist) return;
-  unsigned err = 0;
-  unsigned err2 = 0;
-  HIP_OK(hipMemcpy(&err, reinterpret_cast<unsigned*>(c->tws.lc.p) + 16, 4, hipMemcpyDeviceToHost));
-  HIP_OK(hipMemcpy(&err2, reinterpret_cast<unsigned*>(c->tws.lc.p) + 512 + 16, 4, hipMemcpyDeviceToHost));
-  TTS_CHECK(err == 0 && err2 == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
+  int* pw = c->pinned + 240;
+  pw[0] = pw[1] = 0;
+  const unsigned* words = reinterpret_cast<const unsigned*>(c->tws.lc.p);
+  HIP_OK(hipMemcpyAsync(&pw[0], words + 16, 4, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(&pw[1], words + 512 + 16, 4, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipStreamSynchronize(c->s));
+  TTS_CHECK(pw[0] == 0 && pw[1] == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
 }
 
 void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int B, int Mmax_alloc, int max_q,
