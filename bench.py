@@ -86,36 +86,43 @@ def build_models(device, seed=0):
 
 
 def cpu_baseline(tsd, vsd, tcfg, vcfg, ids, steps, r, budget_s):
-    """Oracle (numpy fp32 restatement) at B=1 per utterance, like the reference CPU path."""
-    from threadpoolctl import threadpool_limits
-    from oracle.melgan_np import MelganOracle
-    from oracle.taco_np import TacoOracle
+    """The reference CPU path's op sequence (oracle/torch_cpu.py: PyTorch-CPU ATen restatement, SURVEY
+    8d) at B=1 per utterance, Tacotron2 then MB-MelGAN, on the host's cores. Timed beside the imported
+    reference in the build container by tools/cpu_baseline_check.py (profiles/r03/)."""
+    from oracle.torch_cpu import MelganTorchCPU, TacoTorchCPU
     from tts_amd.pqmf import pqmf_filters
     from tts_amd.spec import melgan_layers
     cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
     cores = max(1, min(cores, os.cpu_count() or 1))
-    to = TacoOracle(tsd, tcfg.attn_norm, tcfg.r)
-    vo = MelganOracle(vsd, melgan_layers(vcfg), pqmf_filters()[1])
-    frames = 0
-    n = 0
-    with threadpool_limits(limits=cores):
-        # warm-up on the shortest utterance (excluded, as SURVEY §8d asks)
+    prev = torch.get_num_threads()
+    torch.set_num_threads(cores)
+    try:
+        to = TacoTorchCPU(tsd, tcfg.attn_norm, tcfg.r)
+        vo = MelganTorchCPU(vsd, melgan_layers(vcfg), pqmf_filters()[1])
+        # warm-up on the shortest utterance (excluded, as SURVEY 8d asks)
         j = int(np.argmin(steps))
         _, p, _, _ = to.inference(ids[j], r, min(steps[j], 4))
-        t0 = time.perf_counter()
-        for i in range(len(ids)):
-            _, p, _, _ = to.inference(ids[i], r, steps[i])
+        vo.inference(p.T, pad=0)
+        frames = n = 0
+        t_taco = t_voc = 0.0
+        while n < len(ids) and t_taco + t_voc < budget_s:
+            t0 = time.perf_counter()
+            _, p, _, _ = to.inference(ids[n], r, steps[n])
+            t1 = time.perf_counter()
             vo.inference(p.T, pad=0)
+            t_voc += time.perf_counter() - t1
+            t_taco += t1 - t0
             frames += p.shape[0]
             n += 1
-            if time.perf_counter() - t0 > budget_s:
-                break
-        el = time.perf_counter() - t0
+    finally:
+        torch.set_num_threads(prev)
+    el = t_taco + t_voc
     audio = frames * HOP / SAMPLE_RATE
-    return {"value": frames / el, "unit": "mel-frames/s", "cores": cores, "kind": "port",
-            "rtf": el / audio,
+    return {"value": round(frames / el, 1), "unit": "mel-frames/s", "cores": cores, "kind": "port",
+            "rtf": el / audio, "tacotron2_mel_frames_per_s": round(frames / t_taco, 1),
             "sample": f"first {n} of {len(ids)} LJ-profile utterances, B=1 sequential, r={r}, forced length "
-                      f"({frames} frames), numpy fp32 oracle + MB-MelGAN oracle, {el:.1f} s"}
+                      f"({frames} frames): Tacotron2 {t_taco:.1f} s + MB-MelGAN {t_voc:.1f} s, PyTorch-CPU "
+                      f"restatement of the reference op sequence (oracle/torch_cpu.py), {cores} threads"}
 
 
 def main():

@@ -42,8 +42,8 @@ def dconv(x, w, b, d):
     L = x.shape[1]
     xp = np.pad(x, ((0, 0), (p, p)))
     y = np.zeros((cout, L), F32)
-    for k in range(K):
-        y += w[:, :, k] @ xp[:, k * d:k * d + L]
+    for k in range(K):  # contiguous tap slice: a strided one makes numpy skip BLAS (~100x slower)
+        y += np.ascontiguousarray(w[:, :, k]) @ xp[:, k * d:k * d + L]
     if b is not None:
         y += b[:, None]
     return y.astype(F32)

@@ -245,60 +245,79 @@ def ge2e_case(name):
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
+def import_glow_tts():
+    """Make the reference's ``TTS.tts.models.glow_tts`` importable: its package imports the Cython
+    extension ``monotonic_align.core`` (``core.pyx``, never compiled in the checkout). Recipe: cythonize
+    the reference's own ``core.pyx`` where it lies, compile it into a temporary directory (nothing is
+    written under the reference or into this repo), and register the built module under its package
+    name before the package is imported. Then return ``GlowTts``."""
+    import importlib.machinery
+    import importlib.util
+    import tempfile
+    from Cython.Build import cythonize
+    from setuptools import Extension
+    from setuptools.dist import Distribution
+    name = "TTS.tts.layers.glow_tts.monotonic_align.core"
+    if name not in sys.modules:
+        pyx = os.path.join(REF, "TTS/tts/layers/glow_tts/monotonic_align/core.pyx")
+        tmp = tempfile.mkdtemp(prefix="monotonic_align_")
+        ext = Extension("core", [pyx], include_dirs=[np.get_include()])
+        dist = Distribution({"ext_modules": cythonize([ext], build_dir=tmp, quiet=True,
+                                                      compiler_directives={"language_level": 3})})
+        cmd = dist.get_command_obj("build_ext")
+        cmd.build_lib = cmd.build_temp = tmp
+        cmd.ensure_finalized()
+        cmd.run()
+        so = cmd.get_ext_fullpath("core")
+        spec = importlib.util.spec_from_file_location(name, so, loader=importlib.machinery.ExtensionFileLoader(name, so))
+        mod = importlib.util.module_from_spec(spec)
+        spec.loader.exec_module(mod)
+        sys.modules[name] = mod
+    from TTS.tts.models.glow_tts import GlowTts
+    return GlowTts
+
+
 def glow_case(name, encoder_type="gatedconv", seed=23, data_seed=24):
-    """Glow-TTS (gated-conv encoder, as setup_model builds it, TTS/tts/utils/generic_utils.py:105-129).
-    The top-level GlowTts module does not import here (monotonic_align.core is an unbuilt Cython
-    extension), so the reference's Encoder and Decoder modules run under the inference glue of
-    glow_tts.py:166-193 restated below (durations, generate_path, expanded means, noise)."""
-    from TTS.tts.layers.glow_tts.encoder import Encoder
-    from TTS.tts.layers.glow_tts.decoder import Decoder
+    """Glow-TTS as setup_model builds it (TTS/tts/utils/generic_utils.py:105-129), run through the
+    reference's own ``GlowTts.inference`` (glow_tts.py:159-185) after import_glow_tts() built its
+    Cython dependency. The prior noise is drawn inside inference by ``torch.randn_like``; re-seeding
+    torch reproduces it for the fixture (the encoder and decoder draw nothing in eval mode)."""
     from tts_amd.spec import GlowConfig, glow_spec
+    GlowTts = import_glow_tts()
     cfg = GlowConfig(encoder_type=encoder_type)
-    enc = Encoder(cfg.num_chars, out_channels=80, hidden_channels=192, filter_channels=768, filter_channels_dp=256,
-                  encoder_type=encoder_type, num_heads=2, num_layers=6, kernel_size=3, dropout_p=0.1, mean_only=True,
-                  use_prenet=True, c_in_channels=0)
-    dec = Decoder(80, 192, 5, 1, 12, 4, dropout_p=0.05, num_splits=4, num_sqz=2, sigmoid_scale=False,
-                  c_in_channels=0)
-    ref_keys = {**{"encoder." + k: tuple(v.shape) for k, v in enc.state_dict().items()},
-                **{"decoder." + k: tuple(v.shape) for k, v in dec.state_dict().items()}}
+    m = GlowTts(num_chars=cfg.num_chars, hidden_channels=192, filter_channels=768, filter_channels_dp=256,
+                out_channels=80, kernel_size=3, num_heads=2, num_layers_enc=6, encoder_type=encoder_type,
+                dropout_p=0.1, num_flow_blocks_dec=12, kernel_size_dec=5, dilation_rate=1, num_block_layers=4,
+                dropout_p_dec=0.05, num_speakers=0, c_in_channels=0, num_splits=4, num_sqz=2, sigmoid_scale=False,
+                mean_only=True, hidden_channels_enc=192, hidden_channels_dec=192, use_encoder_prenet=True)
+    ref_keys = {k: tuple(v.shape) for k, v in m.state_dict().items()}
     spec = {n: tuple(sh) for n, sh, _ in glow_spec(cfg)}
     assert spec == ref_keys, "glow_spec does not match the reference state_dict"
     sd = synth_state_dict(glow_spec(cfg), seed)
-    enc.load_state_dict({k[8:]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("encoder.")})
-    dec.load_state_dict({k[8:]: torch.from_numpy(v) for k, v in sd.items() if k.startswith("decoder.")})
-    enc.eval()
-    dec.eval()
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m.eval()
     rs = np.random.RandomState(data_seed)
-    out = {"seed": np.int64(seed), "noise_scale": np.float32(0.66), "encoder_type": encoder_type}
+    out = {"seed": np.int64(seed), "noise_scale": np.float32(m.noise_scale), "encoder_type": encoder_type,
+           "source": "GlowTts.inference"}
     for u, T in enumerate((17, 31)):
         ids = rs.randint(1, cfg.num_chars, size=T).astype(np.int64)
         with torch.no_grad():
             x = torch.from_numpy(ids[None])
-            x_len = torch.tensor([T])
-            o_mean, o_log_scale, o_dur_log, x_mask = enc(x, x_len, g=None)
-            w = (torch.exp(o_dur_log) - 1) * x_mask * 1.0
-            w_ceil = torch.ceil(w)
-            y_lengths = torch.clamp_min(torch.sum(w_ceil, [1, 2]), 1).long()
-            Ty = int(y_lengths.max())
-            y_mask = (torch.arange(Ty)[None] < y_lengths[:, None]).unsqueeze(1).to(x_mask.dtype)
-            attn_mask = torch.unsqueeze(x_mask, -1) * torch.unsqueeze(y_mask, 2)
-            cum = torch.cumsum(w_ceil.squeeze(1), 1)                       # generate_path
-            path = (torch.arange(Ty, dtype=cum.dtype)[None, None] < cum[:, :, None]).to(x_mask.dtype)
-            path = path - torch.nn.functional.pad(path, (0, 0, 1, 0))[:, :-1]
-            attn = (path * attn_mask.squeeze(1)).unsqueeze(1)
-            y_mean = torch.matmul(attn.squeeze(1).transpose(1, 2), o_mean.transpose(1, 2)).transpose(1, 2)
-            noise = torch.from_numpy(rs.normal(0, 1, size=(1, 80, Ty)).astype(np.float32))
-            z = (y_mean + torch.exp(torch.zeros_like(y_mean)) * noise * 0.66) * y_mask
-            y, _ = dec(z, y_mask, g=None, reverse=True)
+            torch.manual_seed(100 + u)
+            y, _, y_mean, y_log_scale, attn, o_dur_log, _ = m.inference(x, torch.tensor([T]))
+            torch.manual_seed(100 + u)
+            noise = torch.randn_like(y_mean)
+        Ty = int(attn.shape[1])
         k = f"u{u}"
         out[f"{k}_ids"] = ids
         out[f"{k}_noise"] = noise[0].numpy()
         out[f"{k}_y"] = y[0].numpy()
         out[f"{k}_ymean"] = y_mean[0].numpy()
-        out[f"{k}_attn"] = attn[0, 0].T.numpy()  # (Ty, Tx), as GlowTts.inference returns it
+        out[f"{k}_attn"] = attn[0].numpy()  # (Ty, Tx), as GlowTts.inference returns it
         out[f"{k}_logw"] = o_dur_log[0, 0].numpy()
-        out[f"{k}_ylen"] = np.int64(y_lengths[0])
-        print(f"[{name}] u{u} T={T} Ty={Ty} y {tuple(y.shape)} |y|max {y.abs().max():.3f}")
+        out[f"{k}_ylen"] = np.int64(Ty)  # B = 1: y_lengths.max() (glow_tts.py:168-172)
+        print(f"[{name}] u{u} T={T} Ty={Ty} ylen={int(out[k + '_ylen'])} y {tuple(y.shape)} "
+              f"|y|max {y.abs().max():.3f}")
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 

@@ -1297,3 +1297,126 @@ def test_pwgan_lj_batch_full_size_batched_equals_single():
             assert y1.shape[-1] == n
             assert np.array_equal(yb[i, 0, :n], y1[0, 0]), i
             assert not yb[i, 0, n:].any(), i
+
+
+def test_c5_chained_shard_vs_oracle_chain():
+    """Config C5's per-GPU shard as ONE chained GPU run (tools/c5_bench.py's models and workload):
+    GE2E SpeakerEncoder.inference on 16 reference mels (160 frames x 40) -> their 256-d embeddings into
+    the multi-speaker Tacotron2 (speaker_embeddings, models/tacotron2.py:152-155) on 16 LJ-profile
+    sentences (forced lengths, r = 2) -> the full-band MelGAN (base 512, 8x8x2x2, 3 residual blocks) on
+    the batched mels. Every row against the B = 1 oracle chain (Ge2eOracle -> TacoOracle(speaker=...)
+    -> MelganOracle.generator): embeddings <= 1e-5, mel <= 1e-4, alignment argmax identical, waveform
+    <= 1e-4 and zero past its length (speaker_encoder/model.py:62-88, melgan_generator.py:83-89)."""
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import c5_bench
+    from oracle.ge2e_np import Ge2eOracle
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import Ge2eConfig, MelganConfig, TacotronConfig, ge2e_spec, melgan_spec, tacotron2_spec
+    from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids
+    dev = _dev()
+    r, B = 2, 16
+    taco, spk, voc = c5_bench.build(dev, r)
+    T, M = lj_profile()
+    T, M = T[:B], M[:B]
+    ids = synthetic_ids(T)
+    batch, lens = pad_batch(ids)
+    steps = forced_steps(M, r)
+    ref_mels = np.random.RandomState(5).normal(0, 1, (B, 160, 40)).astype(np.float32)
+    with torch.no_grad():
+        emb = spk.inference(torch.from_numpy(ref_mels).to(dev))
+        _, post, align, _ = taco.inference(torch.from_numpy(batch).to(dev), text_lengths=lens, max_decoder_steps=steps,
+                                           speaker_embeddings=emb)
+        assert list(taco.last_steps) == list(steps)
+        wav = voc.inference(post.transpose(1, 2), lengths=taco.last_mel_lengths).cpu().numpy()
+    emb, post, align = emb.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy()
+    tcfg = TacotronConfig(num_speakers=8, speaker_embedding_dim=256)
+    tsd = synth_state_dict(tacotron2_spec(tcfg), 11)
+    tsd["decoder.stopnet.1.linear_layer.bias"] = np.array([-1e4], np.float32)
+    go = Ge2eOracle(synth_state_dict(ge2e_spec(Ge2eConfig()), 12))
+    to = TacoOracle(tsd, tcfg.attn_norm, tcfg.r)
+    vcfg = MelganConfig(out_channels=1, base_channels=512, upsample_factors=(8, 8, 2, 2), num_res_blocks=3, pqmf=False)
+    vo = melgan_oracle(vcfg, synth_state_dict(melgan_spec(vcfg, weight_norm=True), 13))
+    worst = [0.0, 0.0, 0.0]
+    for i in range(B):
+        e = go.inference(ref_mels[i])
+        worst[0] = max(worst[0], float(np.abs(emb[i] - e).max()))
+        assert worst[0] <= 1e-5, i
+        _, p, a, _ = to.inference(ids[i], r, steps[i], speaker=e)
+        n = steps[i] * r
+        worst[1] = max(worst[1], float(np.abs(post[i, :n] - p).max()))
+        assert worst[1] <= MEL_TOL, i
+        assert (align[i, :steps[i], :len(ids[i])].argmax(1) == a.argmax(1)).all(), i
+        w = vo.generator(p.T)[0]
+        assert w.size == 256 * n
+        worst[2] = max(worst[2], float(np.abs(wav[i, 0, :w.size] - w).max()))
+        assert worst[2] <= WAV_TOL, i
+        assert not wav[i, 0, w.size:].any(), i
+    print(f"C5 shard, 16 rows: worst embedding {worst[0]:.2e}, mel {worst[1]:.2e}, waveform {worst[2]:.2e}")
+
+
+def test_c4_glow_pwgan_batch64_vs_oracle():
+    """Config C4 at its stated batch of 64 (1 x MI355X): Glow-TTS on 64 LJ-length utterances (the
+    LJ profile twice, ids continuing the RandomState(0) stream) with explicit prior noise at
+    noise_scale 0.66, every utterance against the oracle at B = 1 (glow_tts.py:159-193: y_lengths and
+    the monotonic path exact, mel <= 1e-4); then ParallelWaveGAN on the 64 Glow mels in ONE batched
+    call (per-row lengths, inference_padding 0, explicit noise), its shortest, a short and the median
+    row against the PWGAN oracle on the same mel and noise (parallel_wavegan_generator.py:90-125,
+    <= 1e-4), and every row zero past its length. length_scale avoids ceil ties as in the 32-row test."""
+    import dataclasses
+    from oracle.glow_np import GlowOracle
+    from oracle.pwgan_np import PwganOracle
+    from tts_amd import GlowTts, ParallelWaveganGenerator
+    from tts_amd.spec import GlowConfig, PwganConfig, glow_spec, pwgan_spec
+    from tts_amd.workload import lj_profile, pad_batch, synthetic_ids
+    _dev()
+    B = 64
+    cfg = GlowConfig()
+    sd = synth_state_dict(glow_spec(cfg), 3)
+    m = GlowTts(num_chars=cfg.num_chars)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    T, M = lj_profile()
+    T, M = T * 2, M * 2
+    ids = synthetic_ids(T)
+    orc = GlowOracle(sd)
+    w = [np.exp(orc.encode(x)[1].astype(np.float64)).reshape(-1) - 1 for x in ids]
+    base = sum(M) / float(sum(np.ceil(np.maximum(v, 0)).sum() for v in w))
+    ls = next(s for s in base * (1 + 0.01 * np.arange(40))
+              if min(np.abs(v * s - np.round(v * s)).min() for v in w) > 2e-5)
+    tys = [int(max(1, np.ceil(np.maximum(v * ls, 0)).sum())) for v in w]
+    noise = np.random.RandomState(64).normal(0, 1, (B, 80, max(tys))).astype(np.float32)
+    outs = [orc.inference(x, noise[i], 0.66, ls) for i, x in enumerate(ids)]
+    batch, lens = pad_batch(ids)
+    m.length_scale, m.noise_scale = float(ls), 0.66
+    y, _, _, _, attn, _, _ = m.inference(torch.from_numpy(batch).cuda(), lens, noise=torch.from_numpy(noise).cuda())
+    yn, attn = y.cpu().numpy(), attn.cpu().numpy()
+    worst = 0.0
+    for i, (yr, _, ar, _, ty) in enumerate(outs):
+        assert int(m.last_y_lengths[i]) == ty, i
+        assert np.array_equal(attn[i, :ty, :len(ids[i])], ar), i
+        err = float(np.abs(yn[i, :, :yr.shape[1]] - yr).max())
+        worst = max(worst, err)
+        assert err <= 1e-4, (i, err)
+    # ParallelWaveGAN on the batch of 64 Glow mels (each row's own 2 * floor(Ty / 2) frames)
+    pcfg = dataclasses.replace(PwganConfig(), inference_padding=0)
+    psd = synth_state_dict(pwgan_spec(pcfg), 5)
+    g = ParallelWaveganGenerator(inference_padding=0)
+    g.load_state_dict({k: torch.from_numpy(v) for k, v in psd.items()})
+    g = g.cuda().eval()
+    mlens = [o[0].shape[1] for o in outs]
+    pnoise = torch.randn(B, 1, max(mlens) * 256, generator=torch.Generator().manual_seed(3))
+    with torch.no_grad():
+        wav = g.inference(y, lengths=mlens, noise=pnoise.cuda()).cpu().numpy()
+    po = PwganOracle(psd, pcfg)
+    order = np.argsort(mlens, kind="stable")
+    worst_w = 0.0
+    for i in (int(order[0]), int(order[1]), int(order[B // 2])):
+        n = mlens[i] * 256
+        ref = po.inference(yn[i, :, :mlens[i]], pnoise[i, 0, :n].numpy())
+        werr = float(np.abs(wav[i, 0, :n] - ref).max())
+        worst_w = max(worst_w, werr)
+        assert werr <= WAV_TOL, (i, werr)
+    for i in range(B):
+        assert not wav[i, 0, mlens[i] * 256:].any(), i
+    print(f"C4 batch 64: {sum(o[4] for o in outs)} frames, worst mel error {worst:.2e}; PWGAN sampled rows {worst_w:.2e}")

@@ -209,3 +209,34 @@ def test_pwgan_oracle_matches_reference():
         y = orc.inference(fx[f"M{M}_mel"][0], fx[f"M{M}_noise"][0, 0])
         assert y.shape == fx[f"M{M}_wav"][0, 0].shape
         assert np.abs(y - fx[f"M{M}_wav"][0, 0]).max() <= 2e-6
+
+
+@pytest.mark.parametrize("r", [2, 1])
+def test_torch_cpu_baseline_tacotron2_matches_reference(r):
+    """bench.py's cpu_baseline (oracle/torch_cpu.py, the ATen op sequence) against the reference."""
+    from oracle.torch_cpu import TacoTorchCPU
+    fx = load_fixture("taco_sigmoid")
+    cfg, sd = taco_state_dict(fx, r=r)
+    m = TacoTorchCPU(sd, cfg.attn_norm, cfg.r)
+    for u in range(3):
+        k = f"r{r}_u{u}"
+        dec, post, align, stop = m.inference(fx[k + "_ids"], r, int(fx[f"r{r}_max_steps"]))
+        assert len(stop) == len(fx[k + "_stop"])
+        assert np.abs(dec - fx[k + "_dec"]).max() <= 1e-5
+        assert np.abs(post - fx[k + "_post"]).max() <= 1e-5
+        assert np.abs(align - fx[k + "_align"]).max() <= 1e-6
+        assert np.abs(stop - fx[k + "_stop"]).max() <= 1e-5
+
+
+@pytest.mark.parametrize("key", ["M7_p0", "M64_p0", "M5_p2", "M33_p2"])
+def test_torch_cpu_baseline_mbmelgan_matches_reference(key):
+    from oracle.torch_cpu import MelganTorchCPU
+    from tts_amd.pqmf import pqmf_filters
+    from tts_amd.spec import MelganConfig, melgan_layers, melgan_spec
+    from tts_amd.weights import synth_state_dict
+    fx = load_fixture("mbmelgan")
+    cfg = MelganConfig()
+    sd = synth_state_dict(melgan_spec(cfg, weight_norm=True), int(fx["seed"]))
+    m = MelganTorchCPU(sd, melgan_layers(cfg), pqmf_filters()[1])
+    wav = m.inference(fx[key + "_mel"][0], pad=int(key.split("_p")[1]))
+    assert np.abs(wav - fx[key + "_wav"].reshape(-1)).max() <= 1e-5

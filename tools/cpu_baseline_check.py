@@ -37,6 +37,7 @@ def main():
     from TTS.vocoder.models.multiband_melgan_generator import MultibandMelganGenerator
     from oracle.melgan_np import MelganOracle
     from oracle.taco_np import TacoOracle
+    from oracle.torch_cpu import MelganTorchCPU, TacoTorchCPU
     from tts_amd.pqmf import pqmf_filters
 
     torch.set_num_threads(args.threads)
@@ -88,10 +89,21 @@ def main():
         t2 = time.perf_counter()
         return p.shape[0], t1 - t0, t2 - t1, p
 
+    ta = TacoTorchCPU(tsd, tcfg.attn_norm, tcfg.r)
+    va = MelganTorchCPU(vsd, melgan_layers(vcfg), pqmf_filters()[1])
+
+    def aten_one(i):
+        t0 = time.perf_counter()
+        _, p, _, _ = ta.inference(ids[i], r, int(steps[i]))
+        t1 = time.perf_counter()
+        va.inference(p.T, pad=0)
+        t2 = time.perf_counter()
+        return p.shape[0], t1 - t0, t2 - t1, p
+
     res = {}
     j = int(np.argmin(steps))
     with threadpool_limits(limits=args.threads):
-        for name, fn in (("reference", ref_one), ("oracle", orc_one)):
+        for name, fn in (("reference", ref_one), ("aten_port", aten_one), ("oracle", orc_one)):
             fn(j)  # warm-up, excluded
             frames, tt, tv = 0, 0.0, 0.0
             posts = []
@@ -107,10 +119,16 @@ def main():
                          "e2e_rtf": round((tt + tv) / audio, 5)}
             res[name + "_posts"] = posts
             print(name, res[name], flush=True)
-    err = max(float(np.abs(a - b).max()) for a, b in zip(res.pop("reference_posts"), res.pop("oracle_posts")))
+    refp = res.pop("reference_posts")
+    err = max(float(np.abs(a - b).max()) for a, b in zip(refp, res.pop("oracle_posts")))
+    err_a = max(float(np.abs(a - b).max()) for a, b in zip(refp, res.pop("aten_port_posts")))
     out = {"r": r, "threads": args.threads, "utterances": len(ids), "torch": torch.__version__,
-           "cpu": open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": "),
-           "oracle_vs_reference_post_max_abs": err, **res,
+           "cpu": open("/proc/cpuinfo").read().split("model name")[1].split("\n")[0].strip(": \t"),
+           "oracle_vs_reference_post_max_abs": err, "aten_port_vs_reference_post_max_abs": err_a, **res,
+           "aten_port_over_reference_tacotron2": round(res["aten_port"]["tacotron2_frames_per_s"]
+                                                       / res["reference"]["tacotron2_frames_per_s"], 3),
+           "aten_port_over_reference_e2e": round(res["aten_port"]["e2e_frames_per_s"]
+                                                 / res["reference"]["e2e_frames_per_s"], 3),
            "oracle_over_reference_tacotron2": round(res["oracle"]["tacotron2_frames_per_s"]
                                                     / res["reference"]["tacotron2_frames_per_s"], 3),
            "oracle_over_reference_e2e": round(res["oracle"]["e2e_frames_per_s"] / res["reference"]["e2e_frames_per_s"], 3)}
