@@ -118,8 +118,18 @@ def cpu_baseline(tsd, vsd, tcfg, vcfg, ids, steps, r, budget_s):
         torch.set_num_threads(prev)
     el = t_taco + t_voc
     audio = frames * HOP / SAMPLE_RATE
+    calib = None  # this restatement timed beside the imported reference (build container, same weights)
+    cpath = os.path.join(ROOT, "profiles", "r03", f"cpu_baseline_check_r{r}.json")
+    if os.path.exists(cpath):
+        try:
+            cj = json.load(open(cpath))
+            calib = {"port_over_reference_e2e": cj["aten_port_over_reference_e2e"],
+                     "port_vs_reference_post_max_abs": cj["aten_port_vs_reference_post_max_abs"],
+                     "threads": cj["threads"], "source": os.path.relpath(cpath, ROOT)}
+        except Exception:
+            calib = None
     return {"value": round(frames / el, 1), "unit": "mel-frames/s", "cores": cores, "kind": "port",
-            "rtf": el / audio, "tacotron2_mel_frames_per_s": round(frames / t_taco, 1),
+            "rtf": el / audio, "tacotron2_mel_frames_per_s": round(frames / t_taco, 1), "calibration": calib,
             "sample": f"first {n} of {len(ids)} LJ-profile utterances, B=1 sequential, r={r}, forced length "
                       f"({frames} frames): Tacotron2 {t_taco:.1f} s + MB-MelGAN {t_voc:.1f} s, PyTorch-CPU "
                       f"restatement of the reference op sequence (oracle/torch_cpu.py), {cores} threads"}

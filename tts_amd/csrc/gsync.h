@@ -5,6 +5,22 @@
 // write-through past the per-XCD L2) and read with agent-scope loads (sc1, L1 bypass); every wave
 // drains its stores (vmcnt(0)) before the barrier arrival. Barrier waits give up after a limit
 // (error word set, every workgroup exits): a launch that is not co-resident fails loudly.
+//
+// Why relaxed arrivals and a relaxed go-word poll suffice (no release / acquire fences):
+//  * hardware: this is the hand-off form MI355X_MICROARCH.md ("Valid forms", inter-workgroup
+//    visibility) lists in place of a release / acquire pair: EVERY store of the handed-off bytes is
+//    sc1 (reaches the memory side, nothing dirty stays in an XCD L2 to write back) and is drained
+//    (s_waitcnt vmcnt(0)) by its wave before the workgroup barrier that precedes the counter add,
+//    and EVERY load of them is a global_/buffer_ sc1 load to registers issued after the poll and a
+//    workgroup barrier (never L1-served, so no stale line needs invalidating). An agent-scope
+//    release fetch_add would add buffer_wbl2 sc1 (~1.7 us per the guide) and an acquire load
+//    buffer_inv sc1 (+1.7 us measured on this kernel) to every one of the ~5
+//    barriers of a decoder step, for no data that is not already coherent;
+//  * compiler: every point where ordering matters is a compiler barrier: the drain is an asm with
+//    a "memory" clobber followed by __syncthreads(), and the wait ends in lds_barrier() (asm,
+//    "memory" clobber), so no load or store is moved across the arrival or the wait.
+// Plain (non-sc1) accesses of cross-workgroup data are therefore a bug in this scheme; every such
+// access goes through ldc / ldci / ldc4 / stc / stci below.
 // The wait limit sits in word BAR_TMO of each 512-word barrier block, written by arm_barrier at
 // launch: TTS_BARRIER_TIMEOUT_MS (default 2000 ms). The cooperative launch itself guarantees
 // co-residency; the limit only turns an over-admitted grid (occupancy API one workgroup per CU
