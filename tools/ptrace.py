@@ -53,3 +53,13 @@ if at is not None:
                       for i in items])
         print(f"step {s}: {len(items)} items; stamp times after P4 release (us): median / max")
         print("  " + " ".join(f"{labels[k]}={np.nanmedian(d[:, k]):.2f}/{np.nanmax(d[:, k]):.2f}" for k in range(8)))
+    # last arrivers: combine done (ctx written) -> their P4 work end (alignment pass + rest)
+    IW0 = 64
+    tails = []
+    for s in range(7):
+        for i in range(256 - IW0):
+            if at[s][i][7] > 0:
+                tails.append((a[s][5][IW0 + i] - at[s][i][7]) / 100.0)
+    if tails:
+        print("last arrivers: combine done -> P4 end (alignment pass): median %.2f max %.2f us" %
+              (np.median(tails), np.max(tails)))

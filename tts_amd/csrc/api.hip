@@ -339,6 +339,7 @@ struct TacoWS {
   DevBuf ids, post, map;       // rows in decode order (longest first); map = [perm | inverse]
   DevBuf stat;                 // status words for the host, laid out as tts_ctx::pinned (TS_*)
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
+  DevBuf anorm;                // persistent decoder: per-utterance attention normaliser (deferred alignment)
   DevBuf spk, spkid, spkb;     // speaker vectors (decode order), per-row biases [Bp][NSPK]
   DevBuf win_idx, fwd_u, apf;  // windowing argmax, transition probability, forward chunk sums
   DevBuf gh, gmu;              // Graves: N_a hidden (32 x 1024), mixture means (64 x 16)
@@ -873,6 +874,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<int>(W.stat, 256, g);
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
   grow<unsigned>(W.pbar, 2 * 512, g);  // one barrier block per persistent launch (MT = 2, 1)
+  grow<float>(W.anorm, (size_t)2 * BMAX, g);
   grow<float>(W.spk, (size_t)64 * 1024, g);
   grow<int>(W.win_idx, 64, g);
   grow<float>(W.gh, 32 * 1024, g);
@@ -1401,6 +1403,8 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.part_u = W.apu.f();
   a.counter = reinterpret_cast<unsigned*>(W.acnt.p);
   a.nchmax = (W.T_max + persist_attn_tc() - 1) / persist_attn_tc();
+  a.anorm = W.anorm.f();
+  a.defer_align = persist_defer_ok(W.B * a.nchmax) && !std::getenv("TTS_ALIGN_IN_P4");
   a.softmax = M.softmax;
   a.thr = thr;
   a.bar = reinterpret_cast<unsigned*>(W.pbar.p);

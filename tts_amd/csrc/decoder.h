@@ -165,6 +165,11 @@ struct PArgs {
   float* part_m;
   float* part_u;      // (B, nchmax, 512)
   unsigned* counter;  // (B)
+  // deferred alignment pass (plain location attention, items per workgroup <= PDEF_MAXIT): the last
+  // arriver publishes the step's normaliser S and max m per utterance here, and every item workgroup
+  // writes alpha / alpha_cum / the alignment row of its own positions in P6
+  float* anorm;       // (B, 2)
+  int defer_align;
   int nchmax;
   int softmax;
   float thr;
@@ -179,6 +184,7 @@ struct PArgs {
 
 bool persist_supported(int device);
 int persist_attn_tc();  // attention positions per work item (sizes the chunk-partial buffers)
+bool persist_defer_ok(int nitems);  // the deferred alignment pass has room for this many items
 // arm: zero the barrier block first (false: the caller armed it, e.g. in its state fill)
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm = true);
 

@@ -179,10 +179,12 @@ __device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* A
   lds_barrier();  // window reads done before the scratch is reused
 }
 
+// ekeep: (deferred alignment pass) LDS slot [32 energies | valid flag] of this item, kept until P6;
+// null: the last arriver runs the alignment pass itself (decoder variants, many items per workgroup)
 template <int MT, int VAR>
 __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
                                            int* is_last, float (&L)[8], bool haveL,
-                                           f32x4 (&evc)[pec_arr(VAR)], bool load_ev) {
+                                           f32x4 (&evc)[pec_arr(VAR)], bool load_ev, float* ekeep) {
   constexpr int PEC = pec_of(VAR);
   constexpr bool WIN = VAR & 1, FWD = (VAR & 2) != 0;  // compiled-in decoder variants
   constexpr int NT = PT, TC = PTC;
@@ -292,7 +294,13 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     }
     lds_barrier();
   }
-  if (tid < nvalid) stc(P.energy + (long)b * D.T_max + t0 + tid, sv[tid]);
+  if (ekeep) {  // the alignment pass runs in P6 from these (only the last arriver's combine reads
+                // other chunks, and it needs their partials, not their energies)
+    if (tid < TC) ekeep[tid] = sv[tid];
+    if (tid == 0) ekeep[TC] = 1.f;
+  } else if (tid < nvalid) {
+    stc(P.energy + (long)b * D.T_max + t0 + tid, sv[tid]);
+  }
   ATRACE(4);
   // chunk-local normalisation terms (computed once, shared through LDS)
   float m_c = -INFINITY;
@@ -363,8 +371,8 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   // depend on it, and vmcnt is in order, so they land while the partials are summed
   const long ab = (long)b * D.T_max;
   const int tt0 = min(tid, Tm1);
-  const float e_first = ldc(P.energy + ab + tt0);
-  const float acum_first = ldc(P.acum + ab + tt0);
+  const float e_first = ekeep ? 0.f : ldc(P.energy + ab + tt0);
+  const float acum_first = ekeep ? 0.f : ldc(P.acum + ab + tt0);
   // combine: chunk partials in batches of 8, all loads of a batch in flight (clamped)
   const long pb0 = (long)b * P.nchmax;
   constexpr int CB = 8;
@@ -406,6 +414,14 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   float ctx_v = cx / ((FWD && P.fwd) ? Fz : S);
   stc(P.ctx + frag_idx(b, tid, 512), ctx_v);
   ATRACE(7);
+  if (ekeep) {  // deferred alignment pass: publish the normaliser, the items finish in P6
+    if (tid == 0) {
+      stc(P.anorm + 2 * b, S);
+      stc(P.anorm + 2 * b + 1, m);
+      __hip_atomic_store(&P.counter[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    return;
+  }
   float bestv = -INFINITY;
   int besti = 0x7fffffff;
   // forward_attn_mask (common_layers.py:309-318): argmax of the shifted previous alignment
@@ -824,7 +840,9 @@ __device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], 
 constexpr size_t P_LDS_APRE = 96 * 64 * 16;
 constexpr size_t P_LDS_WC = 64 * 128 * 4;
 constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 17 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
-constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH;
+constexpr int PDEF_MAXIT = 8;  // attention items per workgroup the deferred alignment pass keeps
+constexpr size_t P_LDS_EKEEP = PDEF_MAXIT * (32 + 1) * 4;
+constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH + P_LDS_EKEEP;
 
 // phase timestamps of every workgroup for 8 steps (P.trace, optional): [step][16][256]
 // (0-9 phase boundaries, 10-15 points inside P5)
@@ -836,6 +854,7 @@ template <int MT, int VAR>
 __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   constexpr bool GRAVES = (VAR & 4) != 0;  // Graves attention replaces the location-sensitive one
   constexpr bool X3P = (VAR & 8) != 0;     // P3's attention_rnn prenet part on the split-f16 MFMA
+  constexpr bool DEFER = (VAR & 7) == 0;   // plain location attention: alignment pass deferred to P6
   extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
   __shared__ int sflag, is_last, dflag[64];
   constexpr int Bp = MT * 16;
@@ -845,6 +864,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   float* scr = wcomb + 64 * 128;
   float* red0 = scr;                   // [8][Bp][17]
   float* hs = red0 + 8 * Bp * 17;      // [Bp][17]
+  float* ekeep0 = scr + P_LDS_SCRATCH / 4;  // [PDEF_MAXIT][PTC + 1]: deferred alignment pass
   const int g = blockIdx.x, tid0 = threadIdx.x, lane0 = tid0 & 63;
   const int wave0 = __builtin_amdgcn_readfirstlane(tid0 >> 6);
   const int YP = P.ntj * 16;
@@ -1253,10 +1273,15 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       // only lengthen the attention chain; after it they overlap the other items' tails.
       if (g >= IW0) {  // items, then the decoder_rnn h_att part (attention_rnn's waits for P6)
         const int nitems = D.B * P.nchmax;
-        for (int it = g - IW0; it < nitems; it += PW - IW0) {
+        for (int it = g - IW0, k = 0; it < nitems; it += PW - IW0, ++k) {
+          float* ek = nullptr;
+          if (DEFER && P.defer_align) {
+            ek = ekeep0 + k * (PTC + 1);
+            if (tid == 0) ek[PTC] = 0.f;  // set by the item when its utterance is still decoding
+          }
           if constexpr (GRAVES) graves_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, &is_last);
           else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0,
-                                   evc, nitems > PW - IW0 || t == t_first);
+                                   evc, nitems > PW - IW0 || t == t_first, ek);
           lds_barrier();
         }
         // split-f16: the h_att part runs at the start of P5 instead (h_att is still in place), off
@@ -1401,6 +1426,26 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       if constexpr (!X3P)  // split-f16: done in P5 beside the decoder_rnn h_att part
         gemm_seg<MT, 8, 2>(acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
       att_epilogue(red0);
+      if (DEFER && P.defer_align) {
+        // deferred alignment pass (common_layers.py:347-357): this workgroup's items of step t, their
+        // own positions; S and m came from each utterance's last arriver in P4. Off the step's
+        // critical path: the item workgroups' P6 is short beside the projection jobs.
+        const int nitems = D.B * P.nchmax;
+        for (int it = g - IW0, k = 0; it < nitems; it += PW - IW0, ++k) {
+          const float* ek = ekeep0 + k * (PTC + 1);
+          const int b = it / P.nchmax, p0 = (it % P.nchmax) * PTC;
+          const int T = D.lens[b];
+          if (ek[PTC] == 0.f || tid >= min(PTC, T - p0)) continue;
+          const long ab = (long)b * D.T_max + p0 + tid;
+          const float S = ldc(P.anorm + 2 * b), m = ldc(P.anorm + 2 * b + 1);
+          const float e = ek[tid];
+          const float raw = P.softmax ? (e == -INFINITY ? 0.f : expf(e - m)) : 1.f / (1.f + expf(-e));
+          const float al = raw / S;
+          stc(P.acum + ab, ldc(P.acum + ab) + al);
+          stc(P.alpha + ab, al);
+          if (t < D.S_cap) D.align_out[((long)b * D.S_cap + t) * D.T_max + p0 + tid] = al;
+        }
+      }
     }
     PTRACE(9);
     gsync_arrive(P.bar, gen);
@@ -1417,6 +1462,7 @@ bool persist_supported(int device) {
 }
 
 int persist_attn_tc() { return PTC; }
+bool persist_defer_ok(int nitems) { return nitems <= (PW - IW0) * PDEF_MAXIT; }
 
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
   TTS_CHECK(MT == 1 || MT == 2, "persistent decoder: MT must be 1 or 2");
