@@ -125,8 +125,8 @@ static int check(int C, int d, float xscale) {
     }
   }
   const bool ok = err <= 4e-6 * std::max(1.0, mag) && untouched && of == (xscale > 1e4f ? 1u : 0u);
-  printf("check C=%3d d=%2d |x|~%-8g wide %d max|err| %.3e (max|y| %.3e) tail untouched %d oflow %u  %s\n", C, d,
-         xscale, (int)rb_wide(C), err, mag, (int)untouched, of, ok ? "OK" : "FAIL");
+  printf("check C=%3d d=%2d |x|~%-8g max|err| %.3e (max|y| %.3e) tail untouched %d oflow %u  %s\n", C, d, xscale, err,
+         mag, (int)untouched, of, ok ? "OK" : "FAIL");
   return ok ? 0 : 1;
 }
 
@@ -136,15 +136,11 @@ int main(int argc, char** argv) {
   const int prof_C = argc > 1 ? std::atoi(argv[1]) : 0;  // profiling mode: one stage, library tile only
   int fails = 0;
   if (!prof_C) {
-  for (int w : {0, 1}) {  // both kernels (g_rb_wide: 16x16x32 / 32x32x16 where C % 32 == 0)
-    g_rb_wide = w;
-    for (int C : {48, 96, 192})
-      for (int d : {1, 9, 27}) fails += check(C, d, 1.f);
-    for (int C : {32, 64, 128, 256}) fails += check(C, 3, 1.f);
-    fails += check(96, 3, 1e-3f);
-    fails += check(96, 3, 1e5f);  // out of the f16 range: must raise the flag
-  }
-  g_rb_wide = 0;
+  for (int C : {48, 96, 192})
+    for (int d : {1, 9, 27}) fails += check(C, d, 1.f);
+  for (int C : {32, 64, 128, 256}) fails += check(C, 3, 1.f);  // the full-band MelGAN stages
+  fails += check(96, 3, 1e-3f);
+  fails += check(96, 3, 1e5f);  // out of the f16 range: must raise the flag
   }
   int* lens;
   HIP_OK(hipMalloc(&lens, 32 * 4));
@@ -231,20 +227,15 @@ int main(int argc, char** argv) {
     timeit("fp32", [&] { launch_resblock(a, C, S); });
     timeit("split-f16 (library tile)", [&] { launch_resblock_x3(a, kM, C, S); });
     if (C == 192) {
-      timeit("x3 TQ64 12x1 (16x16x32)", [&] { launch_rbx3<192, 64, 12, 1, 3>(a, kM, S); });
-      timeit("w32 TQ64 6x1 (MI1 NI2)", [&] { launch_rbx3w<192, 64, 6, 1, 3>(a, kM, S); });
-      timeit("w32 TQ64 6x2 (MI1 NI1)", [&] { launch_rbx3w<192, 64, 6, 2, 3>(a, kM, S); });
-      timeit("w32 TQ64 3x2 (MI2 NI1)", [&] { launch_rbx3w<192, 64, 3, 2, 3>(a, kM, S); });
-      timeit("w32 TQ64 3x1 (MI2 NI2)", [&] { launch_rbx3w<192, 64, 3, 1, 3>(a, kM, S); });
-      timeit("w32 TQ64 6x1 R4", [&] { launch_rbx3w<192, 64, 6, 1, 4>(a, kM, S); });
-      timeit("w32 TQ64 6x1 R6", [&] { launch_rbx3w<192, 64, 6, 1, 6>(a, kM, S); });
+      timeit("x3 TQ64 12x1", [&] { launch_rbx3<192, 64, 12, 1, 3>(a, kM, S); });
+      timeit("x3 TQ64 4x2 (MI3 NI2)", [&] { launch_rbx3<192, 64, 4, 2, 3>(a, kM, S); });
+      timeit("x3 TQ64 4x1 (MI3 NI4)", [&] { launch_rbx3<192, 64, 4, 1, 3>(a, kM, S); });
+      timeit("x3 TQ64 6x2 (MI2 NI2)", [&] { launch_rbx3<192, 64, 6, 2, 3>(a, kM, S); });
     } else if (C == 96) {
-      timeit("x3 TQ96 6x2 (16x16x32)", [&] { launch_rbx3<96, 96, 6, 2, 3>(a, kM, S); });
-      timeit("w32 TQ96 3x3 (MI1 NI1)", [&] { launch_rbx3w<96, 96, 3, 3, 3>(a, kM, S); });
-      timeit("w32 TQ64 3x2 (MI1 NI1)", [&] { launch_rbx3w<96, 64, 3, 2, 3>(a, kM, S); });
-      timeit("w32 TQ64 3x1 (MI1 NI2)", [&] { launch_rbx3w<96, 64, 3, 1, 3>(a, kM, S); });
-      timeit("w32 TQ96 3x1 (MI1 NI3)", [&] { launch_rbx3w<96, 96, 3, 1, 3>(a, kM, S); });
-      timeit("w32 TQ96 3x3 R6", [&] { launch_rbx3w<96, 96, 3, 3, 6>(a, kM, S); });
+      timeit("x3 TQ128 6x2", [&] { launch_rbx3<96, 128, 6, 2, 3>(a, kM, S); });
+      timeit("x3 TQ96 6x2 (NI3)", [&] { launch_rbx3<96, 96, 6, 2, 3>(a, kM, S); });
+      timeit("x3 TQ96 2x2 (MI3 NI3)", [&] { launch_rbx3<96, 96, 2, 2, 3>(a, kM, S); });
+      timeit("x3 TQ128 2x4 (MI3 NI2)", [&] { launch_rbx3<96, 128, 2, 4, 3>(a, kM, S); });
     } else {
       timeit("x3 TQ128 3x4", [&] { launch_rbx3<48, 128, 3, 4, 3>(a, kM, S); });
       timeit("x3 TQ192 3x4 (NI3)", [&] { launch_rbx3<48, 192, 3, 4, 3>(a, kM, S); });

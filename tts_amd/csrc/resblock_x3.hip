@@ -22,7 +22,6 @@
 #include "split16.h"
 
 #include <algorithm>
-#include <cstdlib>
 
 namespace {
 constexpr int X3_DMAX = 27;   // largest dilation (3^3, num_res_blocks <= 4)
@@ -360,329 +359,11 @@ static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   resblock_x3_kernel<C, TQ, WM, WN, R><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles);
 }
 
-// ---------------------------------------------------------------------------------------------
-// The same block on v_mfma_f32_32x32x16_f16 (C a multiple of 32). Why: the 16x16x32 kernel above
-// reads 1 KiB of B operand from LDS per 8192 MACs and, with one m-tile per wave, keeps the CU's LDS
-// busier than its MFMA pipes (profiles/r03/v1_bench_pmc.txt: ~29 k ds_read_b128 per CU against
-// ~20 % MFMA occupancy at C = 192). A 32x32x16 MFMA does 16384 MACs per 1 KiB B fragment and per
-// 1 KiB A fragment, so the same tile moves half the LDS and weight bytes per MAC.
-//   staging   unchanged (32-channel chunks, [pos][32 hi | 32 lo | 16 pad]); a chunk is 2 k-steps of
-//             16 channels x 3 taps: k-step s = (chunk, tap, half) -> 6 per chunk
-//   phase 2   HX unchanged; k-steps of 16 over [lrelu(h) | x] (2C / 16)
-//   weights   A fragments [m32-tile][k-step][lane][hi 8 | lo 8] (pack_split_a32), same R-slot ring
-//   biases    staged once in LDS (a lane's 16 accumulator rows are 16 different channels)
-template <int C, int TQ, int WM, int WN, int R>
-__global__ __launch_bounds__(64 * WM * WN) void resblock_x3w_kernel(ResArgs a, int ntiles) {
-  constexpr int NTHR = 64 * WM * WN;
-  constexpr int MI = C / 32 / WM;
-  constexpr int NI = TQ / 32 / WN;
-  static_assert(MI * 32 * WM == C && NI * 32 * WN == TQ, "tile split");
-  constexpr int NCH = C / 32;
-  constexpr int NK1 = 6 * NCH;
-  constexpr int NK2 = 2 * C / 16;
-  constexpr int NTOT = NK1 + NK2;
-  static_assert(C % 32 == 0 && NK1 % R == 0 && NK2 % R == 0, "weight ring: R must divide both phases");
-  constexpr int HR = 4 * C + 16;
-  constexpr int SPT = (4 * (TQ + 2 * X3_DMAX) + NTHR - 1) / NTHR;
-  extern __shared__ __attribute__((aligned(16))) _Float16 sh[];
-
-  int t = blockIdx.x;
-  const int d = a.dil;
-  const int ROWS = TQ + 2 * d;
-  _Float16* X0 = sh;
-  _Float16* X1 = sh + ROWS * XR;
-  _Float16* HX = sh + 2 * ROWS * XR;
-  float* bsh = reinterpret_cast<float*>(HX + TQ * HR);  // [bd | bf]
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave / WN, wn = wave % WN;
-  const int nb = wn * 32 * NI + (lane & 31);  // this lane's position (B column) for ni = 0
-  const int kg = 8 * (lane >> 5);             // this lane's k offset inside a k-step
-  const int rg = 4 * (lane >> 5);             // this lane's accumulator row offset
-  const int mt0 = wm * MI;
-  bool bad = false;
-
-  __shared__ int tcum[65], tlen[64];
-  if (wave == 0) {
-    const int L = lane < a.B ? (a.lens[lane] + a.len_add) * a.mul : 0;
-    const int n = (L + TQ - 1) / TQ;
-    int v = n;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(v, o, 64);
-      if (lane >= o) v += y;
-    }
-    tcum[lane] = v - n;
-    tlen[lane] = L;
-    if (lane == 63) tcum[64] = v;
-  }
-  for (int i = tid; i < C; i += NTHR) {
-    bsh[i] = a.bd[i];
-    bsh[C + i] = a.bf[i];
-  }
-  lds_barrier();
-  auto tile_of = [&](int i) {
-    const bool hit = lane < a.B && tcum[lane] <= i && i < tcum[lane + 1];
-    const unsigned long long m = __ballot(hit);
-    const int b = __builtin_amdgcn_readfirstlane(m ? __ffsll((long long)m) - 1 : 0);
-    RbTile r;
-    r.b = b;
-    r.q0 = __builtin_amdgcn_readfirstlane((i - tcum[b]) * TQ);
-    r.L = __builtin_amdgcn_readfirstlane(tlen[b]);
-    return r;
-  };
-
-  int srow[SPT], sg[SPT];
-#pragma unroll
-  for (int j = 0; j < SPT; ++j) {
-    const int e = tid + NTHR * j;
-    sg[j] = e / ROWS;
-    srow[j] = e - sg[j] * ROWS;
-  }
-  float st[2][SPT][8];
-  auto stage_load = [&](const RbTile& T, float (&sr)[SPT][8], int ch) {
-    const __amdgpu_buffer_rsrc_t xr = rsrc(a.x + (long)T.b * a.sb);
-    const int i0 = T.q0 - d;
-    const bool interior = i0 >= 0 && i0 + ROWS <= T.L;
-#pragma unroll
-    for (int j = 0; j < SPT; ++j) {
-      int i = i0 + srow[j];
-      if (!interior) {  // reflection (torch ReflectionPad1d), then clamp
-        if (i < 0) i = -i;
-        if (i >= T.L) i = 2 * (T.L - 1) - i;
-        i = i < 0 ? 0 : (i >= T.L ? T.L - 1 : i);
-      }
-      const int c0 = 32 * ch + 8 * min(sg[j], 3);
-      const int vo = (c0 * a.Ls + i) * 4;
-#pragma unroll
-      for (int c = 0; c < 8; ++c)
-        sr[j][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, c * a.Ls * 4, 0));
-    }
-  };
-  auto stage_store = [&](_Float16* X, const float (&sr)[SPT][8], int ch) {
-#pragma unroll
-    for (int j = 0; j < SPT; ++j) {
-      const int g = sg[j], row = srow[j];
-      if (g < 4) {
-        float v[8], mx = 0.f;
-#pragma unroll
-        for (int c = 0; c < 8; ++c) {
-          v[c] = sr[j][c];
-          mx = fmaxf(mx, __builtin_fabsf(v[c]));
-        }
-        bad |= !(mx < F16_RANGE);
-        float lv[8];
-#pragma unroll
-        for (int c = 0; c < 8; ++c) lv[c] = lrelu_x3(v[c]);
-        h8 hi, lo;
-        split8(lv, hi, lo);
-        *reinterpret_cast<h8*>(X + row * XR + 8 * g) = hi;
-        *reinterpret_cast<h8*>(X + row * XR + 32 + 8 * g) = lo;
-        const int p = row - d;
-        if (p >= 0 && p < TQ) {
-          split8(v, hi, lo);
-          *reinterpret_cast<h8*>(HX + p * HR + C + 32 * ch + 8 * g) = hi;
-          *reinterpret_cast<h8*>(HX + p * HR + 3 * C + 32 * ch + 8 * g) = lo;
-        }
-      }
-    }
-  };
-
-  const __amdgpu_buffer_rsrc_t wdr = rsrc(a.Wd16), wfr = rsrc(a.Wf16);
-  const int wlo = lane * 32;
-  h8 ring[R][MI][2];
-  auto wload = [&](h8 (&r)[MI][2], int seq) {
-    if (seq >= NTOT) seq -= NTOT;
-    const bool p1 = seq < NK1;
-    const __amdgpu_buffer_rsrc_t wr = p1 ? wdr : wfr;
-    const int nk = p1 ? NK1 : NK2;
-    const int ks = p1 ? seq : seq - NK1;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-      const int so = ((mt0 + mi) * nk + ks) * 2048;
-      r[mi][0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo, so, 0));
-      r[mi][1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo + 16, so, 0));
-    }
-  };
-
-  if (t >= ntiles) return;
-  RbTile cur = tile_of(t);
-  stage_load(cur, st[0], 0);
-#pragma unroll
-  for (int u = 0; u < R; ++u) wload(ring[u], u);
-  if (NCH > 1) stage_load(cur, st[1], 1);
-  stage_store(X0, st[0], 0);
-  if (NCH > 2) stage_load(cur, st[0], 2);
-  lds_barrier();
-  f32x16 am[MI][NI], ac[MI][NI];
-  constexpr bool EARLY = NCH % 2 == 0;
-  for (;;) {
-    const int tn = t + gridDim.x;
-    const bool more = tn < ntiles;
-    const RbTile nxt = more ? tile_of(tn) : cur;
-    if (EARLY && NCH == 2) stage_load(nxt, st[0], 0);
-    // ---------------- phase 1: h = Wd . lrelu(x) ----------------
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) am[mi][ni][j] = ac[mi][ni][j] = 0.f;
-#pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
-      const _Float16* X = (ch & 1) ? X1 : X0;
-#pragma unroll
-      for (int kq = 0; kq < 3; ++kq) {
-#pragma unroll
-        for (int hf = 0; hf < 2; ++hf) {
-          const int s1 = (ch * 3 + kq) * 2 + hf;
-          const int sl = s1 % R;
-          h8 bh[NI], bl[NI];
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni) {
-            const _Float16* p = X + (nb + ni * 32 + kq * d) * XR + 16 * hf + kg;
-            bh[ni] = *reinterpret_cast<const h8*>(p);
-            bl[ni] = *reinterpret_cast<const h8*>(p + 32);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-          for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-            for (int ni = 0; ni < NI; ++ni)
-              mfma32_x3(ring[sl][mi][0], ring[sl][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-          wload(ring[sl], s1 + R);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-      if (ch + 1 < NCH) stage_store((ch & 1) ? X0 : X1, st[(ch + 1) & 1], ch + 1);
-      if (ch + 3 < NCH) stage_load(cur, st[(ch + 1) & 1], ch + 3);
-      else if (EARLY && ch + 3 - NCH < 2) stage_load(nxt, st[(ch + 1) & 1], ch + 3 - NCH);
-      lds_barrier();
-    }
-    // lrelu(h + b_d), split, into HX[pos][0:C) (hi) and HX[pos][2C:3C) (lo): a lane's rows come in
-    // runs of 4 consecutive channels -> one 8-byte store per run and half
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const int co = (mt0 + mi) * 32 + 8 * q + rg;
-        const f32x4 bd4 = *reinterpret_cast<const f32x4*>(bsh + co);
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          h4 hi, lo;
-#pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            _Float16 h, l;
-            split_dev(lrelu_x3(x3_value(am[mi][ni][4 * q + j], ac[mi][ni][4 * q + j]) + bd4[j]), h, l, bad);
-            hi[j] = h;
-            lo[j] = l;
-          }
-          const int p = nb + ni * 32;
-          *reinterpret_cast<h4*>(HX + p * HR + co) = hi;
-          *reinterpret_cast<h4*>(HX + p * HR + 2 * C + co) = lo;
-        }
-      }
-#pragma unroll
-      for (int ni = 0; ni < NI; ++ni)
-#pragma unroll
-        for (int j = 0; j < 16; ++j) am[mi][ni][j] = ac[mi][ni][j] = 0.f;
-    }
-    lds_barrier();
-    if (!EARLY) {
-      stage_load(nxt, st[0], 0);
-      if (NCH > 1) stage_load(nxt, st[1], 1);
-    }
-    // ---------------- phase 2: y = [W1 | Wsc] . [lrelu(h); x] ----------------
-#pragma unroll
-    for (int k0 = 0; k0 < NK2; k0 += R) {
-#pragma unroll
-      for (int u = 0; u < R; ++u) {
-        const int kc = k0 + u;
-        h8 bh[NI], bl[NI];
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const _Float16* p = HX + (nb + ni * 32) * HR + kc * 16 + kg;
-          bh[ni] = *reinterpret_cast<const h8*>(p);
-          bl[ni] = *reinterpret_cast<const h8*>(p + 2 * C);
-        }
-        __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-        for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni) mfma32_x3(ring[u][mi][0], ring[u][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-        wload(ring[u], NK1 + kc + R);
-      }
-    }
-    float* yb = a.y + (long)cur.b * a.sb;
-#pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
-#pragma unroll
-      for (int i = 0; i < 16; ++i) {
-        const int co = (mt0 + mi) * 32 + (i & 3) + 8 * (i >> 2) + rg;
-        const float bf = bsh[C + co];
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const int q = cur.q0 + nb + ni * 32;
-          if (q < cur.L) yb[(long)co * a.Ls + q] = x3_value(am[mi][ni][i], ac[mi][ni][i]) + bf;
-        }
-      }
-    }
-    if (!more) break;
-    lds_barrier();
-    cur = nxt;
-    t = tn;
-    stage_store(X0, st[0], 0);
-    if (NCH > 2) stage_load(cur, st[0], 2);
-    lds_barrier();
-  }
-  if (bad) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
-template <int C, int TQ, int WM, int WN, int R>
-static void launch_rbx3w(const ResArgs& a, const int* h_lens, hipStream_t s) {
-  const int ROWS = TQ + 2 * a.dil;
-  const size_t lds = ((size_t)2 * ROWS * XR + (size_t)TQ * (4 * C + 16)) * 2 + (size_t)2 * C * 4;
-  static int ncu = 0;
-  if (!ncu) {
-    HIP_OK(hipFuncSetAttribute((const void*)resblock_x3w_kernel<C, TQ, WM, WN, R>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, RB_DYN_LDS));
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
-  TTS_CHECK(lds <= RB_DYN_LDS, "resblock_x3w: LDS tile too large");
-  long ntiles = 0;
-  for (int b = 0; b < a.B; ++b) ntiles += ((long)(h_lens[b] + a.len_add) * a.mul + TQ - 1) / TQ;
-  TTS_CHECK(ntiles < (1L << 30), "resblock_x3w: too many tiles");
-  if (ntiles == 0) return;
-  const int grid = (int)std::min<long>(ntiles, ncu);
-  resblock_x3w_kernel<C, TQ, WM, WN, R><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles);
-}
-
 bool resblock_x3_supported(int C) { return C == 256 || C == 192 || C == 128 || C == 96 || C == 64 || C == 48 || C == 32; }
-
-// Which kernel a channel count runs (packing and launch must agree). The 32x32x16 kernel measured
-// slower at every C2 shape (tools/rbx3_bench.hip, DESIGN.md 4.3: C = 192 best 762 vs 692 us, C = 96
-// 1151 vs 882 us for 4 blocks), so it runs only when forced: g_rb_wide = 1 (TTS_RB_WIDE=1 for the
-// library, or the benchmark), and only for C a multiple of 32.
-int g_rb_wide = [] {
-  const char* e = std::getenv("TTS_RB_WIDE");
-  return e ? std::atoi(e) : 0;
-}();
-static bool rb_wide(int C) { return g_rb_wide == 1 && C % 32 == 0; }
 
 // host packing of one block's split weights: Wd (C, C, 3) [co][ci][k] and Wf (C, 2C) [co][k]
 void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf, int C,
                       std::vector<uint16_t>& wd16, std::vector<uint16_t>& wf16) {
-  if (rb_wide(C)) {  // k-step of 16: (chunk of 32 channels, tap, half)
-    wd16 = pack_split_a32(C / 32, 6 * (C / 32), [&](int m, int k) -> float {
-      const int step = k / 16, ch = step / 6, kq = (step % 6) / 2, hf = step % 2, ci = 32 * ch + 16 * hf + k % 16;
-      return wd[((size_t)m * C + ci) * 3 + kq];
-    });
-    wf16 = pack_split_a32(C / 32, 2 * C / 16, [&](int m, int k) -> float { return wf[(size_t)m * 2 * C + k]; });
-    return;
-  }
   const int nch = (C + 31) / 32;
   wd16 = pack_split_a(C / 16, 3 * nch, [&](int m, int k) -> float {
     const int step = k / 32, ch = step / 3, kq = step % 3, ci = 32 * ch + k % 32;
@@ -696,20 +377,6 @@ void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t 
   TTS_CHECK(a.Wd16 && a.Wf16 && a.oflow, "resblock_x3: split weights / overflow flag missing");
   TTS_CHECK(a.B <= 64, "resblock_x3: at most 64 utterances per call");
   if (a.max_q <= 0 || a.B <= 0) return;
-  if (rb_wide(C)) {
-    switch (C) {
-      // best tiles of tools/rbx3_bench.hip (C2 shapes)
-      case 192: launch_rbx3w<192, 64, 6, 2, 3>(a, h_lens, s); break;
-      case 96: launch_rbx3w<96, 64, 3, 2, 3>(a, h_lens, s); break;
-      case 256: launch_rbx3w<256, 32, 8, 1, 4>(a, h_lens, s); break;
-      case 128: launch_rbx3w<128, 64, 4, 2, 4>(a, h_lens, s); break;
-      case 64: launch_rbx3w<64, 128, 2, 4, 2>(a, h_lens, s); break;
-      case 32: launch_rbx3w<32, 192, 1, 6, 2>(a, h_lens, s); break;
-      default: TTS_CHECK(false, "resblock_x3w: unsupported channel count");
-    }
-    HIP_OK(hipGetLastError());
-    return;
-  }
   switch (C) {
     // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave
     case 192: launch_rbx3<192, 64, 12, 1, 3>(a, h_lens, s); break;

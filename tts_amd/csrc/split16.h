@@ -79,20 +79,6 @@ std::vector<uint16_t> pack_split_a(int mtiles, int ksteps, F f) {
   return out;
 }
 
-// The same for v_mfma_f32_32x32x16_f16 (32-row tiles, 16-column k-steps): element j of lane l is
-// W[32 mt + (l & 31)][16 ks + 8 (l >> 5) + j]; blocks [mt][ks] of 64 lanes x 32 bytes.
-template <class F>
-std::vector<uint16_t> pack_split_a32(int mtiles, int ksteps, F f) {
-  std::vector<uint16_t> out((size_t)mtiles * ksteps * 64 * 16);
-  for (int mt = 0; mt < mtiles; ++mt)
-    for (int ks = 0; ks < ksteps; ++ks)
-      for (int l = 0; l < 64; ++l) {
-        uint16_t* o = &out[(((size_t)mt * ksteps + ks) * 64 + l) * 16];
-        for (int j = 0; j < 8; ++j) split_host(f(32 * mt + (l & 31), 16 * ks + 8 * (l >> 5) + j), o[j], o[8 + j]);
-      }
-  return out;
-}
-
 #ifdef __HIPCC__
 typedef _Float16 h8 __attribute__((ext_vector_type(8)));
 typedef _Float16 h4 __attribute__((ext_vector_type(4)));
@@ -109,19 +95,6 @@ __device__ __forceinline__ void mfma_x3(const h8& ah, const h8& al, const h8& bh
   ac = MFMA_H(al, bh, ac);
 }
 __device__ __forceinline__ float x3_value(float am, float ac) { return am + ac * SPLIT_INV; }
-
-// 32x32 output, K = 16 (v_mfma_f32_32x32x16_f16, 32 cycles per SIMD): twice the MACs of the
-// 16x16x32 form per operand byte. Lane maps (cdna_hip_programming.md, 32x32x16): A[m = l & 31]
-// [k = 8 (l >> 5) + j], B[k = 8 (l >> 5) + j][n = l & 31]; D element i of lane l is row
-// (i & 3) + 8 (i >> 2) + 4 (l >> 5), column l & 31.
-typedef float f32x16 __attribute__((ext_vector_type(16)));
-#define MFMA32_H(a, b, c) __builtin_amdgcn_mfma_f32_32x32x16_f16((a), (b), (c), 0, 0, 0)
-__device__ __forceinline__ void mfma32_x3(const h8& ah, const h8& al, const h8& bh, const h8& bl, f32x16& am,
-                                          f32x16& ac) {
-  am = MFMA32_H(ah, bh, am);
-  ac = MFMA32_H(ah, bl, ac);
-  ac = MFMA32_H(al, bh, ac);
-}
 
 // device split of one value (no range check): v_cvt_f16_f32 for hi, and lo as one
 // v_fma_mixlo_f16: 2^11 v - 2^11 hi is exact in fp32, so lo takes a single rounding
