@@ -13,6 +13,10 @@
  *   tts_taco_encoder              <- embedding + Encoder.inference (models/tacotron2.py:144-145,
  *                                    layers/tacotron2.py:112-119)
  *   tts_taco_postnet              <- Postnet + residual (models/tacotron2.py:159-160)
+ *   tts_taco_decoder_state        <- the decoder state the reference leaves on `self` after inference
+ *                                    (query, attention_rnn_cell_state, decoder_hidden, decoder_cell,
+ *                                    context, attention_weights(_cum): layers/tacotron2.py:217-233,
+ *                                    259-298; common_layers.py:251-260): per-stage decoder parity
  *   tts_melgan_set_tensor/finalize<- MultibandMelganGenerator.load_state_dict + remove_weight_norm
  *                                    (TTS/server/synthesizer.py:81-91, melgan_generator.py:91-97)
  *   tts_melgan_infer              <- MultibandMelganGenerator.inference (multiband_melgan_generator.py:32-39)
@@ -102,6 +106,15 @@ int tts_taco_encoder(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, 
 int tts_taco_postnet(tts_ctx* ctx, const float* d_dec, const int32_t* h_lens, int B, int M_max, float* d_out,
                      void* stream);
 
+/* Decoder state after the last decoder step of the previous tts_taco_infer* call on this context
+   (persistent decoder path), rows in the caller's order: attention_rnn h and c (B, 1024),
+   decoder_rnn h and c (B, 1024), context (B, 512), attention weights and cumulative weights
+   (B, T_max). Rows that stopped before the call's last step hold the state the batched decode left
+   in them, not their own final state: compare rows that ran the call's full step count. Any output
+   pointer may be NULL (skipped). */
+int tts_taco_decoder_state(tts_ctx* ctx, float* d_att_h, float* d_att_c, float* d_dec_h, float* d_dec_c,
+                           float* d_context, float* d_alpha, float* d_alpha_cum, void* stream);
+
 /* ---- MultiBand-MelGAN generator ---- */
 int tts_melgan_set_tensor(tts_ctx* ctx, const char* name, const float* h_data, const int64_t* shape, int ndim);
 /* upsample_factors: n_up entries (even), base_channels, num_res_blocks, out_channels (4 with PQMF) */
@@ -174,9 +187,10 @@ int tts_ge2e_infer(tts_ctx* ctx, const float* d_x, const int32_t* h_lens, int B,
    which: 0 = decoder LSTM GEMM step kernel (K4), 1 = full decoder step (all 7 kernels). */
 int tts_time_decoder_kernel(tts_ctx* ctx, int which, int iters, float* ms_out);
 
-/* Decoder launches of the last tts_taco_infer: path 1 = persistent kernel (one cooperative
-   launch per batch-tile count, nlaunch <= 2; ms[i] = hipEvent time of launch i, steps[i] =
-   decoder steps it completed), path 0 = step graphs (nlaunch = 0). */
+/* Decoder launches of the last tts_taco_infer: path 1 = persistent kernel (one launch per
+   batch-tile count, 64 / 48 / 32 / 16 rows, nlaunch <= 4: ms and steps must hold 4 entries;
+   ms[i] = hipEvent time of launch i, steps[i] = decoder steps it completed), path 0 = step
+   graphs (nlaunch = 0). */
 int tts_decoder_stats(tts_ctx* ctx, int* path, int* nlaunch, float* ms, int* steps);
 
 /* GEMM arithmetic of the context's kernels. mode 1 (default) = split-f16 MFMA where a kernel has

@@ -235,7 +235,7 @@ class TacoOracle:
                  + sd["decoder.stopnet.1.linear_layer.bias"]).astype(F32)[0]
         return y, st["alpha"], logit
 
-    def decoder_inference(self, inputs, r, max_steps, stop_threshold=0.5, return_logits=False):
+    def decoder_inference(self, inputs, r, max_steps, stop_threshold=0.5, return_logits=False, return_state=False):
         """Decoder.inference (tacotron2.py:335-374) at B=1 (stop iff sigma>thr and t>0)."""
         F = self.F
         T = inputs.shape[0]
@@ -262,6 +262,10 @@ class TacoOracle:
         res = (dec, np.array(stops, F32), np.stack(aligns))
         if return_logits:
             res = res + (np.array(logits, F32),)
+        if return_state:  # what the reference leaves on `self` (layers/tacotron2.py:217-233)
+            res = res + ({"query": st["q"], "attention_rnn_cell_state": st["qc"], "decoder_hidden": st["h"],
+                          "decoder_cell": st["c"], "context": st["ctx"], "attention_weights": st["alpha"],
+                          "attention_weights_cum": st["alpha_cum"]},)
         return res
 
     def postnet(self, dec):
@@ -271,6 +275,11 @@ class TacoOracle:
         for i in range(5):
             o = self.conv_bn_block(f"postnet.convolutions.{i}", o, "tanh" if i < 4 else None)
         return (x + o).T.astype(F32)
+
+    def decoder_state(self, ids, r, max_steps, stop_threshold=0.5):
+        """The decoder state after Tacotron2.inference (one utterance), as the reference keeps it."""
+        enc = self.encoder(np.asarray(ids))
+        return self.decoder_inference(enc, r, max_steps, stop_threshold, return_state=True)[-1]
 
     def inference(self, ids, r, max_steps=1000, stop_threshold=0.5, speaker=None):
         """Tacotron2.inference (models/tacotron2.py:142-163) for one utterance. ``speaker``: the

@@ -172,6 +172,31 @@ def taco_case(name, cfg, seed, utt_lens, r_list, max_steps, min_stopping, id_see
     np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
 
 
+def taco_state_case(name, seed=61, id_seed=62):
+    """The decoder state the reference leaves on `self` after Tacotron2.inference (query,
+    attention_rnn_cell_state, decoder_hidden, decoder_cell, context, attention weights and their
+    cumulative sum: layers/tacotron2.py:217-233,259-298, common_layers.py:251-260), after exactly n
+    decoder steps (stop bias -1e4, max_decoder_steps = n), for per-stage decoder parity."""
+    cfg = TacotronConfig(attn_norm="sigmoid")
+    m = build_taco(cfg, seed, -1e4)
+    rs = np.random.RandomState(id_seed)
+    utts = [rs.randint(1, cfg.num_chars, size=T).astype(np.int64) for T in (15, 29)]
+    out = {"seed": np.int64(seed), "cfg": json.dumps(cfg.__dict__), "overrides": json.dumps(STOP_GAIN)}
+    for r, n in ((2, 1), (2, 7), (1, 4)):
+        for u, ids in enumerate(utts):
+            run_taco(m, ids, r, n)
+            d = m.decoder
+            k = f"r{r}_n{n}_u{u}"
+            out[k + "_ids"] = ids
+            for a, v in (("query", d.query), ("attention_rnn_cell_state", d.attention_rnn_cell_state),
+                         ("decoder_hidden", d.decoder_hidden), ("decoder_cell", d.decoder_cell),
+                         ("context", d.context), ("attention_weights", d.attention.attention_weights),
+                         ("attention_weights_cum", d.attention.attention_weights_cum)):
+                out[f"{k}_{a}"] = v[0].detach().numpy().astype(np.float32)
+        print(f"[{name}] r={r} n={n}: |h_dec| {np.abs(out[k + '_decoder_hidden']).max():.3f}")
+    np.savez_compressed(os.path.join(HERE, name + ".npz"), **out)
+
+
 def vocoder_case(name, seed):
     c = MelganConfig()
     v = MultibandMelganGenerator(in_channels=c.in_channels, out_channels=c.out_channels,
@@ -421,6 +446,8 @@ if __name__ == "__main__":
         glow_case("glow_tdsep", "time-depth-separable", seed=27, data_seed=28)
     if "glow_tfm" in which:
         glow_case("glow_tfm", "transformer", seed=33, data_seed=30)  # seed 29: all durations 0
+    if "taco_state" in which:
+        taco_state_case("taco_state")
     if "taco_amplified" in which:
         # SURVEY 7 "mildly amplified" decoder regime: LSTM weights x2.1, projection x10, attention v x6
         # (|mel| ~9). fp32-vs-fp64 drift grows to 3-5e-6 (r=2) / 1-3e-5 (r=1) over the decode, 20-200x

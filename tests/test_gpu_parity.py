@@ -1420,3 +1420,99 @@ def test_c4_glow_pwgan_batch64_vs_oracle():
     for i in range(B):
         assert not wav[i, 0, mlens[i] * 256:].any(), i
     print(f"C4 batch 64: {sum(o[4] for o in outs)} frames, worst mel error {worst:.2e}; PWGAN sampled rows {worst_w:.2e}")
+
+
+@pytest.mark.parametrize("B", [64, 48])
+def test_tacotron2_persistent_64_row_batch_vs_oracle(B):
+    """Batches of 33-64 rows run on the persistent decoder (batch tiles of 64 / 48 rows, then 32 and
+    16 as rows finish: launches with MT = 4 or 3, 2, 1) instead of the step graphs: every row against
+    its B = 1 oracle run, ragged lengths and forced step counts with the long rows scattered."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd._lib import get_engine
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=29, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    r = 2
+    m.decoder.set_r(r)
+    rs = np.random.RandomState(B)
+    lens = [int(x) for x in rs.randint(1, 60, B)]
+    steps = [int(x) for x in rs.randint(2, 12, B)]
+    for i in range(5, B, 11):
+        steps[i] = 30 + i % 7
+    batch = np.zeros((B, max(lens)), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, L)
+    dec, post, align, stop = m.inference(torch.from_numpy(batch).cuda(), text_lengths=lens, max_decoder_steps=steps)
+    assert list(m.last_steps) == steps
+    path, launches = get_engine("cuda:0").decoder_stats()
+    assert path == 1 and len(launches) == (B + 15) // 16, launches
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    dec, post, align = dec.cpu().numpy(), post.cpu().numpy(), align.cpu().numpy()
+    for i, L in enumerate(lens):
+        d, p, a, _ = orc.inference(batch[i, :L], r, steps[i])
+        n = steps[i] * r
+        assert np.abs(dec[i, :n] - d).max() <= MEL_TOL, i
+        assert np.abs(post[i, :n] - p).max() <= MEL_TOL, i
+        assert np.abs(align[i, :steps[i], :L] - a).max() <= 1e-5, i
+        assert not post[i, n:].any()
+
+
+def test_tacotron2_multispeaker_40_rows_vs_oracle():
+    """Multi-speaker decoding (external 256-d embeddings, models/tacotron2.py:152-155) above the
+    former 32-row cap: 40 rows in one call (batch tiles 48 -> 32 -> 16), each row against the oracle
+    with its own speaker vector."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig(num_speakers=2, speaker_embedding_dim=256)
+    _, sd = taco_state_dict(None, seed=31, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    r = 2
+    m.decoder.set_r(r)
+    B = 40
+    rs = np.random.RandomState(40)
+    lens = [int(x) for x in rs.randint(3, 40, B)]
+    steps = [int(x) for x in rs.randint(3, 20, B)]
+    emb = rs.randn(B, 256).astype(np.float32)
+    emb /= np.linalg.norm(emb, axis=1, keepdims=True)
+    batch = np.zeros((B, max(lens)), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, L)
+    _, post, _, _ = m.inference(torch.from_numpy(batch).cuda(), text_lengths=lens, max_decoder_steps=steps,
+                                speaker_embeddings=torch.from_numpy(emb).cuda())
+    assert list(m.last_steps) == steps
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    post = post.cpu().numpy()
+    for i, L in enumerate(lens):
+        _, p, _, _ = orc.inference(batch[i, :L], r, steps[i], speaker=emb[i])
+        assert np.abs(post[i, :steps[i] * r] - p).max() <= MEL_TOL, i
+
+
+@pytest.mark.parametrize("r,n", [(2, 1), (2, 7), (1, 4)])
+def test_tacotron2_decoder_state_matches_reference(r, n):
+    """Per-stage decoder parity through tts_taco_decoder_state: after exactly n decoder steps (both
+    fixture utterances in one batched call, forced to n steps), the attention_rnn and decoder_rnn
+    LSTM states, the context and the attention weights / cumulative weights equal the state the
+    reference leaves on `self` (layers/tacotron2.py:217-233,259-298; common_layers.py:251-260)."""
+    _dev()
+    fx = load_fixture("taco_state")
+    cfg, sd = taco_state_dict(fx, stop_bias=-1e4)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(r)
+    ids = [fx[f"r{r}_n{n}_u{u}_ids"] for u in range(2)]
+    batch = np.zeros((2, max(len(x) for x in ids)), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    m.inference(torch.from_numpy(batch).cuda(), text_lengths=[len(x) for x in ids], max_decoder_steps=n)
+    assert list(m.last_steps) == [n, n]
+    st = {k: v.cpu().numpy() for k, v in m.decoder_state().items()}
+    for u in range(2):
+        k = f"r{r}_n{n}_u{u}"
+        L = len(ids[u])
+        for a in ("query", "attention_rnn_cell_state", "decoder_hidden", "decoder_cell", "context"):
+            assert np.abs(st[a][u] - fx[f"{k}_{a}"]).max() <= 1e-5, (k, a)
+        for a in ("attention_weights", "attention_weights_cum"):
+            assert np.abs(st[a][u, :L] - fx[f"{k}_{a}"]).max() <= 1e-5, (k, a)
+            assert not st[a][u, L:].any(), (k, a)

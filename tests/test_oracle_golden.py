@@ -240,3 +240,21 @@ def test_torch_cpu_baseline_mbmelgan_matches_reference(key):
     m = MelganTorchCPU(sd, melgan_layers(cfg), pqmf_filters()[1])
     wav = m.inference(fx[key + "_mel"][0], pad=int(key.split("_p")[1]))
     assert np.abs(wav - fx[key + "_wav"].reshape(-1)).max() <= 1e-5
+
+
+STATE_KEYS = ("query", "attention_rnn_cell_state", "decoder_hidden", "decoder_cell", "context",
+              "attention_weights", "attention_weights_cum")
+
+
+@pytest.mark.parametrize("r,n", [(2, 1), (2, 7), (1, 4)])
+def test_tacotron2_oracle_decoder_state_matches_reference(r, n):
+    """Per-stage decoder parity: the state the reference leaves on `self` after n decoder steps
+    (tests/golden/taco_state.npz) against the oracle's."""
+    fx = load_fixture("taco_state")
+    cfg, sd = taco_state_dict(fx, stop_bias=-1e4)
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for u in range(2):
+        k = f"r{r}_n{n}_u{u}"
+        st = orc.decoder_state(fx[k + "_ids"], r, n)
+        for a in STATE_KEYS:
+            assert np.abs(st[a] - fx[f"{k}_{a}"]).max() <= 1e-6, (k, a)

@@ -42,6 +42,7 @@ SIGNATURES = [
     ("tts_taco_set_options", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_taco_encoder", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_taco_postnet", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
+    ("tts_taco_decoder_state", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("tts_melgan_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
     ("tts_melgan_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int]),
@@ -193,6 +194,17 @@ class Engine:
         lens_a, lens_p = _i32(lens)
         _check(self.lib.tts_taco_postnet(self.h, _ptr(dec), lens_p, B, M, _ptr(out), _stream(dec.device)))
 
+    def taco_decoder_state(self, B, T_max, device):
+        """Decoder state after the last Tacotron2 decode (tts_taco_decoder_state), caller row order."""
+        import torch
+        out = {k: torch.empty(B, n, device=device) for k, n in
+               (("query", 1024), ("attention_rnn_cell_state", 1024), ("decoder_hidden", 1024),
+                ("decoder_cell", 1024), ("context", 512), ("attention_weights", T_max),
+                ("attention_weights_cum", T_max))}
+        with self.lock:
+            _check(self.lib.tts_taco_decoder_state(self.h, *[_ptr(out[k]) for k in out], _stream(device)))
+        return out
+
     def load_pwgan(self, tensors: Dict[str, np.ndarray], num_res_blocks, stacks, upsample_factors):
         for k, v in tensors.items():
             self._set(self.lib.tts_pwgan_set_tensor, k, v)
@@ -258,8 +270,8 @@ class Engine:
     def decoder_stats(self):
         """(path, [(ms, steps) per persistent launch]) of the last Tacotron2 decode."""
         path, n = ctypes.c_int(0), ctypes.c_int(0)
-        ms = (ctypes.c_float * 2)()
-        st = (ctypes.c_int * 2)()
+        ms = (ctypes.c_float * 4)()   # up to 4 persistent launches (batch tiles of 64, 48, 32, 16 rows)
+        st = (ctypes.c_int * 4)()
         _check(self.lib.tts_decoder_stats(self.h, ctypes.byref(path), ctypes.byref(n), ms, st))
         return int(path.value), [(float(ms[i]), int(st[i])) for i in range(n.value)]
 

@@ -324,8 +324,9 @@ struct TacoModel {
 // Tacotron2 status words (TacoWS::stat on the device, tts_ctx::pinned on the host; one copy after
 // the call): BiLSTM barrier errors (2), persistent-decoder barrier errors (one per launch), the
 // decoder results (done, steps, status per decode row), the range flag, the launches' end steps
-constexpr int TS_ENC = 16, TS_DEC = 18, TS_RES = 20, TS_FLAG = TS_RES + 3 * BMAX, TS_END = TS_FLAG + 1,
-              TS_N = TS_END + 2;
+constexpr int PMAX_LAUNCH = 4;  // persistent decoder launches per decode (MT = 4, 3, 2, 1)
+constexpr int TS_ENC = 16, TS_DEC = 18, TS_RES = TS_DEC + PMAX_LAUNCH, TS_FLAG = TS_RES + 3 * BMAX,
+              TS_END = TS_FLAG + 1, TS_N = TS_END + PMAX_LAUNCH;
 static_assert(TS_N <= 256, "status words fit the pinned block");
 
 struct TacoWS {
@@ -454,11 +455,11 @@ struct tts_ctx {
   int device = 0;
   hipStream_t s = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_chunk[2] = {nullptr, nullptr};
-  hipEvent_t ev_dec[3] = {nullptr, nullptr, nullptr};  // around the persistent decoder launches
+  hipEvent_t ev_dec[PMAX_LAUNCH + 1] = {};  // around the persistent decoder launches
   int* pinned = nullptr;  // [256]: [0:4) chunk polling, [12] range flag, [TS_*]: status words of the last
                           // Tacotron2 call (one copy of TacoWS::stat)
   bool flag_read = false; // the entry point already fetched the range flag into pinned[12]
-  int dec_end[2] = {0, 0};  // step index after each persistent launch of the last decode
+  int dec_end[PMAX_LAUNCH] = {};  // step index after each persistent launch of the last decode
   int dec_path = 0;       // last decode: 0 = step graphs, 1 = persistent kernel
   // GEMM arithmetic: true = split-f16 MFMA kernels where built (fp32-accurate, split16.h), false =
   // fp32 MFMA everywhere (tts_set_gemm_mode; TTS_GEMM=f32 in the environment starts a context so)
@@ -873,11 +874,11 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<int>(W.map, 2 * BMAX, g);
   grow<int>(W.stat, 256, g);
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
-  grow<unsigned>(W.pbar, 2 * 512, g);  // one barrier block per persistent launch (MT = 2, 1)
+  grow<unsigned>(W.pbar, PMAX_LAUNCH * 512, g);  // one barrier block per persistent launch (MT = 4 .. 1)
   grow<float>(W.anorm, (size_t)2 * BMAX, g);
   grow<float>(W.spk, (size_t)64 * 1024, g);
   grow<int>(W.win_idx, 64, g);
-  grow<float>(W.gh, 32 * 1024, g);
+  grow<float>(W.gh, 64 * 1024, g);
   grow<float>(W.gmu, 64 * 16, g);
   grow<float>(W.fwd_u, 64, g);
   grow<int64_t>(W.spkid, 64, g);
@@ -1059,7 +1060,7 @@ __global__ void bcast_rows_kernel(const float* src, int n, float* dst, int rows)
 //   out[m][n] = base[n] + sum_e spk[m][e] WT[e][n]   (m < B; rows B..Bp-1 get base[n])
 // base = 0 on the attention_rnn / decoder_rnn / processed-inputs columns, the projection bias on
 // the projection columns [pj0, N). With no speaker (Es = 0) only the projection columns are built.
-constexpr int SPK_BMAX = 32;
+constexpr int SPK_BMAX = 64;
 __global__ __launch_bounds__(256) void spk_bias_kernel(const float* __restrict__ spk, int B, int Es,
                                                        const float* __restrict__ WT, int N,
                                                        const float* __restrict__ pjb, int pj0, int Bp,
@@ -1214,6 +1215,26 @@ __global__ void taco_setup_kernel(TacoSetup a, int* map, int* lens, int* ctl) {
   }
 }
 
+// decoder state in the caller's row order (tts_taco_decoder_state): fragment-order activations
+// (h_att, h_dec, ctx) and row-major cells / attention rows of decode row inv[b] -> row b
+__global__ void taco_state_kernel(const float* hatt, const float* catt, const float* hdec, const float* cdec,
+                                  const float* ctx, const float* alpha, const float* acum, const int* inv, int T_max,
+                                  float* o_ha, float* o_ca, float* o_hd, float* o_cd, float* o_ctx, float* o_al,
+                                  float* o_ac) {
+  const int b = blockIdx.y, m = inv[b];
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 1024; k += gridDim.x * blockDim.x) {
+    if (o_ha) o_ha[(long)b * 1024 + k] = hatt[frag_idx(m, k, 1024)];
+    if (o_ca) o_ca[(long)b * 1024 + k] = catt[(long)m * 1024 + k];
+    if (o_hd) o_hd[(long)b * 1024 + k] = hdec[frag_idx(m, k, 1024)];
+    if (o_cd) o_cd[(long)b * 1024 + k] = cdec[(long)m * 1024 + k];
+    if (o_ctx && k < 512) o_ctx[(long)b * 512 + k] = ctx[frag_idx(m, k, 512)];
+  }
+  for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < T_max; k += gridDim.x * blockDim.x) {
+    if (o_al) o_al[(long)b * T_max + k] = alpha[(long)m * T_max + k];
+    if (o_ac) o_ac[(long)b * T_max + k] = acum[(long)m * T_max + k];
+  }
+}
+
 // decode-order mel lengths for the postnet (steps * r), from the decoder results on the device
 __global__ void taco_mlens_kernel(const int* ctl, int B, int r, int* mlens) {
   const int i = threadIdx.x;
@@ -1225,8 +1246,8 @@ __global__ void taco_status_kernel(const unsigned* enc_bar, const unsigned* dec_
                                    const unsigned* flag, int* st) {
   const int i = threadIdx.x;
   if (i < 3 * BMAX) st[TS_RES + i] = ctl[4 + i];
-  if (i < 2) {
-    st[TS_ENC + i] = enc_bar ? (int)enc_bar[i * 512 + 16] : 0;
+  if (i < 2) st[TS_ENC + i] = enc_bar ? (int)enc_bar[i * 512 + 16] : 0;
+  if (i < PMAX_LAUNCH) {
     st[TS_DEC + i] = dec_bar && i < ndec ? (int)dec_bar[i * 512 + 16] : 0;
   }
   if (i == 0) st[TS_FLAG] = flag ? (int)*flag : 0;
@@ -1309,7 +1330,7 @@ void build_pj(tts_ctx* c, int r) {
 bool use_persistent(tts_ctx* c) {
   const char* e = std::getenv("TTS_DECODER");
   if (e && std::string(e) == "graph") return false;
-  return c->tws.MT <= 2 && persist_supported(c->device);
+  return c->tws.MT <= PMAX_LAUNCH && persist_supported(c->device);
 }
 
 // the whole decode as one cooperative launch per batch-tile count (decoder_persist.hip)
@@ -1339,8 +1360,15 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     const int pj0 = M.spk_dim ? 8320 : 0;
     const int Bp = W.MT * 16;
     grow<float>(W.spkb, (size_t)64 * (8320 + 112 * 16), W.gen);
-    TTS_CHECK(W.B <= SPK_BMAX || !M.spk_dim, "multi-speaker decoding: at most 32 utterances per call");
+    TTS_CHECK(W.B <= SPK_BMAX || !M.spk_dim, "multi-speaker decoding: at most 64 utterances per call");
     const int Bs = M.spk_dim ? W.B : 0;
+    static bool spk_attr = false;  // 64 rows of a 512-d speaker vector: 128 KiB of dynamic LDS
+    if (!spk_attr) {
+      HIP_OK(hipFuncSetAttribute((const void*)spk_bias_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                 SPK_BMAX * 512 * 4));
+      spk_attr = true;
+    }
+    TTS_CHECK(M.spk_dim <= 512, "speaker vectors of at most 512 dims");
     spk_bias_kernel<<<(N + 255) / 256, 256, (size_t)Bs * M.spk_dim * 4, s>>>(
         W.spk.f(), Bs, M.spk_dim, M.spk_dim ? M.spk_wT.f() : nullptr, N, M.pj_b.f(), pj0, Bp, W.spkb.f());
     HIP_OK(hipGetLastError());
@@ -1494,13 +1522,13 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   W.thr = thr;
   // speaker vectors in decode order: external embeddings, or rows of the learned table
   TTS_CHECK(!M.variant() || use_persistent(c), "BN prenet / attention windowing / forward / Graves attention run on "
-                                               "the persistent decoder only (<= 32 utterances per call on a 256-CU "
+                                               "the persistent decoder only (<= 64 utterances per call on a 256-CU "
                                                "device)");
   TTS_CHECK(!(M.graves && M.spk_dim), "Graves attention with speaker embeddings is not supported (its weights do "
                                       "not sum to 1, so the speaker columns do not fold into biases)");
   if (M.spk_dim) {
     TTS_CHECK(d_spk_ids || d_spk_emb, "multi-speaker model: speaker ids or speaker embeddings are required");
-    TTS_CHECK(use_persistent(c), "multi-speaker decoding runs on the persistent decoder only (<= 32 utterances "
+    TTS_CHECK(use_persistent(c), "multi-speaker decoding runs on the persistent decoder only (<= 64 utterances "
                                  "per call on a 256-CU device)");
     if (d_spk_emb) {
       gather_rows<float>(d_spk_emb, W.spk.f(), d_map, M.spk_dim, B, s);
@@ -1611,14 +1639,14 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     TTS_CHECK(!W.enc_persist || (pin[TS_ENC] == 0 && pin[TS_ENC + 1] == 0),
               "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past "
               "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
-    TTS_CHECK(!persist || (pin[TS_DEC] == 0 && pin[TS_DEC + 1] == 0),
+    TTS_CHECK(!persist || (pin[TS_DEC] == 0 && pin[TS_DEC + 1] == 0 && pin[TS_DEC + 2] == 0 && pin[TS_DEC + 3] == 0),
               "persistent decoder: grid barrier timed out (workgroups not co-resident) or preempted past "
               "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
     if (c->gemm_x3) {  // with_x3_fallback reads the flag from here
       pin[12] = pin[TS_FLAG];
       c->flag_read = true;
     }
-    for (int i = 0; i < 2; ++i) c->dec_end[i] = persist && i < c->dec_nlaunch ? pin[TS_END + i] : 0;
+    for (int i = 0; i < PMAX_LAUNCH; ++i) c->dec_end[i] = persist && i < c->dec_nlaunch ? pin[TS_END + i] : 0;
   }
   const int* res = c->pinned + TS_RES;
   for (int i = 0; i < B; ++i) {
@@ -2730,7 +2758,8 @@ int tts_ctx_destroy(tts_ctx* c) {
     {
       DeviceGuard g(dev);
       hipStream_t s = c->s;
-      hipEvent_t e[7] = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1], c->ev_dec[0], c->ev_dec[1], c->ev_dec[2]};
+      std::vector<hipEvent_t> e = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1]};
+      for (auto ev : c->ev_dec) e.push_back(ev);
       int* pin = c->pinned;
       delete c;
       for (auto ev : e) (void)hipEventDestroy(ev);
@@ -2855,6 +2884,30 @@ int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int 
       run_postnet(c, d_dec, (long)M_max * 80, W.mlens.i(), B, M_max, maxM, d_out, (long)M_max * 80, c->s);
     });
     HIP_OK(hipStreamSynchronize(c->s));
+    leave(c, stream);
+  });
+}
+
+int tts_taco_decoder_state(tts_ctx* c, float* d_att_h, float* d_att_c, float* d_dec_h, float* d_dec_c,
+                           float* d_context, float* d_alpha, float* d_alpha_cum, void* stream) {
+  return guarded_ctx(c, [&] {
+    TTS_CHECK(c, "null ctx");
+    TTS_CHECK(c->last_B > 0, "run tts_taco_infer first");
+    TTS_CHECK(c->dec_path == 1 && c->dec_nlaunch >= 1, "decoder state: the last decode did not run the persistent "
+                                                       "decoder (TTS_DECODER=graph or a non-256-CU device)");
+    DeviceGuard g(c->device);
+    auto& W = c->tws;
+    // the last executed step t_end - 1 wrote h_dec into hdec[(t_end - 1) & 1 ? 0 : 1]
+    // (decoder_persist.hip P5: hd_nxt = (t & 1) ? hdec0 : hdec1)
+    const int t_end = c->dec_end[c->dec_nlaunch - 1];
+    TTS_CHECK(t_end >= 1, "decoder state: no decoder step ran");
+    const float* hdec = ((t_end - 1) & 1) ? W.hdec0.f() : W.hdec1.f();
+    enter(c, stream);
+    taco_state_kernel<<<dim3(4, c->last_B), 256, 0, c->s>>>(W.hatt.f(), W.catt.f(), hdec, W.cdec.f(), W.ctx.f(),
+                                                            W.alpha.f(), W.acum.f(), W.map.i() + BMAX, c->last_T,
+                                                            d_att_h, d_att_c, d_dec_h, d_dec_c, d_context, d_alpha,
+                                                            d_alpha_cum);
+    HIP_OK(hipGetLastError());
     leave(c, stream);
   });
 }

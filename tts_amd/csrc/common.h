@@ -131,7 +131,7 @@ void swizzle_rows16(const float* Wm, int rows, int rows_pad, int Kdim, float* ds
 // Several buffer fills as ONE launch (each hipMemsetAsync is a ~5 us kernel of its own): entries
 // are (pointer, bytes, 32-bit fill word); bytes a multiple of 4, entries must not overlap.
 struct FillList {
-  static constexpr int N = 24;
+  static constexpr int N = 32;  // the decoder state fill: 14 buffers + 3 per barrier block (4 launches)
   int n = 0;
   void* p[N];
   long words[N];

@@ -49,9 +49,10 @@ constexpr int YROWS = 64;    // rows per projection half (independent of the bat
                              // launch reads what the MT = 2 launch left)
 // encoder rows (of 8 per thread) an attention item keeps in registers across steps: 4 where the
 // kernel stays within 256 VGPRs without spills (split-f16 variants without forward attention), 0
-// elsewhere; pec_arr sizes the (unused) array of the latter
-constexpr int pec_of(int VAR) { return ((VAR & 8) && !(VAR & 2)) ? 4 : 0; }
-constexpr int pec_arr(int VAR) { return pec_of(VAR) > 0 ? pec_of(VAR) : 1; }
+// elsewhere (and for 48 / 64-row batch tiles, whose accumulators need the registers); pec_arr
+// sizes the (unused) array of the latter
+constexpr int pec_of(int VAR, int MT) { return ((VAR & 8) && !(VAR & 2) && MT <= 2) ? 4 : 0; }
+constexpr int pec_arr(int VAR, int MT) { return pec_of(VAR, MT) > 0 ? pec_of(VAR, MT) : 1; }
 constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = NATT;  // NPQ_: query-projection partials
 }  // namespace
 
@@ -77,6 +78,18 @@ __device__ __forceinline__ void acc_to_lds(float* part, int w, int lane, const f
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
     for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
+}
+// chunk c (m-tiles CM c .. CM c + CM - 1) of a wave's MT accumulators into LDS [wave][CM * 16][17]:
+// reductions over the waves go in chunks of at most 2 m-tiles (32 rows, the scratch's size), so
+// MT = 3, 4 (48 / 64 rows) reuse the MT = 2 scratch; rows past MT stay stale and are not read
+template <int MT, int CM>
+__device__ __forceinline__ void acc_chunk_to_lds(float* part, int w, int lane, const f32x4 (&acc)[MT], int c) {
+  float* p = part + w * CM * 16 * 17;
+#pragma unroll
+  for (int mt = 0; mt < CM; ++mt)
+    if (c * CM + mt < MT)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[c * CM + mt][j];
 }
 template <int KS, int Bp>
 __device__ __forceinline__ float lds_sum(const float* part, int m, int n) {
@@ -184,8 +197,8 @@ __device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* A
 template <int MT, int VAR>
 __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
                                            int* is_last, float (&L)[8], bool haveL,
-                                           f32x4 (&evc)[pec_arr(VAR)], bool load_ev, float* ekeep) {
-  constexpr int PEC = pec_of(VAR);
+                                           f32x4 (&evc)[pec_arr(VAR, MT)], bool load_ev, float* ekeep) {
+  constexpr int PEC = pec_of(VAR, MT);
   constexpr bool WIN = VAR & 1, FWD = (VAR & 2) != 0;  // compiled-in decoder variants
   constexpr int NT = PT, TC = PTC;
   constexpr int NPT = NPQ_ / 16;  // query partials per thread (16 groups)
@@ -839,7 +852,7 @@ __device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], 
 // LDS: [att-pre weights 96 x 1 KiB][Wcomb 64 x 128][scratch: GEMM reduction + hs | attention]
 constexpr size_t P_LDS_APRE = 96 * 64 * 16;
 constexpr size_t P_LDS_WC = 64 * 128 * 4;
-constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 32 * 17 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
+constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 64 * 17 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
 constexpr int PDEF_MAXIT = 8;  // attention items per workgroup the deferred alignment pass keeps
 constexpr size_t P_LDS_EKEEP = PDEF_MAXIT * (32 + 1) * 4;
 constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH + P_LDS_EKEEP;
@@ -858,12 +871,16 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
   __shared__ int sflag, is_last, dflag[64];
   constexpr int Bp = MT * 16;
+  constexpr int CM = MT < 2 ? MT : 2;            // m-tiles per LDS reduction chunk
+  constexpr int CB = CM * 16;                    // rows per chunk
+  constexpr int NCK = (MT + CM - 1) / CM;        // chunks (1 for MT <= 2)
+  constexpr int JR = (X3P && MT > 2) ? 4 : 2;    // projection jobs per tile (row blocks / K halves)
   const DecDev& D = P.D;
   f32x4* Wap = smem4;                                              // [96][64]
   float* wcomb = reinterpret_cast<float*>(smem4) + 96 * 64 * 4;    // [64][128]
   float* scr = wcomb + 64 * 128;
-  float* red0 = scr;                   // [8][Bp][17]
-  float* hs = red0 + 8 * Bp * 17;      // [Bp][17]
+  float* red0 = scr;                   // [8][CB][17]
+  float* hs = red0 + 8 * 32 * 17;      // [Bp][17]
   float* ekeep0 = scr + P_LDS_SCRATCH / 4;  // [PDEF_MAXIT][PTC + 1]: deferred alignment pass
   const int g = blockIdx.x, tid0 = threadIdx.x, lane0 = tid0 & 63;
   const int wave0 = __builtin_amdgcn_readfirstlane(tid0 >> 6);
@@ -913,21 +930,24 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   };
   // epilogue constants: decoder_rnn biases of this thread's (row, unit) item, attention_rnn
   // ctx/h-part bias of its column
-  float db[4];
+  float db[NCK][4];
 #pragma unroll
-  for (int q = 0; q < 4; ++q) {  // + the row's speaker part (W_dec,s s, api.hip spk_bias_kernel)
-    db[q] = P.dec_b[g * 16 + q * 4 + (tid & 3)];
-    if (P.spk_dec) db[q] += P.spk_dec[(long)min(tid >> 2, Bp - 1) * P.spk_ld + g * 16 + q * 4 + (tid & 3)];
-  }
+  for (int c = 0; c < NCK; ++c)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {  // + the row's speaker part (W_dec,s s, api.hip spk_bias_kernel)
+      db[c][q] = P.dec_b[g * 16 + q * 4 + (tid & 3)];
+      if (P.spk_dec)
+        db[c][q] += P.spk_dec[(long)min(c * CB + (tid >> 2), Bp - 1) * P.spk_ld + g * 16 + q * 4 + (tid & 3)];
+    }
   const float apb = P.apre_b[g * 16 + (tid & 15)];
   __syncthreads();
 
   unsigned gen = 0;
   float Lr[8];  // location features of the first attention item (attn_loc in P1, used in P4)
-  f32x4 evc[pec_arr(VAR)];  // encoder rows of the first attention item (loaded on its first step)
+  f32x4 evc[pec_arr(VAR, MT)];  // encoder rows of the first attention item (loaded on its first step)
   const int t_first = D.ctl->base;
   int t = t_first;
-  const int pj_jobs = 2 * P.ntj;
+  const int pj_jobs = (X3P && MT > 2 ? 4 : 2) * P.ntj;
   const int pj = g - PJ_WG0;  // projection job of this workgroup (P6), if 0 <= pj < pj_jobs
   const bool is_pj = pj >= 0 && pj < pj_jobs;
   // prenet layer-2 weight chunks of this wave
@@ -950,13 +970,18 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   // attention_rnn ctx/h tile g complete: reduce over the waves, add the biases, publish the next
   // step's gate addends, reset the accumulator
   auto att_epilogue = [&](float* red) {
-    acc_to_lds<MT>(red, wave, lane, acca);
-    lds_barrier();
-    for (int idx = tid; idx < Bp * 16; idx += PT) {
-      const int m = idx >> 4, n = idx & 15;
-      float v = lds_sum<NWV, Bp>(red, m, n) + apb;
-      if (P.spk_att) v += P.spk_att[(long)m * P.spk_ld + g * 16 + n];  // speaker part of the new ctx
-      stc(P.gatt + (long)m * 4096 + g * 16 + n, v);
+#pragma unroll
+    for (int c = 0; c < NCK; ++c) {
+      acc_chunk_to_lds<MT, CM>(red, wave, lane, acca, c);
+      lds_barrier();
+      for (int idx = tid; idx < CB * 16; idx += PT) {
+        const int m = c * CB + (idx >> 4), n = idx & 15;
+        if (m >= Bp) break;
+        float v = lds_sum<NWV, CB>(red, idx >> 4, n) + apb;
+        if (P.spk_att) v += P.spk_att[(long)m * P.spk_ld + g * 16 + n];  // speaker part of the new ctx
+        stc(P.gatt + (long)m * 4096 + g * 16 + n, v);
+      }
+      if (NCK > 1) lds_barrier();
     }
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -986,7 +1011,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (g < 32 && (g >> 4) < MT) {  // prenet layer 2: tile g & 15, batch rows 16 (g >> 4) .. + 15, whole K
+    if (g < 16 * MT) {  // prenet layer 2: tile g & 15, batch rows 16 (g >> 4) .. + 15, whole K
       const int tl2 = g & 15, mt = g >> 4;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
       // t = 0: the prenet input is the zero go-frame: layer 1 gives relu(b1') (BN prenet) or 0
@@ -1064,15 +1089,19 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     gsync_arrive(P.bar, gen);
     // P3 operands that are already final: its epilogue's gate addends (written by P5 of the
     // previous step), c_att, the query-projection weights
-    float ga[4], ca, wq[4];
+    float ga[NCK][4], ca[NCK], wq[4];
     {
-      const int idx = min(tid, 4 * Bp * 4 - 1);
-      const int gl = idx / (Bp * 4), rem = idx % (Bp * 4);
-      const int m = rem >> 2, u = rem & 3;
+      const int idx = min(tid, 4 * CB * 4 - 1);
+      const int gl = idx / (CB * 4), rem = idx % (CB * 4);
+      const int u = rem & 3;
       const int tile = 4 * min(g, NATT - 1) + gl;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) ga[q] = ldc(P.gatt + (long)m * 4096 + tile * 16 + q * 4 + u);
-      ca = P.catt[(long)m * 1024 + tile * 4 + u];
+      for (int c = 0; c < NCK; ++c) {
+        const int m = min(c * CB + (rem >> 2), Bp - 1);
+#pragma unroll
+        for (int q = 0; q < 4; ++q) ga[c][q] = ldc(P.gatt + (long)m * 4096 + tile * 16 + q * 4 + u);
+        ca[c] = P.catt[(long)m * 1024 + tile * 4 + u];
+      }
 #pragma unroll
       // query-projection B operand: Wq^T rows 16 g + 4 q + (lane >> 4), attention dim 16 wave + (lane & 15)
       for (int q = 0; q < 4; ++q)
@@ -1121,95 +1150,112 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         // split-f16 A fragments [MT][8 k-steps][64 lanes][hi | lo]; wave w stages k-step w: lane L
         // holds row L & 15, k = 32 w + 8 (L >> 4) + 0..7, i.e. two fp32 fragments of pb's
         // 16-column chunk 2 w + (L >> 5), lanes l1 and l1 + 16 (frag_idx order)
+        // (MT > 2: two passes of 2 m-tiles each, the staging area holds 32 rows)
         h8* xs = reinterpret_cast<h8*>(wcomb);
         const int l1 = 32 * ((lane >> 4) & 1) + (lane & 15);
         bool bad = false;
-#pragma unroll
-        for (int mt = 0; mt < MT; ++mt) {
-          const int c = mt * 16 + 2 * wave + (lane >> 5);
-          const f32x4 x0 = ldc4(P.pb, (c * 64 + l1) * 16);
-          const f32x4 x1 = ldc4(P.pb, (c * 64 + l1 + 16) * 16);
-          float v[8];
-          float mx = 0.f;
-#pragma unroll
-          for (int q = 0; q < 4; ++q) {
-            v[q] = fmaxf(x0[q], 0.f), v[4 + q] = fmaxf(x1[q], 0.f);
-            mx = fmaxf(mx, fmaxf(v[q], v[4 + q]));
-          }
-          bad |= !(mx < F16_RANGE);
-          h8 hi, lo;
-          split8(v, hi, lo);
-          xs[((mt * 8 + wave) * 64 + lane) * 2] = hi;
-          xs[((mt * 8 + wave) * 64 + lane) * 2 + 1] = lo;
-        }
-        if (bad) __hip_atomic_fetch_or(P.x3flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        lds_barrier();
-        PTRACE(13);
         // waves 2j, 2j+1: tile 4g + j, K halves (4 k-steps each)
         f32x4 am[MT], ac[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) am[mt] = ac[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int i = 0; i < ATTP_NC / 2; ++i) {
-          h8 xh[MT], xl[MT];
+        for (int ps = 0; ps < NCK; ++ps) {
+          if (ps > 0) lds_barrier();  // the previous pass's operand reads are done
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const int ks = 4 * (wave & 1) + i;
-            xh[mt] = xs[((mt * 8 + ks) * 64 + lane) * 2];
-            xl[mt] = xs[((mt * 8 + ks) * 64 + lane) * 2 + 1];
+          for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt) {
+            const int c = mt * 16 + 2 * wave + (lane >> 5);
+            const f32x4 x0 = ldc4(P.pb, (c * 64 + l1) * 16);
+            const f32x4 x1 = ldc4(P.pb, (c * 64 + l1 + 16) * 16);
+            float v[8];
+            float mx = 0.f;
+#pragma unroll
+            for (int q = 0; q < 4; ++q) {
+              v[q] = fmaxf(x0[q], 0.f), v[4 + q] = fmaxf(x1[q], 0.f);
+              mx = fmaxf(mx, fmaxf(v[q], v[4 + q]));
+            }
+            bad |= !(mx < F16_RANGE);
+            h8 hi, lo;
+            split8(v, hi, lo);
+            xs[(((mt - ps * CM) * 8 + wave) * 64 + lane) * 2] = hi;
+            xs[(((mt - ps * CM) * 8 + wave) * 64 + lane) * 2 + 1] = lo;
           }
+          lds_barrier();
+          PTRACE(13);
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) mfma_x3(xh[mt], xl[mt], wx[i][0], wx[i][1], am[mt], ac[mt]);
+          for (int i = 0; i < ATTP_NC / 2; ++i) {
+            h8 xh[CM], xl[CM];
+#pragma unroll
+            for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt) {
+              const int ks = 4 * (wave & 1) + i;
+              xh[mt - ps * CM] = xs[(((mt - ps * CM) * 8 + ks) * 64 + lane) * 2];
+              xl[mt - ps * CM] = xs[(((mt - ps * CM) * 8 + ks) * 64 + lane) * 2 + 1];
+            }
+#pragma unroll
+            for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt)
+              mfma_x3(xh[mt - ps * CM], xl[mt - ps * CM], wx[i][0], wx[i][1], am[mt], ac[mt]);
+          }
         }
+        if (bad) __hip_atomic_fetch_or(P.x3flag, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
           for (int j = 0; j < 4; ++j) acc[mt][j] = x3_value(am[mt][j], ac[mt][j]);
       } else {
-        f32x4* xs = reinterpret_cast<f32x4*>(wcomb);  // [MT * 16 chunks][64 lanes]
+        f32x4* xs = reinterpret_cast<f32x4*>(wcomb);  // [CM * 16 chunks][64 lanes] per pass
 #pragma unroll
-        for (int i = 0; i < 2; ++i)
+        for (int ps = 0; ps < NCK; ++ps) {
+          if (ps > 0) lds_barrier();
 #pragma unroll
-          for (int mt = 0; mt < MT; ++mt) {
-            const int c = mt * 16 + 2 * wave + i;
-            f32x4 x = ldc4(P.pb, (c * 64 + lane) * 16);
+          for (int i = 0; i < 2; ++i)
 #pragma unroll
-            for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
-            xs[c * 64 + lane] = x;
+            for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt) {
+              const int c = mt * 16 + 2 * wave + i;
+              f32x4 x = ldc4(P.pb, (c * 64 + lane) * 16);
+#pragma unroll
+              for (int q = 0; q < 4; ++q) x[q] = fmaxf(x[q], 0.f);
+              xs[(c - ps * CM * 16) * 64 + lane] = x;
+            }
+          lds_barrier();
+          PTRACE(13);
+          // waves 2j, 2j+1: tile 4g + j, K halves (8 chunks each)
+#pragma unroll
+          for (int i = 0; i < ATTP_NC; ++i) {
+            f32x4 x[CM];
+#pragma unroll
+            for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt)
+              x[mt - ps * CM] = xs[((mt - ps * CM) * 16 + 8 * (wave & 1) + i) * 64 + lane];
+#pragma unroll
+            for (int q = 0; q < 4; ++q)
+#pragma unroll
+              for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt)
+                acc[mt] = MFMA16(x[mt - ps * CM][q], wa[i][q], acc[mt]);
           }
-        lds_barrier();
-        PTRACE(13);
-        // waves 2j, 2j+1: tile 4g + j, K halves (8 chunks each)
-#pragma unroll
-        for (int i = 0; i < ATTP_NC; ++i) {
-          f32x4 x[MT];
-#pragma unroll
-          for (int mt = 0; mt < MT; ++mt) x[mt] = xs[(mt * 16 + 8 * (wave & 1) + i) * 64 + lane];
-#pragma unroll
-          for (int q = 0; q < 4; ++q)
-#pragma unroll
-            for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[mt][q], wa[i][q], acc[mt]);
         }
       }
       PTRACE(10);
-      acc_to_lds<MT>(red0 + (wave >> 1) * 2 * Bp * 17, wave & 1, lane, acc);
-      lds_barrier();
-      if (tid < 4 * Bp * 4) {
-        const int gl = tid / (Bp * 4), rem = tid % (Bp * 4);
-        const int m = rem >> 2, u = rem & 3;
-        const int tile = 4 * g + gl;
-        const float* pg = red0 + gl * 2 * Bp * 17;
-        float pre[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<2, Bp>(pg, m, q * 4 + u) + ga[q];
-        const long ci = (long)m * 1024 + tile * 4 + u;
-        const float c = sigm_f(pre[1]) * ca + sigm_f(pre[0]) * tanh_f(pre[2]);
-        const float h = sigm_f(pre[3]) * tanh_f(c);
-        P.catt[ci] = c;
-        stc(P.hatt + frag_idx(m, tile * 4 + u, 1024), h);
-        hs[m * 17 + gl * 4 + u] = h;
+      for (int ck = 0; ck < NCK; ++ck) {
+        acc_chunk_to_lds<MT, CM>(red0 + (wave >> 1) * 2 * CB * 17, wave & 1, lane, acc, ck);
+        lds_barrier();
+        if (tid < 4 * CB * 4) {
+          const int gl = tid / (CB * 4), rem = tid % (CB * 4);
+          const int m = ck * CB + (rem >> 2), u = rem & 3;
+          const int tile = 4 * g + gl;
+          const float* pg = red0 + gl * 2 * CB * 17;
+          if (m < Bp) {
+            float pre[4];
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pre[q] = lds_sum<2, CB>(pg, rem >> 2, q * 4 + u) + ga[ck][q];
+            const long ci = (long)m * 1024 + tile * 4 + u;
+            const float c = sigm_f(pre[1]) * ca[ck] + sigm_f(pre[0]) * tanh_f(pre[2]);
+            const float h = sigm_f(pre[3]) * tanh_f(c);
+            P.catt[ci] = c;
+            stc(P.hatt + frag_idx(m, tile * 4 + u, 1024), h);
+            hs[m * 17 + gl * 4 + u] = h;
+          }
+        }
+        lds_barrier();
       }
-      lds_barrier();
       PTRACE(11);
       if (!GRAVES) {  // partial query projection over this workgroup's 16 units
         // on the MFMA: wave w owns attention dims 16 w .. 16 w + 15, K = this workgroup's 16 units
@@ -1250,14 +1296,18 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) acc[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
         gemm_seg<MT, 8, 2>(acc, P.hatt, 64, 8 * wave, lane, [&](int i) { return wn[i]; });
-        acc_to_lds<MT>(red0, wave, lane, acc);
-        lds_barrier();
-        for (int idx = tid; idx < Bp * 16; idx += PT) {
-          const int m = idx >> 4, n = idx & 15;
-          const float v = lds_sum<NWV, Bp>(red0, m, n) + P.na1_b[gt * 16 + n];
-          stc(P.gh + (long)m * 1024 + gt * 16 + n, fmaxf(v, 0.f));
+#pragma unroll
+        for (int ck = 0; ck < NCK; ++ck) {
+          acc_chunk_to_lds<MT, CM>(red0, wave, lane, acc, ck);
+          lds_barrier();
+          for (int idx = tid; idx < CB * 16; idx += PT) {
+            const int m = ck * CB + (idx >> 4), n = idx & 15;
+            if (m >= Bp) break;
+            const float v = lds_sum<NWV, CB>(red0, idx >> 4, n) + P.na1_b[gt * 16 + n];
+            stc(P.gh + (long)m * 1024 + gt * 16 + n, fmaxf(v, 0.f));
+          }
+          lds_barrier();
         }
-        lds_barrier();
       }
       gsync_arrive(P.bar, gen);
       if (!gsync_wait(P.bar, gen, &sflag)) return;
@@ -1299,7 +1349,9 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     PTRACE(5);
     gsync_arrive(P.bar, gen);
     // P5 epilogue operand (own tile's c_dec), fetched during the barrier
-    const float cd = P.cdec[(long)min(tid >> 2, Bp - 1) * 1024 + g * 4 + (tid & 3)];
+    float cd[NCK];
+#pragma unroll
+    for (int c = 0; c < NCK; ++c) cd[c] = P.cdec[(long)min(c * CB + (tid >> 2), Bp - 1) * 1024 + g * 4 + (tid & 3)];
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(6);
     // ======== P5: ctx parts, then the decoder_rnn cell (tile g) and the next step's
@@ -1319,20 +1371,23 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         gemm_seg2<MT, 4, 4>(accd, acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; },
                             [&](int i) { return Wap[(4 * wave + i) * 64 + lane]; });
       float* red1 = red0;  // two reductions back to back: [2][8][Bp][17] would not fit; reuse
-      acc_to_lds<MT>(red0, wave, lane, accd);
-      lds_barrier();
-      if (tid < Bp * 4) {
-        const int m = tid >> 2, u = tid & 3;
-        float pre[4];
 #pragma unroll
-        for (int q = 0; q < 4; ++q) pre[q] = lds_sum<NWV, Bp>(red0, m, q * 4 + u) + db[q];
-        const long ci = (long)m * 1024 + g * 4 + u;
-        const float c = sigm_f(pre[1]) * cd + sigm_f(pre[0]) * tanh_f(pre[2]);
-        const float h = sigm_f(pre[3]) * tanh_f(c);
-        P.cdec[ci] = c;
-        stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
+      for (int ck = 0; ck < NCK; ++ck) {
+        acc_chunk_to_lds<MT, CM>(red0, wave, lane, accd, ck);
+        lds_barrier();
+        const int m = ck * CB + (tid >> 2), u = tid & 3;
+        if (tid < CB * 4 && m < Bp) {
+          float pre[4];
+#pragma unroll
+          for (int q = 0; q < 4; ++q) pre[q] = lds_sum<NWV, CB>(red0, tid >> 2, q * 4 + u) + db[ck][q];
+          const long ci = (long)m * 1024 + g * 4 + u;
+          const float c = sigm_f(pre[1]) * cd[ck] + sigm_f(pre[0]) * tanh_f(pre[2]);
+          const float h = sigm_f(pre[3]) * tanh_f(c);
+          P.cdec[ci] = c;
+          stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
+        }
+        lds_barrier();
       }
-      lds_barrier();
       if (g < IW0) att_epilogue(red1);
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) accd[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1343,7 +1398,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     f32x4 wp[X3P ? 1 : PJ_NC];
     h8 wpx[X3P ? PJ_NC : 1][2];  // split-f16: the whole K for 16 rows, k-steps 6 wave .. + 5
     {
-      const int q = min(max(pj, 0) >> 1, P.ntj - 1), half = pj & 1;
+      const int q = min(max(pj, 0) / JR, P.ntj - 1), half = pj & 1;
       if constexpr (X3P) {
         (void)half;
         const h8* src = reinterpret_cast<const h8*>(P.pj_x3) + (((long)q * 48 + 6 * wave) * 64 + lane) * 2;
@@ -1361,10 +1416,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (X3P && is_pj && (pj & 1) < MT) {
-      // split-f16: job pj = (tile pj >> 1, batch rows 16 (pj & 1) .. + 15), the whole K, so ypart
+    if (X3P && is_pj && (pj % JR) < MT) {
+      // split-f16: job pj = (tile pj / JR, batch rows 16 (pj % JR) .. + 15), the whole K, so ypart
       // holds one copy (P1, the stop decision and the frame writes read it once)
-      const int mtb = pj & 1;
+      const int mtb = pj % JR;
       f32x4 y[PJ_NC][1][2];
 #pragma unroll
       for (int i = 0; i < PJ_NC; ++i) {
@@ -1388,7 +1443,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         float v = red0[mm * 17 + n];
 #pragma unroll
         for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * 17 + n];
-        stc(P.ypart + (long)(mtb * 16 + mm) * YP + (pj >> 1) * 16 + n, v);
+        stc(P.ypart + (long)(mtb * 16 + mm) * YP + (pj / JR) * 16 + n, v);
       }
       lds_barrier();
     } else if (!X3P && is_pj) {
@@ -1414,13 +1469,17 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
             for (int mt = 0; mt < MT; ++mt) acc2[mt] = MFMA16(y[i][mt][q], wp[i][q], acc2[mt]);
       }
-      acc_to_lds<MT>(red0, wave, lane, acc2);
-      lds_barrier();
-      for (int idx = tid; idx < Bp * 16; idx += PT) {
-        const int m = idx >> 4, n = idx & 15;
-        stc(P.ypart + (long)((pj & 1) * YROWS + m) * YP + (pj >> 1) * 16 + n, lds_sum<NWV, Bp>(red0, m, n));
+#pragma unroll
+      for (int ck = 0; ck < NCK; ++ck) {
+        acc_chunk_to_lds<MT, CM>(red0, wave, lane, acc2, ck);
+        lds_barrier();
+        for (int idx = tid; idx < CB * 16; idx += PT) {
+          const int m = ck * CB + (idx >> 4), n = idx & 15;
+          if (m >= Bp) break;
+          stc(P.ypart + (long)((pj & 1) * YROWS + m) * YP + (pj >> 1) * 16 + n, lds_sum<NWV, CB>(red0, idx >> 4, n));
+        }
+        lds_barrier();
       }
-      lds_barrier();
     }
     if (g >= IW0) {  // item workgroups: attention_rnn h_att part (h_att of step t is still in place)
       if constexpr (!X3P)  // split-f16: done in P5 beside the decoder_rnn h_att part
@@ -1465,8 +1524,8 @@ int persist_attn_tc() { return PTC; }
 bool persist_defer_ok(int nitems) { return nitems <= (PW - IW0) * PDEF_MAXIT; }
 
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
-  TTS_CHECK(MT == 1 || MT == 2, "persistent decoder: MT must be 1 or 2");
-  TTS_CHECK(PJ_WG0 + a.ntj * 2 <= PW && a.ntj >= 17, "persistent decoder: projection job count");
+  TTS_CHECK(MT >= 1 && MT <= 4, "persistent decoder: MT must be in [1, 4]");
+  TTS_CHECK(PJ_WG0 + a.ntj * (MT > 2 ? 4 : 2) <= PW && a.ntj >= 17, "persistent decoder: projection job count");
   TTS_CHECK(a.D.B <= 64 && NATT * 4 * 4 == 1024, "persistent decoder: attention_rnn layout");
   TTS_CHECK(a.nchmax * PTC >= a.D.T_max, "persistent decoder: attention partial buffers too small");
   TTS_CHECK(a.D.B <= 16 * MT, "persistent decoder: rows beyond the batch tile");
@@ -1476,15 +1535,15 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
             "persistent decoder: split-f16 weights incomplete or without a range flag");
   const int var = (a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0)) | (a.attp_x3 ? 8 : 0);
 #define PDK(mt, v) (const void*)persist_decoder_kernel<mt, v>
-  static const void* const fns[2][13] = {
-      {PDK(1, 0), PDK(1, 1), PDK(1, 2), PDK(1, 3), PDK(1, 4), nullptr, nullptr, nullptr, PDK(1, 8), PDK(1, 9),
-       PDK(1, 10), PDK(1, 11), PDK(1, 12)},
-      {PDK(2, 0), PDK(2, 1), PDK(2, 2), PDK(2, 3), PDK(2, 4), nullptr, nullptr, nullptr, PDK(2, 8), PDK(2, 9),
-       PDK(2, 10), PDK(2, 11), PDK(2, 12)}};
+#define PDK_ROW(mt) \
+  {PDK(mt, 0), PDK(mt, 1), PDK(mt, 2), PDK(mt, 3), PDK(mt, 4), nullptr, nullptr, nullptr, PDK(mt, 8), PDK(mt, 9), \
+   PDK(mt, 10), PDK(mt, 11), PDK(mt, 12)}
+  static const void* const fns[4][13] = {PDK_ROW(1), PDK_ROW(2), PDK_ROW(3), PDK_ROW(4)};
+#undef PDK_ROW
 #undef PDK
   const void* f = fns[MT - 1][var];
   TTS_CHECK(f != nullptr, "persistent decoder: variant");
-  static bool attr[2][13] = {};
+  static bool attr[4][13] = {};
   if (!attr[MT - 1][var]) {
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
     attr[MT - 1][var] = true;

@@ -25,7 +25,7 @@ from .params import Container, host_tensors, new_token, populate
 from .spec import TacotronConfig, tacotron2_spec
 
 BATCH_LIMIT = 64
-SPEAKER_BATCH_LIMIT = 32  # multi-speaker / decoder variants run on the persistent decoder (<= 32 rows)
+SPEAKER_BATCH_LIMIT = 64  # multi-speaker / decoder variants run on the persistent decoder (<= 64 rows)
 
 
 class Decoder(Container):
@@ -227,4 +227,23 @@ class Tacotron2(nn.Module):
         self.last_steps = steps
         self.last_mel_lengths = steps * r
         self.last_status = status
+        self._last_call = (B, int(lens.max()), len(outs))
         return dec, post, align, stop[:, :, None]
+
+    @torch.no_grad()
+    def decoder_state(self):
+        """The decoder state the reference leaves on ``self.decoder`` after ``inference`` (query,
+        attention_rnn_cell_state, decoder_hidden, decoder_cell, context,
+        attention.attention_weights / attention_weights_cum; layers/tacotron2.py:217-233,259-298,
+        common_layers.py:251-260), for the last call's rows in caller order: (B, 1024) x 4,
+        (B, 512), (B, T) x 2. Rows that stopped before the call's last step hold the batched
+        decode's state, not their own final one (the reference decodes B = 1)."""
+        B, T, nchunks = getattr(self, "_last_call", (0, 0, 0))
+        if not B:
+            raise RuntimeError("run inference first")
+        if nchunks != 1:
+            raise RuntimeError("decoder_state: the last call was split into several library calls")
+        dev = self.embedding.weight.device
+        eng = get_engine(dev)
+        st = eng.taco_decoder_state(B, T, dev)
+        return st
