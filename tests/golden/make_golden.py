@@ -435,6 +435,13 @@ if __name__ == "__main__":
         taco_case("taco_fwdmask", TacotronConfig(attn_norm="sigmoid", forward_attn=True, trans_agent=True,
                                                  forward_attn_mask=True),
                   seed=25, utt_lens=[27, 16], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=26)
+    if "taco_graves_spk" in which:  # GravesAttention with external speaker embeddings (models/tacotron2.py:152-155)
+        rs = np.random.RandomState(45)
+        embs = [(rs.randn(256) / 16.0).astype(np.float32) for _ in range(2)]
+        embs = [e / np.linalg.norm(e) for e in embs]
+        taco_case("taco_graves_spk", TacotronConfig(attn_norm="sigmoid", attn_type="graves", num_speakers=2,
+                                                    speaker_embedding_dim=256),
+                  seed=43, utt_lens=[22, 14], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=44, speakers=embs)
     if "taco_graves" in which:  # GravesAttention (common_layers.py:113-193)
         taco_case("taco_graves", TacotronConfig(attn_norm="sigmoid", attn_type="graves"), seed=41,
                   utt_lens=[24, 15], r_list=[2], max_steps={2: 50}, min_stopping=1, id_seed=42)

@@ -318,7 +318,7 @@ def test_tacotron2_bidirectional_decoder_checkpoint(taco_sig):
                 m.last_steps, range(3))
 
 
-@pytest.mark.parametrize("name,n", [("taco_multispk", 3), ("taco_extspk", 2)])
+@pytest.mark.parametrize("name,n", [("taco_multispk", 3), ("taco_extspk", 2), ("taco_graves_spk", 2)])
 def test_tacotron2_multispeaker_matches_reference(name, n):
     """Multi-speaker Tacotron2 (models/tacotron2.py:50-58,152-155), every utterance of the fixture
     in ONE batched call with its own speaker: learned table ids, or external 256-d embeddings."""

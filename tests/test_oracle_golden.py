@@ -133,7 +133,7 @@ def test_tacotron2_oracle_multispeaker_matches_reference(name, n):
 
 def test_fixture_fp64_drift_is_small():
     """Every Tacotron2 fixture records its fp32-vs-fp64 drift; the 1e-4 tolerance needs it tiny."""
-    for name in ("taco_sigmoid", "taco_softmax", "taco_multispk", "taco_extspk", "taco_bnprenet", "taco_window",
+    for name in ("taco_sigmoid", "taco_softmax", "taco_multispk", "taco_extspk", "taco_graves_spk", "taco_bnprenet", "taco_window",
                  "taco_window_softmax", "taco_fwdattn", "taco_fwdmask", "taco_graves"):
         fx = load_fixture(name)
         drifts = [float(fx[k]) for k in fx.files if k.endswith("_drift64")]
@@ -258,3 +258,18 @@ def test_tacotron2_oracle_decoder_state_matches_reference(r, n):
         st = orc.decoder_state(fx[k + "_ids"], r, n)
         for a in STATE_KEYS:
             assert np.abs(st[a] - fx[f"{k}_{a}"]).max() <= 1e-6, (k, a)
+
+
+def test_tacotron2_oracle_graves_speakers_matches_reference():
+    """Graves attention with external speaker embeddings (models/tacotron2.py:152-155): the speaker
+    columns enter the context with the Graves weights' own sum (they are not normalised)."""
+    fx = load_fixture("taco_graves_spk")
+    cfg, sd = taco_state_dict(fx, r=2)
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r, attn_type=cfg.attn_type, attn_K=cfg.attn_K)
+    for u in range(2):
+        k = f"r2_u{u}"
+        dec, post, align, stop = orc.inference(fx[k + "_ids"], 2, int(fx["r2_max_steps"]),
+                                               speaker=fx[k + "_spk"])
+        assert len(stop) == len(fx[k + "_stop"])
+        assert np.abs(post - fx[k + "_post"]).max() <= 1e-5
+        assert np.abs(align - fx[k + "_align"]).max() <= 1e-6

@@ -1369,8 +1369,12 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
       spk_attr = true;
     }
     TTS_CHECK(M.spk_dim <= 512, "speaker vectors of at most 512 dims");
+    // Graves with speakers: the projection columns hold W_s s alone; the kernel adds the bias and
+    // scales W_s s by the step's sum of attention weights (PArgs::spk_scale)
+    a.spk_scale = M.graves && M.spk_dim ? 1 : 0;
     spk_bias_kernel<<<(N + 255) / 256, 256, (size_t)Bs * M.spk_dim * 4, s>>>(
-        W.spk.f(), Bs, M.spk_dim, M.spk_dim ? M.spk_wT.f() : nullptr, N, M.pj_b.f(), pj0, Bp, W.spkb.f());
+        W.spk.f(), Bs, M.spk_dim, M.spk_dim ? M.spk_wT.f() : nullptr, N, M.pj_b.f(), a.spk_scale ? N : pj0, Bp,
+        W.spkb.f());
     HIP_OK(hipGetLastError());
     a.spk_ld = N;
     a.pjb_rows = W.spkb.f() + pj0;
@@ -1524,8 +1528,6 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   TTS_CHECK(!M.variant() || use_persistent(c), "BN prenet / attention windowing / forward / Graves attention run on "
                                                "the persistent decoder only (<= 64 utterances per call on a 256-CU "
                                                "device)");
-  TTS_CHECK(!(M.graves && M.spk_dim), "Graves attention with speaker embeddings is not supported (its weights do "
-                                      "not sum to 1, so the speaker columns do not fold into biases)");
   if (M.spk_dim) {
     TTS_CHECK(d_spk_ids || d_spk_emb, "multi-speaker model: speaker ids or speaker embeddings are required");
     TTS_CHECK(use_persistent(c), "multi-speaker decoding runs on the persistent decoder only (<= 64 utterances "

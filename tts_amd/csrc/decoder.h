@@ -124,6 +124,7 @@ struct PArgs {
   const float* spk_dec;
   const float* spk_penc;
   int spk_ld;
+  int spk_scale;  // Graves attention with speakers: speaker biases scale by the row's sum of weights
   // decoder variants (common_layers.py:25-74, 286-372): BN prenet biases (null = original prenet),
   // attention windowing, forward attention (+ transition agent)
   const float* pre1_b0;  // [256] layer-1 bias b1' (BN folded): the prenet input of step 0 is relu(b1')

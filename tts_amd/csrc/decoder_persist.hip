@@ -644,6 +644,10 @@ __device__ __forceinline__ void graves_item(const PArgs& P, int t, int b, int ch
     float u = 0.f;
     for (int i = 0; i < nvalid; ++i) u = fmaf(sw[i], eb[(long)i * 512], u);
     stc(P.part_u + pidx * 512 + tid, u);
+    if (P.spk_scale && wave == 0) {  // chunk sum of the weights: the speaker columns' context factor
+      const float s_c = wave64_sum(lane < nvalid ? sw[lane] : 0.f);
+      if (lane == 0) stc(P.part_s + pidx, s_c);
+    }
   }
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
@@ -658,6 +662,11 @@ __device__ __forceinline__ void graves_item(const PArgs& P, int t, int b, int ch
   float cx = 0.f;
   for (int c = 0; c < nch; ++c) cx += ldc(P.part_u + (pb0 + c) * 512 + tid);
   stc(P.ctx + frag_idx(b, tid, 512), cx);
+  if (P.spk_scale && tid == 0) {  // context of the speaker columns = (sum_j alpha_j) s
+    float sa = 0.f;
+    for (int c = 0; c < nch; ++c) sa += ldc(P.part_s + pb0 + c);
+    stc(P.anorm + 2 * b, sa);
+  }
   if (tid < K) stc(P.gmu + (long)b * 16 + tid, ldc(P.gmu + (long)b * 16 + tid) + softplus_t(gbk[2 * K + tid]));
   if (tid == 0) __hip_atomic_store(&P.counter[b], 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
@@ -936,10 +945,24 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
     for (int q = 0; q < 4; ++q) {  // + the row's speaker part (W_dec,s s, api.hip spk_bias_kernel)
       db[c][q] = P.dec_b[g * 16 + q * 4 + (tid & 3)];
-      if (P.spk_dec)
+      if (P.spk_dec && !(GRAVES && P.spk_scale))  // scaled per step below otherwise
         db[c][q] += P.spk_dec[(long)min(c * CB + (tid >> 2), Bp - 1) * P.spk_ld + g * 16 + q * 4 + (tid & 3)];
     }
   const float apb = P.apre_b[g * 16 + (tid & 15)];
+  // Graves attention with speaker embeddings: its weights do not sum to 1, so the speaker columns'
+  // share of the context is (sum_j alpha_j) s; every speaker bias the context feeds (attention_rnn
+  // and decoder_rnn gates, the projection and the rows folded through it) scales by that per-row
+  // sum of the step the context belongs to (published in P.anorm by the combine)
+  const bool sscale = GRAVES && P.spk_scale;
+  auto spk_sum = [&](int m) { return m < D.B ? ldc(P.anorm + 2 * m) : 0.f; };
+  auto pjb1 = [&](int m, int col) {
+    const float v = P.pjb_rows[(long)m * P.spk_ld + col];
+    return sscale ? P.pj_b[col] + spk_sum(m) * v : v;
+  };
+  auto pjb4 = [&](int m, int col) {
+    const f32x4 v = *reinterpret_cast<const f32x4*>(P.pjb_rows + (long)m * P.spk_ld + col);
+    return sscale ? *reinterpret_cast<const f32x4*>(P.pj_b + col) + spk_sum(m) * v : v;
+  };
   __syncthreads();
 
   unsigned gen = 0;
@@ -978,7 +1001,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         const int m = c * CB + (idx >> 4), n = idx & 15;
         if (m >= Bp) break;
         float v = lds_sum<NWV, CB>(red, idx >> 4, n) + apb;
-        if (P.spk_att) v += P.spk_att[(long)m * P.spk_ld + g * 16 + n];  // speaker part of the new ctx
+        if (P.spk_att) v += (sscale ? spk_sum(m) : 1.f) * P.spk_att[(long)m * P.spk_ld + g * 16 + n];  // speaker part of the new ctx
         stc(P.gatt + (long)m * 4096 + g * 16 + n, v);
       }
       if (NCK > 1) lds_barrier();
@@ -997,7 +1020,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       const int m = idx / FR, c = idx - m * FR;
       if (!ldci(D.done + m) || ldci(D.steps + m) > s) {
         const float v = ldc(P.ypart + (long)m * YP + 16 + c) + (X3P ? 0.f : ldc(P.ypart + (long)(YROWS + m) * YP + 16 + c)) +
-                        P.pjb_rows[(long)m * P.spk_ld + 16 + c];
+                        pjb1(m, 16 + c);
         D.dec_out[((long)m * D.S_cap + s) * FR + c] = v;
       }
     }
@@ -1023,7 +1046,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           const int kc = 8 * h + wave;
           const int col = P.nt_proj * 16 + kc * 16 + 4 * (lane >> 4);
           if (t > 0) {
-            const f32x4 bb = *reinterpret_cast<const f32x4*>(P.pjb_rows + (long)m * P.spk_ld + col);
+            const f32x4 bb = pjb4(m, col);
             x[h] = X3P ? ldc4(P.ypart, (m * YP + col) * 4) + bb
                        : ldc4(P.ypart, (m * YP + col) * 4) + ldc4(P.ypart, ((YROWS + m) * YP + col) * 4) + bb;
           } else {
@@ -1063,7 +1086,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         int dn = ldci(D.done + m);
         if (t >= 1 && !dn) {
           const float logit = ldc(P.ypart + (long)m * YP) + (X3P ? 0.f : ldc(P.ypart + (long)(YROWS + m) * YP)) +
-                              P.pjb_rows[(long)m * P.spk_ld];
+                              pjb1(m, 0);
           const float sg = sigm(logit);
           if (t - 1 < D.S_cap) D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
           const bool st = (sg > P.thr) && (t - 1) > 0;
@@ -1380,6 +1403,11 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           float pre[4];
 #pragma unroll
           for (int q = 0; q < 4; ++q) pre[q] = lds_sum<NWV, CB>(red0, tid >> 2, q * 4 + u) + db[ck][q];
+          if (sscale) {
+            const float sa = spk_sum(m);
+#pragma unroll
+            for (int q = 0; q < 4; ++q) pre[q] += sa * P.spk_dec[(long)m * P.spk_ld + g * 16 + q * 4 + u];
+          }
           const long ci = (long)m * 1024 + g * 4 + u;
           const float c = sigm_f(pre[1]) * cd[ck] + sigm_f(pre[0]) * tanh_f(pre[2]);
           const float h = sigm_f(pre[3]) * tanh_f(c);

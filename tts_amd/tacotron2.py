@@ -57,8 +57,6 @@ class Tacotron2(nn.Module):
             unsupported.append("GST")
         if attn_type not in ("original", "graves"):
             unsupported.append(f"attn_type={attn_type}")
-        if attn_type == "graves" and num_speakers > 1:
-            unsupported.append("Graves attention with speaker embeddings")
         if trans_agent and not forward_attn:
             unsupported.append("trans_agent without forward_attn")
         if not location_attn:
