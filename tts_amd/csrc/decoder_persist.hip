@@ -878,7 +878,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   constexpr bool X3P = (VAR & 8) != 0;     // P3's attention_rnn prenet part on the split-f16 MFMA
   constexpr bool DEFER = (VAR & 7) == 0;   // plain location attention: alignment pass deferred to P6
   extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
-  __shared__ int sflag, is_last, dflag[64];
+  __shared__ int sflag, is_last;
   constexpr int Bp = MT * 16;
   constexpr int CM = MT < 2 ? MT : 2;            // m-tiles per LDS reduction chunk
   constexpr int CB = CM * 16;                    // rows per chunk
@@ -1080,10 +1080,13 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     const int it0 = g - IW0;
     if (!GRAVES && it0 >= 0 && it0 < D.B * P.nchmax)
       attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
-    if (g == IW0 - 1) {  // stop decision: an attention_rnn workgroup that is not a prenet one
+    // stop decision: an attention_rnn workgroup that is not a prenet one (MT <= 2), or the last
+    // item workgroup once every attention_rnn workgroup runs a prenet job (MT = 3, 4)
+    if (g == (MT <= 2 ? IW0 - 1 : PW - 1)) {
+      int dn = 1;
       if (tid < D.B) {
         const int m = tid;
-        int dn = ldci(D.done + m);
+        dn = ldci(D.done + m);
         if (t >= 1 && !dn) {
           const float logit = ldc(P.ypart + (long)m * YP) + (X3P ? 0.f : ldc(P.ypart + (long)(YROWS + m) * YP)) +
                               pjb1(m, 0);
@@ -1097,15 +1100,14 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
             dn = 1;
           }
         }
-        dflag[m] = dn;
       }
-      lds_barrier();
-      if (tid == 0) {
-        int last = -1;
-        for (int k = 0; k < D.B; ++k)
-          if (!dflag[k]) last = k;
-        stci(&D.ctl->all_done, last < 0);
-        stci(&D.ctl->active_tiles, last / 16 + 1);
+      if (tid < 64) {  // rows still decoding: one ballot over wave 0 (B <= 64), no serial scan
+        const unsigned long long act = __ballot(tid < D.B && !dn);
+        if (tid == 0) {
+          const int last = act ? 63 - __builtin_clzll(act) : -1;
+          stci(&D.ctl->all_done, act == 0);
+          stci(&D.ctl->active_tiles, last / 16 + 1);
+        }
       }
     }
     PTRACE(1);
