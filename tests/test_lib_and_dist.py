@@ -45,6 +45,18 @@ def _free_port():
     return p
 
 
+STEPS = [5, 2, 4, 3, 2, 4]
+
+
+def test_lpt_shards_balance_steps():
+    from tts_amd.workload import lpt_shards
+    sh = lpt_shards([float(s) for s in STEPS], 2)
+    assert sorted(sum(sh, [])) == list(range(len(STEPS))) and all(len(x) == 3 for x in sh)
+    loads = [sum(STEPS[i] for i in x) for x in sh]
+    assert max(loads) - min(loads) <= max(STEPS) - min(STEPS)
+    assert {max(STEPS[i] for i in x) for x in sh} == {5, 4}  # the two longest land on different ranks
+
+
 def _worker(rank, world, port, q):
     os.environ["MASTER_ADDR"] = "127.0.0.1"
     os.environ["MASTER_PORT"] = str(port)
@@ -57,16 +69,17 @@ def _worker(rank, world, port, q):
     _, sd = taco_state_dict(None, seed=2, overrides={}, stop_bias=-1e4, cfg=cfg)
     orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
     T, _ = lj_profile()
-    T = [min(t, 12) for t in T[:4]]             # 4 short utterances, 3 decoder steps each
+    T = [min(t, 12) for t in T[:6]]             # 6 short utterances with their own step counts
     ids = synthetic_ids(T)
-    shards = lpt_shards([float(t) for t in T], world)
+    # shards balance the decoder step counts (a batch's time is set by its decode length)
+    shards = lpt_shards([float(s) for s in STEPS], world)
     mine = shards[rank]
-    mels = {i: orc.inference(ids[i], 2, 3)[1] for i in mine}   # no collective on the data path
+    mels = {i: orc.inference(ids[i], 2, STEPS[i])[1] for i in mine}   # no collective on the data path
     # optional final gather to rank 0: variable-length results as padded tensors
-    M = 6
+    M = 2 * max(STEPS)
     buf = torch.zeros(len(T), M, 80)
     for i, p in mels.items():
-        buf[i] = torch.from_numpy(p)
+        buf[i, :len(p)] = torch.from_numpy(p)
     gathered = [torch.zeros_like(buf) for _ in range(world)]
     dist.all_gather(gathered, buf)
     if rank == 0:
@@ -95,7 +108,7 @@ def test_two_rank_sharded_decode_equals_single_process():
     _, sd = taco_state_dict(None, seed=2, overrides={}, stop_bias=-1e4, cfg=cfg)
     orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
     T, _ = lj_profile()
-    ids = synthetic_ids([min(t, 12) for t in T[:4]])
-    for i in range(4):
-        ref = orc.inference(ids[i], 2, 3)[1]
-        assert np.array_equal(out[i], ref)
+    ids = synthetic_ids([min(t, 12) for t in T[:6]])
+    for i in range(6):
+        ref = orc.inference(ids[i], 2, STEPS[i])[1]
+        assert np.array_equal(out[i, :len(ref)], ref) and not out[i, len(ref):].any()
