@@ -81,7 +81,8 @@ int tts_taco_infer(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, in
    (TTS/tts/models/tacotron2.py:142-156; speaker vector concatenated to the encoder outputs,
    tacotron_abstract.py:213-217). Exactly one of d_spk_ids (int64 (B), rows of the learned
    speaker_embedding table) or d_spk_emb (float (B, spk_dim), external per-sample embeddings) is
-   non-null. At most 32 utterances per call. Other arguments as tts_taco_infer. */
+   non-null. At most 64 utterances per call, speaker vectors of at most 512 dims. Other arguments
+   as tts_taco_infer. */
 int tts_taco_infer_spk(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
                        const int32_t* h_max_steps, int S_cap, float stop_threshold, const int64_t* d_spk_ids,
                        const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
