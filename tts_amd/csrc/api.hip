@@ -1451,6 +1451,13 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     const char* t0 = std::getenv("TTS_PTRACE_T0");
     a.trace_t0 = t0 ? std::atoi(t0) : 100;
   }
+  // TTS_PTRACE_LAUNCH: which launch of the MT cascade is traced (default 0, the first)
+  const int trace_li = [] {
+    const char* e = std::getenv("TTS_PTRACE_LAUNCH");
+    return e ? std::atoi(e) : 0;
+  }();
+  unsigned long long* const trace_p = a.trace;
+  unsigned long long* const atrace_p = a.atrace;
   HIP_OK(hipEventRecord(c->ev_dec[0], s));
   c->dec_nlaunch = 0;
   for (int mt = W.MT; mt >= 1; --mt) {
@@ -1458,8 +1465,10 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     a.bar = reinterpret_cast<unsigned*>(W.pbar.p) + 512 * li;
     a.base_out = W.stat.i() + TS_END + li;
     a.D = make_dev(c, std::min(W.B, 16 * mt));
+    a.trace = li == trace_li ? trace_p : nullptr;
+    a.atrace = li == trace_li ? atrace_p : nullptr;
     launch_persist_decoder(a, mt, s, false);
-    if (tr) {  // only the first launch is traced
+    if (tr && li == trace_li) {  // one launch is traced
       HIP_OK(hipStreamSynchronize(s));
       std::vector<unsigned long long> h((size_t)8 * 24 * 256);
       HIP_OK(hipMemcpy(h.data(), trace_buf.p, h.size() * 8, hipMemcpyDeviceToHost));
@@ -1798,6 +1807,15 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
   G.ready = true;
 }
 
+// blocks 0-2 of a C = 48 ResidualStack as one kernel (TTS_STACK_FUSE=0: block by block, for A/B)
+static bool stack_fuse_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TTS_STACK_FUSE");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
+
 // returns total upsampling factor; writes bands (B, out_ch, up*(M_max+2pad)) into `out`
 int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int M_max, int pad, float* out,
                   hipStream_t s, GenTail* tail = nullptr, const int64_t* mel_strides = nullptr) {
@@ -1883,7 +1901,34 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     C = Cn;
     Ls = Ln;
     mul *= u;
-    for (int bk = 0; bk < G.nres; ++bk) {  // fused ResidualStack blocks (resblock.hip)
+    int bk0 = 0;
+    if (cc.oflow && G.nres >= 3 && stack_fuse_on() && G.rb_wd16[i * G.nres].p) {
+      int dil[3];
+      for (int k = 0; k < 3; ++k) dil[k] = G.dconv[i * G.nres + k].dil;
+      if (resstack_x3_supported(C, dil, 3)) {  // blocks 0-2 in one pass over the stage (resstack_x3.hip)
+        StackArgs sa{};
+        sa.x = x;
+        sa.y = xo;
+        sa.sb = (long)C * Ls;
+        sa.Ls = (int)Ls;
+        sa.lens = W.lens.i();
+        sa.len_add = 2 * pad;
+        sa.mul = mul;
+        sa.B = B;
+        for (int k = 0; k < 3; ++k) {
+          sa.dil[k] = dil[k];
+          sa.wd16[k] = G.rb_wd16[i * G.nres + k].p;
+          sa.wf16[k] = G.rb_wf16[i * G.nres + k].p;
+          sa.bd[k] = G.dconv[i * G.nres + k].bias.f();
+          sa.bf[k] = G.fused[i * G.nres + k].bias.f();
+        }
+        sa.oflow = cc.oflow;
+        launch_resstack_x3(sa, lens.data(), C, s);
+        std::swap(x, xo);
+        bk0 = 3;
+      }
+    }
+    for (int bk = bk0; bk < G.nres; ++bk) {  // fused ResidualStack blocks (resblock.hip)
       const ConvLayer& dl = G.dconv[i * G.nres + bk];
       const ConvLayer& fl = G.fused[i * G.nres + bk];
       ResArgs ra{};

@@ -180,6 +180,26 @@ void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t 
 void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf, int C,
                       std::vector<uint16_t>& wd16, std::vector<uint16_t>& wf16);
 
+// Blocks 0-2 of a ResidualStack fused per time tile (resstack_x3.hip), split-f16 weights in the
+// pack_resblock_x3 layout; y = block2(block1(block0(x)))
+struct StackArgs {
+  const float* x;
+  float* y;
+  long sb;
+  int Ls;
+  const int* lens;
+  int len_add, mul, B;
+  int dil[3];
+  int ext[3];  // filled by the launcher
+  const void* wd16[3];
+  const void* wf16[3];
+  const float* bd[3];
+  const float* bf[3];  // b_1x1 + b_sc
+  unsigned* oflow;
+};
+bool resstack_x3_supported(int C, const int* dil, int n);
+void launch_resstack_x3(const StackArgs& a, const int* h_lens, int C, hipStream_t s);
+
 // fused MB-MelGAN output conv (C -> 4, k7, LReLU + reflect pad 3 + tanh) and PQMF synthesis
 // (melgan_out.hip); returns false when the shape is not covered (N != 4, 63 taps, C not 32/48)
 bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, const float* bo, const float* G,

@@ -69,7 +69,8 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   const int nb = wn * 16 * NI + (lane & 15);  // this lane's position (B column) for ni = 0
   const int kg = 8 * (lane >> 4);             // this lane's k offset inside a k-step
   const int mt0 = wm * MI;
-  bool bad = false;
+  bool bad = false;   // staged inputs: ordered compare (catches NaN)
+  float vmax = 0.f;   // h values: running max of |h| (split16.h absmax4)
 
   // tile index -> (utterance, first position): per-utterance tile offsets (exclusive scan over the
   // <= 64 lengths, once per workgroup, in LDS); a lookup is one LDS read per lane and a ballot
@@ -258,17 +259,13 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       const int co = (mt0 + mi) * 16 + 4 * (lane >> 4);
-      const float(&bd)[4] = bdv[mi];
+      const f32x4 bd{bdv[mi][0], bdv[mi][1], bdv[mi][2], bdv[mi][3]};
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
+        const f32x4 v = lrelu4(x3_value4(am[mi][ni], ac[mi][ni], bd));
+        vmax = absmax4(vmax, v);
         h4 hi, lo;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          _Float16 h, l;
-          split_dev(lrelu_x3(x3_value(am[mi][ni][j], ac[mi][ni][j]) + bd[j]), h, l, bad);
-          hi[j] = h;
-          lo[j] = l;
-        }
+        split4(v, hi, lo);
         const int p = nb + ni * 16;
         *reinterpret_cast<h4*>(HX + p * HR + co) = hi;
         *reinterpret_cast<h4*>(HX + p * HR + 2 * C + co) = lo;
@@ -307,14 +304,15 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     float* yb = a.y + (long)cur.b * a.sb;
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
+      const f32x4 bf{bfv[mi][0], bfv[mi][1], bfv[mi][2], bfv[mi][3]};
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
-        const float bf = bfv[mi][j];
+      for (int ni = 0; ni < NI; ++ni) {
+        const f32x4 v = x3_value4(am[mi][ni], ac[mi][ni], bf);
+        const int q = cur.q0 + nb + ni * 16;
 #pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const int q = cur.q0 + nb + ni * 16;
-          if (q < cur.L) yb[(long)co * a.Ls + q] = x3_value(am[mi][ni][j], ac[mi][ni][j]) + bf;
+        for (int j = 0; j < 4; ++j) {
+          const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
+          if (q < cur.L) yb[(long)co * a.Ls + q] = v[j];
         }
       }
     }
@@ -332,7 +330,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 #endif
   }
 #undef RB_STAMP
-  if (bad) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (bad || !(vmax < F16_RANGE)) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
 // one resident workgroup per CU (the LDS tile allows no more), each looping over tiles; the

@@ -129,4 +129,28 @@ __device__ __forceinline__ void split_dev(float v, _Float16& hi, _Float16& lo, b
   bad |= !(__builtin_fabsf(v) < F16_RANGE);
   split_fast(v, hi, lo);
 }
+
+// ---- packed epilogue forms for one MFMA output fragment (a lane's 4 consecutive rows of one
+// column): v_pk_fma / v_pk_add / v_pk_mul / v_cvt_pk_f16_f32, half the VALU issues of the scalar
+// forms and bit-identical to them (same operations in the same order per element)
+// acc_main + 2^-11 acc_corr + bias
+__device__ __forceinline__ f32x4 x3_value4(const f32x4& am, const f32x4& ac, const f32x4& b) {
+  return am + ac * SPLIT_INV + b;
+}
+__device__ __forceinline__ f32x4 lrelu4(const f32x4& v) {
+  const f32x4 s = v * 0.2f;
+  return f32x4{fmaxf(v[0], s[0]), fmaxf(v[1], s[1]), fmaxf(v[2], s[2]), fmaxf(v[3], s[3])};
+}
+__device__ __forceinline__ void split4(const f32x4& v, h4& hi, h4& lo) {
+  hi = __builtin_convertvector(v, h4);
+  const f32x4 hf = __builtin_convertvector(hi, f32x4);
+  lo = __builtin_convertvector(v * SPLIT_SCALE - hf * SPLIT_SCALE, h4);
+}
+// running maximum of |v| in place of a compare per value: GEMM outputs of finite, in-range
+// operands are finite, so max < F16_RANGE at the end is the whole range check for them (inputs
+// that may be NaN keep the ordered compare of split_dev / the staging check)
+__device__ __forceinline__ float absmax4(float mx, const f32x4& v) {
+  return fmaxf(fmaxf(mx, fmaxf(__builtin_fabsf(v[0]), __builtin_fabsf(v[1]))),
+               fmaxf(__builtin_fabsf(v[2]), __builtin_fabsf(v[3])));
+}
 #endif
