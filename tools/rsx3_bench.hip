@@ -1,6 +1,6 @@
 // Fused ResidualStack blocks 0-2 (resstack_x3.hip) against three resblock_x3 launches at the
-// MB-MelGAN C = 48 stage of the C2 workload: bit-exactness check (same split-f16 arithmetic per
-// row), then timing. Not part of the library:
+// MB-MelGAN C = 48 stage of the C2 workload: agreement check (the same split-f16 arithmetic per
+// row, up to the MFMA orientation of phase 2), then timing. Not part of the library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -I include tools/rsx3_bench.hip -o tools/rsx3_bench
 // Diagnostic builds: -DRS_NO_MFMA (operand traffic only), -DRS_NO_LDS (MFMAs on stale registers).
 #include "../tts_amd/csrc/resblock_x3.hip"
@@ -64,7 +64,8 @@ int main(int argc, char** argv) {
   setvbuf(stdout, nullptr, _IONBF, 0);
   HIP_OK(hipStreamCreate(&S));
   const int nB = argc > 1 ? std::atoi(argv[1]) : 32;
-  constexpr int C = 48, mul = 64, pad = 2;
+  const int C = argc > 2 ? std::atoi(argv[2]) : 48;  // 48 (mul 64) or 96 (mul 32)
+  const int mul = C == 48 ? 64 : 32, pad = 2;
   int Mmax = 0;
   std::vector<int> hl(kM, kM + nB);
   for (int b = 0; b < nB; ++b) Mmax = std::max(Mmax, kM[b]);
@@ -180,12 +181,14 @@ int main(int argc, char** argv) {
   }
 #endif
   const float ts = time_graph(seq), tf = time_graph(fused);
-  printf("B=%d C=48 blocks 0-2: 3 x resblock_x3 %.1f us, fused %.1f us\n", nB, ts, tf);
+  printf("B=%d C=%d blocks 0-2: 3 x resblock_x3 %.1f us, fused %.1f us\n", nB, C, ts, tf);
 #define VAR(TQ, WN, NI) printf("  fused TQ %d WN %d NI %d: %.1f us\n", TQ, WN, NI, time_graph([&] { \
     StackArgs v = sa; v.ext[2] = 0; v.ext[1] = 9; v.ext[0] = 12; launch_rsx3<48, TQ, WN, NI>(v, hl.data(), S); }))
-  VAR(208, 4, 4);
-  VAR(176, 4, 4);
-  VAR(144, 4, 3);
-  VAR(208, 2, 8);
-  return diff == 0 ? 0 : 1;
+  if (C == 48) {
+    VAR(208, 4, 4);
+    VAR(176, 4, 4);
+  }
+  // the fused kernel's blocks 0-1 keep phase 2 untransposed (their output goes to LDS), the
+  // resblock_x3 launches transpose every block: the MFMA's internal order differs, ~1 ulp
+  return md <= 1e-6 * std::max(1.0, mag) ? 0 : 1;
 }

@@ -228,7 +228,72 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
     for (int ni = 0; ni < NI; ++ni)
 #pragma unroll
       for (int j = 0; j < 4; ++j) acc[mi][ni][j] = x3_value(am[mi][ni][j], ac[mi][ni][j]);
-  if (a.merged_u) {  // phase-merged ConvTranspose: row m = co * u + phase
+  // phase-merged ConvTranspose, row m = co * u + phase; a lane's 4 rows (j) are 4 consecutive
+  // phases of one co (u >= 4) or phases 0, 1 of two co (u = 2), written as vectors of consecutive
+  // output samples (the scalar form spent a third of the u = 2 kernel on its stores)
+  const bool vec = a.merged_u && a.ot == 1 && (a.oc & 3) == 0 && (a.ob & 3) == 0 &&
+                   (reinterpret_cast<uintptr_t>(a.out) & 15) == 0 && a.Cout % 16 == 0;
+  if (vec && a.merged_u % 4 == 0) {
+    // u % 8 == 0: phases phs0 .. phs0 + 3 all on one side of u / 2 -> one 16-byte store;
+    // u == 4: two pairs (0, 1 at q) and (2, 3 at q - 1) -> two 8-byte stores
+    const int u = a.merged_u, L = Lin;
+    float* ob = a.out + (long)b * a.ob;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m0 = co0 + wm * 16 * MI + mi * 16 + 4 * (lane >> 4);
+      if (m0 >= a.Cout) continue;
+      const int co = m0 / u, phs0 = m0 - co * u;
+      const int hi0 = 2 * phs0 >= u, hi1 = 2 * (phs0 + 2) >= u;
+      const f32x4 bias{a.bias[m0], a.bias[m0 + 1], a.bias[m0 + 2], a.bias[m0 + 3]};
+      float* orow = ob + (long)co * a.oc;
+#pragma unroll
+      for (int ni = 0; ni < NI; ++ni) {
+        const int q = q0 + nb + ni * 16;
+        const f32x4 v = acc[mi][ni] + bias;
+        if (u % 8 == 0) {
+          if (q - hi0 >= 0 && q - hi0 < L) *reinterpret_cast<f32x4*>(orow + (long)(q - hi0) * u + phs0) = v;
+        } else {
+          typedef float f2 __attribute__((ext_vector_type(2)));
+          if (q - hi0 >= 0 && q - hi0 < L) *reinterpret_cast<f2*>(orow + (long)(q - hi0) * u + phs0) = f2{v[0], v[1]};
+          if (q - hi1 >= 0 && q - hi1 < L) *reinterpret_cast<f2*>(orow + (long)(q - hi1) * u + phs0 + 2) = f2{v[2], v[3]};
+        }
+      }
+    }
+  } else if (vec && a.merged_u == 2) {
+    // u = 2: position q holds out[2q] (phase 0) and out[2q - 1] (phase 1). The aligned pair
+    // (2q, 2q + 1) takes phase 1 from the next position: the next lane of the 16-lane row, or
+    // lane 0 of the next n-tile; a wave's last position stores out[2q] alone and its first
+    // position out[2q - 1] alone (the neighbouring wave / workgroup holds their partners)
+    typedef float f2 __attribute__((ext_vector_type(2)));
+    const int L = Lin;
+    float* ob = a.out + (long)b * a.ob;
+    const int r = lane & 15;
+#pragma unroll
+    for (int mi = 0; mi < MI; ++mi) {
+      const int m0 = co0 + wm * 16 * MI + mi * 16 + 4 * (lane >> 4);
+      if (m0 >= a.Cout) continue;
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        const int co = m0 / 2 + c;
+        const float b0 = a.bias[m0 + 2 * c], b1 = a.bias[m0 + 2 * c + 1];
+        float* orow = ob + (long)co * a.oc;
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni) {
+          const float v0 = acc[mi][ni][2 * c] + b0;
+          const float v1 = acc[mi][ni][2 * c + 1] + b1;
+          const float down = __shfl_down(v1, 1, 16);
+          const float wrap = ni + 1 < NI ? __shfl(acc[mi][ni + 1 < NI ? ni + 1 : ni][2 * c + 1] + b1, lane & ~15) : 0.f;
+          const int q = q0 + nb + ni * 16;
+          const bool last = r == 15 && ni == NI - 1;
+          if (q >= 0 && q < L) {
+            if (last) orow[2 * q] = v0;
+            else *reinterpret_cast<f2*>(orow + 2 * q) = f2{v0, r < 15 ? down : wrap};
+          }
+          if (r == 0 && ni == 0 && q - 1 >= 0 && q - 1 < L) orow[2 * q - 1] = v1;
+        }
+      }
+    }
+  } else if (a.merged_u) {
     const int u = a.merged_u, L = Lin;
     float* ob = a.out + (long)b * a.ob;
 #pragma unroll
@@ -243,7 +308,11 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
           const int qq = q0 + nb + ni * 16 - hi;
+#ifdef CX_PROBE_NOSTORE  // tools/cx3_bench.hip probe: the epilogue without its stores
+          if (qq >= 0 && qq < L && acc[mi][ni][j] + bias == 12345.f) ob[(long)co * a.oc + (long)(qq * u + phs) * a.ot] = 0.f;
+#else
           if (qq >= 0 && qq < L) ob[(long)co * a.oc + (long)(qq * u + phs) * a.ot] = acc[mi][ni][j] + bias;
+#endif
         }
       }
   } else {

@@ -199,15 +199,13 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   constexpr bool EARLY = NCH % 2 == 0;
   // per-channel biases, loaded once (a load inside the tile loop would be the youngest in the
   // vmcnt order and make its wait drain every prefetch)
-  float bdv[MI][4], bfv[MI][4];
+  float bdv[MI][4], bfv[MI];
 #pragma unroll
-  for (int mi = 0; mi < MI; ++mi)
+  for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
-      bdv[mi][j] = a.bd[co];
-      bfv[mi][j] = a.bf[co];
-    }
+    for (int j = 0; j < 4; ++j) bdv[mi][j] = a.bd[(mt0 + mi) * 16 + 4 * (lane >> 4) + j];
+    bfv[mi] = a.bf[(mt0 + mi) * 16 + (lane & 15)];  // phase 2 is transposed: one channel per lane
+  }
 #ifdef RB_TRACE  // tools/rbx3_bench.hip trace mode: s_memrealtime per phase, first 4 tiles of a workgroup
   int it = 0;
 #define RB_STAMP(k)                                                                             \
@@ -296,23 +294,29 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[u][mi][0], ring[u][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
+          for (int ni = 0; ni < NI; ++ni) mfma_x3(bh[ni], bl[ni], ring[u][mi][0], ring[u][mi][1], am[mi][ni], ac[mi][ni]);
         wload(ring[u], NK1 + kc + R);  // past NK2: the next tile's phase-1 weights
       }
     }
     RB_STAMP(3);
     float* yb = a.y + (long)cur.b * a.sb;
+    // transposed phase 2 (operands swapped: D = [lrelu(h); x]^T . Wf^T): a lane holds positions
+    // q .. q + 3 of channel co, one 16-byte store instead of four 4-byte ones
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
-      const f32x4 bf{bfv[mi][0], bfv[mi][1], bfv[mi][2], bfv[mi][3]};
+      const int co = (mt0 + mi) * 16 + (lane & 15);
+      const f32x4 bf{bfv[mi], bfv[mi], bfv[mi], bfv[mi]};
+      float* yr = yb + (long)co * a.Ls;
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
         const f32x4 v = x3_value4(am[mi][ni], ac[mi][ni], bf);
-        const int q = cur.q0 + nb + ni * 16;
+        const int q = cur.q0 + wn * 16 * NI + ni * 16 + 4 * (lane >> 4);
+        if (q + 3 < cur.L) {
+          *reinterpret_cast<f32x4*>(yr + q) = v;
+        } else {
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int co = (mt0 + mi) * 16 + 4 * (lane >> 4) + j;
-          if (q < cur.L) yb[(long)co * a.Ls + q] = v[j];
+          for (int j = 0; j < 4; ++j)
+            if (q + j < cur.L) yr[q + j] = v[j];
         }
       }
     }
@@ -374,6 +378,8 @@ void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t 
   TTS_CHECK(a.dil >= 1 && a.dil <= X3_DMAX, "resblock: dilation must be in [1, 27] (num_res_blocks <= 4)");
   TTS_CHECK(a.Wd16 && a.Wf16 && a.oflow, "resblock_x3: split weights / overflow flag missing");
   TTS_CHECK(a.B <= 64, "resblock_x3: at most 64 utterances per call");
+  TTS_CHECK(a.Ls % 4 == 0 && a.sb % 4 == 0 && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0,
+            "resblock_x3: 16-byte aligned output rows required");
   if (a.max_q <= 0 || a.B <= 0) return;
   switch (C) {
     // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave

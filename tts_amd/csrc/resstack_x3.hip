@@ -310,7 +310,10 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
         RS_SB();
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
-          RS_MMA(ring[s % R][0], ring[s % R][1], bh[ni], bl[ni], am[ni], ac[ni]);
+          if (last)  // transposed (D = HX^T . Wf^T): the stores below write 4 positions of one channel
+            RS_MMA(bh[ni], bl[ni], ring[s % R][0], ring[s % R][1], am[ni], ac[ni]);
+          else
+            RS_MMA(ring[s % R][0], ring[s % R][1], bh[ni], bl[ni], am[ni], ac[ni]);
         wnext(ring[s % R], bi, s);
         RS_SB();
       }
@@ -338,16 +341,26 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
         lds_barrier();
         RS_STAMP(4 * bi + 4);
       } else {
-        float* yb = a.y + (long)cur.b * a.sb;
+        // lane: channel wm * 16 + (lane & 15), rows r .. r + 3 (OFF and TQ are multiples of 4,
+        // so a 4-row group is wholly inside or outside the tile's own positions)
+        const int cl = wm * 16 + (lane & 15);
+        const float b1 = bias[bi][1][cl];
+        const f32x4 bf1{b1, b1, b1, b1};
+        float* yr = a.y + (long)cur.b * a.sb + (long)cl * a.Ls;
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
           if (!act[ni]) continue;
-          const int r = nt[ni] * 16 + (lane & 15);
+          const int r = nt[ni] * 16 + 4 * (lane >> 4);
           const int q = base + r;
-          if (r >= OFF && r < OFF + TQ && q < cur.L) {
-            const f32x4 v = x3_value4(am[ni], ac[ni], bf);
+          if (r >= OFF && r < OFF + TQ) {
+            const f32x4 v = x3_value4(am[ni], ac[ni], bf1);
+            if (q + 3 < cur.L) {
+              *reinterpret_cast<f32x4*>(yr + q) = v;
+            } else {
 #pragma unroll
-            for (int j = 0; j < 4; ++j) yb[(long)(co + j) * a.Ls + q] = v[j];
+              for (int j = 0; j < 4; ++j)
+                if (q + j < cur.L) yr[q + j] = v[j];
+            }
           }
         }
       }
@@ -391,7 +404,7 @@ static void launch_rsx3(const StackArgs& a, const int* h_lens, hipStream_t s) {
 }
 
 bool resstack_x3_supported(int C, const int* dil, int n) {
-  if (C != 48 || n < 3) return false;
+  if ((C != 48 && C != 96) || n < 3) return false;
   int sum = 0;
   for (int k = 0; k < 3; ++k) {
     if (dil[k] < 1) return false;
@@ -403,13 +416,20 @@ bool resstack_x3_supported(int C, const int* dil, int n) {
 void launch_resstack_x3(const StackArgs& a0, const int* h_lens, int C, hipStream_t s) {
   TTS_CHECK(resstack_x3_supported(C, a0.dil, 3), "resstack_x3: shape not covered");
   TTS_CHECK(a0.oflow && a0.B <= 64, "resstack_x3: overflow flag missing or more than 64 utterances");
+  TTS_CHECK(a0.Ls % 4 == 0 && a0.sb % 4 == 0 && (reinterpret_cast<uintptr_t>(a0.y) & 15) == 0,
+            "resstack_x3: 16-byte aligned output rows required");
   for (int b = 0; b < a0.B; ++b)
     TTS_CHECK((h_lens[b] + a0.len_add) * a0.mul > ST_OFF, "resstack_x3: utterance shorter than the reflection pad");
   StackArgs a = a0;
   a.ext[2] = 0;
   a.ext[1] = a.dil[2];
   a.ext[0] = a.dil[1] + a.dil[2];
-  // C = 48: 3 m-tile waves x 4 n-groups; ROWS = 240 = 15 n-tiles, <= 4 per wave
-  launch_rsx3<48, 208, 4, 4>(a, h_lens, s);
+  if (C == 48) {
+    // 3 m-tile waves x 4 n-groups; ROWS = 240 = 15 n-tiles, <= 4 per wave
+    launch_rsx3<48, 208, 4, 4>(a, h_lens, s);
+  } else {
+    // C = 96: 6 m-tile waves x 2 n-groups; ROWS = 128 = 8 n-tiles, 4 per wave (158.5 KB LDS)
+    launch_rsx3<96, 96, 2, 4>(a, h_lens, s);
+  }
   HIP_OK(hipGetLastError());
 }
