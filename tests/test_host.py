@@ -77,7 +77,8 @@ def test_multispeaker_state_dict_keys_and_shapes():
     assert tuple(sd2["decoder.attention_rnn.weight_ih"].shape) == (4096, 256 + 768)
 
 
-@pytest.mark.parametrize("kw", [dict(gst=True), dict(trans_agent=True), dict(prenet_type="xyz"), dict(attn_type="graves", num_speakers=4),
+# (Graves attention with speaker embeddings is supported since round 3: test_gpu_parity graves_spk)
+@pytest.mark.parametrize("kw", [dict(gst=True), dict(trans_agent=True), dict(prenet_type="xyz"),
                                 dict(location_attn=False)])
 def test_unsupported_tacotron_variants_raise(kw):
     with pytest.raises(NotImplementedError):
