@@ -9,6 +9,16 @@
 #include <vector>
 
 __device__ unsigned g_err;
+__device__ int g_skew;  // > 0: each workgroup waits up to g_skew ticks (s_memtime) before arriving
+
+// per-(workgroup, iteration) arrival skew, as a phase of uneven work would give
+__device__ __forceinline__ void arrive_skew(int i) {
+  const int sk = *(volatile int*)&g_skew;
+  if (sk <= 0) return;
+  const unsigned h = (blockIdx.x * 2654435761u) ^ ((unsigned)i * 40503u);
+  const unsigned long long d = (h >> 8) % (unsigned)sk, t0 = __builtin_amdgcn_s_memtime();
+  while (__builtin_amdgcn_s_memtime() - t0 < d) {}
+}
 
 // mode bit 0: agent acquire fence after the barrier; bit 1: s_sleep in the spin
 __device__ __forceinline__ bool grid_sync(unsigned* ctr, unsigned& target, int mode, int* ok) {
@@ -59,6 +69,7 @@ __global__ __launch_bounds__(256) void bar_hier_kernel(unsigned* ctr, int iters)
   unsigned* gc = ctr;
   unsigned* go = ctr + 32;
   for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -90,6 +101,7 @@ __global__ __launch_bounds__(256) void bar_hier8_kernel(unsigned* ctr, int iters
   unsigned* xc = ctr + 64 + xcd * 32;
   unsigned* line = ctr + 32;
   for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -114,11 +126,45 @@ __global__ __launch_bounds__(256) void bar_hier8_kernel(unsigned* ctr, int iters
     if (!ok) return;
   }
 }
+// (G) NC counters (each on its own 128-B line), arrival = one add that returns nothing (no atomic
+// round trip on the arriving workgroup's chain); lanes 0..NC-1 of wave 0 poll every counter until
+// each holds its share of the generation (no leader, no go word)
+template <int NC>
+__global__ __launch_bounds__(256) void bar_ctrs_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  const unsigned per = gridDim.x / NC;
+  unsigned* mine = ctr + 64 + (blockIdx.x % NC) * 32;
+  for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) __hip_atomic_fetch_add(mine, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (threadIdx.x < 64) {
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      int good = 1;
+      const int l = threadIdx.x % NC;
+      const unsigned want = per * (unsigned)(i + 1);
+      while (true) {
+        unsigned v = __hip_atomic_load(ctr + 64 + l * 32, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (__builtin_amdgcn_ballot_w64(v < want) == 0) break;
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      }
+      if (threadIdx.x == 0) ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
 // (C) flag array, no atomics: each workgroup stores its generation to its own slot; wave 0 polls
 // all slots (4 per lane) until the minimum reaches the generation
 __global__ __launch_bounds__(256) void bar_flags_kernel(unsigned* flags, int iters) {
   __shared__ int ok;
   for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) __hip_atomic_store(flags + blockIdx.x, (unsigned)(i + 1), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -148,6 +194,7 @@ __global__ __launch_bounds__(256) void bar_go_kernel(unsigned* ctr, int iters) {
   __shared__ int ok;
   unsigned* go = ctr + 32;
   for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -286,12 +333,17 @@ int main() {
   }
   unsigned* big;
   HIP_OK(hipMalloc(&big, 4096 * 4));
-  for (int v = 0; v < 4; ++v) {
+  for (int sk : {0, 2000, 8000})
+  for (int v = 0; v < 6; ++v) {
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_skew), &sk, 4));
     const void* f = v == 0 ? (const void*)bar_hier_kernel : v == 1 ? (const void*)bar_flags_kernel
-                  : v == 2 ? (const void*)bar_go_kernel : (const void*)bar_hier8_kernel;
-    const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : v == 2 ? "counter + go flag" : "xcd ctr + 8-slot line";
+                  : v == 2 ? (const void*)bar_go_kernel : v == 3 ? (const void*)bar_hier8_kernel
+                  : v == 4 ? (const void*)bar_ctrs_kernel<8> : (const void*)bar_ctrs_kernel<16>;
+    const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : v == 2 ? "counter + go flag"
+                   : v == 3 ? "xcd ctr + 8-slot line" : v == 4 ? "8 ctrs, poll all" : "16 ctrs, poll all";
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
-    for (int nwg : {256, 128}) {
+    if (sk) printf("(arrival skew up to %d memtime ticks)\n", sk);
+    for (int nwg : {256}) {
       const int iters = 2000;
       float ms = timed([&] {
         HIP_OK(hipMemsetAsync(big, 0, 4096 * 4, S));
