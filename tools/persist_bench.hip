@@ -159,6 +159,36 @@ __global__ __launch_bounds__(256) void bar_ctrs_kernel(unsigned* ctr, int iters)
   }
 }
 
+// (H) per-XCD counters (returning add); the last arriver of an XCD adds to the global counter
+// without waiting for the result, and every workgroup polls the global counter itself (8 arrivals
+// per generation): one atomic round trip and the go-word store fewer on the last arriver's chain
+__global__ __launch_bounds__(256) void bar_hier2_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  const int xcd = blockIdx.x & 7;
+  const unsigned per = gridDim.x / 8;
+  unsigned* xc = ctr + 64 + xcd * 32;
+  unsigned* gc = ctr;
+  for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int good = 1;
+      const unsigned old = __hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == per * (i + 1) - 1) __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(gc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < 8u * (i + 1))
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
 // (C) flag array, no atomics: each workgroup stores its generation to its own slot; wave 0 polls
 // all slots (4 per lane) until the minimum reaches the generation
 __global__ __launch_bounds__(256) void bar_flags_kernel(unsigned* flags, int iters) {
@@ -333,14 +363,16 @@ int main() {
   }
   unsigned* big;
   HIP_OK(hipMalloc(&big, 4096 * 4));
-  for (int sk : {0, 2000, 8000})
-  for (int v = 0; v < 6; ++v) {
+  for (int sk : {0, 1000, 2000, 4000, 8000})
+  for (int v : {0, 3, 4, 6}) {
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_skew), &sk, 4));
     const void* f = v == 0 ? (const void*)bar_hier_kernel : v == 1 ? (const void*)bar_flags_kernel
                   : v == 2 ? (const void*)bar_go_kernel : v == 3 ? (const void*)bar_hier8_kernel
-                  : v == 4 ? (const void*)bar_ctrs_kernel<8> : (const void*)bar_ctrs_kernel<16>;
+                  : v == 4 ? (const void*)bar_ctrs_kernel<8> : v == 5 ? (const void*)bar_ctrs_kernel<16>
+                  : (const void*)bar_hier2_kernel;
     const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : v == 2 ? "counter + go flag"
-                   : v == 3 ? "xcd ctr + 8-slot line" : v == 4 ? "8 ctrs, poll all" : "16 ctrs, poll all";
+                   : v == 3 ? "xcd ctr + 8-slot line" : v == 4 ? "8 ctrs, poll all" : v == 5 ? "16 ctrs, poll all"
+                   : "xcd ctr, poll global";
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
     if (sk) printf("(arrival skew up to %d memtime ticks)\n", sk);
     for (int nwg : {256}) {

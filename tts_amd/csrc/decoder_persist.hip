@@ -363,7 +363,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     lds_barrier();
     u = (red[tid] + red[512 + tid]) + (red[1024 + tid] + red[1536 + tid]);
   }
-  stc(P.part_u + pidx * 512 + tid, u);
+  stc_quad(P.part_u, (int)pidx * 512 + tid, u);
   if (tid == 0) {
     stc(P.part_s + pidx, S_c);
     stc(P.part_m + pidx, m_c);
@@ -425,7 +425,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     }
   }
   float ctx_v = cx / ((FWD && P.fwd) ? Fz : S);
-  stc(P.ctx + frag_idx(b, tid, 512), ctx_v);
+  stc_quad(P.ctx, (int)frag_idx(b, tid, 512), ctx_v);
   ATRACE(7);
   if (ekeep) {  // deferred alignment pass: publish the normaliser, the items finish in P6
     if (tid == 0) {
@@ -643,7 +643,7 @@ __device__ __forceinline__ void graves_item(const PArgs& P, int t, int b, int ch
     const float* eb = P.enc + ((long)b * D.T_max + t0) * 512 + tid;
     float u = 0.f;
     for (int i = 0; i < nvalid; ++i) u = fmaf(sw[i], eb[(long)i * 512], u);
-    stc(P.part_u + pidx * 512 + tid, u);
+    stc_quad(P.part_u, (int)pidx * 512 + tid, u);
     if (P.spk_scale && wave == 0) {  // chunk sum of the weights: the speaker columns' context factor
       const float s_c = wave64_sum(lane < nvalid ? sw[lane] : 0.f);
       if (lane == 0) stc(P.part_s + pidx, s_c);
@@ -1002,7 +1002,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         if (m >= Bp) break;
         float v = lds_sum<NWV, CB>(red, idx >> 4, n) + apb;
         if (P.spk_att) v += (sscale ? spk_sum(m) : 1.f) * P.spk_att[(long)m * P.spk_ld + g * 16 + n];  // speaker part of the new ctx
-        stc(P.gatt + (long)m * 4096 + g * 16 + n, v);
+        stc_quad(P.gatt, m * 4096 + g * 16 + n, v);
       }
       if (NCK > 1) lds_barrier();
     }
@@ -1071,7 +1071,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
         for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * 17 + n];
         if (P.pre2_b) v += P.pre2_b[tl2 * 16 + n];  // BN prenet layer-2 bias
-        stc(P.pb + frag_idx(mt * 16 + mm, tl2 * 16 + n, 256), v);
+        stc_quad(P.pb, (int)frag_idx(mt * 16 + mm, tl2 * 16 + n, 256), v);
       }
       lds_barrier();
     }
@@ -1275,7 +1275,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
             const float c = sigm_f(pre[1]) * ca[ck] + sigm_f(pre[0]) * tanh_f(pre[2]);
             const float h = sigm_f(pre[3]) * tanh_f(c);
             P.catt[ci] = c;
-            stc(P.hatt + frag_idx(m, tile * 4 + u, 1024), h);
+            stc_quad(P.hatt, (int)frag_idx(m, tile * 4 + u, 1024), h);
             hs[m * 17 + gl * 4 + u] = h;
           }
         }
@@ -1283,7 +1283,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
       PTRACE(11);
       if (!GRAVES) {  // partial query projection over this workgroup's 16 units
-        // on the MFMA: wave w owns attention dims 16 w .. 16 w + 15, K = this workgroup's 16 units
+        // on the MFMA: wave w owns attention dims 16 w .. 16 w + 15, K = this workgroup's 16 units.
+        // Transposed product (dims x rows): a lane ends with 4 consecutive dims of one batch row,
+        // stored as one 16-byte write (the partials are the step's largest hand-off, 16 KB per
+        // workgroup)
         f32x4 qa[MT];
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) qa[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1291,12 +1294,17 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         for (int q = 0; q < 4; ++q)
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt)
-            qa[mt] = MFMA16(hs[(mt * 16 + (lane & 15)) * 17 + 4 * q + (lane >> 4)], wq[q], qa[mt]);
+            qa[mt] = MFMA16(wq[q], hs[(mt * 16 + (lane & 15)) * 17 + 4 * q + (lane >> 4)], qa[mt]);
+#ifdef TTS_PQ_NARROW
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-          for (int j = 0; j < 4; ++j)
-            stc(P.pq + ((long)g * Bp + mt * 16 + 4 * (lane >> 4) + j) * 128 + 16 * wave + (lane & 15), qa[mt][j]);
+          for (int j = 0; j < 4; ++j) stc(P.pq + ((long)g * Bp + mt * 16 + (lane & 15)) * 128 + 16 * wave + 4 * (lane >> 4) + j, qa[mt][j]);
+#else
+#pragma unroll
+        for (int mt = 0; mt < MT; ++mt)
+          stc4(P.pq, (((g * Bp + mt * 16 + (lane & 15)) * 128) + 16 * wave + 4 * (lane >> 4)) * 4, qa[mt]);
+#endif
       }
       PTRACE(12);
     } else {
@@ -1414,7 +1422,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           const float c = sigm_f(pre[1]) * cd[ck] + sigm_f(pre[0]) * tanh_f(pre[2]);
           const float h = sigm_f(pre[3]) * tanh_f(c);
           P.cdec[ci] = c;
-          stc(hd_nxt + frag_idx(m, g * 4 + u, 1024), h);
+          stc_quad(hd_nxt, (int)frag_idx(m, g * 4 + u, 1024), h);
         }
         lds_barrier();
       }
@@ -1473,7 +1481,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         float v = red0[mm * 17 + n];
 #pragma unroll
         for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * 17 + n];
-        stc(P.ypart + (long)(mtb * 16 + mm) * YP + (pj / JR) * 16 + n, v);
+        stc_quad(P.ypart, (mtb * 16 + mm) * YP + (pj / JR) * 16 + n, v);
       }
       lds_barrier();
     } else if (!X3P && is_pj) {

@@ -107,7 +107,28 @@ __device__ __forceinline__ f32x4 ldc4(const float* base, int off) {
   const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
   return __builtin_amdgcn_raw_buffer_load_b128(r, off, 0, AUX);
 }
+// 16-byte agent-coherent store at byte offset `off` from a wave-uniform base (buffer store, sc1:
+// write-through, one fabric write per lane instead of four 4-byte ones)
+__device__ __forceinline__ void stc4(float* base, int off, f32x4 v) {
+  const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)base, 0, 0x7fffffff, 0x00020000);
+  __builtin_amdgcn_raw_buffer_store_b128(v, r, off, 0, 16);  // lax vector conversion: a bitcast
+}
 
+// 4 consecutive elements held by the 4 lanes of a DPP quad (lane q of the quad: element e0 + q,
+// e0 % 4 == 0, every lane of the quad active): gathered into the quad's lane 0 and written as ONE
+// 16-byte coherent store. TTS_NARROW_STORES keeps the per-lane 4-byte stores (A/B builds).
+__device__ __forceinline__ void stc_quad(float* base, int e, float v) {
+#ifdef TTS_NARROW_STORES
+  stc(base + e, v);
+#else
+  const int b = __float_as_int(v);
+  const f32x4 q = {__int_as_float(__builtin_amdgcn_mov_dpp(b, 0x00, 0xf, 0xf, true)),   // quad_perm(0,0,0,0)
+                   __int_as_float(__builtin_amdgcn_mov_dpp(b, 0x55, 0xf, 0xf, true)),   // (1,1,1,1)
+                   __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xAA, 0xf, 0xf, true)),   // (2,2,2,2)
+                   __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xFF, 0xf, 0xf, true))};  // (3,3,3,3)
+  if ((threadIdx.x & 3) == 0) stc4(base, e * 4, q);
+#endif
+}
 
 // LDS-only workgroup barrier: unlike __syncthreads() (whose workgroup-scope fences wait for every
 // outstanding global load, vmcnt(0)), global loads already in flight stay in flight
