@@ -189,6 +189,179 @@ __global__ __launch_bounds__(256) void bar_hier2_kernel(unsigned* ctr, int iters
   }
 }
 
+// (P) the hierarchical barrier with K go-word polls in flight (issued about RT / K apart): the
+// release is seen within ~RT / K of landing instead of up to one load round trip later
+__device__ __forceinline__ unsigned ald(const unsigned* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+// 4 go-word polls in flight (issued about s_sleep SLP apart, then each reissued as soon as it has
+// been checked: vmcnt(3) waits for the oldest only); true once the word holds gen, false after
+// `rounds` rounds of 4 (the caller then polls with its timeout check)
+template <int SLP>
+__device__ __forceinline__ bool poll4(const unsigned* go, unsigned gen, int rounds) {
+  unsigned a, b, c, d;
+  int hit;
+  asm volatile(
+      "global_load_dword %[a], %[p], off sc1\n"
+      "s_sleep %[slp]\n"
+      "global_load_dword %[b], %[p], off sc1\n"
+      "s_sleep %[slp]\n"
+      "global_load_dword %[c], %[p], off sc1\n"
+      "s_sleep %[slp]\n"
+      "global_load_dword %[d], %[p], off sc1\n"
+      "s_mov_b32 %[hit], 0\n"
+      "1:\n"
+      "s_waitcnt vmcnt(3)\n"
+      "v_cmp_le_u32 vcc, %[g], %[a]\n"
+      "s_nop 4\n"
+      "s_cbranch_vccnz 2f\n"
+      "global_load_dword %[a], %[p], off sc1\n"
+      "s_waitcnt vmcnt(3)\n"
+      "v_cmp_le_u32 vcc, %[g], %[b]\n"
+      "s_nop 4\n"
+      "s_cbranch_vccnz 2f\n"
+      "global_load_dword %[b], %[p], off sc1\n"
+      "s_waitcnt vmcnt(3)\n"
+      "v_cmp_le_u32 vcc, %[g], %[c]\n"
+      "s_nop 4\n"
+      "s_cbranch_vccnz 2f\n"
+      "global_load_dword %[c], %[p], off sc1\n"
+      "s_waitcnt vmcnt(3)\n"
+      "v_cmp_le_u32 vcc, %[g], %[d]\n"
+      "s_nop 4\n"
+      "s_cbranch_vccnz 2f\n"
+      "global_load_dword %[d], %[p], off sc1\n"
+      "s_sub_u32 %[n], %[n], 1\n"
+      "s_cmp_gt_i32 %[n], 0\n"
+      "s_cbranch_scc1 1b\n"
+      "s_branch 3f\n"
+      "2:\n"
+      "s_mov_b32 %[hit], 1\n"
+      "3:\n"
+      "s_waitcnt vmcnt(0)\n"
+      : [a] "=&v"(a), [b] "=&v"(b), [c] "=&v"(c), [d] "=&v"(d), [hit] "=&s"(hit), [n] "+s"(rounds)
+      : [p] "v"(go), [g] "v"(gen), [slp] "i"(SLP)
+      : "vcc", "scc", "memory");
+  return hit != 0;
+}
+
+template <int SLP>
+__global__ __launch_bounds__(256) void bar_asm_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  const int xcd = blockIdx.x & 7;
+  const unsigned per = gridDim.x / 8;
+  unsigned* xc = ctr + 64 + xcd * 32;
+  unsigned* gc = ctr;
+  unsigned* go = ctr + 32;
+  for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int good = 1;
+      const unsigned gen = (unsigned)(i + 1);
+      const unsigned old = __hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == per * gen - 1) {
+        const unsigned g = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g == 8u * gen - 1) __hip_atomic_store(go, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      if (!poll4<SLP>(go, gen, 64)) {
+        const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+        while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen)
+          if (spin_timeout(t0)) {
+            good = 0;
+            break;
+          }
+      }
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
+template <int K, int SLP>
+__global__ __launch_bounds__(256) void bar_pipe_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  const int xcd = blockIdx.x & 7;
+  const unsigned per = gridDim.x / 8;
+  unsigned* xc = ctr + 64 + xcd * 32;
+  unsigned* gc = ctr;
+  unsigned* go = ctr + 32;
+  for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int good = 1;
+      const unsigned gen = (unsigned)(i + 1);
+      const unsigned old = __hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      if (old == per * gen - 1) {
+        const unsigned g = __hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (g == 8u * gen - 1) __hip_atomic_store(go, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      }
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      unsigned v[K];
+#pragma unroll
+      for (int k = 0; k < K; ++k) {
+        v[k] = ald(go);
+        if (k + 1 < K) __builtin_amdgcn_s_sleep(SLP);
+      }
+      bool done = false;
+      while (!done) {
+#pragma unroll
+        for (int k = 0; k < K; ++k) {
+          if (v[k] >= gen) {
+            done = true;
+            break;
+          }
+          v[k] = ald(go);
+        }
+        if (!done && spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      }
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
+// (T) the hierarchical barrier with NC first-level counters (workgroup g -> counter g % NC, STRIDE
+// words apart) feeding the global counter (NC arrivals), then the go word: fewer arrivals contend
+// on each counter when the whole grid arrives at once
+template <int NC, int STRIDE>
+__global__ __launch_bounds__(256) void bar_tree_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  const unsigned per = gridDim.x / NC;
+  unsigned* xc = ctr + 1024 + (blockIdx.x % NC) * STRIDE;
+  unsigned* gc = ctr;
+  unsigned* go = ctr + 32;
+  for (int i = 0; i < iters; ++i) {
+    arrive_skew(i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int good = 1;
+      const unsigned gen = (unsigned)(i + 1);
+      if (__hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per * gen - 1)
+        if (__hip_atomic_fetch_add(gc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)NC * gen - 1)
+          __hip_atomic_store(go, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen)
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
 // (C) flag array, no atomics: each workgroup stores its generation to its own slot; wave 0 polls
 // all slots (4 per lane) until the minimum reaches the generation
 __global__ __launch_bounds__(256) void bar_flags_kernel(unsigned* flags, int iters) {
@@ -362,23 +535,33 @@ int main() {
            (mode >> 1) & 1, ms * 1000.f / iters);
   }
   unsigned* big;
-  HIP_OK(hipMalloc(&big, 4096 * 4));
-  for (int sk : {0, 1000, 2000, 4000, 8000})
-  for (int v : {0, 3, 4, 6}) {
+  HIP_OK(hipMalloc(&big, 80 * 1024 * 4));
+  for (int sk : {0, 500, 1000, 2000})
+  for (int v : {0, 14, 15, 16, 17, 18, 19}) {
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_skew), &sk, 4));
     const void* f = v == 0 ? (const void*)bar_hier_kernel : v == 1 ? (const void*)bar_flags_kernel
                   : v == 2 ? (const void*)bar_go_kernel : v == 3 ? (const void*)bar_hier8_kernel
                   : v == 4 ? (const void*)bar_ctrs_kernel<8> : v == 5 ? (const void*)bar_ctrs_kernel<16>
-                  : (const void*)bar_hier2_kernel;
+                  : v == 6 ? (const void*)bar_hier2_kernel : v == 7 ? (const void*)bar_pipe_kernel<2, 4>
+                  : v == 8 ? (const void*)bar_pipe_kernel<4, 2> : v == 9 ? (const void*)bar_pipe_kernel<4, 0>
+                  : v == 10 ? (const void*)bar_pipe_kernel<8, 1> : v == 11 ? (const void*)bar_asm_kernel<2>
+                  : v == 12 ? (const void*)bar_asm_kernel<4> : v == 13 ? (const void*)bar_asm_kernel<8>
+                  : v == 14 ? (const void*)bar_tree_kernel<8, 1024> : v == 15 ? (const void*)bar_tree_kernel<16, 32>
+                  : v == 16 ? (const void*)bar_tree_kernel<16, 1024> : v == 17 ? (const void*)bar_tree_kernel<32, 32>
+                  : v == 18 ? (const void*)bar_tree_kernel<32, 1024> : (const void*)bar_tree_kernel<64, 1024>;
     const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : v == 2 ? "counter + go flag"
                    : v == 3 ? "xcd ctr + 8-slot line" : v == 4 ? "8 ctrs, poll all" : v == 5 ? "16 ctrs, poll all"
-                   : "xcd ctr, poll global";
+                   : v == 6 ? "xcd ctr, poll global" : v == 7 ? "hier, 2 polls s4" : v == 8 ? "hier, 4 polls s2"
+                   : v == 9 ? "hier, 4 polls s0" : v == 10 ? "hier, 8 polls s1" : v == 11 ? "hier, asm 4 polls s2"
+                   : v == 12 ? "hier, asm 4 polls s4" : v == 13 ? "hier, asm 4 polls s8"
+                   : v == 14 ? "tree 8 x 4KB" : v == 15 ? "tree 16 x 128B" : v == 16 ? "tree 16 x 4KB"
+                   : v == 17 ? "tree 32 x 128B" : v == 18 ? "tree 32 x 4KB" : "tree 64 x 4KB";
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
     if (sk) printf("(arrival skew up to %d memtime ticks)\n", sk);
     for (int nwg : {256}) {
       const int iters = 2000;
       float ms = timed([&] {
-        HIP_OK(hipMemsetAsync(big, 0, 4096 * 4, S));
+        HIP_OK(hipMemsetAsync(big, 0, 80 * 1024 * 4, S));
         int it = iters;
         void* args[] = {&big, &it};
         HIP_OK(hipLaunchCooperativeKernel(f, dim3(nwg), dim3(256), args, lds_force, S));

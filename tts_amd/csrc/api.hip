@@ -874,7 +874,7 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<int>(W.map, 2 * BMAX, g);
   grow<int>(W.stat, 256, g);
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
-  grow<unsigned>(W.pbar, PMAX_LAUNCH * 512, g);  // one barrier block per persistent launch (MT = 4 .. 1)
+  grow<unsigned>(W.pbar, PMAX_LAUNCH * BAR_WORDS, g);  // one barrier block per persistent launch (MT = 4 .. 1)
   grow<float>(W.anorm, (size_t)2 * BMAX, g);
   grow<float>(W.spk, (size_t)64 * 1024, g);
   grow<int>(W.win_idx, 64, g);
@@ -1136,7 +1136,7 @@ void check_encoder_barrier(tts_ctx* c) {
   pw[0] = pw[1] = 0;
   const unsigned* words = reinterpret_cast<const unsigned*>(c->tws.lc.p);
   HIP_OK(hipMemcpyAsync(&pw[0], words + 16, 4, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipMemcpyAsync(&pw[1], words + 512 + 16, 4, hipMemcpyDeviceToHost, c->s));
+  HIP_OK(hipMemcpyAsync(&pw[1], words + BAR_WORDS + 16, 4, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
   TTS_CHECK(pw[0] == 0 && pw[1] == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
 }
@@ -1246,9 +1246,9 @@ __global__ void taco_status_kernel(const unsigned* enc_bar, const unsigned* dec_
                                    const unsigned* flag, int* st) {
   const int i = threadIdx.x;
   if (i < 3 * BMAX) st[TS_RES + i] = ctl[4 + i];
-  if (i < 2) st[TS_ENC + i] = enc_bar ? (int)enc_bar[i * 512 + 16] : 0;
+  if (i < 2) st[TS_ENC + i] = enc_bar ? (int)enc_bar[i * BAR_WORDS + 16] : 0;
   if (i < PMAX_LAUNCH) {
-    st[TS_DEC + i] = dec_bar && i < ndec ? (int)dec_bar[i * 512 + 16] : 0;
+    st[TS_DEC + i] = dec_bar && i < ndec ? (int)dec_bar[i * BAR_WORDS + 16] : 0;
   }
   if (i == 0) st[TS_FLAG] = flag ? (int)*flag : 0;
 }
@@ -1462,7 +1462,7 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   c->dec_nlaunch = 0;
   for (int mt = W.MT; mt >= 1; --mt) {
     const int li = W.MT - mt;  // launch index: its barrier block (armed in taco_infer's state fill)
-    a.bar = reinterpret_cast<unsigned*>(W.pbar.p) + 512 * li;
+    a.bar = reinterpret_cast<unsigned*>(W.pbar.p) + BAR_WORDS * li;
     a.base_out = W.stat.i() + TS_END + li;
     a.D = make_dev(c, std::min(W.B, 16 * mt));
     a.trace = li == trace_li ? trace_p : nullptr;
@@ -2139,7 +2139,7 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
   grow<float>(W.g, (size_t)B * T_max * 4 * H, gen);
   grow<float>(W.o, (size_t)B * T_max * H, gen);
   grow<float>(W.p, (size_t)B * T_max * G.proj, gen);
-  grow<unsigned>(W.bar, 512, gen);
+  grow<unsigned>(W.bar, BAR_WORDS, gen);
   grow<float>(W.hbuf, (size_t)2 * 64 * H, gen);
   std::vector<int> lens(h_lens, h_lens + B);
   HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));

@@ -6,8 +6,9 @@
 // stay on chip for the whole decode:
 //   decoder_rnn   [W_ih | W_hh] (41.9 MB)  VGPRs: workgroup g owns gate tile g, 20 k-chunks per wave
 //   attention_rnn ctx/h part   (25.2 MB)   LDS:   96 KB per workgroup (tile g)
-// and a hierarchical grid barrier (per-XCD counters, then 8 arrivals on a global counter, one go
-// word; tools/persist_bench.hip: 1.9 us) replaces each launch boundary (1.7 us + cold start).
+// and a hierarchical grid barrier (16 first-level counters, then 16 arrivals on a global counter,
+// one go word; tools/persist_bench.hip: 1.8-2.1 us) replaces each launch boundary (1.7 us + cold
+// start).
 //
 // One decoder step t (TTS/tts/layers/tacotron2.py:354-369 -> decode :259-298), 5 phases:
 //   P1  stop decision for t-1 (workgroup 255; tacotron2.py:357-366)

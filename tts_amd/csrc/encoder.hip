@@ -226,10 +226,10 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
       out[((long)m * T_max + t) * O + dir * H + tl * 4 + u] = hn;
     }
     if (step + 1 < T_max) {  // directions are independent: one barrier each
-      gsync_arrive(bar + dir * 512, gen, NT);
+      gsync_arrive(bar + dir * BAR_WORDS, gen, NT);
 #pragma unroll
       for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(step + 1) * G + q * 4];
-      if (!gsync_wait(bar + dir * 512, gen, &sflag)) return;
+      if (!gsync_wait(bar + dir * BAR_WORDS, gen, &sflag)) return;
     }
   }
 }
