@@ -362,6 +362,35 @@ __global__ __launch_bounds__(256) void bar_tree_kernel(unsigned* ctr, int iters)
   }
 }
 
+// (X) a 32-workgroup barrier: one counter + go word, participants either the 32 workgroups of XCD 0
+// (blockIdx % 8 == 0, SAME = 1) or workgroups 0..31 (spread over the 8 XCDs); the rest exit
+template <int SAME>
+__global__ __launch_bounds__(256) void bar32_kernel(unsigned* ctr, int iters) {
+  __shared__ int ok;
+  if (SAME ? (blockIdx.x & 7) != 0 : blockIdx.x >= 32) return;
+  unsigned* xc = ctr + 64;
+  unsigned* go = ctr + 32;
+  for (int i = 0; i < iters; ++i) {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int good = 1;
+      const unsigned gen = (unsigned)(i + 1);
+      if (__hip_atomic_fetch_add(xc, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 32u * gen - 1)
+        __hip_atomic_store(go, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen)
+        if (spin_timeout(t0)) {
+          good = 0;
+          break;
+        }
+      ok = good;
+    }
+    __syncthreads();
+    if (!ok) return;
+  }
+}
+
 // (C) flag array, no atomics: each workgroup stores its generation to its own slot; wave 0 polls
 // all slots (4 per lane) until the minimum reaches the generation
 __global__ __launch_bounds__(256) void bar_flags_kernel(unsigned* flags, int iters) {
@@ -536,8 +565,8 @@ int main() {
   }
   unsigned* big;
   HIP_OK(hipMalloc(&big, 80 * 1024 * 4));
-  for (int sk : {0, 500, 1000, 2000})
-  for (int v : {0, 14, 15, 16, 17, 18, 19}) {
+  for (int sk : {0, 1000})
+  for (int v : {0, 15, 20, 21}) {
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_skew), &sk, 4));
     const void* f = v == 0 ? (const void*)bar_hier_kernel : v == 1 ? (const void*)bar_flags_kernel
                   : v == 2 ? (const void*)bar_go_kernel : v == 3 ? (const void*)bar_hier8_kernel
@@ -548,14 +577,16 @@ int main() {
                   : v == 12 ? (const void*)bar_asm_kernel<4> : v == 13 ? (const void*)bar_asm_kernel<8>
                   : v == 14 ? (const void*)bar_tree_kernel<8, 1024> : v == 15 ? (const void*)bar_tree_kernel<16, 32>
                   : v == 16 ? (const void*)bar_tree_kernel<16, 1024> : v == 17 ? (const void*)bar_tree_kernel<32, 32>
-                  : v == 18 ? (const void*)bar_tree_kernel<32, 1024> : (const void*)bar_tree_kernel<64, 1024>;
+                  : v == 18 ? (const void*)bar_tree_kernel<32, 1024> : v == 19 ? (const void*)bar_tree_kernel<64, 1024>
+                  : v == 20 ? (const void*)bar32_kernel<1> : (const void*)bar32_kernel<0>;
     const char* nm = v == 0 ? "hierarchical" : v == 1 ? "flag array" : v == 2 ? "counter + go flag"
                    : v == 3 ? "xcd ctr + 8-slot line" : v == 4 ? "8 ctrs, poll all" : v == 5 ? "16 ctrs, poll all"
                    : v == 6 ? "xcd ctr, poll global" : v == 7 ? "hier, 2 polls s4" : v == 8 ? "hier, 4 polls s2"
                    : v == 9 ? "hier, 4 polls s0" : v == 10 ? "hier, 8 polls s1" : v == 11 ? "hier, asm 4 polls s2"
                    : v == 12 ? "hier, asm 4 polls s4" : v == 13 ? "hier, asm 4 polls s8"
                    : v == 14 ? "tree 8 x 4KB" : v == 15 ? "tree 16 x 128B" : v == 16 ? "tree 16 x 4KB"
-                   : v == 17 ? "tree 32 x 128B" : v == 18 ? "tree 32 x 4KB" : "tree 64 x 4KB";
+                   : v == 17 ? "tree 32 x 128B" : v == 18 ? "tree 32 x 4KB" : v == 19 ? "tree 64 x 4KB"
+                   : v == 20 ? "32 WGs of one XCD" : "32 WGs over 8 XCDs";
     HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds_force));
     if (sk) printf("(arrival skew up to %d memtime ticks)\n", sk);
     for (int nwg : {256}) {
