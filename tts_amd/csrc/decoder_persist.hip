@@ -821,6 +821,32 @@ __device__ __forceinline__ void gemm_x3_hatt_ctx(f32x4 (&acc1)[MT], f32x4 (&acc2
     }
 }
 
+// m-tiles O .. O + N - 1 of an accumulator array: the split-f16 GEMM helpers keep MT-sized operand
+// and accumulator temporaries, so batch tiles of 48 / 64 rows run them in passes of at most 2 m-tiles
+// (32 rows; the activation base moves by 2 m-tiles, nk 16-column chunks of 256 floats each) and stay
+// within 256 VGPRs
+template <int O, int N, int M>
+__device__ __forceinline__ f32x4 (&msub(f32x4 (&a)[M]))[N] {
+  static_assert(O + N <= M, "m-tile range");
+  return *reinterpret_cast<f32x4(*)[N]>(&a[O]);
+}
+#define X3_PASSES(MT_, CALL)                       \
+  do {                                             \
+    if constexpr ((MT_) <= 2) {                    \
+      constexpr int NM = (MT_), MO = 0;            \
+      CALL;                                        \
+    } else {                                       \
+      {                                            \
+        constexpr int NM = 2, MO = 0;              \
+        CALL;                                      \
+      }                                            \
+      {                                            \
+        constexpr int NM = (MT_) - 2, MO = 2;      \
+        CALL;                                      \
+      }                                            \
+    }                                              \
+  } while (0)
+
 // gemm_seg for two accumulator sets over the SAME activation chunks (one load per chunk feeds both)
 template <int MT, int NC, int G, class WF1, class WF2>
 __device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* base, int nk, int kc0,
@@ -988,7 +1014,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt) accd[mt] = acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto dec_hdec_part = [&](const float* hd) {
-    if constexpr (X3P) gemm_x3<MT, 4>(accd, hd, 64, 4 * wave, lane, wdx_f(6));
+    if constexpr (X3P)
+      X3_PASSES(MT, (gemm_x3<NM, 4>(msub<MO, NM>(accd), hd + MO * 64 * 256, 64, 4 * wave, lane, wdx_f(6))));
     else gemm_seg<MT, 8, 4>(accd, hd, 64, 8 * wave, lane, [&](int i) { return wd[12 + i]; });
   };
   // attention_rnn ctx/h tile g complete: reduce over the waves, add the biases, publish the next
@@ -1373,7 +1400,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         if constexpr (!X3P) gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
       } else {  // no item: both h_att parts and the decoder_rnn h_dec part
         if constexpr (X3P)
-          gemm_x3_pair<MT, 4>(accd, acca, P.hatt, 64, 4 * wave, lane, wdx_f(0), wap_f(16 + 4 * wave));
+          X3_PASSES(MT, (gemm_x3_pair<NM, 4>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.hatt + MO * 64 * 256, 64,
+                                             4 * wave, lane, wdx_f(0), wap_f(16 + 4 * wave))));
         else
           gemm_seg2<MT, 8, 2>(accd, acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; },
                               [&](int i) { return Wap[(32 + 8 * wave + i) * 64 + lane]; });
@@ -1396,10 +1424,12 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     {
       if constexpr (X3P) {
         if (g >= IW0)  // + both h_att parts (moved here from P4 / P6: h_att read once per step)
-          gemm_x3_hatt_ctx<MT, 4, 2>(accd, acca, P.hatt, 64, 4 * wave, P.ctx, 32, 2 * wave, lane, wdx_f(0),
-                                     wap_f(16 + 4 * wave), wdx_f(4), wap_f(2 * wave));
+          X3_PASSES(MT, (gemm_x3_hatt_ctx<NM, 4, 2>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.hatt + MO * 64 * 256, 64,
+                                                    4 * wave, P.ctx + MO * 32 * 256, 32, 2 * wave, lane, wdx_f(0),
+                                                    wap_f(16 + 4 * wave), wdx_f(4), wap_f(2 * wave))));
         else
-          gemm_x3_pair<MT, 2>(accd, acca, P.ctx, 32, 2 * wave, lane, wdx_f(4), wap_f(2 * wave));
+          X3_PASSES(MT, (gemm_x3_pair<NM, 2>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.ctx + MO * 32 * 256, 32,
+                                             2 * wave, lane, wdx_f(4), wap_f(2 * wave))));
       }
       else
         gemm_seg2<MT, 4, 4>(accd, acca, P.ctx, 32, 4 * wave, lane, [&](int i) { return wd[8 + i]; },
