@@ -37,6 +37,17 @@
  * contexts (one per device) run concurrently. The reference model is not re-entrant at all
  * (per-call state on self: TTS/tts/layers/tacotron2.py:221-233).
  *
+ * Host synchronisation: tts_taco_infer(_spk) returns per-utterance step counts and so waits for
+ * its work. In the default split-f16 GEMM mode every other compute entry (postnet, melgan,
+ * pwgan, glow) also ends with one hipStreamSynchronize on its stream, to read the range flag and
+ * re-run the call on the fp32 kernels if an operand left the f16 range (a NaN input counts as out
+ * of range and runs the call twice). With tts_set_gemm_mode(ctx, 0) those entries stay
+ * stream-asynchronous. INTEGRATION.md §3.
+ *
+ * Device use: the persistent kernels need every one of their workgroups resident at once (one per
+ * CU); another process or stream keeping kernels on the same GPU during a call can delay them
+ * past the barrier wait limit below, and the call then fails (retryable).
+ *
  * Grid barriers: the persistent decoder / BiLSTM / GE2E kernels give up a barrier wait after
  * TTS_BARRIER_TIMEOUT_MS (environment, default 2000) and the call returns an error; nothing is
  * left half-written that a retry depends on, so retrying the call is safe.
