@@ -27,6 +27,8 @@
 #include "conv_epi.h"
 #include "split16.h"
 
+#include <cstdlib>
+
 namespace {
 constexpr int CX_XR = 80;  // staging row, halves: 32 hi | 32 lo | 16 pad (160 B)
 
@@ -323,7 +325,8 @@ __global__ __launch_bounds__(64 * WM * WN) void conv_x3_kernel(ConvArgs a, int n
 
 // tiles {MI, NI, WM, WN}: every wave owns >= 32 output channels x >= 32 positions, so each
 // ds_read_b128 of the B operand feeds >= 6 MFMAs and each weight fragment >= 6
-//   128 x 64 : 2,4,4,1  (Cout % 128 == 0)      192 x 64 : 3,4,4,1  (Cout == 192)
+//   128 x 64 : 2,4,4,1  (Cout % 128 == 0, 1x1) 192 x 64 : 3,4,4,1  (Cout == 192)
+//   128 x 48 : 2,3,4,1  (Cout % 128 == 0, K >= 2)
 //    96 x 128: 3,4,2,2  (Cout == 96)             64 x 128: 2,4,2,2  (Cout % 64 == 0)
 //    80 x 128: 5,2,1,4  (Cout == 80)             48 x 128: 3,2,1,4  (Cout == 48)
 enum { CX_T128 = 0, CX_T192, CX_T96, CX_T64, CX_T80, CX_T48, CX_NONE };
@@ -387,7 +390,20 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t s) {
             "conv_x3: time-major source rows must be 16-byte aligned");
   if (a.max_q <= 0 || a.B <= 0) return;
   switch (cx_tile(a.Cout)) {
-    case CX_T128: cx_taps<2, 4, 4, 1, 2>(a, s); break;
+    case CX_T128: {
+      // 128 x 48 tiles for convs with taps (k5 encoder / postnet convs, k7, the phase-merged
+      // ConvTransposes: more, shorter tiles fill the chip better: tools/cx3_bench.hip, encoder conv
+      // 55.8 -> 45.5 us, postnet 512 -> 512 180.5 -> 176.1 us, upsample 1 197.4 -> 173.2 us,
+      // upsample 2 226.7 -> 208.6 us), 128 x 64 for 1x1 convs (BiLSTM input projection 55.0 us
+      // against 68.0 us at 48 positions). TTS_CX_NI128 = 3 / 4 forces one width (A/B builds).
+      static const int force = [] {
+        const char* e = std::getenv("TTS_CX_NI128");
+        return e ? std::atoi(e) : 0;
+      }();
+      if (force == 3 || (force != 4 && a.K >= 2)) cx_taps<2, 3, 4, 1, 2>(a, s);
+      else cx_taps<2, 4, 4, 1, 2>(a, s);
+      break;
+    }
     case CX_T192: cx_taps<3, 4, 4, 1, 2>(a, s); break;
     case CX_T96: cx_taps<3, 4, 2, 2, 1>(a, s); break;
     case CX_T64: cx_taps<2, 4, 2, 2, 1>(a, s); break;
