@@ -222,7 +222,7 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
       }
       cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
       const float hn = sigm_f(pre[3]) * tanh_f(cst);
-      stc(ho + frag_idx(m, tl * 4 + u, H), hn);
+      stc_quad(ho, (int)frag_idx(m, tl * 4 + u, H), hn);  // lanes u = 0..3 of a quad: one 16-byte store
       out[((long)m * T_max + t) * O + dir * H + tl * 4 + u] = hn;
     }
     if (step + 1 < T_max) {  // directions are independent: one barrier each
