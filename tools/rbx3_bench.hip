@@ -228,17 +228,22 @@ int main(int argc, char** argv) {
     timeit("split-f16 (library tile)", [&] { launch_resblock_x3(a, kM, C, S); });
     if (C == 192) {
       timeit("x3 TQ64 12x1", [&] { launch_rbx3<192, 64, 12, 1, 3>(a, kM, S); });
+      timeit("x3 TQ48 12x1 (NI3)", [&] { launch_rbx3<192, 48, 12, 1, 3>(a, kM, S); });
+      timeit("x3 TQ32 12x1 (NI2)", [&] { launch_rbx3<192, 32, 12, 1, 3>(a, kM, S); });
       timeit("x3 TQ64 4x2 (MI3 NI2)", [&] { launch_rbx3<192, 64, 4, 2, 3>(a, kM, S); });
       timeit("x3 TQ64 4x1 (MI3 NI4)", [&] { launch_rbx3<192, 64, 4, 1, 3>(a, kM, S); });
       timeit("x3 TQ64 6x2 (MI2 NI2)", [&] { launch_rbx3<192, 64, 6, 2, 3>(a, kM, S); });
     } else if (C == 96) {
       timeit("x3 TQ128 6x2", [&] { launch_rbx3<96, 128, 6, 2, 3>(a, kM, S); });
       timeit("x3 TQ96 6x2 (NI3)", [&] { launch_rbx3<96, 96, 6, 2, 3>(a, kM, S); });
+      timeit("x3 TQ64 6x2 (NI2)", [&] { launch_rbx3<96, 64, 6, 2, 3>(a, kM, S); });
       timeit("x3 TQ96 2x2 (MI3 NI3)", [&] { launch_rbx3<96, 96, 2, 2, 3>(a, kM, S); });
       timeit("x3 TQ128 2x4 (MI3 NI2)", [&] { launch_rbx3<96, 128, 2, 4, 3>(a, kM, S); });
     } else {
       timeit("x3 TQ128 3x4", [&] { launch_rbx3<48, 128, 3, 4, 3>(a, kM, S); });
       timeit("x3 TQ192 3x4 (NI3)", [&] { launch_rbx3<48, 192, 3, 4, 3>(a, kM, S); });
+      timeit("x3 TQ160 3x4 (NI5/2)", [&] { launch_rbx3<48, 160, 3, 2, 3>(a, kM, S); });
+      timeit("x3 TQ144 3x3 (NI3)", [&] { launch_rbx3<48, 144, 3, 3, 3>(a, kM, S); });
       timeit("x3 TQ192 1x4 (MI3 NI3)", [&] { launch_rbx3<48, 192, 1, 4, 3>(a, kM, S); });
       timeit("x3 TQ128 1x8 (MI3 NI1)", [&] { launch_rbx3<48, 128, 1, 8, 3>(a, kM, S); });
     }
