@@ -28,6 +28,9 @@
 #include "split16.h"
 
 #include <cstdlib>
+#include <algorithm>
+#include <mutex>
+#include <map>
 
 namespace {
 constexpr int CX_XR = 80;  // staging row, halves: 32 hi | 32 lo | 16 pad (160 B)
@@ -366,6 +369,45 @@ static void cx_launch(const ConvArgs& a, hipStream_t s) {
   conv_x3_kernel<MI, NI, WM, WN, KT, RS, SD><<<dim3(8 * per), 64 * WM * WN, lds, s>>>(a, nq, nco, nz);
 }
 
+// estimated cost of a call on one tile shape: rounds of resident workgroups x positions per tile
+// (host-side tile count from max_q, an upper bound for ragged batches; residency from the
+// occupancy query of the instantiation the call would launch, cached per kernel and LDS size)
+template <int MI, int NI, int WM, int WN, int KT, int RS, int SD>
+static long cx_cost_k(const ConvArgs& a) {
+  constexpr int TC = 16 * MI * WM, TQ = 16 * NI * WN;
+  const void* f = (const void*)conv_x3_kernel<MI, NI, WM, WN, KT, RS, SD>;
+  const size_t lds = (size_t)2 * (TQ + (KT - 1) * a.dil) * CX_XR * 2;
+  static std::mutex mu;
+  static std::map<size_t, long> slots_by_lds;
+  long slots;
+  {
+    std::lock_guard<std::mutex> lk(mu);
+    auto it = slots_by_lds.find(lds);
+    if (it == slots_by_lds.end()) {
+      HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
+      int dev = 0, cus = 0, nb = 0;
+      HIP_OK(hipGetDevice(&dev));
+      HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * WM * WN, lds));
+      it = slots_by_lds.emplace(lds, std::max(1L, (long)nb * cus)).first;
+    }
+    slots = it->second;
+  }
+  const long tiles = (long)((a.max_q + TQ - 1) / TQ) * ((a.Cout + TC - 1) / TC) * a.B * a.nphase;
+  return (tiles + slots - 1) / slots * TQ;
+}
+template <int MI, int NI, int WM, int WN, int SD12>
+static long cx_cost(const ConvArgs& a) {
+  switch (a.K) {
+    case 1: return cx_cost_k<MI, NI, WM, WN, 1, 2, SD12>(a);
+    case 2: return cx_cost_k<MI, NI, WM, WN, 2, 2 * SD12, SD12>(a);
+    case 3: return cx_cost_k<MI, NI, WM, WN, 3, 3, 1>(a);
+    case 5: return cx_cost_k<MI, NI, WM, WN, 5, 5, 2>(a);
+    case 7: return cx_cost_k<MI, NI, WM, WN, 7, 7, 1>(a);
+    default: return 0;
+  }
+}
+
 template <int MI, int NI, int WM, int WN, int SD12>
 static void cx_taps(const ConvArgs& a, hipStream_t s) {
   switch (a.K) {
@@ -391,16 +433,19 @@ void launch_conv_x3(const ConvArgs& a, hipStream_t s) {
   if (a.max_q <= 0 || a.B <= 0) return;
   switch (cx_tile(a.Cout)) {
     case CX_T128: {
-      // 128 x 48 tiles for convs with taps (k5 encoder / postnet convs, k7, the phase-merged
-      // ConvTransposes: more, shorter tiles fill the chip better: tools/cx3_bench.hip, encoder conv
-      // 55.8 -> 45.5 us, postnet 512 -> 512 180.5 -> 176.1 us, upsample 1 197.4 -> 173.2 us,
-      // upsample 2 226.7 -> 208.6 us), 128 x 64 for 1x1 convs (BiLSTM input projection 55.0 us
-      // against 68.0 us at 48 positions). TTS_CX_NI128 = 3 / 4 forces one width (A/B builds).
+      // 128 x 48 or 128 x 64 tiles, whichever the round-quantised cost model prefers (ties: 64);
+      // 1x1 convs keep 128 x 64.
+      // tools/cx3_bench.hip (C2 shapes, 48 / 64 wide): encoder conv 45.5 / 55.8 us, postnet
+      // 512 -> 512 176.1 / 180.5 us, upsample 1 173.2 / 197.4 us, upsample 2 208.6 / 226.7 us;
+      // Glow-TTS (WN convs 192 -> 384, 8 k squeezed frames: 513 tiles on 512 slots at 48 wide)
+      // 4.75 / 4.44 ms per call. TTS_CX_NI128 = 3 / 4 forces one width (A/B builds).
       static const int force = [] {
         const char* e = std::getenv("TTS_CX_NI128");
         return e ? std::atoi(e) : 0;
       }();
-      if (force == 3 || (force != 4 && a.K >= 2)) cx_taps<2, 3, 4, 1, 2>(a, s);
+      bool narrow = force == 3;
+      if (!force && a.K >= 2) narrow = cx_cost<2, 3, 4, 1, 2>(a) < cx_cost<2, 4, 4, 1, 2>(a);
+      if (narrow) cx_taps<2, 3, 4, 1, 2>(a, s);
       else cx_taps<2, 4, 4, 1, 2>(a, s);
       break;
     }
