@@ -28,7 +28,8 @@ def main():
     ap.add_argument("--cpu-utts", type=int, default=0)
     a = ap.parse_args()
     T, M = lj_profile()
-    T, M = T[:a.batch], M[:a.batch]
+    T = [T[i % len(T)] for i in range(a.batch)]  # batch 64 (config C4): the 32-utterance profile twice
+    M = [M[i % len(M)] for i in range(a.batch)]
     cfg = GlowConfig()
     m = GlowTts(num_chars=cfg.num_chars)
     sd = synth_state_dict(glow_spec(cfg), 3)

@@ -26,7 +26,7 @@ def main():
     ap.add_argument("--cpu-frames", type=int, default=0)
     a = ap.parse_args()
     _, M = lj_profile()
-    M = M[:a.batch]
+    M = [M[i % len(M)] for i in range(a.batch)]  # batch 64 (config C4): the 32-utterance profile twice
     g = ParallelWaveganGenerator()
     g.load_state_dict({k: torch.from_numpy(v) for k, v in synth_state_dict(pwgan_spec(PwganConfig()), 5).items()})
     g.remove_weight_norm()
