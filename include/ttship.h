@@ -123,9 +123,10 @@ int tts_taco_postnet(tts_ctx* ctx, const float* d_dec, const int32_t* h_lens, in
    decoder_rnn h and c (B, 1024), context (B, 512), attention weights and cumulative weights
    (B, T_max). Rows that stopped before the call's last step hold the state the batched decode left
    in them, not their own final state: compare rows that ran the call's full step count. Any output
-   pointer may be NULL (skipped). */
-int tts_taco_decoder_state(tts_ctx* ctx, float* d_att_h, float* d_att_c, float* d_dec_h, float* d_dec_c,
-                           float* d_context, float* d_alpha, float* d_alpha_cum, void* stream);
+   pointer may be NULL (skipped). B and T_max size the caller's buffers and must equal the last
+   decode's batch and encoder length (an error otherwise, nothing written). */
+int tts_taco_decoder_state(tts_ctx* ctx, int B, int T_max, float* d_att_h, float* d_att_c, float* d_dec_h,
+                           float* d_dec_c, float* d_context, float* d_alpha, float* d_alpha_cum, void* stream);
 
 /* ---- MultiBand-MelGAN generator ---- */
 int tts_melgan_set_tensor(tts_ctx* ctx, const char* name, const float* h_data, const int64_t* shape, int ndim);

@@ -90,3 +90,82 @@ def test_find_endpoint_and_wav_bytes():
     ap.save_wav(wav, buf)
     sr, x = scipy.io.wavfile.read(io.BytesIO(buf.getvalue()))
     assert sr == 22050 and x.dtype == np.int16 and x.max() == 32767
+
+
+def _write_stats(path, ap, wav, audio):
+    """Stats as TTS/bin/compute_statistics.py:40-80 computes and saves them (np.save of a dict,
+    range-normalisation keys removed from the stored audio config) for one waveform."""
+    mel = ap.melspectrogram(wav)
+    lin = ap.spectrogram(wav)
+    n = mel.shape[1]
+    mel_mean = mel.sum(1) / n
+    lin_mean = lin.sum(1) / n
+    stats = {"mel_mean": mel_mean, "mel_std": np.sqrt((mel ** 2).sum(1) / n - mel_mean ** 2),
+             "linear_mean": lin_mean, "linear_std": np.sqrt((lin ** 2).sum(1) / n - lin_mean ** 2)}
+    cfg = dict(audio, stats_path=str(path), signal_norm=True)
+    for k in ("max_norm", "min_level_db", "symmetric_norm", "clip_norm"):
+        del cfg[k]
+    stats["audio_config"] = cfg
+    np.save(path, stats, allow_pickle=True)
+    return stats
+
+
+def _test_wav():
+    rs = np.random.RandomState(3)
+    t = np.arange(2 * 22050) / 22050.0
+    return 0.4 * np.sin(2 * np.pi * (180 + 300 * t) * t) + 0.2 * np.sin(2 * np.pi * 2100 * t) + 0.02 * rs.randn(t.size)
+
+
+def test_mean_var_scaler_roundtrip(tmp_path):
+    """tests/test_audio.py:157-176 (test_scaler): with `stats_path`, melspectrogram() is mean-var
+    scaled and _denormalize() inverts it to the un-normalised mel within 1e-4; the stats file is the
+    object array compute_statistics.py writes. The reference's own tests/inputs/scale_stats.npy is a
+    pickle and is not loaded here (numpy's safe loader refuses it), so the stats are recomputed."""
+    path = tmp_path / "scale_stats.npy"
+    plain = AudioProcessor(**dict(LJ_AUDIO, signal_norm=False))
+    wav = _test_wav()
+    stats = _write_stats(path, plain, wav, LJ_AUDIO)
+    ap = AudioProcessor(**dict(LJ_AUDIO, stats_path=str(path), do_trim_silence=True))
+    assert ap.signal_norm is True and ap.max_norm is None and ap.symmetric_norm is None and ap.clip_norm is None
+    mel_reference = plain.melspectrogram(wav)
+    mel_norm = ap.melspectrogram(wav)
+    assert np.allclose(mel_norm, (mel_reference - stats["mel_mean"][:, None]) / stats["mel_std"][:, None])
+    assert abs(mel_norm.mean(1)).max() < 1e-6 and abs(mel_norm.std(1) - 1).max() < 1e-6
+    mel_denorm = ap._denormalize(mel_norm)
+    assert abs(mel_reference - mel_denorm).max() < 1e-4
+    # the linear branch is selected by fft_size / 2 rows (audio.py:117), so the 513-row linear
+    # spectrogram raises exactly as in the reference
+    import pytest
+    with pytest.raises(RuntimeError, match="Mean-Var stats"):
+        ap.spectrogram(wav)
+    # the stats were computed with other audio parameters: load_stats asserts (audio.py:174-179)
+    with pytest.raises(AssertionError, match="mel_fmin"):
+        AudioProcessor(**dict(LJ_AUDIO, mel_fmin=0.0, stats_path=str(path)))
+
+
+def test_stats_loader_refuses_foreign_globals(tmp_path):
+    """load_stats_file admits numpy array reconstruction and dicts only: a stats file whose pickle
+    names any other callable is refused before that callable runs."""
+    import pickle
+    import pytest
+    from tts_amd.audio import load_stats_file
+
+    hit = tmp_path / "ran"
+
+    class Evil:
+        def __reduce__(self):
+            return (open, (str(hit), "w"))
+
+    arr = np.empty((), dtype=object)
+    arr[()] = {"mel_mean": Evil()}
+    path = tmp_path / "evil.npy"
+    np.save(path, arr, allow_pickle=True)
+    with pytest.raises(pickle.UnpicklingError, match="refused"):
+        load_stats_file(path)
+    assert not hit.exists()
+    # the .npz form (audio_config as JSON) loads with allow_pickle=False
+    npz = tmp_path / "stats.npz"
+    np.savez(npz, mel_mean=np.zeros(80), mel_std=np.ones(80), linear_mean=np.zeros(513),
+             linear_std=np.ones(513), audio_config=json.dumps({"num_mels": 80}))
+    s = load_stats_file(npz)
+    assert s["audio_config"] == {"num_mels": 80} and s["mel_std"].shape == (80,)

@@ -230,6 +230,39 @@ def test_fullband_melgan_generator_vs_oracle(mode):
         assert not wav[i, 0, ref.shape[1]:].any()
 
 
+def test_fullband_default_odd_length_unaligned_rows_vs_oracle():
+    """FullbandMelganGenerator's own defaults (base 512, upsampling 2x8x2x2, 4 residual blocks,
+    inference padding 2): an odd mel length makes the first stage's row length 2 (M + 4) not a
+    multiple of 4, so the split-f16 block kernel stores per position instead of 16 bytes at a time
+    (this shape used to raise). Against the oracle, ragged, padding 2."""
+    from tts_amd import FullbandMelganGenerator
+    from tts_amd.spec import MelganConfig
+    _dev()
+    cfg, sd = melgan_state_dict(9, MelganConfig(out_channels=1, base_channels=512, upsample_factors=(2, 8, 2, 2),
+                                                num_res_blocks=4, pqmf=False))
+    v = FullbandMelganGenerator()
+    full = v.state_dict()
+    full.update({k: torch.from_numpy(t) for k, t in sd.items()})
+    v.load_state_dict(full)
+    v.remove_weight_norm()
+    v = v.cuda().eval()
+    assert v.inference_padding == 2
+    orc = melgan_oracle(cfg, sd)
+    rs = np.random.RandomState(5)
+    lens = [7, 4]
+    batch = np.zeros((2, 80, max(lens)), np.float32)
+    for i, L in enumerate(lens):
+        batch[i, :, :L] = rs.normal(0, 1.5, (80, L))
+    wav = v.inference(torch.from_numpy(batch).cuda(), lengths=lens).cpu().numpy()
+    for i, L in enumerate(lens):
+        c = batch[i, :, :L]
+        c = np.concatenate([np.repeat(c[:, :1], 2, 1), c, np.repeat(c[:, -1:], 2, 1)], 1)  # replicate pad
+        ref = orc.generator(c).reshape(-1)
+        assert ref.size == 256 * (L + 4)
+        assert np.abs(wav[i, 0, :ref.size] - ref).max() <= WAV_TOL, i
+        assert not wav[i, 0, ref.size:].any()
+
+
 def test_mbmelgan_too_short_raises(melgan):
     fx, cfg, sd, v = melgan
     v.inference_padding = 0
@@ -759,16 +792,35 @@ def test_postnet_vs_oracle():
         assert not out[i, L:].any()
 
 
-def _synth_files(tmp_path, with_vocoder=True):
-    import json as _json
+def _synth_models():
+    """The seeded Tacotron2-DDC / MB-MelGAN weights behind _synth_files (also the oracle's)."""
     from tts_amd.spec import MelganConfig, TacotronConfig
     from tts_amd.text import symbols
     cfg = TacotronConfig(num_chars=len(symbols))
     _, sd = taco_state_dict(None, seed=21, overrides={}, stop_bias=-1e4, cfg=cfg)
+    mcfg, msd = melgan_state_dict(seed=5, cfg=MelganConfig())
+    return cfg, sd, mcfg, msd
+
+
+def _synth_files(tmp_path, with_vocoder=True, stats=False):
+    """Checkpoints + configs for Synthesizer. ``stats``: the audio section carries `stats_path`
+    (mean-var scaling), as the reference's DDC and MB-MelGAN configs do, pointing at a stats file
+    written as TTS/bin/compute_statistics.py writes it."""
+    import json as _json
+    cfg, sd, mcfg, msd = _synth_models()
     audio = dict(fft_size=1024, win_length=1024, hop_length=256, sample_rate=22050, preemphasis=0.0,
                  ref_level_db=20, power=1.5, griffin_lim_iters=4, num_mels=80, mel_fmin=50.0, mel_fmax=7600.0,
                  spec_gain=1, signal_norm=True, min_level_db=-100, symmetric_norm=True, max_norm=4.0,
                  clip_norm=True)
+    if stats:
+        rs = np.random.RandomState(11)
+        # spec_gain 1: log10 magnitudes, so LJ-like stats are a few units
+        st = {"mel_mean": rs.uniform(-3, -1, 80), "mel_std": rs.uniform(0.3, 0.8, 80),
+              "linear_mean": rs.uniform(-3, -1, 513), "linear_std": rs.uniform(0.3, 0.8, 513)}
+        acfg = {k: v for k, v in audio.items() if k not in ("max_norm", "min_level_db", "symmetric_norm", "clip_norm")}
+        audio["stats_path"] = acfg["stats_path"] = str(tmp_path / "scale_stats.npy")
+        st["audio_config"] = acfg
+        np.save(tmp_path / "scale_stats.npy", st, allow_pickle=True)
     tcfg = {"model": "Tacotron2", "r": 7, "use_phonemes": False, "text_cleaner": "english_cleaners",
             "audio": audio, "attention_norm": "sigmoid", "double_decoder_consistency": True, "ddc_r": 7,
             "prenet_dropout": False, "separate_stopnet": True, "location_attn": True}
@@ -778,7 +830,6 @@ def _synth_files(tmp_path, with_vocoder=True):
     conf = {"use_cuda": True, "tts_checkpoint": str(tmp_path / "tts.pth"), "tts_config": str(tmp_path / "tts.json"),
             "tts_speakers": None, "vocoder_checkpoint": None, "vocoder_config": None, "wavernn_lib_path": None}
     if with_vocoder:
-        mcfg, msd = melgan_state_dict(seed=5, cfg=MelganConfig())
         vcfg = {"generator_model": "multiband_melgan_generator", "audio": audio,
                 "generator_model_params": {"upsample_factors": list(mcfg.upsample_factors),
                                            "num_res_blocks": mcfg.num_res_blocks}}
@@ -824,6 +875,80 @@ def test_synthesizer_griffin_lim_fallback(tmp_path):
     wavs = synth.synthesize_batch(["Griffin and Lim.", "Phase from noise."])
     for w in wavs:
         assert np.isfinite(w).all() and abs(len(w) - 20 * 256) <= 256
+
+
+def test_synthesizer_mean_var_config_vs_oracle_chain(tmp_path):
+    """Synthesizer from configs carrying `stats_path` (TTS/tts/configs/config.json:40,
+    vocoder/configs/multiband_melgan_config.json:34), checked against the oracle chain: every
+    sentence of synthesize_batch against TacoOracle -> MelganOracle at B = 1 on the same
+    text_to_seqvec ids (server/synthesizer.py:144-158), and tts()'s 16-bit wav against the oracle
+    waveforms cut by find_endpoint, joined with 10000-sample gaps and scaled as save_wav scales
+    (:179-186)."""
+    import io
+    import scipy.io.wavfile
+    from oracle.taco_np import TacoOracle
+    from tts_amd.synthesizer import Synthesizer
+    from tts_amd.text import text_to_seqvec
+    _dev()
+    conf = _synth_files(tmp_path, stats=True)
+    synth = Synthesizer(conf)
+    assert hasattr(synth.ap, "mel_scaler") and synth.ap.signal_norm is True
+    steps, r = 24, 2
+    synth.tts_model.decoder.max_decoder_steps = steps
+    cfg, sd, mcfg, msd = _synth_models()
+    to, vo = TacoOracle(sd, cfg.attn_norm, cfg.r), melgan_oracle(mcfg, msd)
+    sens = ["Hello world.", "This is a longer test of the batched path, with 2 numbers!", "Short one?"]
+    wavs = synth.synthesize_batch(sens)
+    refs = []
+    for s_, w in zip(sens, wavs):
+        ids = text_to_seqvec(s_, synth.tts_config)
+        _, p, _, _ = to.inference(ids, r, steps)
+        ref = vo.inference(p.T, pad=0).reshape(-1)
+        assert w.shape == ref.shape == (steps * r * 256,)
+        err = float(np.abs(w - ref).max())
+        assert err <= WAV_TOL, (s_, err)
+        refs.append(ref)
+    buf = synth.tts(" ".join(sens))
+    sr, x = scipy.io.wavfile.read(io.BytesIO(buf.getvalue()))
+    joined = []
+    for ref in refs:
+        joined += list(ref[:synth.ap.find_endpoint(ref)]) + [0] * 10000
+    joined = np.asarray(joined, np.float32)
+    expect = (joined * (32767 / max(0.01, np.max(np.abs(joined))))).astype(np.int16)
+    assert sr == 22050 and x.dtype == np.int16 and x.shape == expect.shape
+    assert np.abs(x.astype(np.int32) - expect).max() <= 1
+
+
+def test_synthesis_griffin_lim_mean_var_vs_oracle(tmp_path):
+    """synthesis() (tts/utils/synthesis.py:178-262) with a mean-var AudioProcessor: the parsed
+    decoder / postnet outputs against the oracle, and the Griffin-Lim waveform (denormalised by the
+    mel scaler, audio.py:143-145,241-248, trimmed) against Griffin-Lim of the oracle's postnet
+    output under the same random phase."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd.audio import AudioProcessor
+    from tts_amd.factories import load_config
+    from tts_amd.synthesis import synthesis, text_to_seqvec
+    from tts_amd.synthesizer import Synthesizer
+    _dev()
+    conf = _synth_files(tmp_path, with_vocoder=False, stats=True)
+    model = Synthesizer(conf).tts_model
+    steps, r = 10, 2
+    model.decoder.max_decoder_steps = steps
+    C = load_config(conf["tts_config"])
+    ap = AudioProcessor(**C["audio"])
+    text = "Hello there, mean and variance."
+    np.random.seed(7)
+    wav, align, dec, post, stop, _ = synthesis(model, text, C, True, ap, use_griffin_lim=True, do_trim_silence=True)
+    cfg, sd, _, _ = _synth_models()
+    ids = text_to_seqvec(text, C)
+    d, p, a, _ = TacoOracle(sd, cfg.attn_norm, cfg.r).inference(ids, r, steps)
+    assert post.shape == p.shape and np.abs(post - p).max() <= MEL_TOL and np.abs(dec - d).max() <= MEL_TOL
+    assert (align.argmax(1) == a.argmax(1)).all() and stop.shape[0] == steps
+    np.random.seed(7)
+    ref = ap.inv_melspectrogram(p.T)
+    ref = ref[:ap.find_endpoint(ref)]
+    assert wav.shape == ref.shape
+    assert np.abs(wav - ref).max() <= 1e-3 * np.abs(ref).max()
 
 
 # --------------------------------------------------------------------- GE2E speaker encoder

@@ -42,7 +42,7 @@ SIGNATURES = [
     ("tts_taco_set_options", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_taco_encoder", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
     ("tts_taco_postnet", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
-    ("tts_taco_decoder_state", ctypes.c_int, [_vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
+    ("tts_taco_decoder_state", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _vp, _vp, _vp, _vp, _vp, _vp, _vp, _vp]),
     ("tts_melgan_set_tensor", ctypes.c_int, [_vp, ctypes.c_char_p, _vp, _c_i64_p, ctypes.c_int]),
     ("tts_melgan_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p, ctypes.c_int,
                                            ctypes.c_int, ctypes.c_int]),
@@ -194,15 +194,19 @@ class Engine:
         lens_a, lens_p = _i32(lens)
         _check(self.lib.tts_taco_postnet(self.h, _ptr(dec), lens_p, B, M, _ptr(out), _stream(dec.device)))
 
-    def taco_decoder_state(self, B, T_max, device):
-        """Decoder state after the last Tacotron2 decode (tts_taco_decoder_state), caller row order."""
+    def taco_decoder_state(self, B, T_max, device, key=None):
+        """Decoder state after the last Tacotron2 decode (tts_taco_decoder_state), caller row order.
+        ``key``: the calling model's weight key; the read is refused if another model (or another
+        version of this one) decoded on this device since."""
         import torch
         out = {k: torch.empty(B, n, device=device) for k, n in
                (("query", 1024), ("attention_rnn_cell_state", 1024), ("decoder_hidden", 1024),
                 ("decoder_cell", 1024), ("context", 512), ("attention_weights", T_max),
                 ("attention_weights_cum", T_max))}
         with self.lock:
-            _check(self.lib.tts_taco_decoder_state(self.h, *[_ptr(out[k]) for k in out], _stream(device)))
+            if key is not None and self.taco_key != key:
+                raise RuntimeError("decoder_state: another Tacotron2 model decoded on this device since this model's call")
+            _check(self.lib.tts_taco_decoder_state(self.h, B, T_max, *[_ptr(out[k]) for k in out], _stream(device)))
         return out
 
     def load_pwgan(self, tensors: Dict[str, np.ndarray], num_res_blocks, stacks, upsample_factors):

@@ -2,11 +2,14 @@
 trimming and wav writing. Restates `TTS/utils/audio.py` (AudioProcessor) without librosa, which
 is not in this image: the mel filterbank is librosa.filters.mel's published Slaney algorithm,
 STFT/ISTFT are torch.stft/istft with librosa's conventions (periodic Hann, centred frames, the
-config's pad mode), trimming is librosa.effects.trim's frame-RMS rule. None of these touch the
-GPU: the GPU path is the MB-MelGAN vocoder. Parity of the restated librosa pieces is unpinned
+config's pad mode), trimming is librosa.effects.trim's frame-RMS rule. Mean-var scaling (`stats_path`,
+audio.py:80-86,108-186) reads compute_statistics.py's stats file through a restricted loader
+(`load_stats_file`). None of these touch the GPU: the GPU path is the MB-MelGAN vocoder. Parity of the restated librosa pieces is unpinned
 (librosa is not importable here to make fixtures); tests check their defining properties.
 """
 import io
+import json
+import pickle
 
 import numpy as np
 import scipy.io.wavfile
@@ -44,6 +47,86 @@ def mel_filterbank(sr, n_fft, n_mels, fmin=0.0, fmax=None):
     return w.astype(np.float32)
 
 
+class StandardScaler:
+    """tts/utils/data.py:56-76."""
+
+    def set_stats(self, mean, scale):
+        self.mean_ = mean
+        self.scale_ = scale
+
+    def reset_stats(self):
+        delattr(self, "mean_")
+        delattr(self, "scale_")
+
+    def transform(self, X):
+        X = np.asarray(X)
+        X -= self.mean_
+        X /= self.scale_
+        return X
+
+    def inverse_transform(self, X):
+        X = np.asarray(X)
+        X *= self.scale_
+        X += self.mean_
+        return X
+
+
+class _StatsConfig(dict):
+    """Stand-in for `TTS.utils.io.AttrDict`, the class compute_statistics.py pickles the audio
+    config as: keys as attributes, nothing else."""
+
+    def __getattr__(self, k):
+        try:
+            return self[k]
+        except KeyError:
+            raise AttributeError(k) from None
+
+    def __setstate__(self, state):  # the pickled __dict__ is the dict itself (AttrDict)
+        pass
+
+
+class _StatsUnpickler(pickle.Unpickler):
+    """Admits exactly what `np.save(path, stats_dict)` writes: numpy array / dtype / scalar
+    reconstruction, builtin containers, and the reference's AttrDict (as a plain dict). Any other
+    global in the stream is refused before anything from it runs (the same rule as
+    torch.load(weights_only=True))."""
+
+    _NUMPY = {("numpy.core.multiarray", "_reconstruct"), ("numpy._core.multiarray", "_reconstruct"),
+              ("numpy.core.multiarray", "scalar"), ("numpy._core.multiarray", "scalar"),
+              ("numpy", "ndarray"), ("numpy", "dtype")}
+
+    def find_class(self, module, name):
+        if (module, name) in self._NUMPY:
+            return super().find_class(module, name)
+        if name == "AttrDict" and module in ("TTS.utils.io", "mozilla_voice_tts.utils.io"):
+            return _StatsConfig
+        raise pickle.UnpicklingError(f"stats file references {module}.{name}: refused")
+
+
+def load_stats_file(path):
+    """The mean-var stats dict (mel_mean, mel_std, linear_mean, linear_std, audio_config).
+    `.npz`: plain arrays (audio_config as a JSON string), read with allow_pickle=False. `.npy`:
+    the object array compute_statistics.py writes (`np.save(path, dict, allow_pickle=True)`),
+    read through `_StatsUnpickler` instead of numpy's unrestricted pickle load."""
+    if str(path).endswith(".npz"):
+        with np.load(path, allow_pickle=False) as z:
+            out = {k: z[k] for k in ("mel_mean", "mel_std", "linear_mean", "linear_std")}
+            out["audio_config"] = json.loads(str(z["audio_config"]))
+        return out
+    with open(path, "rb") as f:
+        version = np.lib.format.read_magic(f)
+        read_header = (np.lib.format.read_array_header_1_0 if version == (1, 0)
+                       else np.lib.format.read_array_header_2_0)
+        _shape, _fortran, dtype = read_header(f)
+        if not dtype.hasobject:
+            raise ValueError(f"{path}: expected the pickled stats dict, found a plain {dtype} array")
+        arr = _StatsUnpickler(f).load()
+    stats = arr.item() if isinstance(arr, np.ndarray) else arr
+    if not isinstance(stats, dict):
+        raise ValueError(f"{path}: stats file does not hold a dict")
+    return stats
+
+
 class AudioProcessor:
     """The subset of TTS/utils/audio.py:11-345 that Synthesizer.tts uses."""
 
@@ -70,8 +153,9 @@ class AudioProcessor:
         self.clip_norm = clip_norm
         self.do_trim_silence = do_trim_silence
         self.trim_db = trim_db
-        if stats_path:
-            raise NotImplementedError("mean-var stats (stats_path) are not restated in this build")
+        self.frame_shift_ms, self.frame_length_ms = frame_shift_ms, frame_length_ms
+        self.do_sound_norm = _.get("do_sound_norm", False)
+        self.stats_path = stats_path
         if hop_length is None:  # audio.py:99-105
             factor = frame_length_ms / frame_shift_ms
             assert float(factor).is_integer(), " [!] frame_shift_ms should divide frame_length_ms"
@@ -82,11 +166,50 @@ class AudioProcessor:
         assert self.win_length <= self.fft_size, " [!] win_length cannot be larger than fft_size"
         self.mel_basis = mel_filterbank(sample_rate, fft_size, num_mels, self.mel_fmin, self.mel_fmax)
         self.inv_mel_basis = np.linalg.pinv(self.mel_basis)
+        if stats_path:  # audio.py:80-86: mean-var scaling replaces the range normalisation
+            mel_mean, mel_std, linear_mean, linear_std, _cfg = self.load_stats(stats_path)
+            self.setup_scaler(mel_mean, mel_std, linear_mean, linear_std)
+            self.signal_norm = True
+            self.max_norm = None
+            self.clip_norm = None
+            self.symmetric_norm = None
+
+    # -- mean-var scaling (audio.py:165-186, tts/utils/data.py:56-76)
+    def load_stats(self, stats_path):
+        """audio.py:165-180: the stats file `TTS/bin/compute_statistics.py:59-80` writes, checked
+        against this processor's parameters (the same skip list)."""
+        stats = load_stats_file(stats_path)
+        stats_config = stats["audio_config"]
+        skip = ["griffin_lim_iters", "stats_path", "do_trim_silence", "ref_level_db", "power"]
+        for key in stats_config.keys():
+            if key in skip or key == "sample_rate":
+                continue
+            assert stats_config[key] == self.__dict__[key], \
+                f" [!] Audio param {key} does not match the value used for computing mean-var stats. " \
+                f"{stats_config[key]} vs {self.__dict__[key]}"
+        return stats["mel_mean"], stats["mel_std"], stats["linear_mean"], stats["linear_std"], stats_config
+
+    def setup_scaler(self, mel_mean, mel_std, linear_mean, linear_std):
+        self.mel_scaler = StandardScaler()
+        self.mel_scaler.set_stats(mel_mean, mel_std)
+        self.linear_scaler = StandardScaler()
+        self.linear_scaler.set_stats(linear_mean, linear_std)
+
+    def _scaler_for(self, S):
+        """audio.py:114-120 / 143-149: picked by the feature count. The linear branch compares
+        with fft_size / 2 exactly as the reference does."""
+        if S.shape[0] == self.num_mels:
+            return self.mel_scaler
+        if S.shape[0] == self.fft_size / 2:
+            return self.linear_scaler
+        raise RuntimeError(" [!] Mean-Var stats does not match the given feature dimensions.")
 
     # -- normalisation (audio.py:108-163)
     def _normalize(self, S):
         if not self.signal_norm:
             return S.copy()
+        if hasattr(self, "mel_scaler"):
+            return self._scaler_for(S).transform(S.copy().T).T
         S = S - self.ref_level_db
         S_norm = (S - self.min_level_db) / (-self.min_level_db)
         if self.symmetric_norm:
@@ -99,6 +222,8 @@ class AudioProcessor:
         S = S.copy()
         if not self.signal_norm:
             return S
+        if hasattr(self, "mel_scaler"):
+            return self._scaler_for(S).inverse_transform(S.T).T
         if self.symmetric_norm:
             if self.clip_norm:
                 S = np.clip(S, -self.max_norm, self.max_norm)
@@ -138,9 +263,19 @@ class AudioProcessor:
             y = self._istft(S_complex * angles)
         return y
 
+    def _preemph_stft(self, y):
+        if self.preemphasis != 0:  # audio.py:198-202
+            import scipy.signal
+            y = scipy.signal.lfilter([1, -self.preemphasis], [1], y)
+        return self._stft(y)
+
+    def spectrogram(self, y):
+        """audio.py:216-222."""
+        return self._normalize(self._amp_to_db(np.abs(self._preemph_stft(y))))
+
     def melspectrogram(self, y):
-        D = self._stft(y)
-        return self._normalize(self._amp_to_db(self.mel_basis @ np.abs(D)))
+        """audio.py:224-230."""
+        return self._normalize(self._amp_to_db(self.mel_basis @ np.abs(self._preemph_stft(y))))
 
     def inv_melspectrogram(self, mel, rng=None):
         """audio.py:241-248 (no pre-emphasis path: raise as the reference would need scipy lfilter)."""

@@ -1362,12 +1362,8 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     grow<float>(W.spkb, (size_t)64 * (8320 + 112 * 16), W.gen);
     TTS_CHECK(W.B <= SPK_BMAX || !M.spk_dim, "multi-speaker decoding: at most 64 utterances per call");
     const int Bs = M.spk_dim ? W.B : 0;
-    static bool spk_attr = false;  // 64 rows of a 512-d speaker vector: 128 KiB of dynamic LDS
-    if (!spk_attr) {
-      HIP_OK(hipFuncSetAttribute((const void*)spk_bias_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                 SPK_BMAX * 512 * 4));
-      spk_attr = true;
-    }
+    // 64 rows of a 512-d speaker vector: 128 KiB of dynamic LDS
+    ensure_dyn_lds((const void*)spk_bias_kernel, SPK_BMAX * 512 * 4);
     TTS_CHECK(M.spk_dim <= 512, "speaker vectors of at most 512 dims");
     // Graves with speakers: the projection columns hold W_s s alone; the kernel adds the bias and
     // scales W_s s by the step's sum of attention weights (PArgs::spk_scale)
@@ -1907,6 +1903,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
       for (int k = 0; k < 3; ++k) dil[k] = G.dconv[i * G.nres + k].dil;
       if (resstack_x3_supported(C, dil, 3)) {  // blocks 0-2 in one pass over the stage (resstack_x3.hip)
         StackArgs sa{};
+        sa.B = B;
         sa.x = x;
         sa.y = xo;
         sa.sb = (long)C * Ls;
@@ -1923,9 +1920,11 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
           sa.bf[k] = G.fused[i * G.nres + k].bias.f();
         }
         sa.oflow = cc.oflow;
-        launch_resstack_x3(sa, lens.data(), C, s);
-        std::swap(x, xo);
-        bk0 = 3;
+        if (resstack_x3_fits(sa, lens.data())) {
+          launch_resstack_x3(sa, lens.data(), C, s);
+          std::swap(x, xo);
+          bk0 = 3;
+        }
       }
     }
     for (int bk = bk0; bk < G.nres; ++bk) {  // fused ResidualStack blocks (resblock.hip)
@@ -2935,11 +2934,13 @@ int tts_taco_postnet(tts_ctx* c, const float* d_dec, const int32_t* h_lens, int 
   });
 }
 
-int tts_taco_decoder_state(tts_ctx* c, float* d_att_h, float* d_att_c, float* d_dec_h, float* d_dec_c,
-                           float* d_context, float* d_alpha, float* d_alpha_cum, void* stream) {
+int tts_taco_decoder_state(tts_ctx* c, int B, int T_max, float* d_att_h, float* d_att_c, float* d_dec_h,
+                           float* d_dec_c, float* d_context, float* d_alpha, float* d_alpha_cum, void* stream) {
   return guarded_ctx(c, [&] {
     TTS_CHECK(c, "null ctx");
     TTS_CHECK(c->last_B > 0, "run tts_taco_infer first");
+    TTS_CHECK(B == c->last_B && T_max == c->last_T,
+              "decoder state: the buffers' (B, T_max) differ from the last decode on this context");
     TTS_CHECK(c->dec_path == 1 && c->dec_nlaunch >= 1, "decoder state: the last decode did not run the persistent "
                                                        "decoder (TTS_DECODER=graph or a non-256-CU device)");
     DeviceGuard g(c->device);

@@ -2,7 +2,10 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <mutex>
+#include <set>
 #include <string>
+#include <tuple>
 #include <vector>
 
 typedef float f32x4 __attribute__((ext_vector_type(4)));
@@ -28,6 +31,29 @@ void tts_set_error(const std::string& msg);
   do {                                                                                 \
     if (!(cond)) throw std::runtime_error(std::string(msg));                           \
   } while (0)
+
+// Kernel attributes and device facts, per device and thread-safe: contexts on several devices
+// (one host thread each) launch the same templates concurrently
+inline void ensure_dyn_lds(const void* f, int bytes) {
+  static std::mutex m;
+  static std::set<std::tuple<const void*, int, int>> done;
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  std::lock_guard<std::mutex> g(m);
+  if (done.count({f, dev, bytes})) return;
+  HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, bytes));
+  done.insert({f, dev, bytes});
+}
+inline int device_cu_count() {
+  static std::mutex m;
+  static int ncu[64] = {};
+  int dev = 0;
+  HIP_OK(hipGetDevice(&dev));
+  TTS_CHECK(dev >= 0 && dev < 64, "device index out of range");
+  std::lock_guard<std::mutex> g(m);
+  if (!ncu[dev]) HIP_OK(hipDeviceGetAttribute(&ncu[dev], hipDeviceAttributeMultiprocessorCount, dev));
+  return ncu[dev];
+}
 
 // Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, not for its
 // global loads and stores (__syncthreads also drains vmcnt, which would complete every prefetch
@@ -198,6 +224,7 @@ struct StackArgs {
   unsigned* oflow;
 };
 bool resstack_x3_supported(int C, const int* dil, int n);
+bool resstack_x3_fits(const StackArgs& a, const int* h_lens);
 void launch_resstack_x3(const StackArgs& a, const int* h_lens, int C, hipStream_t s);
 
 // fused MB-MelGAN output conv (C -> 4, k7, LReLU + reflect pad 3 + tanh) and PQMF synthesis

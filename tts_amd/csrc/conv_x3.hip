@@ -355,12 +355,7 @@ bool conv_x3_supported(int Cin, int Cout, int K, int dil) {
 template <int MI, int NI, int WM, int WN, int KT, int RS, int SD>
 static void cx_launch(const ConvArgs& a, hipStream_t s) {
   constexpr int TC = 16 * MI * WM, TQ = 16 * NI * WN;
-  static bool attr = false;
-  if (!attr) {
-    HIP_OK(hipFuncSetAttribute((const void*)conv_x3_kernel<MI, NI, WM, WN, KT, RS, SD>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-    attr = true;
-  }
+  ensure_dyn_lds((const void*)conv_x3_kernel<MI, NI, WM, WN, KT, RS, SD>, 160 * 1024);
   const int nq = (a.max_q + TQ - 1) / TQ, nco = (a.Cout + TC - 1) / TC, nz = a.B * a.nphase;
   const long ntile = (long)nq * nco * nz;
   TTS_CHECK(ntile < (1L << 30), "conv_x3: grid too large");
@@ -380,14 +375,13 @@ static long cx_cost_k(const ConvArgs& a) {
   static std::mutex mu;
   static std::map<size_t, long> slots_by_lds;
   long slots;
+  ensure_dyn_lds(f, 160 * 1024);
+  const int cus = device_cu_count();
   {
     std::lock_guard<std::mutex> lk(mu);
     auto it = slots_by_lds.find(lds);
     if (it == slots_by_lds.end()) {
-      HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024));
-      int dev = 0, cus = 0, nb = 0;
-      HIP_OK(hipGetDevice(&dev));
-      HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
+      int nb = 0;
       HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, 64 * WM * WN, lds));
       it = slots_by_lds.emplace(lds, std::max(1L, (long)nb * cus)).first;
     }

@@ -1612,11 +1612,7 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
 #undef PDK
   const void* f = fns[MT - 1][var];
   TTS_CHECK(f != nullptr, "persistent decoder: variant");
-  static bool attr[4][13] = {};
-  if (!attr[MT - 1][var]) {
-    HIP_OK(hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, (int)P_LDS));
-    attr[MT - 1][var] = true;
-  }
+  ensure_dyn_lds(f, (int)P_LDS);
   if (arm) arm_barrier(a.bar, 1, s);
   PArgs copy = a;
   void* kargs[] = {&copy};

@@ -60,6 +60,10 @@ inline void arm_barrier(unsigned* bar, int nblk, hipStream_t s) {
   launch_fills(f, s);
 }
 
+// gsync_arrive's first-level counters each take n / NC arrivals: n must be a multiple of NC
+// (16 for n >= 256, else 8), or a counter never completes and every wait times out
+inline bool gsync_count_ok(unsigned n) { return n > 0 && n % (n >= 256 ? 16u : 8u) == 0; }
+
 // Launch a kernel whose workgroups meet at grid barriers. Every workgroup must be resident at
 // once: that is checked here against the occupancy query, which is all a cooperative launch adds
 // (MI355X_MICROARCH.md "coop-launch": same residency as a plain launch, +15-19 us of host time).
@@ -87,6 +91,8 @@ inline void launch_resident(const void* f, dim3 grid, dim3 block, void** args, s
     cap = it->second;
   }
   TTS_CHECK((long)grid.x * grid.y * grid.z <= cap, "grid-barrier kernel: grid larger than the device holds at once");
+  TTS_CHECK(grid.y == 1 && grid.z == 1 && gsync_count_ok(grid.x),
+            "grid-barrier kernel: a 1-D grid that is a multiple of the barrier's counter fan-in");
   if (coop) HIP_OK(hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)lds, s));
   else HIP_OK(hipLaunchKernel(f, grid, block, args, lds, s));
 }

@@ -39,7 +39,7 @@ struct RbTile {
 };
 
 template <int C, int TQ, int WM, int WN, int R>
-__global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, int ntiles) {
+__global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, int ntiles, bool vec) {
   constexpr int NTHR = 64 * WM * WN;
   constexpr int MI = C / 16 / WM;
   constexpr int NI = TQ / 16 / WN;
@@ -301,7 +301,8 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     RB_STAMP(3);
     float* yb = a.y + (long)cur.b * a.sb;
     // transposed phase 2 (operands swapped: D = [lrelu(h); x]^T . Wf^T): a lane holds positions
-    // q .. q + 3 of channel co, one 16-byte store instead of four 4-byte ones
+    // q .. q + 3 of channel co, one 16-byte store instead of four 4-byte ones where the rows are
+    // 16-byte aligned (vec: Ls, sb multiples of 4 and y aligned), per-position stores otherwise
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
       const int co = (mt0 + mi) * 16 + (lane & 15);
@@ -311,7 +312,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
       for (int ni = 0; ni < NI; ++ni) {
         const f32x4 v = x3_value4(am[mi][ni], ac[mi][ni], bf);
         const int q = cur.q0 + wn * 16 * NI + ni * 16 + 4 * (lane >> 4);
-        if (q + 3 < cur.L) {
+        if (vec && q + 3 < cur.L) {
           *reinterpret_cast<f32x4*>(yr + q) = v;
         } else {
 #pragma unroll
@@ -344,21 +345,16 @@ template <int C, int TQ, int WM, int WN, int R>
 static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   const int ROWS = TQ + 2 * a.dil;
   const size_t lds = ((size_t)2 * ROWS * XR + (size_t)TQ * (4 * C + 16)) * 2;
-  static int ncu = 0;
-  if (!ncu) {
-    HIP_OK(hipFuncSetAttribute((const void*)resblock_x3_kernel<C, TQ, WM, WN, R>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, RB_DYN_LDS));
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+  ensure_dyn_lds((const void*)resblock_x3_kernel<C, TQ, WM, WN, R>, RB_DYN_LDS);
+  const int ncu = device_cu_count();
   TTS_CHECK(lds <= RB_DYN_LDS, "resblock_x3: LDS tile too large");
   long ntiles = 0;
   for (int b = 0; b < a.B; ++b) ntiles += ((long)(h_lens[b] + a.len_add) * a.mul + TQ - 1) / TQ;
   TTS_CHECK(ntiles < (1L << 30), "resblock_x3: too many tiles");
   if (ntiles == 0) return;
   const int grid = (int)std::min<long>(ntiles, ncu);
-  resblock_x3_kernel<C, TQ, WM, WN, R><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles);
+  const bool vec = a.Ls % 4 == 0 && a.sb % 4 == 0 && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
+  resblock_x3_kernel<C, TQ, WM, WN, R><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles, vec);
 }
 
 bool resblock_x3_supported(int C) { return C == 256 || C == 192 || C == 128 || C == 96 || C == 64 || C == 48 || C == 32; }
@@ -378,8 +374,6 @@ void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t 
   TTS_CHECK(a.dil >= 1 && a.dil <= X3_DMAX, "resblock: dilation must be in [1, 27] (num_res_blocks <= 4)");
   TTS_CHECK(a.Wd16 && a.Wf16 && a.oflow, "resblock_x3: split weights / overflow flag missing");
   TTS_CHECK(a.B <= 64, "resblock_x3: at most 64 utterances per call");
-  TTS_CHECK(a.Ls % 4 == 0 && a.sb % 4 == 0 && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0,
-            "resblock_x3: 16-byte aligned output rows required");
   if (a.max_q <= 0 || a.B <= 0) return;
   switch (C) {
     // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave

@@ -387,14 +387,8 @@ static void launch_rsx3(const StackArgs& a, const int* h_lens, hipStream_t s) {
   constexpr int ROWS = TQ + 2 * ST_OFF;
   constexpr size_t lds = (size_t)ROWS * ((2 * C + 16) + (4 * C + 16)) * 2;
   static_assert(lds + 3 * 2 * C * 4 + 65 * 4 + 64 * 4 <= 160 * 1024, "LDS");
-  static int ncu = 0;
-  if (!ncu) {
-    HIP_OK(hipFuncSetAttribute((const void*)resstack_x3_kernel<C, TQ, WN, NI>,
-                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds));
-    int dev = 0;
-    HIP_OK(hipGetDevice(&dev));
-    HIP_OK(hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev));
-  }
+  ensure_dyn_lds((const void*)resstack_x3_kernel<C, TQ, WN, NI>, (int)lds);
+  const int ncu = device_cu_count();
   long ntiles = 0;
   for (int b = 0; b < a.B; ++b) ntiles += ((long)(h_lens[b] + a.len_add) * a.mul + TQ - 1) / TQ;
   TTS_CHECK(ntiles < (1L << 30), "resstack_x3: too many tiles");
@@ -413,13 +407,20 @@ bool resstack_x3_supported(int C, const int* dil, int n) {
   return sum <= ST_OFF;
 }
 
+// the call-dependent conditions: 16-byte aligned output rows and every utterance longer than the
+// stack's reflection reach (callers fall back to the per-block kernels otherwise)
+bool resstack_x3_fits(const StackArgs& a, const int* h_lens) {
+  if (a.B > 64 || a.Ls % 4 != 0 || a.sb % 4 != 0 || (reinterpret_cast<uintptr_t>(a.y) & 15) != 0) return false;
+  for (int b = 0; b < a.B; ++b)
+    if ((long)(h_lens[b] + a.len_add) * a.mul <= ST_OFF) return false;
+  return true;
+}
+
 void launch_resstack_x3(const StackArgs& a0, const int* h_lens, int C, hipStream_t s) {
   TTS_CHECK(resstack_x3_supported(C, a0.dil, 3), "resstack_x3: shape not covered");
-  TTS_CHECK(a0.oflow && a0.B <= 64, "resstack_x3: overflow flag missing or more than 64 utterances");
-  TTS_CHECK(a0.Ls % 4 == 0 && a0.sb % 4 == 0 && (reinterpret_cast<uintptr_t>(a0.y) & 15) == 0,
-            "resstack_x3: 16-byte aligned output rows required");
-  for (int b = 0; b < a0.B; ++b)
-    TTS_CHECK((h_lens[b] + a0.len_add) * a0.mul > ST_OFF, "resstack_x3: utterance shorter than the reflection pad");
+  TTS_CHECK(a0.oflow, "resstack_x3: overflow flag missing");
+  TTS_CHECK(resstack_x3_fits(a0, h_lens), "resstack_x3: unaligned rows, more than 64 utterances or an utterance "
+                                          "shorter than the reflection pad");
   StackArgs a = a0;
   a.ext[2] = 0;
   a.ext[1] = a.dil[2];

@@ -243,5 +243,5 @@ class Tacotron2(nn.Module):
             raise RuntimeError("decoder_state: the last call was split into several library calls")
         dev = self.embedding.weight.device
         eng = get_engine(dev)
-        st = eng.taco_decoder_state(B, T, dev)
+        st = eng.taco_decoder_state(B, T, dev, key=(self._token, self._version))
         return st
