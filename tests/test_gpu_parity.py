@@ -249,10 +249,12 @@ def test_fullband_default_odd_length_unaligned_rows_vs_oracle():
     assert v.inference_padding == 2
     orc = melgan_oracle(cfg, sd)
     rs = np.random.RandomState(5)
-    lens = [7, 4]
+    lens = [13, 11]  # odd: stage 0 rows of 2 (13 + 4) = 34 floats; > the dilation-27 reflection pad
     batch = np.zeros((2, 80, max(lens)), np.float32)
     for i, L in enumerate(lens):
         batch[i, :, :L] = rs.normal(0, 1.5, (80, L))
+    with pytest.raises(RuntimeError, match="ReflectionPad1d"):  # 2 (9 + 4) = 26 <= 27, as torch raises
+        v.inference(torch.from_numpy(batch[:1, :, :9]).cuda())
     wav = v.inference(torch.from_numpy(batch).cuda(), lengths=lens).cpu().numpy()
     for i, L in enumerate(lens):
         c = batch[i, :, :L]

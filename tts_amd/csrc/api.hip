@@ -1822,6 +1822,9 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   for (int b = 0; b < B; ++b) {
     TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= M_max, "mel lens out of range");
     TTS_CHECK(h_lens[b] + 2 * pad >= 4, "ReflectionPad1d(3): mel frames + 2*padding must be >= 4");
+    for (int k = 0; k < G.nres && !G.ups.empty(); ++k)  // ResidualStack ReflectionPad1d(dilation), stage 0
+      TTS_CHECK((long)(h_lens[b] + 2 * pad) * G.ups[0] > G.dconv[k].dil,
+                "ReflectionPad1d: a residual stack's dilation must be < the first stage's length");
   }
   const int Lb = M_max + 2 * pad;
   int up = 1;

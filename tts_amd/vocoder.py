@@ -133,6 +133,11 @@ class MelganGenerator(nn.Module):
         pad = int(self.inference_padding)
         if (lens + 2 * pad < 4).any():
             raise RuntimeError("ReflectionPad1d: padding (3) must be < input length; need frames + 2*padding >= 4")
+        # ResidualStack(dilation 3^k) pads by its dilation (vocoder/layers/melgan.py:14-20): the first
+        # stage's length must exceed the largest one, as torch's ReflectionPad1d requires
+        dmax = 3 ** (self.cfg.num_res_blocks - 1)
+        if ((lens + 2 * pad) * int(self.cfg.upsample_factors[0]) <= dmax).any():
+            raise RuntimeError(f"ReflectionPad1d: padding ({dmax}) must be < input length of the first residual stack")
         return eng, c, lens, pad
 
     @torch.no_grad()
