@@ -29,6 +29,7 @@ sys.path.insert(0, ROOT)
 from tts_amd import MultibandMelganGenerator, Tacotron2  # noqa: E402
 from tts_amd.spec import MelganConfig, TacotronConfig, melgan_spec, tacotron2_spec  # noqa: E402
 from tts_amd.weights import synth_state_dict  # noqa: E402
+from tts_amd.multigpu import shard_plan  # noqa: E402
 from tts_amd.workload import (HOP, SAMPLE_RATE, forced_steps, lj_profile, pad_batch,  # noqa: E402
                               replicated_workload, synthetic_ids)
 
@@ -85,24 +86,60 @@ def build_models(device, seed=0):
     return taco, tsd, voc, vsd, tcfg, vcfg
 
 
+def cpu_facts():
+    """Host CPU share as this process sees it: the affinity mask, and the physical cores behind it
+    (distinct (physical id, core id) pairs of /proc/cpuinfo)."""
+    aff = sorted(os.sched_getaffinity(0))
+    core_of, model = {}, None
+    try:
+        cur = {}
+        for line in open("/proc/cpuinfo"):
+            if ":" not in line:
+                if "processor" in cur:
+                    core_of[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+                cur = {}
+                continue
+            k, v = (x.strip() for x in line.split(":", 1))
+            cur[k] = v
+            if k == "model name" and model is None:
+                model = v
+        if "processor" in cur:
+            core_of[int(cur["processor"])] = (cur.get("physical id", "0"), cur.get("core id", cur["processor"]))
+    except OSError:
+        pass
+    phys = len({core_of[c] for c in aff if c in core_of}) or None
+    return {"affinity_cpus": len(aff), "physical_cores_in_affinity": phys, "machine_cpus": os.cpu_count(),
+            "omp_num_threads": os.environ.get("OMP_NUM_THREADS"), "model": model}
+
+
 def cpu_baseline(tsd, vsd, tcfg, vcfg, ids, steps, r, budget_s):
     """The reference CPU path's op sequence (oracle/torch_cpu.py: PyTorch-CPU ATen restatement, SURVEY
     8d) at B=1 per utterance, Tacotron2 then MB-MelGAN, on the host's cores. Timed beside the imported
-    reference in the build container by tools/cpu_baseline_check.py (profiles/r03/)."""
+    reference in the build container by tools/cpu_baseline_check.py (profiles/r03/).
+    The thread count is the CPU's best: torch.set_num_threads over {1, 2, 4, 8, 16} (capped by the
+    affinity mask) on one short utterance, then the whole batch at the fastest setting, utterance by
+    utterance until ``budget_s`` of CPU work."""
     from oracle.torch_cpu import MelganTorchCPU, TacoTorchCPU
     from tts_amd.pqmf import pqmf_filters
     from tts_amd.spec import melgan_layers
-    cores = int(os.environ.get("OMP_NUM_THREADS", os.cpu_count() or 1))
-    cores = max(1, min(cores, os.cpu_count() or 1))
+    facts = cpu_facts()
+    cap = max(1, facts["affinity_cpus"])
     prev = torch.get_num_threads()
-    torch.set_num_threads(cores)
+    sweep = {}
     try:
         to = TacoTorchCPU(tsd, tcfg.attn_norm, tcfg.r)
         vo = MelganTorchCPU(vsd, melgan_layers(vcfg), pqmf_filters()[1])
-        # warm-up on the shortest utterance (excluded, as SURVEY 8d asks)
-        j = int(np.argmin(steps))
-        _, p, _, _ = to.inference(ids[j], r, min(steps[j], 4))
-        vo.inference(p.T, pad=0)
+        j = int(np.argmin(steps))  # the shortest utterance: warm-up and thread sweep
+        for nt in [n for n in (1, 2, 4, 8, 16) if n <= cap]:
+            torch.set_num_threads(nt)
+            _, p, _, _ = to.inference(ids[j], r, min(steps[j], 4))  # warm-up at this setting (excluded)
+            vo.inference(p.T, pad=0)
+            t0 = time.perf_counter()
+            _, p, _, _ = to.inference(ids[j], r, steps[j])
+            vo.inference(p.T, pad=0)
+            sweep[nt] = round(p.shape[0] / (time.perf_counter() - t0), 1)
+        cores = max(sweep, key=sweep.get)
+        torch.set_num_threads(cores)
         frames = n = 0
         t_taco = t_voc = 0.0
         while n < len(ids) and t_taco + t_voc < budget_s:
@@ -130,9 +167,11 @@ def cpu_baseline(tsd, vsd, tcfg, vcfg, ids, steps, r, budget_s):
             calib = None
     return {"value": round(frames / el, 1), "unit": "mel-frames/s", "cores": cores, "kind": "port",
             "rtf": el / audio, "tacotron2_mel_frames_per_s": round(frames / t_taco, 1), "calibration": calib,
-            "sample": f"first {n} of {len(ids)} LJ-profile utterances, B=1 sequential, r={r}, forced length "
-                      f"({frames} frames): Tacotron2 {t_taco:.1f} s + MB-MelGAN {t_voc:.1f} s, PyTorch-CPU "
-                      f"restatement of the reference op sequence (oracle/torch_cpu.py), {cores} threads"}
+            "thread_sweep_frames_per_s": sweep, "host": facts,
+            "sample": f"{'all' if n == len(ids) else 'first'} {n} of {len(ids)} LJ-profile utterances, B=1 "
+                      f"sequential, r={r}, forced length ({frames} frames): Tacotron2 {t_taco:.1f} s + MB-MelGAN "
+                      f"{t_voc:.1f} s, PyTorch-CPU restatement of the reference op sequence (oracle/torch_cpu.py), "
+                      f"{cores} threads (the fastest of the sweep on utterance {j}, {steps[j] * r} frames)"}
 
 
 def main():
@@ -142,7 +181,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=2)
     ap.add_argument("--r", type=int, default=2)
     ap.add_argument("--per-gpu-batch", type=int, default=32)
-    ap.add_argument("--cpu-seconds", type=float, default=15.0)
+    ap.add_argument("--cpu-seconds", type=float, default=30.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--f32-steps", type=int, default=3, help="steps re-timed with fp32-MFMA GEMMs only (0: skip)")
@@ -160,8 +199,10 @@ def main():
 
     taco, tsd, voc, vsd, tcfg, vcfg = build_models(dev)
     taco.decoder.verbose = False  # forced lengths end every utterance at max_decoder_steps
-    T_all, M_all, shards = replicated_workload(world, args.per_gpu_batch)
-    mine = shards[rank]
+    # the global batch (C3: the 32-utterance profile once per rank) over the ranks through the product
+    # entry point's plan (tts_amd.multigpu: LPT on the decoder step counts, no data-path collective)
+    T_all, M_all, _ = replicated_workload(world, args.per_gpu_batch)
+    mine = shard_plan(forced_steps(M_all, args.r), world)[rank]
     T_prof, M_prof = lj_profile()
     ids = synthetic_ids(T_prof)              # C3 replicates the same 32 utterances
     my_ids = [ids[i % len(ids)] for i in mine]

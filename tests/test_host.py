@@ -174,6 +174,11 @@ def test_replicated_workload_weak_scaling():
         assert len(shards) == n and all(len(s) == 32 for s in shards)
         assert sorted(i for s in shards for i in s) == list(range(32 * n))
         assert sum(M[i] for i in shards[-1]) == 19112
+        # bench.py's plan (tts_amd.multigpu.shard_plan, LPT on the step counts) gives every rank one
+        # copy of each profile utterance: the per-rank work of C2
+        from tts_amd.multigpu import shard_plan
+        plan = shard_plan(forced_steps(M, 2), n)
+        assert all(sorted(i % 32 for i in s) == list(range(32)) for s in plan)
 
 
 def test_glow_tts_constructor_and_keys():

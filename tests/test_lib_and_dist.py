@@ -72,18 +72,21 @@ def _worker(rank, world, port, q):
     T = [min(t, 12) for t in T[:6]]             # 6 short utterances with their own step counts
     ids = synthetic_ids(T)
     # shards balance the decoder step counts (a batch's time is set by its decode length)
-    shards = lpt_shards([float(s) for s in STEPS], world)
-    mine = shards[rank]
-    mels = {i: orc.inference(ids[i], 2, STEPS[i])[1] for i in mine}   # no collective on the data path
-    # optional final gather to rank 0: variable-length results as padded tensors
-    M = 2 * max(STEPS)
-    buf = torch.zeros(len(T), M, 80)
-    for i, p in mels.items():
-        buf[i, :len(p)] = torch.from_numpy(p)
-    gathered = [torch.zeros_like(buf) for _ in range(world)]
-    dist.all_gather(gathered, buf)
+    # the product entry point (tts_amd.multigpu.run_sharded): this rank's LPT shard through the
+    # runner, no collective on the data path, then the optional final gather to rank 0
+    from tts_amd.multigpu import run_sharded, shard_plan
+    assert shard_plan([float(s) for s in STEPS], world) == lpt_shards([float(s) for s in STEPS], world)
+    items = list(zip(ids, STEPS))
+    res, mine = run_sharded(lambda xs: [orc.inference(x, 2, s)[1] for x, s in xs], items, STEPS)
+    assert sorted(mine) == lpt_shards([float(s) for s in STEPS], world)[rank]
     if rank == 0:
-        q.put(torch.stack(gathered).sum(0).numpy())
+        M = 2 * max(STEPS)
+        buf = np.zeros((len(T), M, 80), np.float32)
+        for i, p in enumerate(res):
+            buf[i, :len(p)] = p
+        q.put(buf)
+    else:
+        assert res is None
     dist.destroy_process_group()
 
 
@@ -112,3 +115,41 @@ def test_two_rank_sharded_decode_equals_single_process():
     for i in range(6):
         ref = orc.inference(ids[i], 2, STEPS[i])[1]
         assert np.array_equal(out[i, :len(ref)], ref) and not out[i, len(ref):].any()
+
+
+def _pool_factory(seed, device):
+    """GpuPool stand-in runner for the CPU suite: the oracle decode, tagged with the worker's device."""
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests"))
+    from helpers import taco_state_dict
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import TacotronConfig
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=seed, overrides={}, stop_bias=-1e4, cfg=cfg)
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+
+    def run(items, r=2):
+        return [(device, orc.inference(x, r, s)[1]) for x, s in items]
+    return run
+
+
+def test_gpu_pool_dispatch_and_gather():
+    """tts_amd.multigpu.GpuPool: one spawned worker per device label, LPT shards on the step counts,
+    results gathered back in input order and equal to one process; a failing worker raises."""
+    import functools
+    from tts_amd.multigpu import GpuPool, shard_plan
+    from tts_amd.workload import lj_profile, synthetic_ids
+    T, _ = lj_profile()
+    ids = synthetic_ids([min(t, 12) for t in T[:6]])
+    items = list(zip(ids, STEPS))
+    with GpuPool(functools.partial(_pool_factory, 2), devices=[0, 1]) as pool:
+        out = pool.map(items, costs=STEPS)
+        plan = shard_plan(STEPS, 2)
+        for k, shard in enumerate(plan):
+            assert all(out[i][0] == k for i in shard)
+        ref = _pool_factory(2, -1)(items)
+        for (_, a), (_, b) in zip(out, ref):
+            assert np.array_equal(a, b)
+        assert pool.map([]) == []
+        with pytest.raises(RuntimeError, match="worker failed"):
+            pool.map(items, r=0)  # r = 0 raises inside the workers

@@ -1,0 +1,244 @@
+// Latency skeleton of the persistent decoder's step (decoder_persist.hip): the same 256 x 512-thread
+// grid, workgroup roles and hand-off sizes, no arithmetic (optional spin delays stand in for each
+// role's compute). Measures the step's hand-off chain under two synchronisation schemes:
+//   mode 0: a grid barrier after every phase (gsync.h, as the decoder runs)
+//   mode 1: edge-scoped counters, each consumer waits only for the workgroups it reads
+// Not part of the library:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/chain_bench.hip -o tools/chain_bench
+#include "../tts_amd/csrc/gsync.h"
+
+#include <cstdio>
+#include <cstring>
+#include <vector>
+
+namespace {
+constexpr int PW = 256, PT = 512, NATT = 64, IW0 = 64, NPRE = 32, NPJ = 54, NB = 32, NCH = 6, YP = 432;
+constexpr int STOP_WG = 63;
+
+struct CArgs {
+  float *ypart, *pb, *hatt, *pq, *part_u, *ctx, *hd0, *hd1, *alpha, *sink;
+  unsigned* bar;   // grid barrier block (mode 0)
+  unsigned* ctr;   // edge counters (mode 1), each on its own 128-byte line: [0] y, [32] pb, [64] h, [96] ctx,
+                   // [128] d, [160 + 32 b] per-utterance alignment, [2048 + 32 b] tickets
+  int steps;
+  int dl[6];       // spin delays (100 MHz ticks) per role: prenet, att P3, item P4, P5, pj P6, item P3
+  unsigned* err;
+};
+
+__device__ __forceinline__ void spin(int ticks) {
+  if (ticks <= 0) return;
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  while (__builtin_amdgcn_s_memrealtime() - t0 < (unsigned long long)ticks) {}
+}
+
+// every wave drains its stores, then one lane counts the workgroup in
+__device__ __forceinline__ void edge_arrive(unsigned* c) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) __hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ bool edge_wait(unsigned* c, unsigned target, unsigned* err, int* flag) {
+  if (threadIdx.x == 0) {
+    int good = 1;
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    while (__hip_atomic_load(c, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < target) {
+      if (__builtin_amdgcn_s_memrealtime() - t0 > 200000000ull) {
+        __hip_atomic_fetch_or(err, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        good = 0;
+        break;
+      }
+      if (__hip_atomic_load(err, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+        good = 0;
+        break;
+      }
+    }
+    *flag = good;
+  }
+  lds_barrier();
+  return *flag;
+}
+
+// load n 16-byte granules per thread from base (coherent), fold them into a register sum
+__device__ __forceinline__ float load_sum(const float* base, int n, int stride_bytes) {
+  f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  f32x4 v[16];
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < n) v[i] = ldc4(base, (int)threadIdx.x * 16 + i * stride_bytes);
+#pragma unroll
+  for (int i = 0; i < 16; ++i)
+    if (i < n) s += v[i];
+  return s[0] + s[1] + s[2] + s[3];
+}
+}  // namespace
+
+template <int MODE>
+__global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
+  __shared__ int flag, is_last;
+  __shared__ float red[PT];
+  const int g = blockIdx.x, tid = threadIdx.x;
+  unsigned gen = 0;
+  float acc = 0.f;
+  unsigned* Cy = a.ctr;
+  unsigned* Cpb = a.ctr + 32;
+  unsigned* Ch = a.ctr + 64;
+  unsigned* Cctx = a.ctr + 96;
+  unsigned* Cd = a.ctr + 128;
+  const int it = g - IW0, ib = it / NCH, ich = it % NCH;
+  auto sync = [&](unsigned* c, unsigned target) -> bool {  // mode 0: grid barrier, mode 1: edge wait
+    if (MODE == 0) {
+      gsync_arrive(a.bar, gen);
+      return gsync_wait(a.bar, gen, &flag);
+    }
+    return edge_wait(c, target, a.err, &flag);
+  };
+  for (int t = 0; t < a.steps; ++t) {
+    float* hd_cur = (t & 1) ? a.hd1 : a.hd0;
+    float* hd_nxt = (t & 1) ? a.hd0 : a.hd1;
+    // ---- P1: prenet layer 2 (wg 0..31) || stop (wg 63) || items' location window
+    if (MODE == 1 && (g < NPRE || g == STOP_WG) && t > 0 && !edge_wait(Cy, NPJ * t, a.err, &flag)) return;
+    if (g < NPRE) {
+      acc += load_sum(a.ypart + (g & 1) * 16 * YP, 2, PT * 16);  // 16 rows x 256 columns
+      spin(a.dl[0]);
+      if (tid < 64) stc4(a.pb, ((g * 64 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+    } else if (g == STOP_WG) {
+      acc += tid < 32 ? ldc(a.ypart + tid * YP) : 0.f;
+    } else if (it >= 0 && it < NB * NCH) {
+      if (MODE == 1 && t > 0 && !edge_wait(a.ctr + 160 + 32 * ib, NCH * t, a.err, &flag)) return;
+      acc += tid < 128 ? ldc(a.alpha + ib * 256 + min(max(ich * 32 - 15 + (tid & 63), 0), 191)) : 0.f;
+    }
+    if (MODE == 1 && (g < NPRE || g == STOP_WG)) edge_arrive(Cpb);
+    if (!sync(Cpb, (NPRE + 1) * (t + 1))) return;
+    // ---- P3: attention_rnn (wg 0..63) || h_dec part (items)
+    if (g < NATT) {
+      acc += load_sum(a.pb, 4, PT * 16);  // 32 rows x 256
+      spin(a.dl[1]);
+      if (tid < 128) stc4(a.hatt, ((g * 128 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});  // 2 KB
+      stc4(a.pq, ((g * 1024 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});                 // 16 KB
+      stc4(a.pq, ((g * 1024 + 512 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+      if (MODE == 1) edge_arrive(Ch);
+    } else {
+      acc += load_sum(hd_cur, 16, PT * 16);  // 128 KB
+      spin(a.dl[5]);
+    }
+    if (!sync(Ch, NATT * (t + 1))) return;
+    // ---- P4: attention items || h_att parts (wg 0..63)
+    if (g >= IW0 && it < NB * NCH) {
+      acc += load_sum(a.pq + ib * 128, 4, 32 * 128 * 4 * 4);  // 64 partials x 128 dims of row ib (16 per group)
+      spin(a.dl[2]);
+      stc4(a.part_u, ((it * 128 + (tid & 127)) * 4) * 4, f32x4{acc, acc, acc, acc});
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.ctr + 2048 + 32 * ib, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = prev == (unsigned)(NCH * (t + 1) - 1);
+      }
+      lds_barrier();
+      if (is_last) {
+        acc += load_sum(a.part_u + ib * NCH * 512, 6, 512 * 4) ;
+        stc(a.ctx + ib * 512 + tid, acc);
+        if (MODE == 1) edge_arrive(Cctx);
+      }
+    } else if (g < IW0) {
+      acc += load_sum(a.hatt, 16, PT * 16);
+      acc += load_sum(hd_cur, 16, PT * 16);
+    }
+    if (!sync(Cctx, NB * (t + 1))) return;
+    // ---- P5: ctx parts (+ h_att parts on the items), decoder_rnn cell
+    acc += load_sum(a.ctx, 8, PT * 16);
+    if (g >= IW0) acc += load_sum(a.hatt, 16, PT * 16);
+    spin(a.dl[3]);
+    if (tid < 32) stc4(hd_nxt, ((g * 32 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+    if (MODE == 1) edge_arrive(Cd);
+    if (MODE == 0) {
+      if (!sync(Cd, 0)) return;
+    }
+    // ---- P6: projection jobs (wg 0..53) || alignment pass (items)
+    if (g < NPJ) {
+      if (MODE == 1 && !edge_wait(Cd, PW * (t + 1), a.err, &flag)) return;
+      acc += load_sum(hd_nxt + (g & 1) * 16 * 1024, 8, PT * 16);   // 16 rows x 1024
+      acc += load_sum(a.ctx + (g & 1) * 16 * 512, 4, PT * 16);     // 16 rows x 512
+      spin(a.dl[4]);
+      if (tid < 64) stc4(a.ypart, (((g & 1) * 16 * YP + (g >> 1) * 16) + tid * 4) * 4, f32x4{acc, acc, acc, acc});
+      if (MODE == 1) edge_arrive(Cy);
+    } else if (g >= IW0 && it < NB * NCH) {
+      if (tid < 32) stc(a.alpha + ib * 256 + ich * 32 + tid, acc);
+      if (MODE == 1) edge_arrive(a.ctr + 160 + 32 * ib);
+    }
+    if (MODE == 0 && !sync(nullptr, 0)) return;
+  }
+  if (tid == 0) a.sink[g] = acc;
+}
+
+static hipStream_t S;
+
+int main(int argc, char** argv) {
+  setvbuf(stdout, nullptr, _IONBF, 0);
+  HIP_OK(hipStreamCreate(&S));
+  auto alloc = [](size_t n) {
+    float* p;
+    HIP_OK(hipMalloc(&p, n * 4));
+    HIP_OK(hipMemset(p, 0, n * 4));
+    return p;
+  };
+  CArgs a{};
+  a.ypart = alloc(64 * YP);
+  a.pb = alloc(64 * 256 * 4);
+  a.hatt = alloc(64 * 1024 * 2);
+  a.pq = alloc(64 * 32 * 128 * 2);
+  a.part_u = alloc(NB * NCH * 512 * 2);
+  a.ctx = alloc(64 * 512 * 2);
+  a.hd0 = alloc(64 * 1024 * 2);
+  a.hd1 = alloc(64 * 1024 * 2);
+  a.alpha = alloc(NB * 256);
+  a.sink = alloc(PW);
+  HIP_OK(hipMalloc(&a.bar, BAR_WORDS * 4));
+  HIP_OK(hipMalloc(&a.ctr, 4096 * 4));
+  HIP_OK(hipMalloc(&a.err, 4));
+  const int steps = 400;
+  a.steps = steps;
+  const unsigned tmo = 200000000u;
+  struct Cfg {
+    const char* name;
+    int dl[6];
+  } cfgs[] = {{"no compute", {0, 0, 0, 0, 0, 0}},
+              // compute stand-ins near the MT = 2 kernel's per-role work (us x 100 ticks)
+              {"compute stand-ins", {60, 150, 180, 150, 80, 60}}};
+  for (const Cfg& c : cfgs) {
+    for (int mode : {0, 1}) {
+      std::memcpy(a.dl, c.dl, sizeof(a.dl));
+      const void* f = mode == 0 ? (const void*)chain_kernel<0> : (const void*)chain_kernel<1>;
+      ensure_dyn_lds(f, 128 * 1024);
+      float best = 1e30f;
+      for (int rep = 0; rep < 3; ++rep) {
+        HIP_OK(hipMemsetAsync(a.bar, 0, BAR_WORDS * 4, S));
+        HIP_OK(hipMemcpyAsync(a.bar + BAR_TMO, &tmo, 4, hipMemcpyHostToDevice, S));
+        HIP_OK(hipMemsetAsync(a.ctr, 0, 4096 * 4, S));
+        HIP_OK(hipMemsetAsync(a.err, 0, 4, S));
+        hipEvent_t e0, e1;
+        HIP_OK(hipEventCreate(&e0));
+        HIP_OK(hipEventCreate(&e1));
+        HIP_OK(hipEventRecord(e0, S));
+        CArgs cp = a;
+        void* args[] = {&cp};
+        launch_resident(f, dim3(PW), dim3(PT), args, 128 * 1024, S);
+        HIP_OK(hipEventRecord(e1, S));
+        HIP_OK(hipEventSynchronize(e1));
+        float ms;
+        HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+        unsigned e = 0, eb = 0;
+        HIP_OK(hipMemcpy(&e, a.err, 4, hipMemcpyDeviceToHost));
+        HIP_OK(hipMemcpy(&eb, a.bar + 16, 4, hipMemcpyDeviceToHost));
+        if (e || eb) {
+          printf("%s mode %d: wait timeout\n", c.name, mode);
+          return 1;
+        }
+        best = std::min(best, ms);
+      }
+      printf("%-18s %s: %.2f us per step\n", c.name, mode == 0 ? "grid barriers " : "edge counters ",
+             best * 1000.f / steps);
+    }
+  }
+  printf("done\n");
+  return 0;
+}

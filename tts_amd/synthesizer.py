@@ -9,8 +9,13 @@ Follows `TTS/server/synthesizer.py:21-193`. What differs on purpose:
   * checkpoints load with `torch.load(..., weights_only=True)`;
   * sentence splitting and the text front end are the stand-ins of `tts_amd.text` (pysbd,
     phonemizer, unidecode and inflect are not in this image); phoneme configs need a
-    `phonemize` callable.
+    `phonemize` callable;
+  * several GPUs (config ``num_gpus`` > 1, or an explicit ``gpu_devices`` list): the sentences of a
+    call are sharded over one worker process per GPU (`tts_amd.multigpu.GpuPool`, LPT on the
+    token counts), each worker running this same batched path on its shard; results come back in
+    sentence order. The workers start before this process touches the GPU.
 """
+import functools
 import json
 import os
 import time
@@ -21,7 +26,15 @@ import torch
 from .audio import AudioProcessor, wav_bytes
 from .factories import load_config, setup_generator, setup_model
 from .glow_tts import GlowTts
+from .multigpu import GpuPool
 from .text import make_symbols, phonemes, split_into_sentences, symbols, text_to_seqvec
+
+
+def _pool_synthesizer(config, phonemize, device):
+    """GpuPool factory: a single-GPU Synthesizer on ``device`` inside a worker process."""
+    torch.cuda.set_device(device)
+    synth = Synthesizer(dict(config, num_gpus=1, gpu_devices=None), phonemize=phonemize)
+    return synth.synthesize_batch
 
 
 class Synthesizer:
@@ -31,6 +44,15 @@ class Synthesizer:
         self.config = config
         self.phonemize = phonemize
         self.use_cuda = config["use_cuda"]
+        self.pool = None
+        devices = config.get("gpu_devices")
+        if devices is None and int(config.get("num_gpus") or 1) > 1:
+            devices = list(range(min(int(config["num_gpus"]), torch.cuda.device_count())))
+        if self.use_cuda and devices is not None and len(devices) > 1:
+            # one worker per GPU, started before this process makes any GPU call; the models here
+            # stay on the host (text front end, audio processor and shapes only)
+            self.pool = GpuPool(functools.partial(_pool_synthesizer, dict(config), phonemize), devices)
+            self.use_cuda = False
         if self.use_cuda:
             assert torch.cuda.is_available(), "CUDA is not availabe on this machine."
         self.load_tts(config["tts_checkpoint"], config["tts_config"], self.use_cuda)
@@ -69,7 +91,8 @@ class Synthesizer:
         self.tts_model.eval()
         if isinstance(self.tts_model, GlowTts):
             return
-        self.tts_model.decoder.max_decoder_steps = 3000
+        # synthesizer.py:76 (3000); the optional config key ``max_decoder_steps`` overrides it
+        self.tts_model.decoder.max_decoder_steps = int(self.config.get("max_decoder_steps") or 3000)
         if "r" in cp:
             self.tts_model.decoder.set_r(int(cp["r"]))
             print(f" > model reduction factor: {int(cp['r'])}")
@@ -93,8 +116,11 @@ class Synthesizer:
         return split_into_sentences(text)
 
     def synthesize_batch(self, sentences, speaker_id=None):
-        """Sentences -> list of per-sentence waveforms (float32 numpy), one GPU call per model."""
+        """Sentences -> list of per-sentence waveforms (float32 numpy), one GPU call per model (per
+        GPU when sharded over a pool)."""
         seqs = [text_to_seqvec(s, self.tts_config, self.phonemize) for s in sentences]
+        if self.pool is not None:
+            return self.pool.map(list(sentences), costs=[len(q) for q in seqs], speaker_id=speaker_id)
         lens = [max(1, len(q)) for q in seqs]
         dev = "cuda" if self.use_cuda else "cpu"
         batch = np.zeros((len(seqs), max(lens)), np.int64)
@@ -135,3 +161,8 @@ class Synthesizer:
         print(f" > Processing time: {process_time}")
         print(f" > Real-time factor: {process_time / audio_time}")
         return out
+
+    def close(self):
+        if self.pool is not None:
+            self.pool.close()
+            self.pool = None
