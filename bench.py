@@ -202,7 +202,8 @@ def main():
     # the global batch (C3: the 32-utterance profile once per rank) over the ranks through the product
     # entry point's plan (tts_amd.multigpu: LPT on the decoder step counts, no data-path collective)
     T_all, M_all, _ = replicated_workload(world, args.per_gpu_batch)
-    mine = shard_plan(forced_steps(M_all, args.r), world)[rank]
+    # (step count first, the token count breaking ties: copies of one utterance land on different ranks)
+    mine = shard_plan([s_ * 1e6 + t_ for s_, t_ in zip(forced_steps(M_all, args.r), T_all)], world)[rank]
     T_prof, M_prof = lj_profile()
     ids = synthetic_ids(T_prof)              # C3 replicates the same 32 utterances
     my_ids = [ids[i % len(ids)] for i in mine]

@@ -177,7 +177,7 @@ def test_replicated_workload_weak_scaling():
         # bench.py's plan (tts_amd.multigpu.shard_plan, LPT on the step counts) gives every rank one
         # copy of each profile utterance: the per-rank work of C2
         from tts_amd.multigpu import shard_plan
-        plan = shard_plan(forced_steps(M, 2), n)
+        plan = shard_plan([s_ * 1e6 + t_ for s_, t_ in zip(forced_steps(M, 2), T)], n)
         assert all(sorted(i % 32 for i in s) == list(range(32)) for s in plan)
 
 
