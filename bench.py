@@ -360,13 +360,35 @@ def main():
         # split-f16 mode: the decoder's GEMM parts run 3 f16 MFMAs per fp32 product, so the
         # ceiling is the f16 MFMA peak / 3 in fp32-equivalent FLOP/s; fp32 mode: the fp32 MFMA peak
         peak = X3_PEAK_TFLOPS if gemm_mode == "x3" else F32_PEAK_TFLOPS
+        # what the step actually hits is the latency of its hand-off chain (5 phases per step, each
+        # separated by a grid barrier, each starting with a coherent load of what the previous one
+        # published): tools/chain_bench.hip runs that chain with the decoder's roles and hand-off
+        # sizes and no arithmetic (profiles/r04/chain_floor.json). achieved / peak stay the MFMA
+        # figures (algorithmic FLOPs / launch time against the split-f16 ceiling)
+        floor = None
+        fpath = os.path.join(ROOT, "profiles", "r04", "chain_floor.json")
+        if os.path.exists(fpath):
+            try:
+                floor = json.load(open(fpath))
+            except Exception:
+                floor = None
         roof = {"kernel": "persist_decoder_kernel<2%s> (whole decoder loop, weights resident on chip)"
                           % (", split-f16" if gemm_mode == "x3" else ""),
-                "bound": "mfma", "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
+                "bound": "latency", "compute_bound": "mfma",
+                "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "frac_vs_fp32_mfma_peak": round(achieved / F32_PEAK_TFLOPS, 4),
                 "traffic": traffic,
                 "avg_launch_us": round(ms0 * 1000.0, 1), "algorithmic_flops": flops,
                 "launch_steps": st0, "launches": [[round(m_, 3), s_] for m_, s_ in launches]}
+        if floor:
+            fl = floor["loads_barriers_us"]
+            roof.update({"step_us": round(step_ms * 1000.0, 2),
+                         "latency_floor_us": fl,
+                         "latency_floor_barriers_only_us": floor["noload_barriers_us"],
+                         "latency_floor_with_compute_standins_us": floor["compute_loads_barriers_us"],
+                         "frac_of_latency_floor": round(fl / (step_ms * 1000.0), 4),
+                         "latency_floor_source": os.path.relpath(fpath, ROOT) + ": 5 grid barriers + the phases' "
+                                                 "coherent hand-off loads per step, no arithmetic"})
     else:
         k4_ms = eng.time_decoder_kernel(0, args.kernel_iters)
         step_ms = eng.time_decoder_kernel(1, max(4, args.kernel_iters // 8))

@@ -9,6 +9,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <string>
 #include <vector>
 
 namespace {
@@ -58,9 +59,30 @@ __device__ __forceinline__ bool edge_wait(unsigned* c, unsigned target, unsigned
   return *flag;
 }
 
+// hierarchical edge (mode 2): P producers per step, producer i counts in at first-level counter
+// i % nc (each on its own 128-byte line); the last arrival at a counter counts it in at the top
+// counter, the last of those writes the go word (t + 1); consumers poll only the go word
+struct Edge {
+  unsigned* blk;  // [0] top, [32] go, [64 + 32 c] first-level counters
+  int P, nc;
+};
+__device__ __forceinline__ void hedge_arrive(const Edge& e, int i, int t) {
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const unsigned per = (unsigned)(e.P / e.nc), gen = (unsigned)(t + 1);
+    unsigned* c = e.blk + 64 + (i % e.nc) * 32;
+    if (__hip_atomic_fetch_add(c, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == per * gen - 1)
+      if (__hip_atomic_fetch_add(e.blk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == (unsigned)e.nc * gen - 1)
+        __hip_atomic_store(e.blk + 32, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
 // load n 16-byte granules per thread from base (coherent), fold them into a register sum
+__device__ int g_noload;
 __device__ __forceinline__ float load_sum(const float* base, int n, int stride_bytes) {
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
+  if (g_noload) return 0.f;
   f32x4 v[16];
 #pragma unroll
   for (int i = 0; i < 16; ++i)
@@ -85,18 +107,27 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
   unsigned* Cctx = a.ctr + 96;
   unsigned* Cd = a.ctr + 128;
   const int it = g - IW0, ib = it / NCH, ich = it % NCH;
-  auto sync = [&](unsigned* c, unsigned target) -> bool {  // mode 0: grid barrier, mode 1: edge wait
+  // mode 2: hierarchical edges, one 1024-word block each (ctr + 4096 + 1024 k)
+  const Edge Ey{a.ctr + 4096, NPJ, 6}, Epb{a.ctr + 4096 + 1024, NPRE + 1, 3}, Eh{a.ctr + 4096 + 2048, NATT, 8},
+      Ectx{a.ctr + 4096 + 3072, NB, 8}, Ed{a.ctr + 4096 + 4096, PW, 16};
+  auto go = [&](const Edge& e) { return e.blk + 32; };
+  auto sync = [&](unsigned* c, unsigned target) -> bool {  // mode 0: grid barrier, mode 1/2: edge wait
     if (MODE == 0) {
       gsync_arrive(a.bar, gen);
       return gsync_wait(a.bar, gen, &flag);
     }
     return edge_wait(c, target, a.err, &flag);
   };
+  auto arrive = [&](unsigned* c, const Edge& e, int i, int t_) {
+    if (MODE == 1) edge_arrive(c);
+    if (MODE == 2) hedge_arrive(e, i, t_);
+  };
   for (int t = 0; t < a.steps; ++t) {
     float* hd_cur = (t & 1) ? a.hd1 : a.hd0;
     float* hd_nxt = (t & 1) ? a.hd0 : a.hd1;
     // ---- P1: prenet layer 2 (wg 0..31) || stop (wg 63) || items' location window
     if (MODE == 1 && (g < NPRE || g == STOP_WG) && t > 0 && !edge_wait(Cy, NPJ * t, a.err, &flag)) return;
+    if (MODE == 2 && (g < NPRE || g == STOP_WG) && t > 0 && !edge_wait(go(Ey), t, a.err, &flag)) return;
     if (g < NPRE) {
       acc += load_sum(a.ypart + (g & 1) * 16 * YP, 2, PT * 16);  // 16 rows x 256 columns
       spin(a.dl[0]);
@@ -104,11 +135,11 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
     } else if (g == STOP_WG) {
       acc += tid < 32 ? ldc(a.ypart + tid * YP) : 0.f;
     } else if (it >= 0 && it < NB * NCH) {
-      if (MODE == 1 && t > 0 && !edge_wait(a.ctr + 160 + 32 * ib, NCH * t, a.err, &flag)) return;
+      if (MODE >= 1 && t > 0 && !edge_wait(a.ctr + 160 + 32 * ib, NCH * t, a.err, &flag)) return;
       acc += tid < 128 ? ldc(a.alpha + ib * 256 + min(max(ich * 32 - 15 + (tid & 63), 0), 191)) : 0.f;
     }
-    if (MODE == 1 && (g < NPRE || g == STOP_WG)) edge_arrive(Cpb);
-    if (!sync(Cpb, (NPRE + 1) * (t + 1))) return;
+    if (g < NPRE || g == STOP_WG) arrive(Cpb, Epb, g < NPRE ? g : NPRE, t);
+    if (!sync(MODE == 2 ? go(Epb) : Cpb, MODE == 2 ? t + 1 : (NPRE + 1) * (t + 1))) return;
     // ---- P3: attention_rnn (wg 0..63) || h_dec part (items)
     if (g < NATT) {
       acc += load_sum(a.pb, 4, PT * 16);  // 32 rows x 256
@@ -116,12 +147,12 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
       if (tid < 128) stc4(a.hatt, ((g * 128 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});  // 2 KB
       stc4(a.pq, ((g * 1024 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});                 // 16 KB
       stc4(a.pq, ((g * 1024 + 512 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
-      if (MODE == 1) edge_arrive(Ch);
+      arrive(Ch, Eh, g, t);
     } else {
       acc += load_sum(hd_cur, 16, PT * 16);  // 128 KB
       spin(a.dl[5]);
     }
-    if (!sync(Ch, NATT * (t + 1))) return;
+    if (!sync(MODE == 2 ? go(Eh) : Ch, MODE == 2 ? t + 1 : NATT * (t + 1))) return;
     // ---- P4: attention items || h_att parts (wg 0..63)
     if (g >= IW0 && it < NB * NCH) {
       acc += load_sum(a.pq + ib * 128, 4, 32 * 128 * 4 * 4);  // 64 partials x 128 dims of row ib (16 per group)
@@ -137,33 +168,34 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
       if (is_last) {
         acc += load_sum(a.part_u + ib * NCH * 512, 6, 512 * 4) ;
         stc(a.ctx + ib * 512 + tid, acc);
-        if (MODE == 1) edge_arrive(Cctx);
+        arrive(Cctx, Ectx, ib, t);
       }
     } else if (g < IW0) {
       acc += load_sum(a.hatt, 16, PT * 16);
       acc += load_sum(hd_cur, 16, PT * 16);
     }
-    if (!sync(Cctx, NB * (t + 1))) return;
+    if (!sync(MODE == 2 ? go(Ectx) : Cctx, MODE == 2 ? t + 1 : NB * (t + 1))) return;
     // ---- P5: ctx parts (+ h_att parts on the items), decoder_rnn cell
     acc += load_sum(a.ctx, 8, PT * 16);
     if (g >= IW0) acc += load_sum(a.hatt, 16, PT * 16);
     spin(a.dl[3]);
     if (tid < 32) stc4(hd_nxt, ((g * 32 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
-    if (MODE == 1) edge_arrive(Cd);
+    arrive(Cd, Ed, g, t);
     if (MODE == 0) {
       if (!sync(Cd, 0)) return;
     }
     // ---- P6: projection jobs (wg 0..53) || alignment pass (items)
     if (g < NPJ) {
       if (MODE == 1 && !edge_wait(Cd, PW * (t + 1), a.err, &flag)) return;
+      if (MODE == 2 && !edge_wait(go(Ed), t + 1, a.err, &flag)) return;
       acc += load_sum(hd_nxt + (g & 1) * 16 * 1024, 8, PT * 16);   // 16 rows x 1024
       acc += load_sum(a.ctx + (g & 1) * 16 * 512, 4, PT * 16);     // 16 rows x 512
       spin(a.dl[4]);
       if (tid < 64) stc4(a.ypart, (((g & 1) * 16 * YP + (g >> 1) * 16) + tid * 4) * 4, f32x4{acc, acc, acc, acc});
-      if (MODE == 1) edge_arrive(Cy);
+      arrive(Cy, Ey, g, t);
     } else if (g >= IW0 && it < NB * NCH) {
       if (tid < 32) stc(a.alpha + ib * 256 + ich * 32 + tid, acc);
-      if (MODE == 1) edge_arrive(a.ctr + 160 + 32 * ib);
+      if (MODE >= 1) edge_arrive(a.ctr + 160 + 32 * ib);
     }
     if (MODE == 0 && !sync(nullptr, 0)) return;
   }
@@ -193,7 +225,7 @@ int main(int argc, char** argv) {
   a.alpha = alloc(NB * 256);
   a.sink = alloc(PW);
   HIP_OK(hipMalloc(&a.bar, BAR_WORDS * 4));
-  HIP_OK(hipMalloc(&a.ctr, 4096 * 4));
+  HIP_OK(hipMalloc(&a.ctr, 16384 * 4));
   HIP_OK(hipMalloc(&a.err, 4));
   const int steps = 400;
   a.steps = steps;
@@ -204,16 +236,20 @@ int main(int argc, char** argv) {
   } cfgs[] = {{"no compute", {0, 0, 0, 0, 0, 0}},
               // compute stand-ins near the MT = 2 kernel's per-role work (us x 100 ticks)
               {"compute stand-ins", {60, 150, 180, 150, 80, 60}}};
+  std::string js = "{";
+  for (int noload : {0, 1})
   for (const Cfg& c : cfgs) {
-    for (int mode : {0, 1}) {
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_noload), &noload, 4));
+    for (int mode : {0, 1, 2}) {
       std::memcpy(a.dl, c.dl, sizeof(a.dl));
-      const void* f = mode == 0 ? (const void*)chain_kernel<0> : (const void*)chain_kernel<1>;
+      const void* f = mode == 0 ? (const void*)chain_kernel<0> : mode == 1 ? (const void*)chain_kernel<1>
+                                                                              : (const void*)chain_kernel<2>;
       ensure_dyn_lds(f, 128 * 1024);
       float best = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
         HIP_OK(hipMemsetAsync(a.bar, 0, BAR_WORDS * 4, S));
         HIP_OK(hipMemcpyAsync(a.bar + BAR_TMO, &tmo, 4, hipMemcpyHostToDevice, S));
-        HIP_OK(hipMemsetAsync(a.ctr, 0, 4096 * 4, S));
+        HIP_OK(hipMemsetAsync(a.ctr, 0, 16384 * 4, S));
         HIP_OK(hipMemsetAsync(a.err, 0, 4, S));
         hipEvent_t e0, e1;
         HIP_OK(hipEventCreate(&e0));
@@ -235,10 +271,20 @@ int main(int argc, char** argv) {
         }
         best = std::min(best, ms);
       }
-      printf("%-18s %s: %.2f us per step\n", c.name, mode == 0 ? "grid barriers " : "edge counters ",
-             best * 1000.f / steps);
+      printf("%-18s %-9s %s: %.2f us per step\n", c.name, noload ? "no loads" : "loads",
+             mode == 0 ? "grid barriers     " : mode == 1 ? "edge counters     " : "hierarchical edges", best * 1000.f / steps);
+      js += std::string(js.size() > 1 ? ", " : "") + "\"" + (c.dl[0] ? "compute_" : "") + (noload ? "noload_" : "loads_") +
+            (mode == 0 ? "barriers" : mode == 1 ? "edge_counters" : "hier_edges") + "_us\": " +
+            std::to_string(best * 1000.f / steps);
     }
   }
-  printf("done\n");
+  js += "}";
+  if (argc > 1) {
+    if (FILE* f = std::fopen(argv[1], "w")) {
+      std::fprintf(f, "%s\n", js.c_str());
+      std::fclose(f);
+    }
+  }
+  printf("%s\ndone\n", js.c_str());
   return 0;
 }
