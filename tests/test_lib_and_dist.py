@@ -153,3 +153,14 @@ def test_gpu_pool_dispatch_and_gather():
         assert pool.map([]) == []
         with pytest.raises(RuntimeError, match="worker failed"):
             pool.map(items, r=0)  # r = 0 raises inside the workers
+
+
+def test_library_matches_build_record():
+    """__graft_entry__.build() records which sources libttship.so was built from; the library that
+    loads must be that build of this tree's sources (no stale .so)."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import __graft_entry__ as g
+    if not os.path.exists(g.BUILD_INFO):
+        pytest.skip("library not built through __graft_entry__.build()")
+    assert "built" in g.build_check()

@@ -202,6 +202,94 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
   if (tid == 0) a.sink[g] = acc;
 }
 
+// mode 3: grid barriers, but a workgroup whose phase work feeds nothing in the next phase arrives
+// BEFORE that work (its stores are covered by a later barrier it arrives at afterwards): each
+// barrier completes when its real producers arrive. Items' location window moves from P1 to P3,
+// items' P6 stores (alignment) are covered by the next step's P1 barrier.
+__global__ __launch_bounds__(PT) void early_kernel(CArgs a) {
+  __shared__ int flag, is_last;
+  const int g = blockIdx.x, tid = threadIdx.x;
+  unsigned gen = 0;
+  float acc = 0.f;
+  const int it = g - IW0, ib = it / NCH, ich = it % NCH;
+  const bool item = g >= IW0 && it < NB * NCH;
+  auto wait = [&]() { return gsync_wait(a.bar, gen, &flag); };
+  for (int t = 0; t < a.steps; ++t) {
+    float* hd_cur = (t & 1) ? a.hd1 : a.hd0;
+    float* hd_nxt = (t & 1) ? a.hd0 : a.hd1;
+    // P1: producers prenet + stop
+    const bool p1 = g < NPRE || g == STOP_WG;
+    if (!p1) gsync_arrive(a.bar, gen);
+    if (g < NPRE) {
+      acc += load_sum(a.ypart + (g & 1) * 16 * YP, 2, PT * 16);
+      spin(a.dl[0]);
+      if (tid < 64) stc4(a.pb, ((g * 64 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+    } else if (g == STOP_WG) {
+      acc += tid < 32 ? ldc(a.ypart + tid * YP) : 0.f;
+    }
+    if (p1) gsync_arrive(a.bar, gen);
+    if (!wait()) return;
+    // P3: producers att
+    if (g >= NATT) gsync_arrive(a.bar, gen);
+    if (g < NATT) {
+      acc += load_sum(a.pb, 4, PT * 16);
+      spin(a.dl[1]);
+      if (tid < 128) stc4(a.hatt, ((g * 128 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+      stc4(a.pq, ((g * 1024 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+      stc4(a.pq, ((g * 1024 + 512 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+      gsync_arrive(a.bar, gen);
+    } else {
+      if (item) acc += tid < 128 ? ldc(a.alpha + ib * 256 + min(max(ich * 32 - 15 + (tid & 63), 0), 191)) : 0.f;
+      acc += load_sum(hd_cur, 16, PT * 16);
+      spin(a.dl[5]);
+    }
+    if (!wait()) return;
+    // P4: producers items
+    if (g < IW0) gsync_arrive(a.bar, gen);
+    if (item) {
+      acc += load_sum(a.pq + ib * 128, 4, 32 * 128 * 4 * 4);
+      spin(a.dl[2]);
+      stc4(a.part_u, ((it * 128 + (tid & 127)) * 4) * 4, f32x4{acc, acc, acc, acc});
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+      if (tid == 0) {
+        const unsigned prev = __hip_atomic_fetch_add(a.ctr + 2048 + 32 * ib, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = prev == (unsigned)(NCH * (t + 1) - 1);
+      }
+      lds_barrier();
+      if (is_last) {
+        acc += load_sum(a.part_u + ib * NCH * 512, 6, 512 * 4);
+        stc(a.ctx + ib * 512 + tid, acc);
+      }
+    } else {
+      acc += load_sum(a.hatt, 16, PT * 16);
+      acc += load_sum(hd_cur, 16, PT * 16);
+    }
+    if (g >= IW0) gsync_arrive(a.bar, gen);
+    if (!wait()) return;
+    // P5: everyone
+    acc += load_sum(a.ctx, 8, PT * 16);
+    if (g >= IW0) acc += load_sum(a.hatt, 16, PT * 16);
+    spin(a.dl[3]);
+    if (tid < 32) stc4(hd_nxt, ((g * 32 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+    gsync_arrive(a.bar, gen);
+    if (!wait()) return;
+    // P6: producers pj
+    if (g >= NPJ) gsync_arrive(a.bar, gen);
+    if (g < NPJ) {
+      acc += load_sum(hd_nxt + (g & 1) * 16 * 1024, 8, PT * 16);
+      acc += load_sum(a.ctx + (g & 1) * 16 * 512, 4, PT * 16);
+      spin(a.dl[4]);
+      if (tid < 64) stc4(a.ypart, (((g & 1) * 16 * YP + (g >> 1) * 16) + tid * 4) * 4, f32x4{acc, acc, acc, acc});
+      gsync_arrive(a.bar, gen);
+    } else if (item) {
+      if (tid < 32) stc(a.alpha + ib * 256 + ich * 32 + tid, acc);
+    }
+    if (!wait()) return;
+  }
+  if (tid == 0) a.sink[g] = acc;
+}
+
 static hipStream_t S;
 
 int main(int argc, char** argv) {
@@ -240,10 +328,10 @@ int main(int argc, char** argv) {
   for (int noload : {0, 1})
   for (const Cfg& c : cfgs) {
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_noload), &noload, 4));
-    for (int mode : {0, 1, 2}) {
+    for (int mode : {0, 1, 2, 3}) {
       std::memcpy(a.dl, c.dl, sizeof(a.dl));
       const void* f = mode == 0 ? (const void*)chain_kernel<0> : mode == 1 ? (const void*)chain_kernel<1>
-                                                                              : (const void*)chain_kernel<2>;
+                    : mode == 2 ? (const void*)chain_kernel<2> : (const void*)early_kernel;
       ensure_dyn_lds(f, 128 * 1024);
       float best = 1e30f;
       for (int rep = 0; rep < 3; ++rep) {
@@ -272,9 +360,10 @@ int main(int argc, char** argv) {
         best = std::min(best, ms);
       }
       printf("%-18s %-9s %s: %.2f us per step\n", c.name, noload ? "no loads" : "loads",
-             mode == 0 ? "grid barriers     " : mode == 1 ? "edge counters     " : "hierarchical edges", best * 1000.f / steps);
+             mode == 0 ? "grid barriers     " : mode == 1 ? "edge counters     " : mode == 2 ? "hierarchical edges" : "early arrivals    ",
+             best * 1000.f / steps);
       js += std::string(js.size() > 1 ? ", " : "") + "\"" + (c.dl[0] ? "compute_" : "") + (noload ? "noload_" : "loads_") +
-            (mode == 0 ? "barriers" : mode == 1 ? "edge_counters" : "hier_edges") + "_us\": " +
+            (mode == 0 ? "barriers" : mode == 1 ? "edge_counters" : mode == 2 ? "hier_edges" : "early_arrival") + "_us\": " +
             std::to_string(best * 1000.f / steps);
     }
   }

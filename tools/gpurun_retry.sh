@@ -3,12 +3,12 @@
 # infrastructure status before the command started). Any other outcome is returned as is.
 # usage: tools/gpurun_retry.sh <timeout> '<command>' <log>
 to=$1; cmd=$2; log=$3
-for i in 1 2 3 4 5 6 7 8; do
+for i in $(seq 1 ${GPURUN_TRIES:-8}); do
   /usr/local/graft/bin/gpurun --timeout "$to" -- "$cmd" > "$log" 2>&1
   rc=$?
   if [ $rc -eq 3 ] || grep -q "status=transient rc=None" "$log"; then
     echo "attempt $i: no box ($rc), retrying in 150 s" >> "$log.retries"
-    sleep 150
+    sleep ${GPURUN_SLEEP:-150}
     continue
   fi
   exit $rc
