@@ -80,6 +80,8 @@ __device__ __forceinline__ void hedge_arrive(const Edge& e, int i, int t) {
 
 // load n 16-byte granules per thread from base (coherent), fold them into a register sum
 __device__ int g_noload;
+__device__ int g_rep;  // copies of each broadcast buffer (hatt, ctx, h_dec, pb); consumer wg g reads copy g % rep
+constexpr long S_HATT = 64 * 1024, S_CTX = 32 * 1024, S_HD = 64 * 1024, S_PB = 16 * 1024;  // floats per copy
 __device__ __forceinline__ float load_sum(const float* base, int n, int stride_bytes) {
   f32x4 s = {0.f, 0.f, 0.f, 0.f};
   if (g_noload) return 0.f;
@@ -131,7 +133,7 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
     if (g < NPRE) {
       acc += load_sum(a.ypart + (g & 1) * 16 * YP, 2, PT * 16);  // 16 rows x 256 columns
       spin(a.dl[0]);
-      if (tid < 64) stc4(a.pb, ((g * 64 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+      if (tid < 64) for (int c = 0; c < g_rep; ++c) stc4(a.pb + c * S_PB, ((g * 64 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
     } else if (g == STOP_WG) {
       acc += tid < 32 ? ldc(a.ypart + tid * YP) : 0.f;
     } else if (it >= 0 && it < NB * NCH) {
@@ -142,14 +144,14 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
     if (!sync(MODE == 2 ? go(Epb) : Cpb, MODE == 2 ? t + 1 : (NPRE + 1) * (t + 1))) return;
     // ---- P3: attention_rnn (wg 0..63) || h_dec part (items)
     if (g < NATT) {
-      acc += load_sum(a.pb, 4, PT * 16);  // 32 rows x 256
+      acc += load_sum(a.pb + (g % g_rep) * S_PB, 4, PT * 16);  // 32 rows x 256
       spin(a.dl[1]);
-      if (tid < 128) stc4(a.hatt, ((g * 128 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});  // 2 KB
+      if (tid < 128) for (int c = 0; c < g_rep; ++c) stc4(a.hatt + c * S_HATT, ((g * 128 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});  // 2 KB
       stc4(a.pq, ((g * 1024 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});                 // 16 KB
       stc4(a.pq, ((g * 1024 + 512 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
       arrive(Ch, Eh, g, t);
     } else {
-      acc += load_sum(hd_cur, 16, PT * 16);  // 128 KB
+      acc += load_sum(hd_cur + (g % g_rep) * S_HD, 16, PT * 16);  // 128 KB
       spin(a.dl[5]);
     }
     if (!sync(MODE == 2 ? go(Eh) : Ch, MODE == 2 ? t + 1 : NATT * (t + 1))) return;
@@ -167,19 +169,19 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
       lds_barrier();
       if (is_last) {
         acc += load_sum(a.part_u + ib * NCH * 512, 6, 512 * 4) ;
-        stc(a.ctx + ib * 512 + tid, acc);
+        for (int c = 0; c < g_rep; ++c) stc(a.ctx + c * S_CTX + ib * 512 + tid, acc);
         arrive(Cctx, Ectx, ib, t);
       }
     } else if (g < IW0) {
-      acc += load_sum(a.hatt, 16, PT * 16);
-      acc += load_sum(hd_cur, 16, PT * 16);
+      acc += load_sum(a.hatt + (g % g_rep) * S_HATT, 16, PT * 16);
+      acc += load_sum(hd_cur + (g % g_rep) * S_HD, 16, PT * 16);
     }
     if (!sync(MODE == 2 ? go(Ectx) : Cctx, MODE == 2 ? t + 1 : NB * (t + 1))) return;
     // ---- P5: ctx parts (+ h_att parts on the items), decoder_rnn cell
-    acc += load_sum(a.ctx, 8, PT * 16);
-    if (g >= IW0) acc += load_sum(a.hatt, 16, PT * 16);
+    acc += load_sum(a.ctx + (g % g_rep) * S_CTX, 8, PT * 16);
+    if (g >= IW0) acc += load_sum(a.hatt + (g % g_rep) * S_HATT, 16, PT * 16);
     spin(a.dl[3]);
-    if (tid < 32) stc4(hd_nxt, ((g * 32 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+    if (tid < 32) for (int c = 0; c < g_rep; ++c) stc4(hd_nxt + c * S_HD, ((g * 32 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
     arrive(Cd, Ed, g, t);
     if (MODE == 0) {
       if (!sync(Cd, 0)) return;
@@ -188,8 +190,8 @@ __global__ __launch_bounds__(PT) void chain_kernel(CArgs a) {
     if (g < NPJ) {
       if (MODE == 1 && !edge_wait(Cd, PW * (t + 1), a.err, &flag)) return;
       if (MODE == 2 && !edge_wait(go(Ed), t + 1, a.err, &flag)) return;
-      acc += load_sum(hd_nxt + (g & 1) * 16 * 1024, 8, PT * 16);   // 16 rows x 1024
-      acc += load_sum(a.ctx + (g & 1) * 16 * 512, 4, PT * 16);     // 16 rows x 512
+      acc += load_sum(hd_nxt + (g % g_rep) * S_HD + (g & 1) * 16 * 1024, 8, PT * 16);   // 16 rows x 1024
+      acc += load_sum(a.ctx + (g % g_rep) * S_CTX + (g & 1) * 16 * 512, 4, PT * 16);     // 16 rows x 512
       spin(a.dl[4]);
       if (tid < 64) stc4(a.ypart, (((g & 1) * 16 * YP + (g >> 1) * 16) + tid * 4) * 4, f32x4{acc, acc, acc, acc});
       arrive(Cy, Ey, g, t);
@@ -223,7 +225,7 @@ __global__ __launch_bounds__(PT) void early_kernel(CArgs a) {
     if (g < NPRE) {
       acc += load_sum(a.ypart + (g & 1) * 16 * YP, 2, PT * 16);
       spin(a.dl[0]);
-      if (tid < 64) stc4(a.pb, ((g * 64 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+      if (tid < 64) for (int c = 0; c < g_rep; ++c) stc4(a.pb + c * S_PB, ((g * 64 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
     } else if (g == STOP_WG) {
       acc += tid < 32 ? ldc(a.ypart + tid * YP) : 0.f;
     }
@@ -232,15 +234,15 @@ __global__ __launch_bounds__(PT) void early_kernel(CArgs a) {
     // P3: producers att
     if (g >= NATT) gsync_arrive(a.bar, gen);
     if (g < NATT) {
-      acc += load_sum(a.pb, 4, PT * 16);
+      acc += load_sum(a.pb + (g % g_rep) * S_PB, 4, PT * 16);
       spin(a.dl[1]);
-      if (tid < 128) stc4(a.hatt, ((g * 128 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+      if (tid < 128) for (int c = 0; c < g_rep; ++c) stc4(a.hatt + c * S_HATT, ((g * 128 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
       stc4(a.pq, ((g * 1024 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
       stc4(a.pq, ((g * 1024 + 512 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
       gsync_arrive(a.bar, gen);
     } else {
       if (item) acc += tid < 128 ? ldc(a.alpha + ib * 256 + min(max(ich * 32 - 15 + (tid & 63), 0), 191)) : 0.f;
-      acc += load_sum(hd_cur, 16, PT * 16);
+      acc += load_sum(hd_cur + (g % g_rep) * S_HD, 16, PT * 16);
       spin(a.dl[5]);
     }
     if (!wait()) return;
@@ -259,26 +261,26 @@ __global__ __launch_bounds__(PT) void early_kernel(CArgs a) {
       lds_barrier();
       if (is_last) {
         acc += load_sum(a.part_u + ib * NCH * 512, 6, 512 * 4);
-        stc(a.ctx + ib * 512 + tid, acc);
+        for (int c = 0; c < g_rep; ++c) stc(a.ctx + c * S_CTX + ib * 512 + tid, acc);
       }
     } else {
-      acc += load_sum(a.hatt, 16, PT * 16);
-      acc += load_sum(hd_cur, 16, PT * 16);
+      acc += load_sum(a.hatt + (g % g_rep) * S_HATT, 16, PT * 16);
+      acc += load_sum(hd_cur + (g % g_rep) * S_HD, 16, PT * 16);
     }
     if (g >= IW0) gsync_arrive(a.bar, gen);
     if (!wait()) return;
     // P5: everyone
-    acc += load_sum(a.ctx, 8, PT * 16);
-    if (g >= IW0) acc += load_sum(a.hatt, 16, PT * 16);
+    acc += load_sum(a.ctx + (g % g_rep) * S_CTX, 8, PT * 16);
+    if (g >= IW0) acc += load_sum(a.hatt + (g % g_rep) * S_HATT, 16, PT * 16);
     spin(a.dl[3]);
-    if (tid < 32) stc4(hd_nxt, ((g * 32 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
+    if (tid < 32) for (int c = 0; c < g_rep; ++c) stc4(hd_nxt + c * S_HD, ((g * 32 + tid) * 4) * 4, f32x4{acc, acc, acc, acc});
     gsync_arrive(a.bar, gen);
     if (!wait()) return;
     // P6: producers pj
     if (g >= NPJ) gsync_arrive(a.bar, gen);
     if (g < NPJ) {
-      acc += load_sum(hd_nxt + (g & 1) * 16 * 1024, 8, PT * 16);
-      acc += load_sum(a.ctx + (g & 1) * 16 * 512, 4, PT * 16);
+      acc += load_sum(hd_nxt + (g % g_rep) * S_HD + (g & 1) * 16 * 1024, 8, PT * 16);
+      acc += load_sum(a.ctx + (g % g_rep) * S_CTX + (g & 1) * 16 * 512, 4, PT * 16);
       spin(a.dl[4]);
       if (tid < 64) stc4(a.ypart, (((g & 1) * 16 * YP + (g >> 1) * 16) + tid * 4) * 4, f32x4{acc, acc, acc, acc});
       gsync_arrive(a.bar, gen);
@@ -303,13 +305,13 @@ int main(int argc, char** argv) {
   };
   CArgs a{};
   a.ypart = alloc(64 * YP);
-  a.pb = alloc(64 * 256 * 4);
-  a.hatt = alloc(64 * 1024 * 2);
+  a.pb = alloc(8 * S_PB);
+  a.hatt = alloc(8 * S_HATT);
   a.pq = alloc(64 * 32 * 128 * 2);
   a.part_u = alloc(NB * NCH * 512 * 2);
-  a.ctx = alloc(64 * 512 * 2);
-  a.hd0 = alloc(64 * 1024 * 2);
-  a.hd1 = alloc(64 * 1024 * 2);
+  a.ctx = alloc(8 * S_CTX);
+  a.hd0 = alloc(8 * S_HD);
+  a.hd1 = alloc(8 * S_HD);
   a.alpha = alloc(NB * 256);
   a.sink = alloc(PW);
   HIP_OK(hipMalloc(&a.bar, BAR_WORDS * 4));
@@ -325,10 +327,14 @@ int main(int argc, char** argv) {
               // compute stand-ins near the MT = 2 kernel's per-role work (us x 100 ticks)
               {"compute stand-ins", {60, 150, 180, 150, 80, 60}}};
   std::string js = "{";
+  for (int rep : {1, 2, 4, 8})
   for (int noload : {0, 1})
   for (const Cfg& c : cfgs) {
+    if (rep > 1 && noload) continue;
     HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_noload), &noload, 4));
+    HIP_OK(hipMemcpyToSymbol(HIP_SYMBOL(g_rep), &rep, 4));
     for (int mode : {0, 1, 2, 3}) {
+      if (rep > 1 && (mode == 1 || mode == 2)) continue;
       std::memcpy(a.dl, c.dl, sizeof(a.dl));
       const void* f = mode == 0 ? (const void*)chain_kernel<0> : mode == 1 ? (const void*)chain_kernel<1>
                     : mode == 2 ? (const void*)chain_kernel<2> : (const void*)early_kernel;
@@ -359,10 +365,11 @@ int main(int argc, char** argv) {
         }
         best = std::min(best, ms);
       }
-      printf("%-18s %-9s %s: %.2f us per step\n", c.name, noload ? "no loads" : "loads",
+      printf("rep %d %-18s %-9s %s: %.2f us per step\n", rep, c.name, noload ? "no loads" : "loads",
              mode == 0 ? "grid barriers     " : mode == 1 ? "edge counters     " : mode == 2 ? "hierarchical edges" : "early arrivals    ",
              best * 1000.f / steps);
-      js += std::string(js.size() > 1 ? ", " : "") + "\"" + (c.dl[0] ? "compute_" : "") + (noload ? "noload_" : "loads_") +
+      js += std::string(js.size() > 1 ? ", " : "") + "\"" + (rep > 1 ? "rep" + std::to_string(rep) + "_" : std::string()) +
+            (c.dl[0] ? "compute_" : "") + (noload ? "noload_" : "loads_") +
             (mode == 0 ? "barriers" : mode == 1 ? "edge_counters" : mode == 2 ? "hier_edges" : "early_arrival") + "_us\": " +
             std::to_string(best * 1000.f / steps);
     }

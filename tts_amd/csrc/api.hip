@@ -1433,10 +1433,6 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.nchmax = (W.T_max + persist_attn_tc() - 1) / persist_attn_tc();
   a.anorm = W.anorm.f();
   a.defer_align = persist_defer_ok(W.B * a.nchmax) && !std::getenv("TTS_ALIGN_IN_P4");
-  a.early = [] {  // TTS_EARLY_ARRIVE=0: every workgroup arrives after its phase work (A/B)
-    const char* e = std::getenv("TTS_EARLY_ARRIVE");
-    return !e || std::atoi(e) != 0;
-  }() ? 1 : 0;
   a.softmax = M.softmax;
   a.thr = thr;
   a.bar = reinterpret_cast<unsigned*>(W.pbar.p);

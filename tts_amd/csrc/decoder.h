@@ -171,7 +171,6 @@ struct PArgs {
   // writes alpha / alpha_cum / the alignment row of its own positions in P6
   float* anorm;       // (B, 2)
   int defer_align;
-  int early;          // early barrier arrival of each phase's non-producers (decoder_persist.hip P1)
   int nchmax;
   int softmax;
   float thr;

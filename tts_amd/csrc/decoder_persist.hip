@@ -1062,14 +1062,6 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    // early arrival (P.early): a workgroup whose work in a phase feeds nothing that the next phase
-    // reads arrives at that phase's barrier BEFORE the work, so each barrier completes when its
-    // real producers arrive (fewer simultaneous arrivals, no non-critical work on its path); stores
-    // of such work are drained at the next barrier it arrives at after them. P1's producers: the
-    // prenet workgroups (pb) and the stop workgroup (done flags, the control block)
-    const int stop_wg = MT <= 2 ? IW0 - 1 : PW - 1;
-    const bool p1_prod = g < 16 * MT || g == stop_wg;
-    if (P.early && !p1_prod) gsync_arrive(P.bar, gen);
     if (g < 16 * MT) {  // prenet layer 2: tile g & 15, batch rows 16 (g >> 4) .. + 15, whole K
       const int tl2 = g & 15, mt = g >> 4;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -1113,14 +1105,12 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     }
     // location features of this workgroup's first attention item for step t (alpha of t-1 is
     // final); items sit on workgroups IW0.. so that they miss the prenet workgroups
-    // (early arrival: in P3 instead, where the item workgroups have slack; alpha of t-1 is then
-    // covered by this barrier, at which the items arrive after their P6 alignment pass)
     const int it0 = g - IW0;
-    if (!P.early && !GRAVES && it0 >= 0 && it0 < D.B * P.nchmax)
+    if (!GRAVES && it0 >= 0 && it0 < D.B * P.nchmax)
       attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
     // stop decision: an attention_rnn workgroup that is not a prenet one (MT <= 2), or the last
     // item workgroup once every attention_rnn workgroup runs a prenet job (MT = 3, 4)
-    if (g == stop_wg) {
+    if (g == (MT <= 2 ? IW0 - 1 : PW - 1)) {
       int dn = 1;
       if (tid < D.B) {
         const int m = tid;
@@ -1149,7 +1139,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
     }
     PTRACE(1);
-    if (!P.early || p1_prod) gsync_arrive(P.bar, gen);
+    gsync_arrive(P.bar, gen);
     // P3 operands that are already final: its epilogue's gate addends (written by P5 of the
     // previous step), c_att, the query-projection weights
     float ga[NCK][4], ca[NCK], wq[4];
@@ -1203,7 +1193,6 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (P.early && g >= NATT) gsync_arrive(P.bar, gen);  // the items' P3 work is private (early arrival)
     if (g < NATT) {
       // relu(prenet output) staged once per workgroup in LDS (the Wcomb area: attention_rnn
       // workgroups have no attention item); wave w loads k-chunks 2w, 2w+1
@@ -1347,13 +1336,11 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
       PTRACE(12);
     } else {
-      if (P.early && !GRAVES && it0 >= 0 && it0 < D.B * P.nchmax)  // location features (moved from P1)
-        attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
       dec_hdec_part(hd_cur);
       write_frames(t - 1, NATT, PW - NATT);
     }
     PTRACE(3);
-    if (!P.early || g < NATT) gsync_arrive(P.bar, gen);
+    gsync_arrive(P.bar, gen);
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     if constexpr (GRAVES) {
       // ======== P3g: N_a hidden = relu(W1 h_att + b1), 16 units per workgroup IW0 .. IW0+63 ========
@@ -1391,7 +1378,6 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    if (P.early && g < IW0) gsync_arrive(P.bar, gen);  // their GEMM parts are private (early arrival)
     {
       // The h_att parts run AFTER this workgroup's attention item: fp32 MFMA occupies the SIMD
       // (no co-issue with the attention's VALU work on the other wave), so under the item they
@@ -1423,7 +1409,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
     }
     PTRACE(5);
-    if (!P.early || g >= IW0) gsync_arrive(P.bar, gen);
+    gsync_arrive(P.bar, gen);
     // P5 epilogue operand (own tile's c_dec), fetched during the barrier
     float cd[NCK];
 #pragma unroll
@@ -1499,10 +1485,6 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
     wave = opaque_s(wave0);
-    // P6's producers are the projection jobs (ypart); the items' gate addends and alignment pass are
-    // read only after the next step's P1 barrier, at which the items arrive after this work
-    const bool pj_act = X3P ? (is_pj && (pj % JR) < MT) : is_pj;
-    if (P.early && !pj_act) gsync_arrive(P.bar, gen);
     if (X3P && is_pj && (pj % JR) < MT) {
       // split-f16: job pj = (tile pj / JR, batch rows 16 (pj % JR) .. + 15), the whole K, so ypart
       // holds one copy (P1, the stop decision and the frame writes read it once)
@@ -1594,7 +1576,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
     }
     PTRACE(9);
-    if (!P.early || pj_act) gsync_arrive(P.bar, gen);
+    gsync_arrive(P.bar, gen);
     if (!gsync_wait(P.bar, gen, &sflag)) return;
   }
 }
