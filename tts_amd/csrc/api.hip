@@ -20,8 +20,8 @@
 
 void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int num_rows, int D,
                          const int* lens, int B, float* out, hipStream_t s);
-bool launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
-                           int B, float* hbuf, unsigned* bar, float* out, hipStream_t s);
+int launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                          int B, float* hbuf, unsigned* bar, float* out, hipStream_t s);
 void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, const float* beta, const float* res,
                        long rb, float* out, long ob, const int* lens, int B, int T, hipStream_t s);
 void launch_ln(float* x, long xb, int C, const float* gamma, const float* beta, const int* lens, int B, int T,
@@ -345,6 +345,7 @@ struct TacoWS {
   DevBuf win_idx, fwd_u, apf;  // windowing argmax, transition probability, forward chunk sums
   DevBuf gh, gmu;              // Graves: N_a hidden (32 x 1024), mixture means (64 x 16)
   bool enc_persist = false;    // the last encoder ran the persistent BiLSTM (lc = its barrier words)
+  int enc_ndom = 0;            // its recurrences (directions x row groups), one barrier block each
   // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
   // longest-first rows finish); all share one configuration key
   hipGraphExec_t graphs[5] = {nullptr, nullptr, nullptr, nullptr, nullptr};
@@ -1120,10 +1121,11 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
   // one cooperative launch for the whole recurrence (W.lc then holds its grid-barrier words);
   // per-step launches when cooperative launch is unavailable or TTS_ENCODER=steps
   const char* e = std::getenv("TTS_ENCODER");
-  W.enc_persist = !(e && std::string(e) == "steps") &&
-                  launch_bilstm_persist(W.gin.f(), M.whhT.f(), c->gemm_x3 ? M.whhT16.h() : nullptr, lens, T_max, B,
-                                        W.lh.f(),
-                                        reinterpret_cast<unsigned*>(W.lc.p), enc_out, s);
+  W.enc_ndom = (e && std::string(e) == "steps")
+                   ? 0
+                   : launch_bilstm_persist(W.gin.f(), M.whhT.f(), c->gemm_x3 ? M.whhT16.h() : nullptr, lens, T_max, B,
+                                           W.lh.f(), reinterpret_cast<unsigned*>(W.lc.p), enc_out, s);
+  W.enc_persist = W.enc_ndom > 0;
   if (!W.enc_persist) launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
 }
 
@@ -1132,13 +1134,13 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
 // null-stream copy would not be), then the stream is drained before they are looked at.
 void check_encoder_barrier(tts_ctx* c) {
   if (!c->tws.enc_persist) return;
-  int* pw = c->pinned + 240;
-  pw[0] = pw[1] = 0;
+  int* pw = c->pinned + 240;  // one error word per recurrence (2 directions x up to 2 row groups)
+  const int nd = std::min(c->tws.enc_ndom, 4);
+  pw[0] = pw[1] = pw[2] = pw[3] = 0;
   const unsigned* words = reinterpret_cast<const unsigned*>(c->tws.lc.p);
-  HIP_OK(hipMemcpyAsync(&pw[0], words + 16, 4, hipMemcpyDeviceToHost, c->s));
-  HIP_OK(hipMemcpyAsync(&pw[1], words + BAR_WORDS + 16, 4, hipMemcpyDeviceToHost, c->s));
+  for (int i = 0; i < nd; ++i) HIP_OK(hipMemcpyAsync(&pw[i], words + i * BAR_WORDS + 16, 4, hipMemcpyDeviceToHost, c->s));
   HIP_OK(hipStreamSynchronize(c->s));
-  TTS_CHECK(pw[0] == 0 && pw[1] == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
+  TTS_CHECK(pw[0] == 0 && pw[1] == 0 && pw[2] == 0 && pw[3] == 0, "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
 }
 
 void run_postnet(tts_ctx* c, const float* dec, long dec_b, const int* mlens, int B, int Mmax_alloc, int max_q,

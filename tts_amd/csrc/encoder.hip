@@ -114,6 +114,10 @@ __global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restric
 //   hbuf: [2 ping-pong][dir][Bp x H] fragment order      out : (B, T_max, NDIR*H)
 //   Whh16 (X3): the same tiles split-f16 (split16.h pack_split_a, [dir * H/4 + tile][H/32][64][16]);
 //   h is loaded from the fp32 fragment buffer and split in registers (|h| <= 1: always in range)
+// Row groups (RG > 1, round 4): the batch rows split into RG independent recurrences of MT tiles
+// each, on RG x NDIR x NT workgroups (the encoder BiLSTM at B = 17..64: 2 x 2 x 64 = every CU),
+// each group with its own h buffers and barrier: half the rows per step on every workgroup.
+//   hbuf: [2 ping-pong][RG][dir][Bp x H]
 constexpr int LSTM_NW = 8;  // waves per workgroup: the K = H reduction split 8 ways
 template <int MT, int H, int NDIR, bool X3>
 __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float* __restrict__ Whh,
@@ -129,7 +133,11 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
   static_assert(NKC % NW == 0 && KPW % 2 == 0 && NT % 8 == 0, "LSTM geometry");
   __shared__ float part[NW * Bp * 17];
   __shared__ int sflag;
-  const int dir = blockIdx.x / NT, tl = blockIdx.x % NT;
+  const int RG = gridDim.x / (NDIR * NT);      // row groups (the launcher sizes the grid)
+  const int rg = blockIdx.x / (NDIR * NT);
+  const int dir = (blockIdx.x / NT) % NDIR, tl = blockIdx.x % NT;
+  const int dom = rg * NDIR + dir;             // this workgroup's recurrence: h buffers and barrier
+  const int r0 = rg * Bp;                      // its first batch row
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   constexpr int KSW = KPW / 2;  // split-f16 k-steps (32) per wave
   f32x4 w[X3 ? 1 : KPW];
@@ -144,9 +152,10 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
     for (int k = 0; k < KPW; ++k) w[k] = Wv[(long)k * 64];
   }
   const int m = min(tid >> 2, Bp - 1), u = tid & 3;
-  const bool row = (tid >> 2) < Bp && m < B;
-  const int Tm = lens[min(m, B - 1)];
-  const float* gbase = Gin + (long)min(m, B - 1) * T_max * G + dir * 4 * H + tl * 16 + u;
+  const int ma = r0 + m;  // absolute batch row
+  const bool row = (tid >> 2) < Bp && ma < B;
+  const int Tm = lens[min(ma, B - 1)];
+  const float* gbase = Gin + (long)min(ma, B - 1) * T_max * G + dir * 4 * H + tl * 16 + u;
   float cst = 0.f;
   unsigned gen = 0;
   // input-projection gates of a step do not depend on h: loaded one step ahead, under the barrier
@@ -155,8 +164,8 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
 #pragma unroll
   for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(0) * G + q * 4];
   for (int step = 0; step < T_max; ++step) {
-    const float* hi = hbuf + (size_t)(step & 1) * NDIR * Bp * H + (long)dir * Bp * H;
-    float* ho = hbuf + (size_t)((step + 1) & 1) * NDIR * Bp * H + (long)dir * Bp * H;
+    const float* hi = hbuf + (size_t)(step & 1) * RG * NDIR * Bp * H + (long)dom * Bp * H;
+    float* ho = hbuf + (size_t)((step + 1) & 1) * RG * NDIR * Bp * H + (long)dom * Bp * H;
     const int t = tpos(step);
     f32x4 acc[MT];
 #pragma unroll
@@ -223,27 +232,38 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
       cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
       const float hn = sigm_f(pre[3]) * tanh_f(cst);
       stc_quad(ho, (int)frag_idx(m, tl * 4 + u, H), hn);  // lanes u = 0..3 of a quad: one 16-byte store
-      out[((long)m * T_max + t) * O + dir * H + tl * 4 + u] = hn;
+      out[((long)ma * T_max + t) * O + dir * H + tl * 4 + u] = hn;
     }
-    if (step + 1 < T_max) {  // directions are independent: one barrier each
-      gsync_arrive(bar + dir * BAR_WORDS, gen, NT);
+    if (step + 1 < T_max) {  // directions and row groups are independent: one barrier each
+      unsigned* db = bar + dom * BAR_WORDS;
+      gsync_arrive(db, gen, NT);
 #pragma unroll
       for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(step + 1) * G + q * 4];
-      if (!gsync_wait(bar + dir * BAR_WORDS, gen, &sflag)) return;
+      if (!gsync_wait(db, gen, &sflag)) return;
     }
   }
 }
 
+// returns the number of recurrences launched (row groups x directions, each with its own barrier
+// block), 0 when a cooperative launch is unavailable
 template <int H, int NDIR>
-static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
-                                  int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
+static int launch_lstm_persist_t(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                                 int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
   int dev = 0, coop = 0;
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
-  if (!coop) return false;
-  const int MT = (B + 15) / 16, Bp = MT * 16;
-  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * NDIR * Bp * H * 4, s));
-  arm_barrier(bar, NDIR, s);
+  if (!coop) return 0;
+  // row groups: two recurrences of half the batch tiles each when every workgroup of both still
+  // fits the device (the encoder BiLSTM, B > 16: 2 x 2 x 64 = 256); TTS_LSTM_RG=1 turns it off
+  static const bool rg_on = [] {
+    const char* e = std::getenv("TTS_LSTM_RG");
+    return !e || std::atoi(e) != 1;
+  }();
+  const int MT0 = (B + 15) / 16;
+  const int RG = (rg_on && MT0 % 2 == 0 && 2 * NDIR * (H / 4) <= device_cu_count()) ? 2 : 1;
+  const int MT = MT0 / RG, Bp = MT * 16;
+  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * RG * NDIR * Bp * H * 4, s));
+  arm_barrier(bar, RG * NDIR, s);
   void* args[] = {(void*)&Whh, (void*)&Whh16, (void*)&Gin, (void*)&lens, (void*)&T_max,
                   (void*)&B,   (void*)&hbuf,  (void*)&out, (void*)&bar};
 #define LPK(mt, x) (const void*)lstm_persist_kernel<mt, H, NDIR, x>
@@ -251,13 +271,14 @@ static bool launch_lstm_persist_t(const float* Gin, const float* Whh, const uint
                                         {LPK(1, true), LPK(2, true), LPK(3, true), LPK(4, true)}};
 #undef LPK
   const void* f = fns[Whh16 ? 1 : 0][MT - 1];
-  launch_resident(f, dim3(NDIR * H / 4), dim3(64 * LSTM_NW), args, 0, s);
-  return true;
+  launch_resident(f, dim3(RG * NDIR * H / 4), dim3(64 * LSTM_NW), args, 0, s);
+  return RG * NDIR;
 }
 
-// encoder BiLSTM (H = 256, both directions); false = cooperative launch unavailable
-bool launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
-                           int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
+// encoder BiLSTM (H = 256, both directions): the number of recurrences (barrier blocks in `bar`),
+// 0 = cooperative launch unavailable
+int launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
+                          int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
   return launch_lstm_persist_t<256, 2>(Gin, Whh, Whh16, lens, T_max, B, hbuf, bar, out, s);
 }
 
@@ -265,7 +286,7 @@ bool launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* W
 bool launch_lstm768_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
                             int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
   TTS_CHECK(B >= 1 && B <= 64, "speaker encoder: 1..64 sequences per launch");
-  return launch_lstm_persist_t<768, 1>(Gin, Whh, Whh16, lens, T_max, B, hbuf, bar, out, s);
+  return launch_lstm_persist_t<768, 1>(Gin, Whh, Whh16, lens, T_max, B, hbuf, bar, out, s) > 0;
 }
 
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
