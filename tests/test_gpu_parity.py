@@ -299,6 +299,38 @@ def test_encoder_matches_reference(taco_sig):
     assert not out[1, len(ids[1]):].any()
 
 
+@pytest.mark.parametrize("B", [32, 64, 24])
+def test_encoder_row_groups_vs_oracle(B):
+    """The persistent BiLSTM's row groups (B = 17..32 and 49..64 run as two independent recurrences
+    per direction on all 256 CUs): every row's encoder output against the oracle encoder at B = 1,
+    ragged lengths up to the LJ maximum, zero past each length."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd._lib import get_engine
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=4, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    eng = get_engine("cuda:0")
+    m._sync(eng)
+    rs = np.random.RandomState(B)
+    lens = rs.randint(2, 169, size=B)
+    lens[B // 3] = 168
+    ids = [rs.randint(1, 129, size=L).astype(np.int64) for L in lens]
+    T = int(lens.max())
+    batch = np.zeros((B, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    out = torch.empty(B, T, 512, device="cuda")
+    eng.taco_encoder(torch.from_numpy(batch).cuda(), [int(L) for L in lens], out)
+    out = out.cpu().numpy()
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for i in range(B):
+        ref = orc.encoder(ids[i])
+        assert np.abs(out[i, :lens[i]] - ref).max() <= 1e-5, i
+        assert not out[i, lens[i]:].any(), i
+
+
 def _check_taco(fx, r, dec, post, align, stop, steps, utts):
     for i in utts:
         k = f"r{r}_u{i}"
