@@ -180,6 +180,14 @@ int tts_glow_set_tensor(tts_ctx* ctx, const char* name, const float* host, const
 int tts_glow_finalize(tts_ctx* ctx, int num_chars, int enc_layers, int num_flow_blocks, int num_block_layers);
 int tts_glow_encode(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max,
                     float length_scale, int32_t* h_ylens, void* stream);
+/* tts_glow_encode_spk <- GlowTts.inference(x, x_lengths, g) (glow_tts.py:159-176) for a
+   multi-speaker model (num_speakers > 1, c_in_channels > 0): h_speaker_ids (B) index emb_g;
+   g = F.normalize(emb_g(ids)) joins the duration predictor input (encoder.py:131-135) and, through
+   each coupling block's cond_layer, the WN gates of the following tts_glow_decode (glow.py:119-130).
+   h_speaker_ids = NULL is tts_glow_encode. Errors as the reference fails: ids given to a model
+   without emb_g or cond_layer, no ids for a model with c_in_channels > 0, an id out of range. */
+int tts_glow_encode_spk(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, const int32_t* h_speaker_ids,
+                        int B, int T_max, float length_scale, int32_t* h_ylens, void* stream);
 int tts_glow_decode(tts_ctx* ctx, const float* d_noise, float noise_scale, int Ty, float* d_y, float* d_ymean,
                     float* d_attn, float* d_logw, void* stream);
 

@@ -15,6 +15,9 @@ here: its ``monotonic_align.core`` Cython extension is not built), see make_gold
 * ``models/glow_tts.py:170-193``  w_ceil, y_lengths, generate_path, expanded means, noise
 * ``layers/glow_tts/decoder.py:6-33,81-95``  squeeze / unsqueeze, flows reversed
 * ``layers/glow_tts/glow.py:85-138,171-205,245-262``  WN, InvConvNear reverse, CouplingBlock reverse
+* speaker conditioning: ``models/glow_tts.py:159-161`` g = F.normalize(emb_g(speaker)),
+  ``encoder.py:131-135`` [x; g] into the duration predictor, ``glow.py:119-130`` cond_layer(g) sliced
+  per WN layer and added before the gate (pinned by ``tests/golden/glow_spk.npz``)
 """
 
 import numpy as np
@@ -119,7 +122,13 @@ class GlowOracle:
                            sd[f"encoder.encoder.norm_layers_2.{i}.beta"])
         return x
 
-    def encode(self, ids):
+    def speaker(self, spk):
+        """F.normalize(emb_g(spk)) (glow_tts.py:159-161): x / max(||x||_2, 1e-12), shape (c_in,)."""
+        e = self.sd["emb_g.weight"][int(spk)]
+        n = np.sqrt(np.sum(e.astype(np.float64) ** 2))
+        return (e / F32(max(n, 1e-12))).astype(F32)
+
+    def encode(self, ids, g=None):
         sd = self.sd
         H = sd["encoder.emb.weight"].shape[1]
         x = (sd["encoder.emb.weight"][ids] * F32(np.sqrt(H))).T.astype(F32)        # (H, T)
@@ -131,11 +140,12 @@ class GlowOracle:
             p = f"encoder.encoder."
             o = conv1d(x, sd[p + f"conv_layers.{i}.weight"], sd[p + f"conv_layers.{i}.bias"], 2)
             o = layer_norm(o, sd[p + f"norm_layers.{i}.gamma"], sd[p + f"norm_layers.{i}.beta"])
-            a, g = o[:H], o[H:]
-            x = (x + a * (F32(1) / (F32(1) + np.exp(-g)))).astype(F32)
+            a, gate = o[:H], o[H:]
+            x = (x + a * (F32(1) / (F32(1) + np.exp(-gate)))).astype(F32)
         o_mean = conv1d(x, sd["encoder.proj_m.weight"], sd["encoder.proj_m.bias"])
         d = "encoder.duration_predictor."
-        h = np.maximum(conv1d(x, sd[d + "conv_1.weight"], sd[d + "conv_1.bias"], 1), F32(0))
+        x_dp = x if g is None else np.concatenate([x, np.repeat(g[:, None], x.shape[1], 1)], 0)
+        h = np.maximum(conv1d(x_dp, sd[d + "conv_1.weight"], sd[d + "conv_1.bias"], 1), F32(0))
         h = layer_norm(h, sd[d + "norm_1.gamma"], sd[d + "norm_1.beta"])
         h = np.maximum(conv1d(h, sd[d + "conv_2.weight"], sd[d + "conv_2.bias"], 1), F32(0))
         h = layer_norm(h, sd[d + "norm_2.gamma"], sd[d + "norm_2.beta"])
@@ -147,10 +157,12 @@ class GlowOracle:
         w_ceil = np.ceil(((np.exp(logw) - F32(1)) * F32(length_scale)).astype(F32))
         return w_ceil, max(int(w_ceil.sum()), 1)
 
-    def inference(self, ids, noise=None, noise_scale=0.66, length_scale=1.0):
-        """one utterance: (y (80, 2*floor(Ty/2)), y_mean (80, Ty), attn (Ty, Tx), logw (Tx,), Ty)"""
+    def inference(self, ids, noise=None, noise_scale=0.66, length_scale=1.0, spk=None):
+        """one utterance: (y (80, 2*floor(Ty/2)), y_mean (80, Ty), attn (Ty, Tx), logw (Tx,), Ty);
+        ``spk``: speaker index into emb_g (multi-speaker models)"""
         sd = self.sd
-        o_mean, logw = self.encode(np.asarray(ids))
+        g = None if spk is None else self.speaker(spk)
+        o_mean, logw = self.encode(np.asarray(ids), g)
         w_ceil, Ty = self.durations(logw, length_scale)
         cum = np.cumsum(w_ceil)
         j = np.arange(Ty, dtype=F32)[None, :]
@@ -162,22 +174,25 @@ class GlowOracle:
         K = Ty // 2
         x = z[:, :2 * K].reshape(C, K, 2).transpose(2, 0, 1).reshape(2 * C, K)         # squeeze
         for k in range(self.flows - 1, -1, -1):
-            x = self._coupling_rev(x, f"decoder.flows.{3 * k + 2}.")
+            x = self._coupling_rev(x, f"decoder.flows.{3 * k + 2}.", g)
             x = self._invconv_rev(x, sd[f"decoder.flows.{3 * k + 1}.weight"])
             a = f"decoder.flows.{3 * k}."
             x = ((x - sd[a + "bias"].reshape(-1, 1)) * np.exp(-sd[a + "logs"].reshape(-1, 1))).astype(F32)
         y = x.reshape(2, C, K).transpose(1, 2, 0).reshape(C, 2 * K)                    # unsqueeze
         return y.astype(F32), y_mean, path.T.copy(), logw, Ty
 
-    def _coupling_rev(self, x, p):
+    def _coupling_rev(self, x, p, g=None):
         sd = self.sd
         C = x.shape[0] // 2
         x0, x1 = x[:C], x[C:]
         h = conv1d(x0, wn(sd, p + "start"), sd[p + "start.bias"])
         H = h.shape[0]
         out = np.zeros_like(h)
+        gc = None if g is None else conv1d(g[:, None], wn(sd, p + "wn.cond_layer"), sd[p + "wn.cond_layer.bias"])
         for i in range(self.wn_layers):
             a = conv1d(h, wn(sd, p + f"wn.in_layers.{i}"), sd[p + f"wn.in_layers.{i}.bias"], 2)
+            if gc is not None:
+                a = (a + gc[2 * H * i:2 * H * (i + 1)]).astype(F32)
             acts = (np.tanh(a[:H]) * (F32(1) / (F32(1) + np.exp(-a[H:])))).astype(F32)
             rs = conv1d(acts, wn(sd, p + f"wn.res_skip_layers.{i}"), sd[p + f"wn.res_skip_layers.{i}.bias"])
             if i < self.wn_layers - 1:

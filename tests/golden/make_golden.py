@@ -302,18 +302,18 @@ def import_glow_tts():
     return GlowTts
 
 
-def glow_case(name, encoder_type="gatedconv", seed=23, data_seed=24):
+def glow_case(name, encoder_type="gatedconv", seed=23, data_seed=24, num_speakers=0, c_in=0):
     """Glow-TTS as setup_model builds it (TTS/tts/utils/generic_utils.py:105-129), run through the
     reference's own ``GlowTts.inference`` (glow_tts.py:159-185) after import_glow_tts() built its
     Cython dependency. The prior noise is drawn inside inference by ``torch.randn_like``; re-seeding
     torch reproduces it for the fixture (the encoder and decoder draw nothing in eval mode)."""
     from tts_amd.spec import GlowConfig, glow_spec
     GlowTts = import_glow_tts()
-    cfg = GlowConfig(encoder_type=encoder_type)
+    cfg = GlowConfig(encoder_type=encoder_type, num_speakers=num_speakers, c_in_channels=c_in)
     m = GlowTts(num_chars=cfg.num_chars, hidden_channels=192, filter_channels=768, filter_channels_dp=256,
                 out_channels=80, kernel_size=3, num_heads=2, num_layers_enc=6, encoder_type=encoder_type,
                 dropout_p=0.1, num_flow_blocks_dec=12, kernel_size_dec=5, dilation_rate=1, num_block_layers=4,
-                dropout_p_dec=0.05, num_speakers=0, c_in_channels=0, num_splits=4, num_sqz=2, sigmoid_scale=False,
+                dropout_p_dec=0.05, num_speakers=num_speakers, c_in_channels=c_in, num_splits=4, num_sqz=2, sigmoid_scale=False,
                 mean_only=True, hidden_channels_enc=192, hidden_channels_dec=192, use_encoder_prenet=True)
     ref_keys = {k: tuple(v.shape) for k, v in m.state_dict().items()}
     spec = {n: tuple(sh) for n, sh, _ in glow_spec(cfg)}
@@ -323,18 +323,22 @@ def glow_case(name, encoder_type="gatedconv", seed=23, data_seed=24):
     m.eval()
     rs = np.random.RandomState(data_seed)
     out = {"seed": np.int64(seed), "noise_scale": np.float32(m.noise_scale), "encoder_type": encoder_type,
-           "source": "GlowTts.inference"}
+           "source": "GlowTts.inference", "num_speakers": np.int64(num_speakers), "c_in": np.int64(c_in)}
     for u, T in enumerate((17, 31)):
         ids = rs.randint(1, cfg.num_chars, size=T).astype(np.int64)
+        spk = (2, 0)[u] if num_speakers > 1 else None
         with torch.no_grad():
             x = torch.from_numpy(ids[None])
             torch.manual_seed(100 + u)
-            y, _, y_mean, y_log_scale, attn, o_dur_log, _ = m.inference(x, torch.tensor([T]))
+            g = None if spk is None else torch.tensor([spk])
+            y, _, y_mean, y_log_scale, attn, o_dur_log, _ = m.inference(x, torch.tensor([T]), g=g)
             torch.manual_seed(100 + u)
             noise = torch.randn_like(y_mean)
         Ty = int(attn.shape[1])
         k = f"u{u}"
         out[f"{k}_ids"] = ids
+        if spk is not None:
+            out[f"{k}_spk"] = np.int64(spk)
         out[f"{k}_noise"] = noise[0].numpy()
         out[f"{k}_y"] = y[0].numpy()
         out[f"{k}_ymean"] = y_mean[0].numpy()
@@ -453,6 +457,10 @@ if __name__ == "__main__":
         glow_case("glow_tdsep", "time-depth-separable", seed=27, data_seed=28)
     if "glow_tfm" in which:
         glow_case("glow_tfm", "transformer", seed=33, data_seed=30)  # seed 29: all durations 0
+    if "glow_spk" in which:
+        # multi-speaker Glow-TTS built directly (setup_model passes c_in_channels=0, which cannot
+        # take g): 4 speakers, c_in 36 (not a multiple of 16, to cover the channel padding)
+        glow_case("glow_spk", seed=41, data_seed=42, num_speakers=4, c_in=36)
     if "taco_state" in which:
         taco_state_case("taco_state")
     if "taco_amplified" in which:

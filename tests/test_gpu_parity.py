@@ -1066,6 +1066,79 @@ def test_glow_tts_matches_reference(name, enc):
         assert not y[i, :, ref.shape[1]:].any()
 
 
+def _glow_spk_model(fx):
+    from tts_amd import GlowTts
+    from tts_amd.spec import GlowConfig, glow_spec
+    cfg = GlowConfig(num_speakers=int(fx["num_speakers"]), c_in_channels=int(fx["c_in"]))
+    sd = synth_state_dict(glow_spec(cfg), int(fx["seed"]))
+    m = GlowTts(num_chars=cfg.num_chars, num_speakers=cfg.num_speakers, c_in_channels=cfg.c_in_channels)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    return m.cuda().eval(), sd
+
+
+def test_glow_multispeaker_matches_reference():
+    """Multi-speaker GlowTts (4 speakers, c_in 36) with g = speaker ids: the reference's own
+    GlowTts.inference(x, x_lengths, g) output (make_golden.py glow_spk), both utterances (speakers 2
+    and 0) in ONE batched call: durations / path exact, means and mel <= 1e-4."""
+    _dev()
+    fx = load_fixture("glow_spk")
+    m, _ = _glow_spk_model(fx)
+    ids = [fx["u0_ids"], fx["u1_ids"]]
+    T = max(len(x) for x in ids)
+    batch = np.zeros((2, T), np.int64)
+    for i, x in enumerate(ids):
+        batch[i, :len(x)] = x
+    Ty = max(int(fx["u0_ylen"]), int(fx["u1_ylen"]))
+    noise = np.zeros((2, 80, Ty), np.float32)
+    for i in range(2):
+        nz = fx[f"u{i}_noise"]
+        noise[i, :, :nz.shape[1]] = nz
+    g = torch.tensor([int(fx["u0_spk"]), int(fx["u1_spk"])])
+    y, _, y_mean, _, attn, logw, _ = m.inference(torch.from_numpy(batch).cuda(), [len(x) for x in ids], g=g,
+                                                 noise=torch.from_numpy(noise).cuda())
+    y, y_mean, attn, logw = y.cpu().numpy(), y_mean.cpu().numpy(), attn.cpu().numpy(), logw.cpu().numpy()
+    for i in range(2):
+        k = f"u{i}"
+        ty, tx = int(fx[k + "_ylen"]), len(ids[i])
+        assert m.last_y_lengths[i] == ty
+        assert np.abs(logw[i, 0, :tx] - fx[k + "_logw"]).max() <= 1e-5
+        assert np.array_equal(attn[i, :ty, :tx], fx[k + "_attn"])
+        assert np.abs(y_mean[i, :, :ty] - fx[k + "_ymean"]).max() <= MEL_TOL
+        ref = fx[k + "_y"]
+        assert np.abs(y[i, :, :ref.shape[1]] - ref).max() <= MEL_TOL
+
+
+def test_glow_multispeaker_all_speakers_vs_oracle():
+    """One utterance under every speaker of the table in one batch (g = 0..3) against the oracle;
+    the speakers give different outputs (the conditioning reaches the flows), and misuse raises as
+    the reference does (g on a single-speaker model, no g on a c_in > 0 model, id out of range)."""
+    from oracle.glow_np import GlowOracle
+    from tts_amd import GlowTts
+    _dev()
+    fx = load_fixture("glow_spk")
+    m, sd = _glow_spk_model(fx)
+    orc = GlowOracle(sd)
+    ids = fx["u1_ids"]
+    outs = [orc.inference(ids, None, 0.0, 1.0, spk=s) for s in range(4)]
+    Ty = max(o[4] for o in outs)
+    m.noise_scale = 0.0
+    x = torch.from_numpy(np.repeat(ids[None], 4, 0)).cuda()
+    y, _, ym, _, attn, logw, _ = m.inference(x, [len(ids)] * 4, g=torch.arange(4))
+    y, attn = y.cpu().numpy(), attn.cpu().numpy()
+    for s, (y_ref, ym_ref, attn_ref, logw_ref, ty) in enumerate(outs):
+        assert int(m.last_y_lengths[s]) == ty
+        assert np.array_equal(attn[s, :ty], attn_ref)
+        assert np.abs(y[s, :, :y_ref.shape[1]] - y_ref).max() <= MEL_TOL
+    assert np.abs(outs[0][0][:, :8] - outs[1][0][:, :8]).max() > 1e-2
+    with pytest.raises(RuntimeError):
+        m.inference(x[:1], [len(ids)])
+    with pytest.raises(IndexError):
+        m.inference(x[:1], [len(ids)], g=torch.tensor([4]))
+    single = GlowTts(num_chars=m.num_chars).cuda().eval()
+    with pytest.raises(AttributeError):
+        single.inference(x[:1], [len(ids)], g=torch.tensor([0]))
+
+
 # --------------------------------------------------------------------------------- ParallelWaveGAN
 def test_pwgan_matches_reference():
     """ParallelWaveganGenerator.inference with the reference's own prior noise, both fixture mels in

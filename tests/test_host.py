@@ -191,11 +191,40 @@ def test_glow_tts_constructor_and_keys():
     assert tuple(sd["decoder.flows.1.weight"].shape) == (4, 4)
     assert m.noise_scale == 0.66 and m.length_scale == 1.
     for kw in (dict(encoder_type="transformer", rel_attn_window_size=4, use_encoder_prenet=True),
-               dict(encoder_type="transformer"), dict(num_speakers=4, c_in_channels=256), dict(mean_only=False)):
+               dict(encoder_type="transformer"), dict(mean_only=False)):
         with pytest.raises(NotImplementedError):
             GlowTts(num_chars=130, **kw)
     with pytest.raises(RuntimeError, match="no CPU fallback"):
         m.inference(torch.ones(1, 5, dtype=torch.long), [5])
+
+
+def test_glow_tts_multispeaker_keys_and_misuse():
+    """Multi-speaker GlowTts (glow_tts.py:97-99, encoder.py:112-114, glow.py:87-91): emb_g, the
+    duration predictor's hidden + c_in inputs, one weight-normed cond_layer per coupling block, in
+    the reference's key order (pinned against the reference module by make_golden.py glow_spk); g
+    misuse fails before any GPU work, with the reference's exception types."""
+    from tts_amd import GlowTts
+    m = GlowTts(num_chars=130, num_speakers=4, c_in_channels=36)
+    sd = m.state_dict()
+    keys = list(sd)
+    assert keys[-1] == "emb_g.weight" and tuple(sd["emb_g.weight"].shape) == (4, 36)
+    assert tuple(sd["encoder.duration_predictor.conv_1.weight"].shape) == (256, 192 + 36, 3)
+    assert tuple(sd["decoder.flows.2.wn.cond_layer.weight_v"].shape) == (2 * 192 * 4, 36, 1)
+    assert keys.index("decoder.flows.2.wn.cond_layer.bias") == keys.index("decoder.flows.2.wn.res_skip_layers.3.weight_v") + 1
+    assert sum(k.endswith("cond_layer.weight_g") for k in keys) == 12
+    x = torch.ones(1, 5, dtype=torch.long)
+    with pytest.raises(RuntimeError, match="pass g"):
+        m.inference(x, [5])
+    with pytest.raises(IndexError):
+        m.inference(x, [5], g=torch.tensor([4]))
+    with pytest.raises(AttributeError, match="emb_g"):
+        GlowTts(num_chars=130).inference(x, [5], g=torch.tensor([0]))
+    # setup_model's multi-speaker call (num_speakers > 1, c_in_channels = 0): an empty emb_g, and g
+    # cannot reach a cond_layer
+    m0 = GlowTts(num_chars=130, num_speakers=4)
+    assert tuple(m0.state_dict()["emb_g.weight"].shape) == (4, 0)
+    with pytest.raises(AttributeError, match="cond_layer"):
+        m0.inference(x, [5], g=torch.tensor([0]))
 
 
 def test_pwgan_keys_match_reference_and_factory():

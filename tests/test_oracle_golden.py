@@ -175,20 +175,24 @@ def test_tacotron2_oracle_decoder_variants_match_reference(name):
 
 
 @pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable"),
-                                      ("glow_tfm", "transformer")])
+                                      ("glow_tfm", "transformer"), ("glow_spk", "gatedconv")])
 def test_glow_oracle_matches_reference(name, enc):
-    """Glow-TTS, both encoders the reference configs use (gated conv; time-depth-separable with the
-    ConvLayerNorm prenet): the reference's Encoder / Decoder modules under the inference glue of
-    glow_tts.py:166-193 (make_golden.py glow / glow_tdsep); fixed prior noise."""
+    """Glow-TTS, every encoder the reference configs use (gated conv; time-depth-separable and
+    transformer with the ConvLayerNorm prenet) and the multi-speaker model (glow_spk: emb_g of 4
+    speakers, c_in 36, g given): the reference's own GlowTts.inference (glow_tts.py:159-185, make_golden.py
+    glow / glow_tdsep / glow_tfm / glow_spk); fixed prior noise."""
     from oracle.glow_np import GlowOracle
     from tts_amd.spec import GlowConfig, glow_spec
     from tts_amd.weights import synth_state_dict
     fx = load_fixture(name)
-    orc = GlowOracle(synth_state_dict(glow_spec(GlowConfig(encoder_type=enc)), int(fx["seed"])), encoder_type=enc,
+    cfg = GlowConfig(encoder_type=enc, num_speakers=int(fx["num_speakers"]) if "num_speakers" in fx else 0,
+                     c_in_channels=int(fx["c_in"]) if "c_in" in fx else 0)
+    orc = GlowOracle(synth_state_dict(glow_spec(cfg), int(fx["seed"])), encoder_type=enc,
                      enc_layers=6 if enc == "transformer" else 9)
     for u in range(2):
         k = f"u{u}"
-        y, ym, attn, logw, Ty = orc.inference(fx[k + "_ids"], fx[k + "_noise"], float(fx["noise_scale"]))
+        spk = int(fx[k + "_spk"]) if k + "_spk" in fx else None
+        y, ym, attn, logw, Ty = orc.inference(fx[k + "_ids"], fx[k + "_noise"], float(fx["noise_scale"]), spk=spk)
         assert Ty == int(fx[k + "_ylen"])
         assert np.abs(logw - fx[k + "_logw"]).max() <= 1e-5
         assert np.array_equal(attn, fx[k + "_attn"])

@@ -65,6 +65,8 @@ SIGNATURES = [
     ("tts_glow_finalize", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_glow_encode", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_float, _c_int_p,
                                        _vp]),
+    ("tts_glow_encode_spk", ctypes.c_int, [_vp, _vp, _c_int_p, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_float,
+                                           _c_int_p, _vp]),
     ("tts_glow_decode", ctypes.c_int, [_vp, _vp, ctypes.c_float, ctypes.c_int, _vp, _vp, _vp, _vp, _vp]),
     ("tts_time_decoder_kernel", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_f_p]),
     ("tts_decoder_stats", ctypes.c_int, [_vp, _c_i_p, _c_i_p, _c_f_p, _c_i_p]),
@@ -226,12 +228,19 @@ class Engine:
             self._set(self.lib.tts_glow_set_tensor, k, v)
         _check(self.lib.tts_glow_finalize(self.h, num_chars, enc_layers, flows, wn_layers))
 
-    def glow_encode(self, ids, lens, length_scale):
+    def glow_encode(self, ids, lens, length_scale, speaker_ids=None):
         B, T = ids.shape
         lens_a, lens_p = _i32(lens)
         ylens = np.zeros(B, np.int32)
-        _check(self.lib.tts_glow_encode(self.h, _ptr(ids), lens_p, B, T, float(length_scale),
-                                        ylens.ctypes.data_as(_c_int_p), _stream(ids.device)))
+        if speaker_ids is None:
+            _check(self.lib.tts_glow_encode(self.h, _ptr(ids), lens_p, B, T, float(length_scale),
+                                            ylens.ctypes.data_as(_c_int_p), _stream(ids.device)))
+        else:
+            spk_a, spk_p = _i32(speaker_ids)
+            if len(spk_a) != B:
+                raise ValueError("one speaker id per utterance")
+            _check(self.lib.tts_glow_encode_spk(self.h, _ptr(ids), lens_p, spk_p, B, T, float(length_scale),
+                                                ylens.ctypes.data_as(_c_int_p), _stream(ids.device)))
         return ylens
 
     def glow_decode(self, noise, noise_scale, Ty, y, y_mean, attn, logw):

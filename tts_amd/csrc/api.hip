@@ -51,6 +51,7 @@ void pack_pw_layer_x3(const std::vector<float>& m1, const std::vector<float>& m2
 void launch_pw_out(const float* skip, float scale, const float* W3, const float* b3, const float* w4,
                    const float* b4, const int* lens, int len_add, int hop, int Tmax, float* out, int B,
                    hipStream_t st);
+void launch_glow_speaker(const int* spk, const float* table, int c_in, int c_pad, float* g, int B, hipStream_t s);
 void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
                        int B, hipStream_t s);
 bool launch_lstm768_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
@@ -217,6 +218,7 @@ struct ConvCall {
   long rb = 0;
   int rc = 0, rt = 0, resid_rows = 0;
   const float* aux = nullptr;
+  long auxb = 0;              // epi 3: batch stride of the per-utterance gate bias in aux
   int max_q = 0, B = 0;
   unsigned* oflow = nullptr;  // set: run the split-f16 kernel where the layer has split weights
   int merged_u = 0;           // phase-merged ConvTranspose (layer from pack_conv_x3_only)
@@ -256,6 +258,7 @@ void run_conv(const ConvLayer& L, const ConvCall& c, hipStream_t st) {
   a.rt = c.rt;
   a.resid_rows = c.resid_rows;
   a.aux = c.aux;
+  a.auxb = c.auxb;
   a.max_q = c.max_q;
   a.B = c.B;
   a.merged_u = c.merged_u;
@@ -400,7 +403,7 @@ struct Ge2eWS {
 };
 
 // Glow-TTS (TTS/tts/models/glow_tts.py, the reference configs' gated-conv encoder, mean_only,
-// num_sqz 2, num_splits 4, dilation 1, no speaker conditioning)
+// num_sqz 2, num_splits 4, dilation 1; optional speaker conditioning)
 struct GlowModel {
   bool ready = false;
   int num_chars = 0, H = 192, Fdp = 256, C = 80, enc_layers = 9, flows = 12, wn_layers = 4;
@@ -425,12 +428,22 @@ struct GlowModel {
   std::vector<ConvLayer> start, end;
   std::vector<DevBuf> invtab;
   std::vector<ConvLayer> wn_in, wn_rs;  // [block * wn_layers + i]
+  // speaker conditioning (glow_tts.py:97-99,159-161; encoder.py:131-135; glow.py:87-91,119-130):
+  // c_in channels of g padded to c_pad (multiple of 16); the duration predictor's conv_1 reads
+  // [x; g] (g broadcast over time by a time stride of 0); every block's cond_layer stacked into one
+  // 1x1 conv (c_pad -> flows * wn_layers * 2H, rows interleaved like wn_in) whose output is the
+  // per-utterance gate bias of each WN in-layer
+  int c_in = 0, c_pad = 0, n_spk = 0;
+  DevBuf emb_g;
+  ConvLayer cond;
 };
 
 struct GlowWS {
   int B = 0, Tx = 0, Ty = 0;
   DevBuf ids, lens, klens, ylens, xa, xb, h2, hdp, logw, cum, wceil, om, z, sq, sq2, whs, wacts, big;
-  std::vector<int> h_ylens, h_klens;
+  DevBuf spk, ones, g, gcond;  // speaker ids, unit lengths, normalized g (B, c_pad), cond biases
+  bool has_g = false;          // the last glow_encode was given speaker ids
+  std::vector<int> h_ylens, h_klens, h_spk;
 };
 
 // ParallelWaveGAN generator (TTS/vocoder/models/parallel_wavegan_generator.py, setup_generator's
@@ -2339,7 +2352,32 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
   pack_conv(G.proj_m, need(h, "encoder.proj_m.weight", {C, H, 1}).d, need(h, "encoder.proj_m.bias", {C}).d, H, C, 1, 1,
             1, p0);
   const std::string dp = "encoder.duration_predictor.";
-  pack_conv(G.dp1, need(h, dp + "conv_1.weight", {F, H, 3}).d, need(h, dp + "conv_1.bias", {F}).d, H, F, 3, 1, 1, p1);
+  {
+    auto it = h.find(dp + "conv_1.weight");
+    TTS_CHECK(it != h.end() && it->second.shape.size() == 3, "missing tensor: " + dp + "conv_1.weight");
+    G.c_in = (int)it->second.shape[1] - H;
+    TTS_CHECK(G.c_in >= 0 && G.c_in <= 4096, "glow: duration predictor input channels");
+  }
+  const int cin = G.c_in, cpad = (cin + 15) / 16 * 16;
+  G.c_pad = cpad;
+  {
+    // [x; g] input of conv_1, g's channels zero-padded to c_pad
+    const auto& w = need(h, dp + "conv_1.weight", {F, H + cin, 3}).d;
+    std::vector<float> wp((size_t)F * (H + cpad) * 3, 0.f);
+    for (int o = 0; o < F; ++o)
+      std::copy(w.begin() + (size_t)o * (H + cin) * 3, w.begin() + (size_t)(o + 1) * (H + cin) * 3,
+                wp.begin() + (size_t)o * (H + cpad) * 3);
+    pack_conv(G.dp1, wp, need(h, dp + "conv_1.bias", {F}).d, H + cpad, F, 3, 1, 1, p1);
+  }
+  G.n_spk = 0;
+  G.emb_g.reset();
+  if (h.count("emb_g.weight")) {
+    auto it = h.find("emb_g.weight");
+    TTS_CHECK(it->second.shape.size() == 2 && it->second.shape[1] == cin && it->second.shape[0] >= 1,
+              "glow: emb_g.weight must be (num_speakers, c_in_channels)");
+    G.n_spk = (int)it->second.shape[0];
+    if (cin > 0) G.emb_g.upload(it->second.d);
+  }
   pack_conv(G.dp2, need(h, dp + "conv_2.weight", {F, F, 3}).d, need(h, dp + "conv_2.bias", {F}).d, F, F, 3, 1, 1, p1);
   pack_conv(G.dp_proj, need(h, dp + "proj.weight", {1, F, 1}).d, need(h, dp + "proj.bias", {1}).d, F, 1, 1, 1, 1, p0);
   G.dp_g1.upload(need(h, dp + "norm_1.gamma", {1, F, 1}).d);
@@ -2356,6 +2394,8 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
   G.wn_in.resize(flows * wn_layers);
   G.wn_rs.clear();
   G.wn_rs.resize(flows * wn_layers);
+  std::vector<float> cond_w(cin > 0 ? (size_t)flows * wn_layers * 2 * H * cpad : 0, 0.f);
+  std::vector<float> cond_b(cin > 0 ? (size_t)flows * wn_layers * 2 * H : 0, 0.f);
   for (int k = 0; k < flows; ++k) {
     const std::string an = "decoder.flows." + std::to_string(3 * k) + ".";
     const std::string ic = "decoder.flows." + std::to_string(3 * k + 1) + ".";
@@ -2375,6 +2415,22 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
       const int rsc = i == wn_layers - 1 ? H : 2 * H;
       pack_conv(G.wn_rs[k * wn_layers + i], wn_weight(h, wr, {rsc, H, 1}), need(h, wr + ".bias", {rsc}).d, H, rsc, 1,
                 1, 1, p0);
+    }
+    if (cin > 0) {  // cond_layer (2H * wn_layers, c_in): per layer slice interleaved like wn_in
+      const int L2 = 2 * H * wn_layers;
+      const auto w = wn_weight(h, cp + "wn.cond_layer", {L2, cin, 1});
+      const auto& cb = need(h, cp + "wn.cond_layer.bias", {L2}).d;
+      for (int i = 0; i < wn_layers; ++i) {
+        std::vector<float> wl(w.begin() + (size_t)i * 2 * H * cin, w.begin() + (size_t)(i + 1) * 2 * H * cin);
+        std::vector<float> bl(cb.begin() + (size_t)i * 2 * H, cb.begin() + (size_t)(i + 1) * 2 * H);
+        auto [wi, bi] = interleave_halves(wl, bl, H, cin);
+        const size_t r0 = ((size_t)k * wn_layers + i) * 2 * H;
+        for (int r = 0; r < 2 * H; ++r) {
+          std::copy(wi.begin() + (size_t)r * cin, wi.begin() + (size_t)(r + 1) * cin,
+                    cond_w.begin() + (r0 + r) * cpad);
+          cond_b[r0 + r] = bi[r];
+        }
+      }
     }
     // reverse of [ActNorm, InvConvNear] (glow.py:48-58, 184-201): output channel c' = i*C + 2j + k
     // (split s' = 2i + k) = (sum_s winv[s'][s] x[c_s] - bias[c']) * exp(-logs[c']), c_s = i_s*C + 2j + k_s
@@ -2408,18 +2464,30 @@ void glow_finalize(tts_ctx* c, int num_chars, int enc_layers, int flows, int wn_
     }
     G.invtab[k].upload(tab);
   }
+  if (cin > 0) pack_conv(G.cond, cond_w, cond_b, cpad, flows * wn_layers * 2 * H, 1, 1, 1, p0);
   HIP_OK(hipDeviceSynchronize());
   G.ready = true;
 }
 
 // encoder + duration predictor + durations: h_ylens out (per-utterance frames)
-void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T, float length_scale,
-                 int32_t* h_ylens) {
+void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, const int32_t* h_spk, int B, int T,
+                 float length_scale, int32_t* h_ylens) {
   auto& G = c->glow;
   auto& W = c->glws;
   TTS_CHECK(G.ready, "glow weights not finalized");
   TTS_CHECK(B >= 1 && B <= 64 && T >= 1 && T <= 4096, "glow: bad sizes");
   for (int b = 0; b < B; ++b) TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= T, "glow: lens out of range");
+  if (h_spk) {
+    // the reference looks g up in emb_g (absent unless num_speakers > 1) and feeds it to every WN
+    // cond_layer (absent unless c_in_channels > 0): glow_tts.py:160, glow.py:119-120
+    TTS_CHECK(G.n_spk > 1, "glow: speaker ids given but the model has no emb_g (num_speakers <= 1)");
+    TTS_CHECK(G.c_in > 0, "glow: speaker ids given but the model has no cond_layer (c_in_channels = 0)");
+    for (int b = 0; b < B; ++b) TTS_CHECK(h_spk[b] >= 0 && h_spk[b] < G.n_spk, "glow: speaker id out of range");
+  } else {
+    // without g the reference's duration predictor reads x alone (encoder.py:136), which its
+    // conv_1 rejects when it was built for hidden + c_in_channels inputs
+    TTS_CHECK(G.c_in == 0, "glow: this model's duration predictor expects speaker conditioning (c_in_channels > 0)");
+  }
   hipStream_t s = c->s;
   const int H = G.H, C = G.C, F = G.Fdp;
   long gen = 0;
@@ -2437,9 +2505,36 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
   if (G.tfm) grow<float>(W.big, (size_t)B * 768 * T, gen);
   W.B = B;
   W.Tx = T;
+  W.has_g = h_spk != nullptr;
   std::vector<int> lens(h_lens, h_lens + B);
   HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
   const int* dl = W.lens.i();
+  if (W.has_g) {
+    // g, then every WN layer's gate bias cond_layer(g) as one (B, flows * wn_layers * 2H) 1x1 conv
+    // over a length-1 sequence
+    const int NC = G.flows * G.wn_layers * 2 * H;
+    grow<int>(W.spk, 64, gen);
+    grow<float>(W.g, (size_t)B * G.c_pad, gen);
+    grow<float>(W.gcond, (size_t)B * NC, gen);
+    if (!W.ones.p) {
+      std::vector<int> one(64, 1);
+      W.ones.upload(one);
+    }
+    W.h_spk.assign(h_spk, h_spk + B);
+    HIP_OK(hipMemcpyAsync(W.spk.p, W.h_spk.data(), B * 4, hipMemcpyHostToDevice, s));
+    launch_glow_speaker(W.spk.i(), G.emb_g.f(), G.c_in, G.c_pad, W.g.f(), B, s);
+    ConvCall cc;
+    cc.lens = W.ones.i();
+    cc.B = B;
+    cc.oflow = x3_flag(c);
+    cc.max_q = 1;
+    cc.s[0] = src_of(W.g.f(), G.c_pad, 1, 1, G.c_pad, 0);
+    cc.out = W.gcond.f();
+    cc.ob = NC;
+    cc.oc = 1;
+    cc.ot = 1;
+    run_conv(G.cond, cc, s);
+  }
   float* x = W.xa.f();   // (B, H, T) current activations
   float* x2 = W.xb.f();  // ping-pong
   launch_glow_embed(d_ids, T, G.emb.f(), G.num_chars, H, dl, x, B, s);
@@ -2500,8 +2595,25 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B,
     std::swap(x, x2);
   }
   conv(G.proj_m, x, H, W.om.f(), C, 0);  // o_mean (encoder.py:125)
-  // DurationPredictor (duration_predictor.py:29-40): conv -> relu -> LN, twice, then proj
-  conv(G.dp1, x, H, W.hdp.f(), F, 1);
+  // DurationPredictor (duration_predictor.py:29-40): conv -> relu -> LN, twice, then proj; the
+  // input is [x; g] with g constant over time (encoder.py:131-135), masked like x by the conv
+  if (G.c_pad > 0) {
+    ConvCall cc;
+    cc.lens = dl;
+    cc.B = B;
+    cc.max_q = T;
+    cc.nsrc = 2;
+    cc.s[0] = src_of(x, (long)H * T, T, 1, H, 0);
+    cc.s[1] = src_of(W.g.f(), G.c_pad, 1, 0, G.c_pad, 0);
+    cc.out = W.hdp.f();
+    cc.ob = (long)F * T;
+    cc.oc = T;
+    cc.ot = 1;
+    cc.epi = 1;
+    run_conv(G.dp1, cc, s);
+  } else {
+    conv(G.dp1, x, H, W.hdp.f(), F, 1);
+  }
   launch_ln(W.hdp.f(), (long)F * T, F, G.dp_g1.f(), G.dp_b1.f(), dl, B, T, s);
   conv(G.dp2, W.hdp.f(), F, W.h2.f(), F, 1);
   launch_ln(W.h2.f(), (long)F * T, F, G.dp_g2.f(), G.dp_b2.f(), dl, B, T, s);
@@ -2563,6 +2675,7 @@ void glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, fl
     cc.epi = epi;
     cc.resid_rows = resid_rows;
     cc.aux = aux;
+    cc.auxb = (long)G.flows * G.wn_layers * 2 * H;  // epi 3: gcond's batch stride
     run_conv(L, cc, s);
   };
   float* x = W.sq.f();
@@ -2572,9 +2685,10 @@ void glow_decode(tts_ctx* c, const float* d_noise, float noise_scale, int Ty, fl
   for (int k = G.flows - 1; k >= 0; --k) {
     // CouplingBlock reverse (glow.py:245-262): WN over start(x0), then z1 = (x1 - m) exp(-logs)
     conv(G.start[k], x, C2, hid, 2 * H, nullptr, 0);
-    for (int i = 0; i < G.wn_layers; ++i) {  // WN (glow.py:118-138), g = None
+    for (int i = 0; i < G.wn_layers; ++i) {  // WN (glow.py:118-138)
       const int li = k * G.wn_layers + i;
-      conv(G.wn_in[li], hid, 2 * H, W.wacts.f(), H, nullptr, 3);  // gate fused
+      // gate fused; with g, cond_layer(g)'s slice for this layer is a per-utterance gate bias
+      conv(G.wn_in[li], hid, 2 * H, W.wacts.f(), H, nullptr, 3, 0, W.has_g ? W.gcond.f() + (size_t)li * 2 * H : nullptr);
       // skip rows start at the first layer's output (no accumulate), hidden rows add the residual
       if (i < G.wn_layers - 1) conv(G.wn_rs[li], W.wacts.f(), H, hid, 2 * H, hid, 0, i == 0 ? H : 0);
       else conv(G.wn_rs[li], W.wacts.f(), H, skip, 2 * H, i == 0 ? nullptr : skip, 0);
@@ -3014,7 +3128,18 @@ int tts_glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int
     TTS_CHECK(c && d_ids && h_lens && h_ylens, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
-    with_x3_fallback(c, [&] { glow_encode(c, d_ids, h_lens, B, T_max, length_scale, h_ylens); });
+    with_x3_fallback(c, [&] { glow_encode(c, d_ids, h_lens, nullptr, B, T_max, length_scale, h_ylens); });
+    leave(c, stream);
+  });
+}
+
+int tts_glow_encode_spk(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, const int32_t* h_speaker_ids, int B,
+                        int T_max, float length_scale, int32_t* h_ylens, void* stream) {
+  return guarded_ctx(c, [&] {
+    TTS_CHECK(c && d_ids && h_lens && h_ylens, "null argument");
+    DeviceGuard g(c->device);
+    enter(c, stream);
+    with_x3_fallback(c, [&] { glow_encode(c, d_ids, h_lens, h_speaker_ids, B, T_max, length_scale, h_ylens); });
     leave(c, stream);
   });
 }

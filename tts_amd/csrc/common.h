@@ -121,7 +121,9 @@ struct ConvArgs {
   long rb;
   int rc, rt;
   int resid_rows;     // > 0: the residual applies to output rows < resid_rows only
-  const float* aux;   // epi 5: per output channel {w[4], actnorm bias, exp(-logs)}
+  const float* aux;   // epi 5: per output channel {w[4], actnorm bias, exp(-logs)}; epi 3 (optional):
+                      // per-utterance gate bias aux[b * auxb + co] (Glow WN speaker conditioning)
+  long auxb;
   int max_q;          // max over batch of output positions per phase (grid x extent)
   int B;
   // split-f16 variant (conv_x3.hip): pre-split A fragments [co16][k-step][64][hi 8 | lo 8] per

@@ -79,7 +79,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& a, f32x4 (&acc)[MI
           const int co = co0 + wm * 16 * MI + mi * 16 + g4 + j;
           if (co >= a.Cout) continue;
           const int c = co >> 1;
-          const float u = acc[mi][ni][j] + bias4[j], g = acc[mi][ni][j + 1] + bias4[j + 1];
+          float u = acc[mi][ni][j] + bias4[j], g = acc[mi][ni][j + 1] + bias4[j + 1];
+          if (a.epi_act == 3 && a.aux) {  // glow.py:125-131: x_in + g_l before the gate
+            u += a.aux[(long)b * a.auxb + co];
+            g += a.aux[(long)b * a.auxb + co + 1];
+          }
           float v;
           if (a.epi_act == 3) v = tanhf(u) / (1.f + expf(-g));
           else if (a.epi_act == 6) v = u / (1.f + expf(-g));  // GLU

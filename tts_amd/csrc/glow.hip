@@ -227,6 +227,26 @@ void launch_glow_unsqueeze(const float* x, int C2, int K, const int* ylens, floa
   glow_unsqueeze_kernel<<<dim3((K + 63) / 64, B), 256, 0, s>>>(x, C2, K, ylens, y, T);
   HIP_OK(hipGetLastError());
 }
+// g = F.normalize(emb_g(speaker)) (glow_tts.py:159-161): x / max(||x||_2, 1e-12), one workgroup per
+// utterance, written as (B, c_pad) with zeros in the padding channels [c_in, c_pad)
+__global__ __launch_bounds__(256) void glow_speaker_kernel(const int* __restrict__ spk, const float* __restrict__ table,
+                                                           int c_in, int c_pad, float* __restrict__ g) {
+  __shared__ float part[4];
+  const int b = blockIdx.x, tid = threadIdx.x;
+  const float* row = table + (long)spk[b] * c_in;
+  float ss = 0.f;
+  for (int j = tid; j < c_in; j += 256) ss = fmaf(row[j], row[j], ss);
+  for (int o = 32; o > 0; o >>= 1) ss += __shfl_xor(ss, o);
+  if ((tid & 63) == 0) part[tid >> 6] = ss;
+  __syncthreads();
+  const float n = fmaxf(sqrtf(part[0] + part[1] + part[2] + part[3]), 1e-12f);
+  for (int j = tid; j < c_pad; j += 256) g[(long)b * c_pad + j] = j < c_in ? row[j] / n : 0.f;
+}
+void launch_glow_speaker(const int* spk, const float* table, int c_in, int c_pad, float* g, int B, hipStream_t s) {
+  glow_speaker_kernel<<<B, 256, 0, s>>>(spk, table, c_in, c_pad, g);
+  HIP_OK(hipGetLastError());
+}
+
 // encoder.py:107: emb(x) * sqrt(hidden) (the scale is folded into the table), channel-major out
 __global__ __launch_bounds__(256) void glow_embed_kernel(const int64_t* __restrict__ ids, int T, const float* table,
                                                          int rows, int D, const int* lens, float* __restrict__ out) {

@@ -9,6 +9,14 @@ num_splits 4, mean_only): the constructor signature, the checkpoint keys (``enco
 ``inference(x, x_lengths, g=None)`` returning ``(y, logdet, y_mean, y_log_scale, attn, o_dur_log,
 o_attn_dur)`` (``:166-193``). Batched rows are independent; row i equals the B = 1 call.
 
+Multi-speaker models (``num_speakers > 1``, ``c_in_channels > 0``, built directly as the reference
+allows; ``setup_model`` itself passes ``c_in_channels=0``) take ``g`` as a (B,) LongTensor of speaker
+ids: ``emb_g`` (``:97-99``), ``g = F.normalize(emb_g(g))`` (``:159-161``), the duration predictor over
+``[x; g]`` (``layers/glow_tts/encoder.py:131-135``) and each WN layer's slice of ``cond_layer(g)``
+added before its gate (``layers/glow_tts/glow.py:119-130``). Misuse fails as the reference does: g
+for a model without ``emb_g`` or ``cond_layer`` raises AttributeError, no g for a model built with
+``c_in_channels > 0`` raises RuntimeError.
+
 The prior sample ``z = y_mean + exp(y_log_scale) * randn * noise_scale`` draws its noise with torch
 on the model's device (``torch.randn_like`` in the reference); pass ``noise=`` to fix it.
 """
@@ -47,14 +55,15 @@ class GlowTts(nn.Module):
             bad.append("non-reference layer sizes")
         if dilation_rate != 1 or num_splits != 4 or num_sqz != 2 or sigmoid_scale or not mean_only:
             bad.append("non-reference flow options")
-        if num_speakers > 1 or c_in_channels:
-            bad.append("speaker conditioning")
+        if c_in_channels < 0:
+            bad.append("c_in_channels < 0")
         if bad:
             raise NotImplementedError("tts_amd GlowTts implements the reference configs only: " + ", ".join(bad))
         self.num_chars = num_chars
         self.cfg = GlowConfig(num_chars=num_chars, num_layers_enc=num_layers_enc,
                               num_flow_blocks_dec=num_flow_blocks_dec, num_block_layers=num_block_layers,
-                              encoder_type=encoder_type.lower())
+                              encoder_type=encoder_type.lower(), num_speakers=num_speakers,
+                              c_in_channels=c_in_channels)
         self.noise_scale = 0.66
         self.length_scale = 1.
         populate(self, glow_spec(self.cfg))
@@ -91,8 +100,18 @@ class GlowTts(nn.Module):
 
     @torch.no_grad()
     def inference(self, x, x_lengths, g=None, noise: Optional[torch.Tensor] = None):
+        spk = None
         if g is not None:
-            raise NotImplementedError("speaker conditioning (g) is not implemented")
+            if self.cfg.num_speakers <= 1:
+                raise AttributeError("'GlowTts' object has no attribute 'emb_g'")
+            if not self.cfg.c_in_channels:
+                raise AttributeError("'WN' object has no attribute 'cond_layer'")
+            spk = np.asarray(torch.as_tensor(g).cpu(), np.int64).reshape(-1)
+            if spk.min() < 0 or spk.max() >= self.cfg.num_speakers:
+                raise IndexError("index out of range in self")  # nn.Embedding's message
+        elif self.cfg.c_in_channels:
+            raise RuntimeError(f"the duration predictor expects {192 + self.cfg.c_in_channels} input channels "
+                               "(c_in_channels > 0): pass g")
         dev = self.encoder.emb.weight.device
         eng = get_engine(dev)
         with eng.lock:  # encode and decode share the context's Glow workspace
@@ -107,7 +126,9 @@ class GlowTts(nn.Module):
                 raise ValueError("x_lengths must have B entries in [1, T]")
             if B > 64:
                 raise ValueError("at most 64 utterances per call")
-            ylens = eng.glow_encode(x, lens, float(self.length_scale))
+            if spk is not None and len(spk) != B:
+                raise ValueError("g must hold one speaker id per utterance")
+            ylens = eng.glow_encode(x, lens, float(self.length_scale), spk)
             Ty = int(ylens.max())
             if noise is None:
                 noise = torch.randn(B, 80, Ty, device=dev)

@@ -299,6 +299,11 @@ class GlowConfig:
     num_flow_blocks_dec: int = 12
     num_block_layers: int = 4
     kernel_size_dec: int = 5
+    # speaker conditioning (glow_tts.py:97-99, encoder.py:112-114,131-135, glow.py:87-91,119-130):
+    # emb_g (num_speakers, c_in) when num_speakers > 1; c_in extra duration-predictor input channels
+    # and a weight-normed cond_layer (c_in -> 2 H L) per coupling block when c_in > 0
+    num_speakers: int = 0
+    c_in_channels: int = 0
 
 
 def glow_spec(c: GlowConfig) -> Spec:
@@ -357,7 +362,7 @@ def glow_spec(c: GlowConfig) -> Spec:
                   (f"encoder.encoder.norm_layers.{i}.beta", (1, 2 * H, 1), "bias")]
     dp = "encoder.duration_predictor"
     s += [("encoder.proj_m.weight", (C, H, 1), "conv"), ("encoder.proj_m.bias", (C,), "bias"),
-          (f"{dp}.conv_1.weight", (F, H, 3), "conv"), (f"{dp}.conv_1.bias", (F,), "bias"),
+          (f"{dp}.conv_1.weight", (F, H + c.c_in_channels, 3), "conv"), (f"{dp}.conv_1.bias", (F,), "bias"),
           (f"{dp}.norm_1.gamma", (1, F, 1), "ln_g"), (f"{dp}.norm_1.beta", (1, F, 1), "bias"),
           (f"{dp}.conv_2.weight", (F, F, 3), "conv"), (f"{dp}.conv_2.bias", (F,), "bias"),
           (f"{dp}.norm_2.gamma", (1, F, 1), "ln_g"), (f"{dp}.norm_2.beta", (1, F, 1), "bias"),
@@ -380,6 +385,12 @@ def glow_spec(c: GlowConfig) -> Spec:
             s += [(f"{f}.wn.res_skip_layers.{i}.bias", (rs,), "bias"),
                   (f"{f}.wn.res_skip_layers.{i}.weight_g", (rs, 1, 1), "wn_g"),
                   (f"{f}.wn.res_skip_layers.{i}.weight_v", (rs, H, 1), "conv")]
+        if c.c_in_channels:
+            L2 = 2 * H * c.num_block_layers
+            s += [(f"{f}.wn.cond_layer.bias", (L2,), "bias"), (f"{f}.wn.cond_layer.weight_g", (L2, 1, 1), "wn_g"),
+                  (f"{f}.wn.cond_layer.weight_v", (L2, c.c_in_channels, 1), "conv")]
+    if c.num_speakers > 1:
+        s.append(("emb_g.weight", (c.num_speakers, c.c_in_channels), "glow_spk"))
     return s
 
 

@@ -90,6 +90,8 @@ def synth_tensor(name: str, shape: Tuple[int, ...], kind: str, seed: int,
         if np.linalg.det(q) < 0:
             q[:, 0] = -q[:, 0]
         x = q.reshape(-1)
+    elif kind == "glow_spk":  # uniform_(-0.1, 0.1) (glow_tts.py:98-99)
+        x = 0.1 * u
     elif kind == "speaker_emb":  # normal_(0, 0.3) in the reference: same std, uniform
         x = u * (0.3 * math.sqrt(3.0))
     elif kind == "bias":
