@@ -1000,6 +1000,25 @@ def test_synthesizer_gpu_pool_vs_oracle_chain(tmp_path):
     assert "pool ok" in r.stdout
 
 
+def test_mbmelgan_fused_convtranspose_bit_identical(tmp_path):
+    """The last upsample's ConvTranspose computed inside the C = 48 ResidualStack kernel
+    (resstack_x3.hip CTU = 2, the default) gives the same waveform bits as its own conv_x3 launch
+    (TTS_CT_FUSE=0), on a ragged batch: the two modes run in child processes (the switch is read
+    once per process) through tools/voc_dump.py."""
+    import subprocess
+    import sys
+    _dev()
+    outs = []
+    for f in ("0", "1"):
+        path = str(tmp_path / f"w{f}.npy")
+        env = dict(os.environ, TTS_CT_FUSE=f)
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "voc_dump.py"), path], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs.append(np.load(path))
+    assert outs[0].shape == outs[1].shape and np.array_equal(outs[0], outs[1])
+
+
 # --------------------------------------------------------------------- GE2E speaker encoder
 @pytest.mark.parametrize("tag,proj", [("proj", True), ("noproj", False)])
 def test_ge2e_speaker_encoder_matches_reference(tag, proj):

@@ -1826,6 +1826,15 @@ static bool stack_fuse_on() {
   }();
   return on;
 }
+// the last upsample's ConvTranspose inside the C = 48 stack kernel (resstack_x3.hip CTU = 2);
+// TTS_CT_FUSE=0 keeps the separate conv_x3 launch
+static bool ct_fuse_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TTS_CT_FUSE");
+    return !e || std::atoi(e) != 0;
+  }();
+  return on;
+}
 
 // returns total upsampling factor; writes bands (B, out_ch, up*(M_max+2pad)) into `out`
 int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int M_max, int pad, float* out,
@@ -1888,8 +1897,54 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   cc.ot = 1;
   run_conv(G.conv_in, cc, s);
   cc.rep_pad = 0;
+  // blocks 0-2 of stage i as one resstack_x3 launch (x: the stage input; with ct, x is the
+  // ConvTranspose input and the kernel computes the stage input per tile): false if not covered
+  auto stack3 = [&](size_t i, int Cs, long Lss, int muls, const float* xs, float* ys, const ConvLayer* ct,
+                    const float* xin, int Cin, long Lin) {
+    if (!(cc.oflow && G.nres >= 3 && stack_fuse_on() && G.rb_wd16[i * G.nres].p)) return false;
+    int dil[3];
+    for (int k = 0; k < 3; ++k) dil[k] = G.dconv[i * G.nres + k].dil;
+    if (!resstack_x3_supported(Cs, dil, 3)) return false;
+    StackArgs sa{};
+    sa.B = B;
+    sa.x = xs;
+    sa.y = ys;
+    sa.sb = (long)Cs * Lss;
+    sa.Ls = (int)Lss;
+    sa.lens = W.lens.i();
+    sa.len_add = 2 * pad;
+    sa.mul = muls;
+    for (int k = 0; k < 3; ++k) {
+      sa.dil[k] = dil[k];
+      sa.wd16[k] = G.rb_wd16[i * G.nres + k].p;
+      sa.wf16[k] = G.rb_wf16[i * G.nres + k].p;
+      sa.bd[k] = G.dconv[i * G.nres + k].bias.f();
+      sa.bf[k] = G.fused[i * G.nres + k].bias.f();
+    }
+    sa.oflow = cc.oflow;
+    if (ct) {
+      sa.xin = xin;
+      sa.sb_in = (long)Cin * Lin;
+      sa.Ls_in = (int)Lin;
+      sa.ct16 = ct->W16.p;
+      sa.ct_bias = ct->bias.f();
+    }
+    if (!resstack_x3_fits(sa, lens.data())) return false;
+    launch_resstack_x3(sa, lens.data(), Cs, s);
+    return true;
+  };
   for (size_t i = 0; i < G.ups.size(); ++i) {
     const int u = G.ups[i];
+    int bk0 = 0;
+    if (u == 2 && C == 96 && ct_fuse_on() && cc.oflow && G.convTm[i].W16.p &&
+        stack3(i, C / 2, Ls * u, mul * u, nullptr, xo, &G.convTm[i], x, C, Ls)) {
+      // LeakyReLU + ConvTranspose1d + blocks 0-2 in one launch (resstack_x3.hip CTU = 2)
+      std::swap(x, xo);
+      C /= 2;
+      Ls *= u;
+      mul *= u;
+      bk0 = 3;
+    }
     // LeakyReLU + ConvTranspose1d as u polyphase 2-tap convs
     ConvCall t = cc;
     t.s[0] = src_of(x, (long)C * Ls, Ls, 1, C, 1);
@@ -1903,46 +1958,23 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     t.ob = (long)Cn * Ln;
     t.oc = Ln;
     t.ot = 1;
-    if (t.oflow && G.convTm[i].W16.p) {  // all u phases as one GEMM over input positions 0 .. L
-      t.out_mul = 1;
-      t.max_q = Lb * mul + 1;
-      t.merged_u = u;
-      run_conv(G.convTm[i], t, s);
-    } else {
-      run_conv(G.convT[i], t, s);
-    }
-    std::swap(x, xo);
-    C = Cn;
-    Ls = Ln;
-    mul *= u;
-    int bk0 = 0;
-    if (cc.oflow && G.nres >= 3 && stack_fuse_on() && G.rb_wd16[i * G.nres].p) {
-      int dil[3];
-      for (int k = 0; k < 3; ++k) dil[k] = G.dconv[i * G.nres + k].dil;
-      if (resstack_x3_supported(C, dil, 3)) {  // blocks 0-2 in one pass over the stage (resstack_x3.hip)
-        StackArgs sa{};
-        sa.B = B;
-        sa.x = x;
-        sa.y = xo;
-        sa.sb = (long)C * Ls;
-        sa.Ls = (int)Ls;
-        sa.lens = W.lens.i();
-        sa.len_add = 2 * pad;
-        sa.mul = mul;
-        sa.B = B;
-        for (int k = 0; k < 3; ++k) {
-          sa.dil[k] = dil[k];
-          sa.wd16[k] = G.rb_wd16[i * G.nres + k].p;
-          sa.wf16[k] = G.rb_wf16[i * G.nres + k].p;
-          sa.bd[k] = G.dconv[i * G.nres + k].bias.f();
-          sa.bf[k] = G.fused[i * G.nres + k].bias.f();
-        }
-        sa.oflow = cc.oflow;
-        if (resstack_x3_fits(sa, lens.data())) {
-          launch_resstack_x3(sa, lens.data(), C, s);
-          std::swap(x, xo);
-          bk0 = 3;
-        }
+    if (bk0 == 0) {
+      if (t.oflow && G.convTm[i].W16.p) {  // all u phases as one GEMM over input positions 0 .. L
+        t.out_mul = 1;
+        t.max_q = Lb * mul + 1;
+        t.merged_u = u;
+        run_conv(G.convTm[i], t, s);
+      } else {
+        run_conv(G.convT[i], t, s);
+      }
+      std::swap(x, xo);
+      C = Cn;
+      Ls = Ln;
+      mul *= u;
+      // blocks 0-2 in one pass over the stage (resstack_x3.hip)
+      if (stack3(i, C, Ls, mul, x, xo, nullptr, nullptr, 0, 0)) {
+        std::swap(x, xo);
+        bk0 = 3;
       }
     }
     for (int bk = bk0; bk < G.nres; ++bk) {  // fused ResidualStack blocks (resblock.hip)

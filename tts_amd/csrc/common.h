@@ -224,6 +224,14 @@ struct StackArgs {
   const float* bd[3];
   const float* bf[3];  // b_1x1 + b_sc
   unsigned* oflow;
+  // fused ConvTranspose (resstack_x3 with CTU = 2, C = 48): x_0 = ConvT(lrelu(xin)) computed per
+  // tile from the 2C-channel input at half the rate (x is then unused); ct16 / ct_bias: the
+  // phase-merged split weights and per-merged-row bias of conv_x3.hip (merged_u = 2)
+  const float* xin;
+  long sb_in;
+  int Ls_in;
+  const void* ct16;
+  const float* ct_bias;
 };
 bool resstack_x3_supported(int C, const int* dil, int n);
 bool resstack_x3_fits(const StackArgs& a, const int* h_lens);

@@ -62,7 +62,7 @@ constexpr int ST_OFF = 16;  // halo rows per side (>= the sum of the fused dilat
 #define RS_MMA(ah, al, bh, bl, am, ac) mfma_x3(ah, al, bh, bl, am, ac)
 #endif
 
-template <int C, int TQ, int WN, int NI>
+template <int C, int TQ, int WN, int NI, int CTU>
 __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackArgs a, int ntiles) {
   constexpr int NB = 3;
   constexpr int WM = C / 16;
@@ -79,11 +79,21 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
   constexpr int XLR = 2 * C + 16;
   constexpr int HR = 4 * C + 16;
   constexpr int NG = C / 8;  // channel octets of a staged row
-  constexpr int SPT = (NG * ROWS + NTHR - 1) / NTHR;
+  // fused ConvTranspose geometry: CIN input channels in CROWS staged rows of CRS halves (stride
+  // 100 dwords: the 16 rows of a ds_read_b128 group on distinct banks); CMT m-tiles of merged rows,
+  // CNT n-tiles of input columns, CKS k-steps (32 channels x 2 taps)
+  constexpr int CIN = 2 * C, NGI = CIN / 8, CROWS = 128, CRS = 2 * CIN + 8;
+  constexpr int CMT = CTU ? C * CTU / 16 : 1, CNT = CROWS / 16, CKS = CIN / 32 * 2;
+  static_assert(CTU == 0 || (C == 48 && CTU == 2 && ROWS / 2 + 2 <= CROWS && CROWS * CRS <= ROWS * (2 * C + 16) &&
+                             WM * WN == 2 * CMT && CNT == 2 * NI),
+                "fused ConvTranspose geometry");
+  constexpr int SPT0 = (NG * ROWS + NTHR - 1) / NTHR, SPT1 = (NGI * CROWS + NTHR - 1) / NTHR;
+  constexpr int SPT = CTU ? SPT1 : SPT0;
   extern __shared__ __attribute__((aligned(16))) _Float16 sh[];
   _Float16* XL = sh;
   _Float16* HX = sh + ROWS * XLR;
   __shared__ float bias[NB][2][C];
+  __shared__ __attribute__((aligned(16))) float bct[CTU ? C * CTU : 4];  // fused ConvTranspose bias per merged row
   __shared__ int tcum[65], tlen[64];
 
   const int tid = threadIdx.x;
@@ -116,6 +126,9 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
     const float* p = w ? pick3(a.bf[0], a.bf[1], a.bf[2], blk) : pick3(a.bd[0], a.bd[1], a.bd[2], blk);
     bias[blk][w][c] = p[c];
   }
+  if constexpr (CTU) {
+    for (int i = tid; i < C * CTU; i += NTHR) bct[i] = a.ct_bias[i];
+  }
   lds_barrier();
   struct Tile {
     int b, q0, L;
@@ -132,14 +145,53 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
   };
 
   // ---- staging of x_0: item = (channel octet, row), rows fastest (coalesced per channel)
+  constexpr int SROWS = CTU ? CROWS : ROWS;
   int srow[SPT], sg[SPT];
 #pragma unroll
   for (int j = 0; j < SPT; ++j) {
     const int e = tid + NTHR * j;
-    sg[j] = e / ROWS;
-    srow[j] = e - sg[j] * ROWS;
+    sg[j] = e / SROWS;
+    srow[j] = e - sg[j] * SROWS;
   }
   float st[SPT][8];
+  // CTU: the ConvTranspose input of a tile, rows = input positions (q0 - OFF) / CTU - 1 + row
+  auto stage_load_ct = [&](const Tile& T) {
+    const __amdgpu_buffer_rsrc_t xr = rsrc_s(a.xin + (long)T.b * a.sb_in);
+    constexpr int U = CTU ? CTU : 1;
+    const int Lin = T.L / U, qb = (T.q0 - OFF) / U - 1;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      int p = qb + srow[j];
+      p = p < 0 ? 0 : (p >= Lin ? Lin - 1 : p);
+      const int vo = (8 * min(sg[j], NGI - 1) * a.Ls_in + p) * 4;
+#pragma unroll
+      for (int c = 0; c < 8; ++c)
+        st[j][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, c * a.Ls_in * 4, 0));
+    }
+  };
+  auto stage_store_ct = [&](const Tile& T) {
+    constexpr int U = CTU ? CTU : 1;
+    const int Lin = T.L / U, qb = (T.q0 - OFF) / U - 1;
+#pragma unroll
+    for (int j = 0; j < SPT; ++j) {
+      if (sg[j] >= NGI) continue;
+      const int p = qb + srow[j];
+      const bool in = p >= 0 && p < Lin;  // the ConvTranspose's zero padding
+      float lv[8], mx = 0.f;
+#pragma unroll
+      for (int c = 0; c < 8; ++c) {
+        const float v = in ? st[j][c] : 0.f;
+        mx = fmaxf(mx, __builtin_fabsf(v));
+        lv[c] = lrelu_s(v);
+      }
+      bad |= !(mx < F16_RANGE);
+      h8 hi, lo;
+      split8(lv, hi, lo);
+      _Float16* xl = XL + srow[j] * CRS + 8 * sg[j];
+      *reinterpret_cast<h8*>(xl) = hi;
+      *reinterpret_cast<h8*>(xl + CIN) = lo;
+    }
+  };
   auto stage_load = [&](const Tile& T) {
     const __amdgpu_buffer_rsrc_t xr = rsrc_s(a.x + (long)T.b * a.sb);
 #pragma unroll
@@ -177,35 +229,112 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
     }
   };
 
+  auto load_tile = [&](const Tile& T) {
+    if constexpr (CTU) stage_load_ct(T);
+    else stage_load(T);
+  };
+  auto store_tile = [&](const Tile& T) {
+    if constexpr (CTU) stage_store_ct(T);
+    else stage_store(T);
+  };
   // ---- weights: block k's phase-1 then phase-2 fragments ([mt][k-step][lane][hi | lo], the
   //      resblock_x3 packing) through a 3-slot ring that runs on across blocks and tiles
   const int wlo = lane * 32;
   h8 ring[R][2];
+  // CTU: the fused ConvTranspose is "block -1" of every tile, CKS k-steps of this wave's merged-row
+  // m-tile (wave % CMT) ahead of block 0 in the ring sequence (CKS % R == 0 keeps slots fixed)
+  static_assert(CTU == 0 || CKS % R == 0, "weight ring over the fused ConvTranspose");
   auto wload = [&](h8 (&r)[2], int blk, int s) {  // s: k-step within block blk (compile-time)
+    if (CTU && blk < 0) {
+      const __amdgpu_buffer_rsrc_t wr = rsrc_s(a.ct16);
+      const int so = ((wave % CMT) * CKS + s) * 2048;
+      r[0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo, so, 0));
+      r[1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo + 16, so, 0));
+      return;
+    }
     const bool p1 = s < NK1;
     const __amdgpu_buffer_rsrc_t wr = rsrc_s(p1 ? pick3(a.wd16[0], a.wd16[1], a.wd16[2], blk) : pick3(a.wf16[0], a.wf16[1], a.wf16[2], blk));
     const int so = (wm * (p1 ? NK1 : NK2) + (p1 ? s : s - NK1)) * 2048;
     r[0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo, so, 0));
     r[1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo + 16, so, 0));
   };
-  // after k-step s of block blk: load the k-step R ahead (into the next block past NKB)
+  // after k-step s of block blk: load the k-step R ahead (into the next block past its end)
   auto wnext = [&](h8 (&r)[2], int blk, int s) {
 #ifdef RS_NO_WLOAD
     return;
 #endif
-    if (s + R < NKB) wload(r, blk, s + R);
-    else wload(r, blk + 1 == NB ? 0 : blk + 1, s + R - NKB);
+    const int nk = (CTU && blk < 0) ? CKS : NKB;
+    if (s + R < nk) wload(r, blk, s + R);
+    else wload(r, blk + 1 == NB ? (CTU ? -1 : 0) : blk + 1, s + R - nk);
+  };
+
+  f32x4 am[NI], ac[NI];
+  // CTU prologue (after store_tile + barrier): x_0 of every row of the tile from the staged input.
+  // Wave w: merged-row m-tile w % CMT, input-column n-tiles w / CMT + 2 n (the 4 accumulator pairs
+  // of a block's n-tiles); the epilogue waits until every wave is done with the staging (it shares
+  // the XL region)
+  auto ct_prologue = [&](const Tile& T) __attribute__((always_inline)) {
+    const int mt = wave % CMT, g = wave / CMT;
+    // the row / column index of this lane, opaque per tile: the LDS addresses derived from it are
+    // recomputed here instead of hoisted out of the tile loop (where they spilled)
+    int lrow = lane & 15;
+    asm volatile("" : "+v"(lrow));
+#pragma unroll
+    for (int n = 0; n < NI; ++n) am[n] = ac[n] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < CKS; ++ks) {  // k-step = chunk * 2 + tap, as pack_conv_x3 (K = 2)
+      const int ch = ks >> 1, tap = ks & 1;
+      h8 bh[NI], bl[NI];
+#pragma unroll
+      for (int n = 0; n < NI; ++n) {
+        const int j = min((g + 2 * n) * 16 + lrow + tap, CROWS - 1);
+        const _Float16* p = XL + j * CRS + 32 * ch + kg;
+        bh[n] = RS_LD(p);
+        bl[n] = RS_LD(p + CIN);
+      }
+      RS_SB();
+#pragma unroll
+      for (int n = 0; n < NI; ++n) RS_MMA(ring[ks % R][0], ring[ks % R][1], bh[n], bl[n], am[n], ac[n]);
+      wnext(ring[ks % R], -1, ks);
+      RS_SB();
+    }
+    lds_barrier();  // the staged input (XL region) is dead from here
+    const int m0 = mt * 16 + 4 * (lane >> 4), co0 = m0 / 2;  // rows m0 .. m0 + 3 = (co0, co0 + 1) x phases 0, 1
+    const f32x4 b4 = *reinterpret_cast<const f32x4*>(bct + m0);
+    const int P0 = T.q0 - OFF;
+#pragma unroll
+    for (int n = 0; n < NI; ++n) {
+      const int c = (g + 2 * n) * 16 + lrow;  // input column q' = P0 / 2 + c
+      const f32x4 v = x3_value4(am[n], ac[n], b4);
+      vmax = absmax4(vmax, v);
+#pragma unroll
+      for (int ph = 0; ph < 2; ++ph) {
+        const int r = 2 * c - ph;  // phase 0: output 2 q', phase 1: 2 q' - 1
+        if (r < 0 || r >= ROWS) continue;
+        const int p = P0 + r;
+        const bool in = p >= 0 && p < T.L;
+        const f32x2_ x2{in ? v[ph] : 0.f, in ? v[2 + ph] : 0.f};
+        h2_ hi, lo;
+        split2(x2, hi, lo);
+        *reinterpret_cast<h2_*>(HX + r * HR + C + co0) = hi;
+        *reinterpret_cast<h2_*>(HX + r * HR + 3 * C + co0) = lo;
+        split2(f32x2_{lrelu_s(x2[0]), lrelu_s(x2[1])}, hi, lo);
+        *reinterpret_cast<h2_*>(XL + r * XLR + co0) = hi;
+        *reinterpret_cast<h2_*>(XL + r * XLR + C + co0) = lo;
+      }
+    }
+    lds_barrier();
   };
 
   if (t >= ntiles) return;
   Tile cur = tile_of(t);
-  stage_load(cur);
+  load_tile(cur);
 #pragma unroll
-  for (int u = 0; u < R; ++u) wload(ring[u], 0, u);
-  stage_store(cur);
+  for (int u = 0; u < R; ++u) wload(ring[u], CTU ? -1 : 0, u);
+  store_tile(cur);
   lds_barrier();
+  if constexpr (CTU) ct_prologue(cur);
 
-  f32x4 am[NI], ac[NI];
 #ifdef RS_TRACE
   int it_ = 0;
 #endif
@@ -247,7 +376,7 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
         }
       }
       RS_STAMP(4 * bi + 1);
-      if (RS_STAGE_AT == 1 && last) stage_load(nxt);
+      if (RS_STAGE_AT == 1 && last) load_tile(nxt);
       // ---------------- phase 1: h = Wd . lrelu(x_k) ----------------
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) am[ni] = ac[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -293,7 +422,7 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
       }
       lds_barrier();
       RS_STAMP(4 * bi + 2);
-      if (RS_STAGE_AT == 0 && last) stage_load(nxt);  // in flight during the last phase 2 and the stores
+      if (RS_STAGE_AT == 0 && last) load_tile(nxt);  // in flight during the last phase 2 and the stores
       // ---------------- phase 2: y = [W1 | Wsc] . [lrelu(h); x_k] ----------------
 #pragma unroll
       for (int kc = 0; kc < NK2; ++kc) {
@@ -319,7 +448,7 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
       }
       const f32x4 bf = *reinterpret_cast<const f32x4*>(bias[bi][1] + co);
       RS_STAMP(4 * bi + 3);
-      if (RS_STAGE_AT == 2 && last) stage_load(nxt);
+      if (RS_STAGE_AT == 2 && last) load_tile(nxt);
       if (!last) {
         lds_barrier();  // every wave is done reading x_k
 #pragma unroll
@@ -372,8 +501,9 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
     lds_barrier();  // every wave is done with this tile's XL / HX
     cur = nxt;
     t = tn;
-    stage_store(cur);
+    store_tile(cur);
     lds_barrier();
+    if constexpr (CTU) ct_prologue(cur);
     RS_STAMP(15);
 #ifdef RS_TRACE
     ++it_;
@@ -382,19 +512,19 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
   if (bad || !(vmax < F16_RANGE)) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-template <int C, int TQ, int WN, int NI>
+template <int C, int TQ, int WN, int NI, int CTU = 0>
 static void launch_rsx3(const StackArgs& a, const int* h_lens, hipStream_t s) {
   constexpr int ROWS = TQ + 2 * ST_OFF;
   constexpr size_t lds = (size_t)ROWS * ((2 * C + 16) + (4 * C + 16)) * 2;
   static_assert(lds + 3 * 2 * C * 4 + 65 * 4 + 64 * 4 <= 160 * 1024, "LDS");
-  ensure_dyn_lds((const void*)resstack_x3_kernel<C, TQ, WN, NI>, (int)lds);
+  ensure_dyn_lds((const void*)resstack_x3_kernel<C, TQ, WN, NI, CTU>, (int)lds);
   const int ncu = device_cu_count();
   long ntiles = 0;
   for (int b = 0; b < a.B; ++b) ntiles += ((long)(h_lens[b] + a.len_add) * a.mul + TQ - 1) / TQ;
   TTS_CHECK(ntiles < (1L << 30), "resstack_x3: too many tiles");
   if (ntiles == 0) return;
   const int grid = (int)std::min<long>(ntiles, ncu);
-  resstack_x3_kernel<C, TQ, WN, NI><<<grid, 64 * (C / 16) * WN, lds, s>>>(a, (int)ntiles);
+  resstack_x3_kernel<C, TQ, WN, NI, CTU><<<grid, 64 * (C / 16) * WN, lds, s>>>(a, (int)ntiles);
 }
 
 bool resstack_x3_supported(int C, const int* dil, int n) {
@@ -425,10 +555,14 @@ void launch_resstack_x3(const StackArgs& a0, const int* h_lens, int C, hipStream
   a.ext[2] = 0;
   a.ext[1] = a.dil[2];
   a.ext[0] = a.dil[1] + a.dil[2];
-  if (C == 48) {
+  if (C == 48 && a.ct16) {
+    TTS_CHECK(a.xin && a.ct_bias && a.mul % 2 == 0, "resstack_x3: fused ConvTranspose arguments");
+    launch_rsx3<48, 208, 4, 4, 2>(a, h_lens, s);
+  } else if (C == 48) {
     // 3 m-tile waves x 4 n-groups; ROWS = 240 = 15 n-tiles, <= 4 per wave
     launch_rsx3<48, 208, 4, 4>(a, h_lens, s);
   } else {
+    TTS_CHECK(!a.ct16, "resstack_x3: fused ConvTranspose only at C = 48");
     // C = 96: 6 m-tile waves x 2 n-groups; ROWS = 128 = 8 n-tiles, 4 per wave (158.5 KB LDS)
     launch_rsx3<96, 96, 2, 4>(a, h_lens, s);
   }
