@@ -1227,6 +1227,24 @@ def test_synthesizer_glow_tts_and_pwgan(tmp_path):
         assert w.shape == (256 * 2 * (int(yl) // 2),) and np.isfinite(w).all() and np.abs(w).max() > 0
 
 
+def test_pwgan_persistent_kernel_bit_identical(tmp_path):
+    """The persistent, weight-resident residual-block kernel (pw_layer_x3p_kernel, the default) gives
+    the same waveform bits as the per-tile kernel (TTS_PWGAN_TILE=1) on a ragged 3-utterance LJ
+    batch with one seeded prior; the two modes run in child processes (tools/pwgan_bench.py --dump)."""
+    import subprocess
+    import sys
+    _dev()
+    outs = []
+    for f in ("0", "1"):
+        path = str(tmp_path / f"p{f}.npy")
+        env = dict(os.environ, TTS_PWGAN_TILE=f)
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "pwgan_bench.py"), "--batch", "3", "--steps", "1",
+                            "--warmup", "0", "--dump", path], env=env, capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        outs.append(np.load(path))
+    assert outs[0].shape == outs[1].shape and np.array_equal(outs[0], outs[1])
+
+
 def test_pwgan_inference_padding_zero_vs_oracle():
     """inference_padding = 0 (what Synthesizer sets, server/synthesizer.py:86) against the fp32
     oracle on the fixture weights and mel (parity pinned through the oracle, <= 2e-6 of the reference)."""

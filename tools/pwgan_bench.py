@@ -24,6 +24,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--batch", type=int, default=32)
     ap.add_argument("--cpu-frames", type=int, default=0)
+    ap.add_argument("--dump", default="", help="save the last call's waveforms (.npy) for bit-identity checks")
     a = ap.parse_args()
     _, M = lj_profile()
     M = [M[i % len(M)] for i in range(a.batch)]  # batch 64 (config C4): the 32-utterance profile twice
@@ -37,14 +38,17 @@ def main():
         mel[i, :, :m] = rs.uniform(-1, 1, size=(80, m))
     mel = torch.from_numpy(mel).cuda()
     T = 256 * (max(M) + 4)
+    torch.manual_seed(0)  # the same prior in every process (--dump comparisons)
     noise = torch.randn(len(M), 1, T, device="cuda")
     for _ in range(a.warmup):
         g.inference(mel, lengths=M, noise=noise)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for _ in range(a.steps):
-        g.inference(mel, lengths=M, noise=noise)
+        y = g.inference(mel, lengths=M, noise=noise)
     torch.cuda.synchronize()
+    if a.dump:
+        np.save(a.dump, y.cpu().numpy())
     dt = (time.perf_counter() - t0) / a.steps
     samples = 256 * (sum(M) + 4 * len(M))
     flops = samples * 30 * 2 * (128 * 272 + 128 * 64)

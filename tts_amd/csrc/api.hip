@@ -44,8 +44,8 @@ void launch_pw_layer(const float* x, const float* c, float* xn, float* skip, con
                      const float* W2, const float* b2, const int* lens, const float* zeros, int len_add, int hop,
                      int Tmax, int dil, int first, int B, int variant, hipStream_t st);
 void launch_pw_layer_x3(const float* x, const float* c, float* xn, float* skip, const void* W1x, const float* b1,
-                        const void* W2x, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
-                        int first, int B, unsigned* oflow, hipStream_t st);
+                        const void* W2x, const float* b2, const int* lens, const int* h_lens, int len_add, int hop,
+                        int Tmax, int dil, int first, int B, unsigned* oflow, hipStream_t st);
 void pack_pw_layer_x3(const std::vector<float>& m1, const std::vector<float>& m2, std::vector<uint16_t>& w1x,
                       std::vector<uint16_t>& w2x);
 void launch_pw_out(const float* skip, float scale, const float* W3, const float* b3, const float* w4,
@@ -2884,8 +2884,8 @@ void pwgan_infer(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int
   unsigned* flag = x3_flag(c);
   for (int l = 0; l < P.layers; ++l) {
     if (flag && P.W1x[l].p)
-      launch_pw_layer_x3(x, cfeat, xn, W.skip.f(), P.W1x[l].p, P.b1[l].f(), P.W2x[l].p, P.b2[l].f(), dl, 2 * pad,
-                         hop, Tmax, 1 << (l % per_stack), l == 0, B, flag, s);
+      launch_pw_layer_x3(x, cfeat, xn, W.skip.f(), P.W1x[l].p, P.b1[l].f(), P.W2x[l].p, P.b2[l].f(), dl, h_lens,
+                         2 * pad, hop, Tmax, 1 << (l % per_stack), l == 0, B, flag, s);
     else
       launch_pw_layer(x, cfeat, xn, W.skip.f(), P.W1[l].f(), P.b1[l].f(), P.W2[l].f(), P.b2[l].f(), dl, W.zeros.f(),
                       2 * pad, hop, Tmax, 1 << (l % per_stack), l == 0, B, variant, s);

@@ -13,6 +13,8 @@
 //   epilogue  x' = (out + b + x) / 4  -> ping-pong buffer;  skip (+)= s + b  (in place)
 // HBM per sample per block: x (+halo, L2) 256 B, c 320 B, skip r/w 512 B, x' 256 B.
 #include "common.h"
+
+#include <cstdlib>
 #include "split16.h"
 
 namespace {
@@ -68,12 +70,10 @@ __global__ __launch_bounds__(256) void pw_first_kernel(const float* __restrict__
     x[((long)b * PW_R + ch) * Tmax + t] = t < T ? fmaf(w[ch], n, bias[ch]) : 0.f;
 }
 
-// tanh(u) * sigmoid(g) on the hardware exp / rcp (|error| ~1e-7 absolute; tanh = 1 - 2 / (1 + e^2u)
-// saturates cleanly at both ends)
-__device__ __forceinline__ float pw_gate(float u, float g) {
-  const float t = 1.f - 2.f * __frcp_rn(1.f + __expf(2.f * u));
-  return t * __frcp_rn(1.f + __expf(-g));
-}
+// tanh(u) * sigmoid(g) on the hardware exp / rcp (common.h tanh_f / sigm_f: |error| < 2e-7 absolute).
+// Round 4: __frcp_rn compiled to the IEEE division sequence (div_scale / div_fmas / div_fixup, ~10
+// VALU per reciprocal), a third of the persistent residual-block kernel's VALU issue.
+__device__ __forceinline__ float pw_gate(float u, float g) { return tanh_f(u) * sigm_f(g); }
 
 struct PwLayerArgs {
   const float* x;      // (B, 64, Tmax)
@@ -511,7 +511,9 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
   const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W1x), 0, 0x7fffffff, 0x00020000);
   const __amdgpu_buffer_rsrc_t w2r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W2x), 0, 0x7fffffff, 0x00020000);
   const int mt0 = wm * 2;
-  h8 ring[3][2][2];
+  constexpr int RSL = 3;  // weight ring slots
+  constexpr int SD = 2;   // staging depth (k-steps ahead)
+  h8 ring[RSL][2][2];
   auto wload = [&](h8 (&r)[2][2], int seq) {
     seq = min(seq, PX_NK1 + PX_NK2 - 1);
     const bool g1 = seq < PX_NK1;
@@ -528,20 +530,23 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
   // the epilogue's residual operands (x for the conv1x1_out rows, the running skip sum for the
   // skip rows), loaded now so their latency hides under the GEMMs
   float res[2][4][4];
+  auto res_load = [&]() {
 #pragma unroll
-  for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < 2; ++mi)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      const int R = wm * 32 + mi * 16 + 4 * (lane >> 4) + j;
-      const bool out_row = R < PW_R;
-      const float* src = out_row ? a.x : a.skip;
-      const long rowb = ((long)b * 64 + (out_row ? R : R - PW_R)) * a.Tmax;
+      for (int j = 0; j < 4; ++j) {
+        const int R = wm * 32 + mi * 16 + 4 * (lane >> 4) + j;
+        const bool out_row = R < PW_R;
+        const float* src = out_row ? a.x : a.skip;
+        const long rowb = ((long)b * 64 + (out_row ? R : R - PW_R)) * a.Tmax;
 #pragma unroll
-      for (int ni = 0; ni < 4; ++ni) {
-        const int t = min(t0 + nb + ni * 16, T - 1);
-        res[mi][j][ni] = src[rowb + t];  // the skip rows' value is unused on the first block
+        for (int ni = 0; ni < 4; ++ni) {
+          const int t = min(t0 + nb + ni * 16, T - 1);
+          res[mi][j][ni] = src[rowb + t];  // the skip rows' value is unused on the first block
+        }
       }
-    }
+  };
+  res_load();
   f32x4 am[2][4], ac[2][4];
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi)
@@ -566,18 +571,30 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
   // stored to LDS buffer s & 1 after step s - 1's)
   stage_load(st[0], sok[0], 0);
 #pragma unroll
-  for (int u = 0; u < 3; ++u) wload(ring[u], u);
-  stage_load(st[1], sok[1], 1);
-  stage_store(Xs, st[0], sok[0]);
-  stage_load(st[0], sok[0], 2);
+  for (int u = 0; u < RSL; ++u) wload(ring[u], u);
+  if constexpr (SD == 2) {
+    stage_load(st[1], sok[1], 1);
+    stage_store(Xs, st[0], sok[0]);
+    stage_load(st[0], sok[0], 2);
+  } else {
+    stage_store(Xs, st[0], sok[0]);
+  }
   lds_barrier();
 #pragma unroll
   for (int ks = 0; ks < PX_NK1; ++ks) {
-    kstep(Xs + (ks & 1) * PX_PLANE, ring[ks % 3]);
-    wload(ring[ks % 3], ks + 3);
+    if constexpr (SD == 1) {
+      if (ks + 1 < PX_NK1) stage_load(st[0], sok[0], ks + 1);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    kstep(Xs + (ks & 1) * PX_PLANE, ring[ks % RSL]);
+    wload(ring[ks % RSL], ks + RSL);
     __builtin_amdgcn_sched_barrier(0);
-    if (ks + 1 < PX_NK1) stage_store(Xs + ((ks + 1) & 1) * PX_PLANE, st[(ks + 1) & 1], sok[(ks + 1) & 1]);
-    if (ks + 3 < PX_NK1) stage_load(st[(ks + 1) & 1], sok[(ks + 1) & 1], ks + 3);
+    if constexpr (SD == 2) {
+      if (ks + 1 < PX_NK1) stage_store(Xs + ((ks + 1) & 1) * PX_PLANE, st[(ks + 1) & 1], sok[(ks + 1) & 1]);
+      if (ks + 3 < PX_NK1) stage_load(st[(ks + 1) & 1], sok[(ks + 1) & 1], ks + 3);
+    } else {
+      if (ks + 1 < PX_NK1) stage_store(Xs + ((ks + 1) & 1) * PX_PLANE, st[0], sok[0]);
+    }
     lds_barrier();
   }
   // gate: rows R = wm * 32 + mi * 16 + 4 (lane >> 4) + j, pairs (R, R + 1) -> z[R / 2]
@@ -601,9 +618,9 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
     }
   }
   lds_barrier();
-  // GEMM2 (weights 9, 10 already in ring slots 0, 1)
+  // GEMM2 (weights 9, 10 already in the ring)
 #pragma unroll
-  for (int ks = 0; ks < PX_NK2; ++ks) kstep(Zs + ks * PX_PLANE, ring[ks]);
+  for (int ks = 0; ks < PX_NK2; ++ks) kstep(Zs + ks * PX_PLANE, ring[(PX_NK1 + ks) % RSL]);
   // x' = (out + b + x) * 0.25 (parallel_wavegan.py:85); skip (+)= s + b
 #pragma unroll
   for (int mi = 0; mi < 2; ++mi) {
@@ -627,12 +644,258 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
   if (bad) __hip_atomic_fetch_or(oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
+// Persistent form (round 4): one 4-wave workgroup per CU loops over the (utterance, 64-position)
+// tiles with every weight in registers. The register-ring kernel above spent most of a tile
+// waiting: one workgroup per CU (320 VGPRs), a barrier per k-step and its operands two k-steps
+// (~0.4 us of MFMA) ahead of ~2 us of load latency. Here
+//   * a wave's 2 m-tiles x 11 k-steps of split A fragments (176 VGPRs) load once per launch;
+//   * a tile's whole GEMM1 operand (9 k-steps, 32 floats per thread) is staged into 9 LDS planes at
+//     once, and the next tile's is loaded into registers while this tile's GEMMs run (nothing
+//     else is loaded between, so the in-order vmcnt waits of the GEMMs never wait for them);
+//   * the epilogue operands (x, running skip) load before the next tile's operands.
+// Same arithmetic, k-step order and epilogue as pw_layer_x3_kernel: bit-identical results.
+__global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, const void* W1x, const void* W2x,
+                                                              unsigned* oflow, int B, int ntiles) {
+  constexpr int TQ = 64;
+  constexpr int PLANE = TQ * PX_XR;  // halves
+  extern __shared__ __attribute__((aligned(16))) _Float16 shp[];
+  _Float16* Xs = shp;                   // PX_NK1 planes
+  _Float16* Zs = shp + PX_NK1 * PLANE;  // 2 planes
+  h8* W2s = reinterpret_cast<h8*>(shp + (PX_NK1 + 2) * PLANE);  // GEMM2 A fragments [m16][k-step][lane][2]
+  __shared__ int tcum[65], tlen[64];
+  __shared__ float b1s[PW_G], b2s[PW_G];
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = wave;  // 4 x 1 waves: 32 rows x 64 positions each
+  const int nb = lane & 15, kg = 8 * (lane >> 4);
+  bool bad = false;
+  if (wave == 0) {  // tiles per utterance, exclusive prefix sum
+    const int L = lane < B ? (a.lens[lane] + a.len_add) * a.hop : 0;
+    const int n = (L + TQ - 1) / TQ;
+    int v = n;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int y = __shfl_up(v, o, 64);
+      if (lane >= o) v += y;
+    }
+    tcum[lane] = v - n;
+    tlen[lane] = L;
+    if (lane == 63) tcum[64] = v;
+  }
+  __syncthreads();
+  struct Tile {
+    int b, t0, T;
+  };
+  auto tile_of = [&](int i) {
+    const bool hit = lane < B && tcum[lane] <= i && i < tcum[lane + 1];
+    const unsigned long long m = __ballot(hit);
+    Tile r;
+    r.b = __builtin_amdgcn_readfirstlane(m ? __ffsll((long long)m) - 1 : 0);
+    r.t0 = __builtin_amdgcn_readfirstlane((i - tcum[r.b]) * TQ);
+    r.T = __builtin_amdgcn_readfirstlane(tlen[r.b]);
+    return r;
+  };
+
+  // GEMM1 weights [m16 (8)][k-step][lane][hi 8 | lo 8] in registers (this wave's m-tiles 2 wm,
+  // 2 wm + 1); GEMM2's (32 KB) and the biases in LDS
+  h8 w1[PX_NK1][2][2];
+  {
+    const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W1x), 0, 0x7fffffff, 0x00020000);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ks = 0; ks < PX_NK1; ++ks) {
+        const int so = ((2 * wm + mi) * PX_NK1 + ks) * 2048;
+        w1[ks][mi][0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(w1r, lane * 32, so, 0));
+        w1[ks][mi][1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(w1r, lane * 32 + 16, so, 0));
+      }
+    const h8* w2g = reinterpret_cast<const h8*>(W2x);
+    for (int i = tid; i < 8 * PX_NK2 * 64 * 2; i += 256) W2s[i] = w2g[i];
+    for (int i = tid; i < PW_G; i += 256) {
+      b1s[i] = a.b1[i];
+      b2s[i] = a.b2[i];
+    }
+  }
+  __syncthreads();
+
+  // staging item of this thread: channel octet sg (0..3) of a k-step, position sq (0..63)
+  const int sg = tid / TQ, sq = tid % TQ;
+  float st[PX_NK1][8];
+  unsigned sok = 0;  // bit ks: k-step ks's item is inside the utterance
+  // raw buffer loads: the utterance's rows as the resource (SGPRs), one 32-bit VGPR offset per
+  // item and the channel inside the octet as an SGPR offset (64-bit flat addresses per load pushed
+  // the kernel past its registers, and the spill reloads' vmcnt waits drained the prefetch)
+  auto rsrc_rows = [&](const float* base, int rows) {
+    return __builtin_amdgcn_make_buffer_rsrc(const_cast<float*>(base), 0, rows * a.Tmax * 4, 0x00020000);
+  };
+  auto stage_load = [&](const Tile& Tl, int ks) {
+    const bool xs = ks < 6;
+    const int c0 = xs ? 32 * (ks & 1) + 8 * sg : 32 * (ks - 6) + 8 * sg;
+    const int off = xs ? (ks / 2 - 1) * a.dil : 0;
+    const int cmax = xs ? PW_R : PW_A;
+    const __amdgpu_buffer_rsrc_t r = xs ? rsrc_rows(a.x + (long)Tl.b * PW_R * a.Tmax, PW_R)
+                                        : rsrc_rows(a.c + (long)Tl.b * PW_A * a.Tmax, PW_A);
+    const int t = Tl.t0 + sq + off;
+    const bool ok = t >= 0 && t < Tl.T && c0 < cmax;
+    sok = ok ? (sok | (1u << ks)) : (sok & ~(1u << ks));
+    const int vo = (min(c0, cmax - 8) * a.Tmax + (ok ? t : 0)) * 4;
+#pragma unroll
+    for (int c = 0; c < 8; ++c) st[ks][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, c * a.Tmax * 4, 0));
+  };
+  auto stage_store = [&](int ks) {
+    float mx = 0.f, v[8];
+#pragma unroll
+    for (int c = 0; c < 8; ++c) {
+      v[c] = ((sok >> ks) & 1u) ? st[ks][c] : 0.f;
+      mx = fmaxf(mx, __builtin_fabsf(v[c]));
+    }
+    bad |= !(mx < F16_RANGE);
+    h8 hi, lo;
+    split8(v, hi, lo);
+    _Float16* X = Xs + ks * PLANE;
+    *reinterpret_cast<h8*>(X + sq * PX_XR + 8 * sg) = hi;
+    *reinterpret_cast<h8*>(X + sq * PX_XR + 32 + 8 * sg) = lo;
+  };
+  float res[2][4][4];
+  auto res_load = [&](const Tile& Tl) {
+    // waves 0, 1 hold conv1x1_out rows (residual x), waves 2, 3 skip rows (the running skip sum)
+    const __amdgpu_buffer_rsrc_t r = rsrc_rows((wm < 2 ? a.x : a.skip) + (long)Tl.b * 64 * a.Tmax, 64);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int ch = (wm & 1) * 32 + mi * 16 + 4 * (lane >> 4) + j;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int t = min(Tl.t0 + nb + ni * 16, Tl.T - 1);
+          res[mi][j][ni] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, (ch * a.Tmax + t) * 4, 0, 0));
+        }
+      }
+  };
+  f32x4 am[2][4], ac[2][4];
+  // B operands two n-tiles at a time (16 VGPRs instead of 32: the kernel is at its register limit)
+  auto kstep = [&](const _Float16* X, const h8 (&w)[2][2]) __attribute__((always_inline)) {
+#pragma unroll
+    for (int n2 = 0; n2 < 4; n2 += 2) {
+      h8 bh[2], bl[2];
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const _Float16* q = X + (nb + (n2 + u) * 16) * PX_XR + kg;
+        bh[u] = *reinterpret_cast<const h8*>(q);
+        bl[u] = *reinterpret_cast<const h8*>(q + 32);
+      }
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+        for (int u = 0; u < 2; ++u) mfma_x3(w[mi][0], w[mi][1], bh[u], bl[u], am[mi][n2 + u], ac[mi][n2 + u]);
+    }
+  };
+
+  int t = blockIdx.x;
+  if (t >= ntiles) return;
+  Tile cur = tile_of(t);
+#pragma unroll
+  for (int ks = 0; ks < PX_NK1; ++ks) stage_load(cur, ks);
+  for (;;) {
+#pragma unroll
+    for (int ks = 0; ks < PX_NK1; ++ks) stage_store(ks);
+    res_load(cur);
+    lds_barrier();
+    const int tn = t + (int)gridDim.x;
+    const bool more = tn < ntiles;
+    const Tile nxt = more ? tile_of(tn) : cur;
+    // unconditional (the last tile reloads itself): a conditional load would make the compiler
+    // count none of them at its merge, and the epilogue's waits for the residual operands would
+    // then drain these too
+#pragma unroll
+    for (int ks = 0; ks < PX_NK1; ++ks) stage_load(nxt, ks);
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi)
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int ks = 0; ks < PX_NK1; ++ks) kstep(Xs + ks * PLANE, w1[ks]);
+    // gate: rows R = wm * 32 + mi * 16 + 4 (lane >> 4) + j, pairs (R, R + 1) -> z[R / 2]
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+      const int R = wm * 32 + mi * 16 + 4 * (lane >> 4);
+      const int zc = R >> 1;
+      _Float16* Z = Zs + (zc >> 5) * PLANE + (zc & 31);
+#pragma unroll
+      for (int ni = 0; ni < 4; ++ni) {
+        const int q = nb + ni * 16;
+        f32x4 v;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) v[j] = x3_value(am[mi][ni][j], ac[mi][ni][j]);
+        h2_ zh, zl;
+        split2(f32x2_{pw_gate(v[0] + b1s[R], v[1] + b1s[R + 1]), pw_gate(v[2] + b1s[R + 2], v[3] + b1s[R + 3])}, zh,
+               zl);
+        *reinterpret_cast<h2_*>(Z + q * PX_XR) = zh;
+        *reinterpret_cast<h2_*>(Z + q * PX_XR + 32) = zl;
+        am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
+      }
+    }
+    lds_barrier();
+#pragma unroll
+    for (int ks = 0; ks < PX_NK2; ++ks) {
+      h8 w2[2][2];
+#pragma unroll
+      for (int mi = 0; mi < 2; ++mi) {
+        const h8* q = W2s + (((2 * wm + mi) * PX_NK2 + ks) * 64 + lane) * 2;
+        w2[mi][0] = q[0];
+        w2[mi][1] = q[1];
+      }
+      kstep(Zs + ks * PLANE, w2);
+    }
+    // x' = (out + b + x) * 0.25 (parallel_wavegan.py:85); skip (+)= s + b
+#pragma unroll
+    for (int mi = 0; mi < 2; ++mi) {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int R = wm * 32 + mi * 16 + 4 * (lane >> 4) + j;
+        const bool out_row = R < PW_R;
+        const int ch = out_row ? R : R - PW_R;
+#pragma unroll
+        for (int ni = 0; ni < 4; ++ni) {
+          const int tt = cur.t0 + nb + ni * 16;
+          if (tt >= cur.T) continue;
+          const float v = x3_value(am[mi][ni][j], ac[mi][ni][j]) + b2s[R];
+          const long i = ((long)cur.b * 64 + ch) * a.Tmax + tt;
+          if (out_row) a.xn[i] = (v + res[mi][j][ni]) * 0.25f;
+          else a.skip[i] = a.first ? v : res[mi][j][ni] + v;
+        }
+      }
+    }
+    if (!more) break;
+    lds_barrier();  // every wave is done with this tile's planes
+    cur = nxt;
+    t = tn;
+  }
+  if (bad) __hip_atomic_fetch_or(oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 void launch_pw_layer_x3(const float* x, const float* c, float* xn, float* skip, const void* W1x, const float* b1,
-                        const void* W2x, const float* b2, const int* lens, int len_add, int hop, int Tmax, int dil,
-                        int first, int B, unsigned* oflow, hipStream_t st) {
+                        const void* W2x, const float* b2, const int* lens, const int* h_lens, int len_add, int hop,
+                        int Tmax, int dil, int first, int B, unsigned* oflow, hipStream_t st) {
   TTS_CHECK(W1x && W2x && oflow, "pwgan split-f16: weights / range flag missing");
   PwLayerArgs a{x, c, xn, skip, nullptr, b1, nullptr, b2, lens, nullptr, len_add, hop, Tmax, dil, first};
-  // two 4-wave workgroups per CU (64 positions each) overlap one another's staging and epilogue
+  static const int var = [] {
+    const char* e = std::getenv("TTS_PWGAN_TILE");
+    return e ? std::atoi(e) : 0;
+  }();
+  if (B <= 64 && h_lens && var != 1) {  // persistent, weights in registers (TTS_PWGAN_TILE=1: the per-tile kernel)
+    long ntiles = 0;
+    for (int b = 0; b < B; ++b) ntiles += ((long)(h_lens[b] + len_add) * hop + 63) / 64;
+    TTS_CHECK(ntiles < (1L << 30), "pwgan: too many tiles");
+    if (ntiles == 0) return;
+    constexpr int lds = (PX_NK1 + 2) * 64 * PX_XR * 2 + 8 * PX_NK2 * 64 * 32;
+    ensure_dyn_lds((const void*)pw_layer_x3p_kernel, lds);
+    const int grid = (int)std::min<long>(ntiles, device_cu_count());
+    pw_layer_x3p_kernel<<<grid, 256, lds, st>>>(a, W1x, W2x, oflow, B, (int)ntiles);
+    HIP_OK(hipGetLastError());
+    return;
+  }
+  // per-tile kernel (B > 64, or TTS_PWGAN_TILE=1): one 4-wave workgroup per tile of 64 positions
   constexpr int WN = 1;
   const dim3 grid((Tmax + 64 * WN - 1) / (64 * WN), B);
   pw_layer_x3_kernel<WN><<<grid, 256 * WN, 0, st>>>(a, W1x, W2x, oflow);
