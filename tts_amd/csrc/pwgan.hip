@@ -654,8 +654,12 @@ __global__ __launch_bounds__(256 * WN) void pw_layer_x3_kernel(PwLayerArgs a, co
 //     else is loaded between, so the in-order vmcnt waits of the GEMMs never wait for them);
 //   * the epilogue operands (x, running skip) load before the next tile's operands.
 // Same arithmetic, k-step order and epilogue as pw_layer_x3_kernel: bit-identical results.
-__global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, const void* W1x, const void* W2x,
-                                                              unsigned* oflow, int B, int ntiles) {
+template <int NW>
+__global__ __launch_bounds__(64 * NW, 1) void pw_layer_x3p_kernel(PwLayerArgs a, const void* W1x, const void* W2x,
+                                                                  unsigned* oflow, int B, int ntiles) {
+  // NW = 4: 2 m-tiles per wave, one wave per SIMD; NW = 8: 1 m-tile per wave, two waves per SIMD
+  constexpr int NTH = 64 * NW, MI = 8 / NW, CPI = 32 / NW;  // m-tiles per wave, staged channels per item
+  static_assert(NW == 4 || NW == 8, "waves");
   constexpr int TQ = 64;
   constexpr int PLANE = TQ * PX_XR;  // halves
   extern __shared__ __attribute__((aligned(16))) _Float16 shp[];
@@ -665,7 +669,7 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
   __shared__ int tcum[65], tlen[64];
   __shared__ float b1s[PW_G], b2s[PW_G];
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = wave;  // 4 x 1 waves: 32 rows x 64 positions each
+  const int wm = wave;  // NW x 1 waves: 16 MI rows x 64 positions each
   const int nb = lane & 15, kg = 8 * (lane >> 4);
   bool bad = false;
   if (wave == 0) {  // tiles per utterance, exclusive prefix sum
@@ -695,31 +699,31 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
     return r;
   };
 
-  // GEMM1 weights [m16 (8)][k-step][lane][hi 8 | lo 8] in registers (this wave's m-tiles 2 wm,
-  // 2 wm + 1); GEMM2's (32 KB) and the biases in LDS
-  h8 w1[PX_NK1][2][2];
+  // GEMM1 weights [m16 (8)][k-step][lane][hi 8 | lo 8] in registers (this wave's m-tiles MI wm ..
+  // MI wm + MI - 1); GEMM2's (32 KB) and the biases in LDS
+  h8 w1[PX_NK1][MI][2];
   {
     const __amdgpu_buffer_rsrc_t w1r = __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(W1x), 0, 0x7fffffff, 0x00020000);
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ks = 0; ks < PX_NK1; ++ks) {
-        const int so = ((2 * wm + mi) * PX_NK1 + ks) * 2048;
+        const int so = ((MI * wm + mi) * PX_NK1 + ks) * 2048;
         w1[ks][mi][0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(w1r, lane * 32, so, 0));
         w1[ks][mi][1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(w1r, lane * 32 + 16, so, 0));
       }
     const h8* w2g = reinterpret_cast<const h8*>(W2x);
-    for (int i = tid; i < 8 * PX_NK2 * 64 * 2; i += 256) W2s[i] = w2g[i];
-    for (int i = tid; i < PW_G; i += 256) {
+    for (int i = tid; i < 8 * PX_NK2 * 64 * 2; i += NTH) W2s[i] = w2g[i];
+    for (int i = tid; i < PW_G; i += NTH) {
       b1s[i] = a.b1[i];
       b2s[i] = a.b2[i];
     }
   }
   __syncthreads();
 
-  // staging item of this thread: channel octet sg (0..3) of a k-step, position sq (0..63)
+  // staging item of this thread: channel group sg (CPI channels) of a k-step, position sq (0..63)
   const int sg = tid / TQ, sq = tid % TQ;
-  float st[PX_NK1][8];
+  float st[PX_NK1][CPI];
   unsigned sok = 0;  // bit ks: k-step ks's item is inside the utterance
   // raw buffer loads: the utterance's rows as the resource (SGPRs), one 32-bit VGPR offset per
   // item and the channel inside the octet as an SGPR offset (64-bit flat addresses per load pushed
@@ -729,7 +733,7 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
   };
   auto stage_load = [&](const Tile& Tl, int ks) {
     const bool xs = ks < 6;
-    const int c0 = xs ? 32 * (ks & 1) + 8 * sg : 32 * (ks - 6) + 8 * sg;
+    const int c0 = xs ? 32 * (ks & 1) + CPI * sg : 32 * (ks - 6) + CPI * sg;
     const int off = xs ? (ks / 2 - 1) * a.dil : 0;
     const int cmax = xs ? PW_R : PW_A;
     const __amdgpu_buffer_rsrc_t r = xs ? rsrc_rows(a.x + (long)Tl.b * PW_R * a.Tmax, PW_R)
@@ -737,33 +741,42 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
     const int t = Tl.t0 + sq + off;
     const bool ok = t >= 0 && t < Tl.T && c0 < cmax;
     sok = ok ? (sok | (1u << ks)) : (sok & ~(1u << ks));
-    const int vo = (min(c0, cmax - 8) * a.Tmax + (ok ? t : 0)) * 4;
+    const int vo = (min(c0, cmax - CPI) * a.Tmax + (ok ? t : 0)) * 4;
 #pragma unroll
-    for (int c = 0; c < 8; ++c) st[ks][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, c * a.Tmax * 4, 0));
+    for (int c = 0; c < CPI; ++c) st[ks][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(r, vo, c * a.Tmax * 4, 0));
   };
   auto stage_store = [&](int ks) {
-    float mx = 0.f, v[8];
+    float mx = 0.f, v[CPI];
 #pragma unroll
-    for (int c = 0; c < 8; ++c) {
+    for (int c = 0; c < CPI; ++c) {
       v[c] = ((sok >> ks) & 1u) ? st[ks][c] : 0.f;
       mx = fmaxf(mx, __builtin_fabsf(v[c]));
     }
     bad |= !(mx < F16_RANGE);
-    h8 hi, lo;
-    split8(v, hi, lo);
-    _Float16* X = Xs + ks * PLANE;
-    *reinterpret_cast<h8*>(X + sq * PX_XR + 8 * sg) = hi;
-    *reinterpret_cast<h8*>(X + sq * PX_XR + 32 + 8 * sg) = lo;
+    _Float16* X = Xs + ks * PLANE + sq * PX_XR + CPI * sg;
+    if constexpr (CPI == 8) {
+      h8 hi, lo;
+      split8(v, hi, lo);
+      *reinterpret_cast<h8*>(X) = hi;
+      *reinterpret_cast<h8*>(X + 32) = lo;
+    } else {
+      h4 hi, lo;
+      split4(f32x4{v[0], v[1], v[2], v[3]}, hi, lo);  // bit-identical to split8 per element
+      *reinterpret_cast<h4*>(X) = hi;
+      *reinterpret_cast<h4*>(X + 32) = lo;
+    }
   };
-  float res[2][4][4];
+  float res[MI][4][4];
   auto res_load = [&](const Tile& Tl) {
-    // waves 0, 1 hold conv1x1_out rows (residual x), waves 2, 3 skip rows (the running skip sum)
-    const __amdgpu_buffer_rsrc_t r = rsrc_rows((wm < 2 ? a.x : a.skip) + (long)Tl.b * 64 * a.Tmax, 64);
+    // the first half of the waves hold conv1x1_out rows (residual x), the rest skip rows (the
+    // running skip sum)
+    const bool outw = wm < NW / 2;
+    const __amdgpu_buffer_rsrc_t r = rsrc_rows((outw ? a.x : a.skip) + (long)Tl.b * 64 * a.Tmax, 64);
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int ch = (wm & 1) * 32 + mi * 16 + 4 * (lane >> 4) + j;
+        const int ch = wm * 16 * MI + mi * 16 + 4 * (lane >> 4) + j - (outw ? 0 : PW_R);
 #pragma unroll
         for (int ni = 0; ni < 4; ++ni) {
           const int t = min(Tl.t0 + nb + ni * 16, Tl.T - 1);
@@ -771,9 +784,9 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
         }
       }
   };
-  f32x4 am[2][4], ac[2][4];
+  f32x4 am[MI][4], ac[MI][4];
   // B operands two n-tiles at a time (16 VGPRs instead of 32: the kernel is at its register limit)
-  auto kstep = [&](const _Float16* X, const h8 (&w)[2][2]) __attribute__((always_inline)) {
+  auto kstep = [&](const _Float16* X, const h8 (&w)[MI][2]) __attribute__((always_inline)) {
 #pragma unroll
     for (int n2 = 0; n2 < 4; n2 += 2) {
       h8 bh[2], bl[2];
@@ -784,7 +797,7 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
         bl[u] = *reinterpret_cast<const h8*>(q + 32);
       }
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi)
+      for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
         for (int u = 0; u < 2; ++u) mfma_x3(w[mi][0], w[mi][1], bh[u], bl[u], am[mi][n2 + u], ac[mi][n2 + u]);
     }
@@ -810,15 +823,15 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
     for (int ks = 0; ks < PX_NK1; ++ks) stage_load(nxt, ks);
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi)
+    for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ni = 0; ni < 4; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int ks = 0; ks < PX_NK1; ++ks) kstep(Xs + ks * PLANE, w1[ks]);
-    // gate: rows R = wm * 32 + mi * 16 + 4 (lane >> 4) + j, pairs (R, R + 1) -> z[R / 2]
+    // gate: rows R = 16 MI wm + 16 mi + 4 (lane >> 4) + j, pairs (R, R + 1) -> z[R / 2]
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
-      const int R = wm * 32 + mi * 16 + 4 * (lane >> 4);
+    for (int mi = 0; mi < MI; ++mi) {
+      const int R = wm * 16 * MI + mi * 16 + 4 * (lane >> 4);
       const int zc = R >> 1;
       _Float16* Z = Zs + (zc >> 5) * PLANE + (zc & 31);
 #pragma unroll
@@ -838,10 +851,10 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
     lds_barrier();
 #pragma unroll
     for (int ks = 0; ks < PX_NK2; ++ks) {
-      h8 w2[2][2];
+      h8 w2[MI][2];
 #pragma unroll
-      for (int mi = 0; mi < 2; ++mi) {
-        const h8* q = W2s + (((2 * wm + mi) * PX_NK2 + ks) * 64 + lane) * 2;
+      for (int mi = 0; mi < MI; ++mi) {
+        const h8* q = W2s + (((MI * wm + mi) * PX_NK2 + ks) * 64 + lane) * 2;
         w2[mi][0] = q[0];
         w2[mi][1] = q[1];
       }
@@ -849,10 +862,10 @@ __global__ __launch_bounds__(256, 1) void pw_layer_x3p_kernel(PwLayerArgs a, con
     }
     // x' = (out + b + x) * 0.25 (parallel_wavegan.py:85); skip (+)= s + b
 #pragma unroll
-    for (int mi = 0; mi < 2; ++mi) {
+    for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
-        const int R = wm * 32 + mi * 16 + 4 * (lane >> 4) + j;
+        const int R = wm * 16 * MI + mi * 16 + 4 * (lane >> 4) + j;
         const bool out_row = R < PW_R;
         const int ch = out_row ? R : R - PW_R;
 #pragma unroll
@@ -889,9 +902,14 @@ void launch_pw_layer_x3(const float* x, const float* c, float* xn, float* skip, 
     TTS_CHECK(ntiles < (1L << 30), "pwgan: too many tiles");
     if (ntiles == 0) return;
     constexpr int lds = (PX_NK1 + 2) * 64 * PX_XR * 2 + 8 * PX_NK2 * 64 * 32;
-    ensure_dyn_lds((const void*)pw_layer_x3p_kernel, lds);
     const int grid = (int)std::min<long>(ntiles, device_cu_count());
-    pw_layer_x3p_kernel<<<grid, 256, lds, st>>>(a, W1x, W2x, oflow, B, (int)ntiles);
+    if (var == 2) {  // TTS_PWGAN_TILE=2: 4 waves, 2 m-tiles each
+      ensure_dyn_lds((const void*)pw_layer_x3p_kernel<4>, lds);
+      pw_layer_x3p_kernel<4><<<grid, 256, lds, st>>>(a, W1x, W2x, oflow, B, (int)ntiles);
+    } else {
+      ensure_dyn_lds((const void*)pw_layer_x3p_kernel<8>, lds);
+      pw_layer_x3p_kernel<8><<<grid, 512, lds, st>>>(a, W1x, W2x, oflow, B, (int)ntiles);
+    }
     HIP_OK(hipGetLastError());
     return;
   }
