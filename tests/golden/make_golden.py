@@ -461,6 +461,9 @@ if __name__ == "__main__":
         # multi-speaker Glow-TTS built directly (setup_model passes c_in_channels=0, which cannot
         # take g): 4 speakers, c_in 36 (not a multiple of 16, to cover the channel padding)
         glow_case("glow_spk", seed=41, data_seed=42, num_speakers=4, c_in=36)
+    if "glow_spk_tfm" in which:
+        # the same conditioning behind the transformer encoder, c_in 64 (no channel padding)
+        glow_case("glow_spk_tfm", "transformer", seed=43, data_seed=44, num_speakers=3, c_in=64)
     if "taco_state" in which:
         taco_state_case("taco_state")
     if "taco_amplified" in which:

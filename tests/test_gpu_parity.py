@@ -1088,19 +1088,23 @@ def test_glow_tts_matches_reference(name, enc):
 def _glow_spk_model(fx):
     from tts_amd import GlowTts
     from tts_amd.spec import GlowConfig, glow_spec
-    cfg = GlowConfig(num_speakers=int(fx["num_speakers"]), c_in_channels=int(fx["c_in"]))
+    enc = str(fx["encoder_type"])
+    cfg = GlowConfig(encoder_type=enc, num_speakers=int(fx["num_speakers"]), c_in_channels=int(fx["c_in"]))
     sd = synth_state_dict(glow_spec(cfg), int(fx["seed"]))
-    m = GlowTts(num_chars=cfg.num_chars, num_speakers=cfg.num_speakers, c_in_channels=cfg.c_in_channels)
+    m = GlowTts(num_chars=cfg.num_chars, num_speakers=cfg.num_speakers, c_in_channels=cfg.c_in_channels,
+                encoder_type=enc, use_encoder_prenet=enc != "gatedconv")
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     return m.cuda().eval(), sd
 
 
-def test_glow_multispeaker_matches_reference():
-    """Multi-speaker GlowTts (4 speakers, c_in 36) with g = speaker ids: the reference's own
-    GlowTts.inference(x, x_lengths, g) output (make_golden.py glow_spk), both utterances (speakers 2
-    and 0) in ONE batched call: durations / path exact, means and mel <= 1e-4."""
+@pytest.mark.parametrize("name", ["glow_spk", "glow_spk_tfm"])
+def test_glow_multispeaker_matches_reference(name):
+    """Multi-speaker GlowTts with g = speaker ids: the reference's own GlowTts.inference(x,
+    x_lengths, g) output (make_golden.py glow_spk: gated-conv encoder, 4 speakers, c_in 36;
+    glow_spk_tfm: transformer encoder, 3 speakers, c_in 64), both utterances (speakers 2 and 0) in
+    ONE batched call: durations / path exact, means and mel <= 1e-4."""
     _dev()
-    fx = load_fixture("glow_spk")
+    fx = load_fixture(name)
     m, _ = _glow_spk_model(fx)
     ids = [fx["u0_ids"], fx["u1_ids"]]
     T = max(len(x) for x in ids)

@@ -175,7 +175,8 @@ def test_tacotron2_oracle_decoder_variants_match_reference(name):
 
 
 @pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable"),
-                                      ("glow_tfm", "transformer"), ("glow_spk", "gatedconv")])
+                                      ("glow_tfm", "transformer"), ("glow_spk", "gatedconv"),
+                                      ("glow_spk_tfm", "transformer")])
 def test_glow_oracle_matches_reference(name, enc):
     """Glow-TTS, every encoder the reference configs use (gated conv; time-depth-separable and
     transformer with the ConvLayerNorm prenet) and the multi-speaker model (glow_spk: emb_g of 4
