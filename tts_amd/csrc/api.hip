@@ -1075,28 +1075,43 @@ __global__ void bcast_rows_kernel(const float* src, int n, float* dst, int rows)
 // base = 0 on the attention_rnn / decoder_rnn / processed-inputs columns, the projection bias on
 // the projection columns [pj0, N). With no speaker (Es = 0) only the projection columns are built.
 constexpr int SPK_BMAX = 64;
+// Per-row speaker biases W_s s (+ the projection bias for the projection columns): out[m][n] for
+// rows m < Bp. Workgroup = 64 columns x 4 waves, wave q summing the speaker dims e = q, q + 4, ...
+// (the speaker values are wave-uniform scalar loads), the 4 partials added in a fixed order
+// through LDS. Round 4: the previous form (one column per thread over all dims, 64 accumulators
+// predicated on B) ran ~40 workgroups for ~400 us per call.
+template <int MB>
 __global__ __launch_bounds__(256) void spk_bias_kernel(const float* __restrict__ spk, int B, int Es,
                                                        const float* __restrict__ WT, int N,
                                                        const float* __restrict__ pjb, int pj0, int Bp,
                                                        float* __restrict__ out) {
-  extern __shared__ float sv[];  // [B][Es]
-  for (int i = threadIdx.x; i < B * Es; i += blockDim.x) sv[i] = spk[i];
-  __syncthreads();
-  const int n = blockIdx.x * blockDim.x + threadIdx.x;
-  if (n >= N) return;
-  float acc[SPK_BMAX];
+  __shared__ float red[3][MB][64];
+  const int c = threadIdx.x & 63;
+  const int q = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int n = blockIdx.x * 64 + c;
+  const int nc = min(n, N - 1);
+  float acc[MB];
 #pragma unroll
-  for (int m = 0; m < SPK_BMAX; ++m) acc[m] = 0.f;
-  for (int e = 0; e < Es; ++e) {
-    const float w = WT[(long)e * N + n];
+  for (int m = 0; m < MB; ++m) acc[m] = 0.f;
+  for (int e = q; e < Es; e += 4) {
+    const float w = WT[(long)e * N + nc];
 #pragma unroll
-    for (int m = 0; m < SPK_BMAX; ++m)
-      if (m < B) acc[m] = fmaf(sv[m * Es + e], w, acc[m]);
+    for (int m = 0; m < MB; ++m) {
+      const float sv = m < B ? spk[m * Es + e] : 0.f;  // wave-uniform
+      acc[m] = fmaf(sv, w, acc[m]);
+    }
   }
+  if (q > 0) {
+#pragma unroll
+    for (int m = 0; m < MB; ++m) red[q - 1][m][c] = acc[m];
+  }
+  __syncthreads();
+  if (q != 0 || n >= N) return;
   const float base = n >= pj0 ? pjb[n - pj0] : 0.f;
 #pragma unroll
-  for (int m = 0; m < SPK_BMAX; ++m)
-    if (m < Bp) out[(long)m * N + n] = base + (m < B ? acc[m] : 0.f);
+  for (int m = 0; m < MB; ++m)
+    if (m < Bp) out[(long)m * N + n] = base + (m < B ? ((acc[m] + red[0][m][c]) + red[1][m][c]) + red[2][m][c] : 0.f);
+  for (int m = MB; m < Bp; ++m) out[(long)m * N + n] = base;  // rows past the speaker rows (Bp > MB)
 }
 
 void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_out, hipStream_t s) {
@@ -1377,15 +1392,18 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     grow<float>(W.spkb, (size_t)64 * (8320 + 112 * 16), W.gen);
     TTS_CHECK(W.B <= SPK_BMAX || !M.spk_dim, "multi-speaker decoding: at most 64 utterances per call");
     const int Bs = M.spk_dim ? W.B : 0;
-    // 64 rows of a 512-d speaker vector: 128 KiB of dynamic LDS
-    ensure_dyn_lds((const void*)spk_bias_kernel, SPK_BMAX * 512 * 4);
     TTS_CHECK(M.spk_dim <= 512, "speaker vectors of at most 512 dims");
     // Graves with speakers: the projection columns hold W_s s alone; the kernel adds the bias and
     // scales W_s s by the step's sum of attention weights (PArgs::spk_scale)
     a.spk_scale = M.graves && M.spk_dim ? 1 : 0;
-    spk_bias_kernel<<<(N + 255) / 256, 256, (size_t)Bs * M.spk_dim * 4, s>>>(
-        W.spk.f(), Bs, M.spk_dim, M.spk_dim ? M.spk_wT.f() : nullptr, N, M.pj_b.f(), a.spk_scale ? N : pj0, Bp,
-        W.spkb.f());
+    {
+      const float* wt = M.spk_dim ? M.spk_wT.f() : nullptr;
+      const int es = M.spk_dim, p0 = a.spk_scale ? N : pj0;
+      const dim3 g((N + 63) / 64);
+      if (Bs <= 16) spk_bias_kernel<16><<<g, 256, 0, s>>>(W.spk.f(), Bs, es, wt, N, M.pj_b.f(), p0, Bp, W.spkb.f());
+      else if (Bs <= 32) spk_bias_kernel<32><<<g, 256, 0, s>>>(W.spk.f(), Bs, es, wt, N, M.pj_b.f(), p0, Bp, W.spkb.f());
+      else spk_bias_kernel<64><<<g, 256, 0, s>>>(W.spk.f(), Bs, es, wt, N, M.pj_b.f(), p0, Bp, W.spkb.f());
+    }
     HIP_OK(hipGetLastError());
     a.spk_ld = N;
     a.pjb_rows = W.spkb.f() + pj0;
@@ -1755,7 +1773,10 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
           }
     }
     pack_conv(G.convT[i], Wm, need(m, nm + ".bias", {cout}).d, cin, cout, 2, 1, u, pls);
-    if (G.convT[i].W16.p && conv_x3_supported(cin, u * cout, 2, 1)) {
+    bool wm_in_range = true;
+    for (float v : Wm) wm_in_range &= std::fabs(v) < F16_RANGE;
+    // the merged GEMM has u * cout rows, so it is covered even where cout alone is not (full-band 64 -> 32)
+    if (wm_in_range && conv_x3_supported(cin, u * cout, 2, 1)) {
       const auto& bias = need(m, nm + ".bias", {cout}).d;
       std::vector<float> bm((size_t)u * cout);
       for (size_t r = 0; r < bm.size(); ++r) bm[r] = bias[r / u];
@@ -1804,6 +1825,9 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
         for (int ci = 0; ci < C; ++ci)
           for (int k = 0; k < 7; ++k) wo[((size_t)ci * 7 + k) * 4 + o] = w[((size_t)o * C + ci) * 7 + k];
       G.out_w.upload(wo);
+      G.out_b.upload(bo);
+    } else if (out_ch == 1) {  // full-band: [c][k] for launch_out_conv1
+      G.out_w.upload(w);
       G.out_b.upload(bo);
     }
   }
@@ -2014,6 +2038,12 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     tail->mul = mul;
     return up;
   }
+  if (G.out_ch == 1) {  // full-band output stage on the VALU (melgan_out.hip)
+    HIP_OK(hipMemsetAsync(out, 0, (size_t)B * Ls * 4, s));
+    launch_out_conv1(x, (long)C * Ls, Ls, C, G.out_w.f(), G.out_b.f(), W.lens.i(), 2 * pad, mul, (int)(Lb * mul), B,
+                     out, Ls, s);
+    return up;
+  }
   ConvCall o = cc;
   o.s[0] = src_of(x, (long)C * Ls, Ls, 1, C, 1);
   o.pad_mode = 1;
@@ -2200,6 +2230,7 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
     ConvCall cc;  // gates_in = x W_ih^T + b  (time-major rows, K = 1)
     cc.lens = W.lens.i();
     cc.B = B;
+    cc.oflow = x3_flag(c);
     cc.max_q = T_max;
     cc.s[0] = src_of(in, (long)T_max * din, 1, din, din, 0);
     cc.out = W.g.f();
@@ -2215,6 +2246,7 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
       ConvCall cp;
       cp.lens = W.lens.i();
       cp.B = B;
+      cp.oflow = x3_flag(c);
       cp.max_q = T_max;
       cp.s[0] = src_of(W.o.f(), (long)T_max * H, 1, H, H, 0);
       cp.out = W.p.f();
@@ -3210,7 +3242,7 @@ int tts_ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, i
     TTS_CHECK(c && d_x && h_lens && d_out, "null argument");
     DeviceGuard g(c->device);
     enter(c, stream);
-    ge2e_infer(c, d_x, h_lens, B, T_max, d_out);
+    with_x3_fallback(c, [&] { ge2e_infer(c, d_x, h_lens, B, T_max, d_out); });
     leave(c, stream);
   });
 }

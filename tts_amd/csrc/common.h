@@ -239,6 +239,8 @@ void launch_resstack_x3(const StackArgs& a, const int* h_lens, int C, hipStream_
 
 // fused MB-MelGAN output conv (C -> 4, k7, LReLU + reflect pad 3 + tanh) and PQMF synthesis
 // (melgan_out.hip); returns false when the shape is not covered (N != 4, 63 taps, C not 32/48)
+void launch_out_conv1(const float* x, long xb, long xc, int C, const float* W, const float* bo, const int* lens,
+                      int len_add, int L_mul, int maxL, int B, float* y, long yb, hipStream_t s);
 bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, const float* bo, const float* G,
                      int N, int taps, const int* lens, int len_add, int L_mul, int maxL, int B, float* y, long yb,
                      hipStream_t s);

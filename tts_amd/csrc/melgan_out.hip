@@ -161,3 +161,89 @@ bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, c
   HIP_OK(hipGetLastError());
   return true;
 }
+
+// Full-band MelGAN output stage (round 4): y = tanh(Conv1d(C -> 1, k7)(ReflectionPad1d(3)(LeakyReLU(x))))
+// (melgan_generator.py:75-81) on the VALU. The generic MFMA conv pads the single output channel to
+// a 16-row tile (16x the work, ~430 us at 2.35 M positions); here a thread makes OC1_P consecutive
+// positions from an (OC1_P + 8)-value window per channel (16-byte loads away from the utterance
+// ends, where ReflectionPad1d needs per-element indices), weights [c][k] wave-uniform.
+constexpr int OC1_P = 16;
+
+__global__ __launch_bounds__(256) void out_conv1_kernel(const float* __restrict__ x, long xb, long xc, int C,
+                                                        const float* __restrict__ W, const float* __restrict__ bo,
+                                                        const int* __restrict__ lens, int len_add, int L_mul,
+                                                        float* __restrict__ y, long yb, int vec) {
+  constexpr int P = OC1_P, NV = P + 8;
+  const int b = blockIdx.y;
+  const int L = (lens[b] + len_add) * L_mul;
+  const int t0 = (blockIdx.x * 256 + threadIdx.x) * P;
+  if (t0 >= L) return;
+  const float* xr = x + b * xb;
+  const float b0 = bo[0];
+  float acc[P];
+#pragma unroll
+  for (int j = 0; j < P; ++j) acc[j] = b0;
+  if (vec && t0 >= 4 && t0 + P + 4 <= L) {
+    // v[i] = x[t0 - 4 + i]; position t0 + j, tap k reads x[t0 + j + k - 3] = v[j + k + 1]
+    for (int c = 0; c < C; ++c) {
+      const float4* p = reinterpret_cast<const float4*>(xr + (long)c * xc + t0 - 4);
+      float v[NV];
+#pragma unroll
+      for (int i = 0; i < NV / 4; ++i) {
+        const float4 q = p[i];
+        v[4 * i] = lrelu02(q.x);
+        v[4 * i + 1] = lrelu02(q.y);
+        v[4 * i + 2] = lrelu02(q.z);
+        v[4 * i + 3] = lrelu02(q.w);
+      }
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const float w = W[c * 7 + k];
+#pragma unroll
+        for (int j = 0; j < P; ++j) acc[j] = fmaf(w, v[j + k + 1], acc[j]);
+      }
+    }
+  } else {
+    int idx[P + 6];
+#pragma unroll
+    for (int i = 0; i < P + 6; ++i) {  // ReflectionPad1d(3), then clamped (positions past L are never stored)
+      int p = t0 - 3 + i;
+      if (p < 0) p = -p;
+      if (p >= L) p = 2 * (L - 1) - p;
+      idx[i] = p < 0 ? 0 : (p >= L ? L - 1 : p);
+    }
+    for (int c = 0; c < C; ++c) {
+      const float* xc_ = xr + (long)c * xc;
+      float v[P + 6];
+#pragma unroll
+      for (int i = 0; i < P + 6; ++i) v[i] = lrelu02(xc_[idx[i]]);
+#pragma unroll
+      for (int k = 0; k < 7; ++k) {
+        const float w = W[c * 7 + k];
+#pragma unroll
+        for (int j = 0; j < P; ++j) acc[j] = fmaf(w, v[j + k], acc[j]);
+      }
+    }
+  }
+  float* yr = y + b * yb + t0;
+  if (vec && t0 + P <= L) {
+#pragma unroll
+    for (int j = 0; j < P; j += 4)
+      *reinterpret_cast<float4*>(yr + j) = make_float4(tanhf(acc[j]), tanhf(acc[j + 1]), tanhf(acc[j + 2]), tanhf(acc[j + 3]));
+  } else {
+#pragma unroll
+    for (int j = 0; j < P; ++j)
+      if (t0 + j < L) yr[j] = tanhf(acc[j]);
+  }
+}
+
+void launch_out_conv1(const float* x, long xb, long xc, int C, const float* W, const float* bo, const int* lens,
+                      int len_add, int L_mul, int maxL, int B, float* y, long yb, hipStream_t s) {
+  if (maxL <= 0 || B <= 0) return;
+  const int vec = (reinterpret_cast<uintptr_t>(x) & 15) == 0 && (reinterpret_cast<uintptr_t>(y) & 15) == 0 &&
+                  xb % 4 == 0 && xc % 4 == 0 && yb % 4 == 0;
+  const int per = 256 * OC1_P;
+  out_conv1_kernel<<<dim3((maxL + per - 1) / per, B), 256, 0, s>>>(x, xb, xc, C, W, bo, lens, len_add, L_mul, y, yb,
+                                                                    vec);
+  HIP_OK(hipGetLastError());
+}
