@@ -1044,6 +1044,32 @@ def test_ge2e_speaker_encoder_matches_reference(tag, proj):
     assert np.abs(cemb - fx[f"{tag}_cemb"]).max() <= 1e-5
 
 
+@pytest.mark.parametrize("proj", [True, False])
+def test_ge2e_layer_pipeline_matches_per_layer_path(proj):
+    """The speaker encoder's layer-pipelined launch (B <= 16, encoder.hip ge2e_pipe_kernel, the
+    previous layer's Linear folded into W_ih) against the per-layer launches (B > 16 takes them):
+    18 ragged sequences in one call (per-layer) and as two calls of 9 (pipelined), <= 1e-5."""
+    from tts_amd import SpeakerEncoder
+    from tts_amd.spec import Ge2eConfig, ge2e_spec
+    from tts_amd.weights import synth_state_dict
+    _dev()
+    m = SpeakerEncoder(40, 256, 768, 3, proj)
+    sd = synth_state_dict(ge2e_spec(Ge2eConfig(use_lstm_with_projection=proj)), 7)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    rng = np.random.RandomState(3)
+    lens = [int(v) for v in rng.randint(20, 97, 18)]
+    x = np.zeros((18, max(lens), 40), np.float32)
+    for i, n in enumerate(lens):
+        x[i, :n] = rng.rand(n, 40).astype(np.float32)
+    xt = torch.from_numpy(x).cuda()
+    full = m.inference(xt, lengths=lens).cpu().numpy()
+    halves = np.concatenate([m.inference(xt[:9], lengths=lens[:9]).cpu().numpy(),
+                             m.inference(xt[9:], lengths=lens[9:]).cpu().numpy()])
+    assert np.isfinite(full).all()
+    assert np.abs(full - halves).max() <= 1e-5
+
+
 # --------------------------------------------------------------------------------- Glow-TTS
 @pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable"),
                                       ("glow_tfm", "transformer")])

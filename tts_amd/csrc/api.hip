@@ -54,6 +54,8 @@ void launch_pw_out(const float* skip, float scale, const float* W3, const float*
 void launch_glow_speaker(const int* spk, const float* table, int c_in, int c_pad, float* g, int B, hipStream_t s);
 void launch_glow_embed(const int64_t* ids, int T, const float* table, int rows, int D, const int* lens, float* out,
                        int B, hipStream_t s);
+bool launch_ge2e_pipe(const uint16_t* const* w16, const float* const* bias, int nl, const float* gin0, const int* lens,
+                      int T_max, int B, float* hbuf, unsigned* bar, float* out, hipStream_t s);
 bool launch_lstm768_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
                             int B, float* hbuf, unsigned* bar, float* out, hipStream_t s);
 void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_max, int B, float* hbuf, float* cbuf,
@@ -396,6 +398,10 @@ struct Ge2eModel {
   DevBuf whh16[4];       // W_hh split-f16 (empty if out of the f16 range)
   ConvLayer proj_l[4];   // with_proj: Linear(768 -> proj) per layer as a K = 1 conv
   DevBuf lin_w, lin_b;   // without projection: final Linear (proj x H) + bias
+  // layer pipeline (encoder.hip ge2e_pipe_kernel): layer l >= 1 as split-f16 [W_hh | W_in] rows
+  // (W_in = W_ih^l W_proj^{l-1} folded in fp64, or W_ih^l) and b_ih + b_hh, tile order
+  DevBuf wpipe[4], bpipe[4];
+  bool pipe_ok = false;
 };
 
 struct Ge2eWS {
@@ -2199,6 +2205,44 @@ void ge2e_finalize(tts_ctx* c, int in_dim, int proj, int lstm, int nl, int with_
     G.lin_w.upload(need(h, "layers.linear.weight", {proj, H}).d);
     G.lin_b.upload(need(h, "layers.linear.bias", {proj}).d);
   }
+  G.pipe_ok = G.whh16[0].p != nullptr;
+  for (int l = 1; l < nl && G.pipe_ok; ++l) {
+    const std::string pfx = with_proj ? "layers." + std::to_string(l) + ".lstm." : "layers.lstm.";
+    const std::string sfx = with_proj ? "_l0" : "_l" + std::to_string(l);
+    const int din = with_proj ? proj : H;
+    const auto& wih = need(h, pfx + "weight_ih" + sfx, {4 * H, din}).d;
+    const auto& whh = need(h, pfx + "weight_hh" + sfx, {4 * H, H}).d;
+    const auto& bih = need(h, pfx + "bias_ih" + sfx, {4 * H}).d;
+    const auto& bhh = need(h, pfx + "bias_hh" + sfx, {4 * H}).d;
+    std::vector<float> win;
+    if (with_proj) {  // the previous layer's Linear (no bias, model.py:22) folded into W_ih
+      const auto& wl = need(h, "layers." + std::to_string(l - 1) + ".linear.weight", {proj, H}).d;
+      win.assign((size_t)4 * H * H, 0.f);
+      std::vector<double> acc(H);
+      for (int r = 0; r < 4 * H; ++r) {
+        std::fill(acc.begin(), acc.end(), 0.0);
+        for (int j = 0; j < proj; ++j) {
+          const double a = wih[(size_t)r * proj + j];
+          const float* wr = &wl[(size_t)j * H];
+          for (int k = 0; k < H; ++k) acc[k] += a * wr[k];
+        }
+        for (int k = 0; k < H; ++k) win[(size_t)r * H + k] = (float)acc[k];
+      }
+    } else {
+      win = wih;
+    }
+    const auto t1 = lstm_tile_rows(whh, H, H), t2 = lstm_tile_rows(win, H, H);
+    std::vector<float> wc((size_t)4 * H * 2 * H);
+    for (int r = 0; r < 4 * H; ++r) {
+      std::memcpy(&wc[(size_t)r * 2 * H], &t1[(size_t)r * H], H * 4);
+      std::memcpy(&wc[(size_t)r * 2 * H + H], &t2[(size_t)r * H], H * 4);
+    }
+    upload_split_rows(G.wpipe[l], wc, 4 * H, 2 * H);
+    std::vector<float> bs(4 * H);
+    for (int i = 0; i < 4 * H; ++i) bs[i] = bih[i] + bhh[i];
+    G.bpipe[l].upload(lstm_tile_rows(bs, H, 1));
+    G.pipe_ok = G.wpipe[l].p != nullptr;
+  }
   HIP_OK(hipDeviceSynchronize());
   G.ready = true;
 }
@@ -2226,7 +2270,48 @@ void ge2e_infer(tts_ctx* c, const float* d_x, const int32_t* h_lens, int B, int 
   HIP_OK(hipGetLastError());
   const float* in = W.x.f();
   int din = G.in_pad;
-  for (int l = 0; l < G.nl; ++l) {
+  // all layers in one persistent launch (encoder.hip ge2e_pipe_kernel); TTS_GE2E_PIPE=0 keeps
+  // one launch per layer with the input projections as convs
+  static const bool pipe_env = [] {
+    const char* e = std::getenv("TTS_GE2E_PIPE");
+    return !(e && std::string(e) == "0");
+  }();
+  bool piped = false;
+  if (pipe_env && c->gemm_x3 && G.pipe_ok && B <= 16) {
+    ConvCall cc;  // layer-0 input gates
+    cc.lens = W.lens.i();
+    cc.B = B;
+    cc.oflow = x3_flag(c);
+    cc.max_q = T_max;
+    cc.s[0] = src_of(in, (long)T_max * din, 1, din, din, 0);
+    cc.out = W.g.f();
+    cc.ob = (long)T_max * 4 * H;
+    cc.oc = 1;
+    cc.ot = 4 * H;
+    run_conv(G.gin[0], cc, s);
+    const uint16_t* w16[4] = {nullptr, nullptr, nullptr, nullptr};
+    const float* bias[4] = {nullptr, nullptr, nullptr, nullptr};
+    for (int l = 0; l < G.nl; ++l) {
+      w16[l] = l == 0 ? G.whh16[0].h() : G.wpipe[l].h();
+      bias[l] = l == 0 ? nullptr : G.bpipe[l].f();
+    }
+    piped = launch_ge2e_pipe(w16, bias, G.nl, W.g.f(), W.lens.i(), T_max, B, W.hbuf.f(),
+                             reinterpret_cast<unsigned*>(W.bar.p), W.o.f(), s);
+    if (piped && G.with_proj) {  // the last layer's Linear
+      ConvCall cp;
+      cp.lens = W.lens.i();
+      cp.B = B;
+      cp.oflow = x3_flag(c);
+      cp.max_q = T_max;
+      cp.s[0] = src_of(W.o.f(), (long)T_max * H, 1, H, H, 0);
+      cp.out = W.p.f();
+      cp.ob = (long)T_max * G.proj;
+      cp.oc = 1;
+      cp.ot = G.proj;
+      run_conv(G.proj_l[G.nl - 1], cp, s);
+    }
+  }
+  for (int l = 0; l < G.nl && !piped; ++l) {
     ConvCall cc;  // gates_in = x W_ih^T + b  (time-major rows, K = 1)
     cc.lens = W.lens.i();
     cc.B = B;

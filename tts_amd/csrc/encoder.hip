@@ -308,3 +308,166 @@ void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_ma
   }
   HIP_OK(hipGetLastError());
 }
+
+// GE2E layer pipeline (round 4): the nl 768-unit LSTM layers of the speaker encoder
+// (TTS/speaker_encoder/model.py:7-58: LSTMWithProjection x nl, or one nl-layer nn.LSTM) in ONE
+// persistent launch. Layer l computes time t = s - l in global step s, so a call takes T + nl - 1
+// grid-barrier steps instead of nl x T, and the layers' input projections run inside the
+// recurrence instead of as convs between layer launches:
+//   gates^l_t = W_hh^l h^l_{t-1} + W_in^l h^{l-1}_t + b^l   (l >= 1; layer 0 reads its precomputed
+//   input gates), W_in^l = W_ih^l W_proj^{l-1} (the projection folded on the host, fp64) or W_ih^l.
+// h^{l-1}_t was written by layer l - 1 in step s - 1, like h^l_{t-1}: one barrier per step covers
+// both edges. Workgroup (l, tile) owns hidden units 12 tile .. 12 tile + 11 (3 gate-interleaved
+// 16-row tiles, lstm_tile_rows order); its 8 waves split the K range (layer >= 1: waves 0-3 the
+// recurrent half, 4-7 the input half) for all 3 tiles, with every weight fragment in VGPRs, and
+// combine through LDS; thread (m, unit) keeps the cell state. Split-f16 only (|h| <= 1, weights
+// range-checked at pack time), B <= 16.
+//   w16  : per layer [192 m-tiles][NKS k-steps][64][16] (split16.h pack_split_a), NKS = 24 / 48
+//   hbuf : [2 ping-pong][nl][16 x 768] fragment order (zeroed by the launcher)
+//   out  : (B, T_max, 768), the last layer's h
+struct GePipeArgs {
+  const uint16_t* w16[4];
+  const float* bias[4];
+  const float* gin0;  // (B, T_max, 3072) layer-0 input gates incl. biases, tile order
+  const int* lens;
+  int T_max, B, nl;
+  float* hbuf;
+  float* out;
+  unsigned* bar;
+};
+constexpr int GP_TILES = 64, GP_NW = 8;
+
+template <class T>
+__device__ __forceinline__ T pick4(T v0, T v1, T v2, T v3, int i) {  // wave-uniform, no indexed kernarg
+  return i == 0 ? v0 : (i == 1 ? v1 : (i == 2 ? v2 : v3));
+}
+
+__global__ __launch_bounds__(64 * GP_NW) void ge2e_pipe_kernel(GePipeArgs a) {
+  constexpr int H = 768, KSH = H / 32;  // 24 k-steps per 768-wide operand
+  __shared__ float part[GP_NW][3][16 * 17];
+  __shared__ int sflag;
+  const int l = blockIdx.x / GP_TILES, tile = blockIdx.x % GP_TILES;
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int KS = l == 0 ? KSH / GP_NW : 2 * KSH / GP_NW;  // k-steps per wave: 3 / 6
+  const int nks = l == 0 ? KSH : 2 * KSH;
+  const h8* W = reinterpret_cast<const h8*>(pick4(a.w16[0], a.w16[1], a.w16[2], a.w16[3], l));
+  h8 w[6][3][2];
+#pragma unroll
+  for (int j = 0; j < 6; ++j)
+#pragma unroll
+    for (int mi = 0; mi < 3; ++mi) {
+      const int ks = wave * KS + (j < KS ? j : 0);
+      const long f = (((long)(3 * tile + mi) * nks + ks) * 64 + lane) * 2;
+      w[j][mi][0] = W[f];
+      w[j][mi][1] = W[f + 1];
+    }
+  // epilogue threads: (batch row m, unit uu of the workgroup's 12)
+  const bool eth = tid < 192;
+  const int m = eth ? tid / 12 : 0, uu = tid % 12, mi_e = uu >> 2, u = uu & 3;
+  const int Tm = m < a.B ? a.lens[m] : 0;
+  const int unit = 12 * tile + uu, trow = (3 * tile + mi_e) * 16;
+  const float* bl = pick4(a.bias[0], a.bias[1], a.bias[2], a.bias[3], l);
+  float bq[4] = {0.f, 0.f, 0.f, 0.f};
+  if (l > 0) {
+#pragma unroll
+    for (int q = 0; q < 4; ++q) bq[q] = bl[trow + q * 4 + u];
+  }
+  const float* g0 = a.gin0 + (long)min(m, a.B - 1) * a.T_max * 3072 + trow + u;
+  float gin[4] = {0.f, 0.f, 0.f, 0.f};
+  auto load_gin = [&](int t) {
+    const int tc = min(max(t, 0), a.T_max - 1);
+#pragma unroll
+    for (int q = 0; q < 4; ++q) gin[q] = g0[(long)tc * 3072 + q * 4];
+  };
+  if (l == 0) load_gin(0);
+  const int l1 = 32 * ((lane >> 4) & 1) + (lane & 15);
+  const int S = a.T_max + a.nl - 1;
+  float cst = 0.f;
+  unsigned gen = 0;
+  for (int s = 0; s < S; ++s) {
+    const int t = s - l;
+    if (t >= 0 && t < a.T_max) {
+      const size_t slab = (size_t)16 * H;
+      const float* hp = a.hbuf + ((size_t)(s & 1) * a.nl + l) * slab;
+      const float* hin = a.hbuf + ((size_t)(s & 1) * a.nl + (l > 0 ? l - 1 : 0)) * slab;
+      // this wave's operand: the recurrent half (k-steps < 24) or the input half, never both
+      const bool inh = wave * KS >= KSH;
+      const float* src = inh ? hin : hp;
+      const int k0 = wave * KS - (inh ? KSH : 0);
+      f32x4 x[6][2];
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (j < KS) {
+          const int c = 2 * (k0 + j) + (lane >> 5);
+          x[j][0] = ldc4(src, (c * 64 + l1) * 16);
+          x[j][1] = ldc4(src, (c * 64 + l1 + 16) * 16);
+        }
+      f32x4 am[3], ac[3];
+#pragma unroll
+      for (int mi = 0; mi < 3; ++mi) am[mi] = ac[mi] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int j = 0; j < 6; ++j)
+        if (j < KS) {
+          const float v[8] = {x[j][0][0], x[j][0][1], x[j][0][2], x[j][0][3],
+                              x[j][1][0], x[j][1][1], x[j][1][2], x[j][1][3]};
+          h8 xh, xl;
+          split8(v, xh, xl);
+#pragma unroll
+          for (int mi = 0; mi < 3; ++mi) mfma_x3(xh, xl, w[j][mi][0], w[j][mi][1], am[mi], ac[mi]);
+        }
+#pragma unroll
+      for (int mi = 0; mi < 3; ++mi)
+#pragma unroll
+        for (int jj = 0; jj < 4; ++jj)
+          part[wave][mi][(4 * (lane >> 4) + jj) * 17 + (lane & 15)] = x3_value(am[mi][jj], ac[mi][jj]);
+      lds_barrier();
+      if (eth && m < a.B && t < Tm) {
+        float pre[4];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          const int n = q * 4 + u;
+          float sum = part[0][mi_e][m * 17 + n];
+#pragma unroll
+          for (int wv = 1; wv < GP_NW; ++wv) sum += part[wv][mi_e][m * 17 + n];
+          pre[q] = sum + (l == 0 ? gin[q] : bq[q]);
+        }
+        cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
+        const float hn = sigm_f(pre[3]) * tanh_f(cst);
+        float* ho = a.hbuf + ((size_t)((s + 1) & 1) * a.nl + l) * slab;
+        stc_quad(ho, (int)frag_idx(m, unit, H), hn);  // a quad = 4 units of one row: one 16-byte store
+        if (l == a.nl - 1) a.out[((long)m * a.T_max + t) * H + unit] = hn;
+      }
+    }
+    if (s + 1 < S) {
+      gsync_arrive(a.bar, gen);
+      if (l == 0) load_gin(t + 1);
+      if (!gsync_wait(a.bar, gen, &sflag)) return;
+    }
+  }
+}
+
+// false: B or nl outside the pipeline's geometry (the caller runs the per-layer kernels)
+bool launch_ge2e_pipe(const uint16_t* const* w16, const float* const* bias, int nl, const float* gin0, const int* lens,
+                      int T_max, int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
+  if (B < 1 || B > 16 || nl < 1 || nl > 4 || GP_TILES * nl > device_cu_count()) return false;
+  for (int l = 0; l < nl; ++l)
+    if (!w16[l] || (l > 0 && !bias[l])) return false;
+  GePipeArgs a{};
+  for (int l = 0; l < 4; ++l) {
+    a.w16[l] = w16[l < nl ? l : 0];
+    a.bias[l] = l > 0 && l < nl ? bias[l] : nullptr;
+  }
+  a.gin0 = gin0;
+  a.lens = lens;
+  a.T_max = T_max;
+  a.B = B;
+  a.nl = nl;
+  a.hbuf = hbuf;
+  a.out = out;
+  a.bar = bar;
+  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * nl * 16 * 768 * 4, s));
+  arm_barrier(bar, 1, s);
+  void* args[] = {(void*)&a};
+  launch_resident((const void*)ge2e_pipe_kernel, dim3(GP_TILES * nl), dim3(64 * GP_NW), args, 0, s);
+  return true;
+}
