@@ -341,6 +341,7 @@ static int cx_tile(int Cout) {
   if (Cout == 80) return CX_T80;
   if (Cout == 48) return CX_T48;
   if (Cout % 64 == 0) return CX_T64;
+  if (Cout % 80 == 0) return CX_T80;  // several 80-row tiles (Glow-TTS end convs: 160 rows)
   return CX_NONE;
 }
 
