@@ -2963,6 +2963,7 @@ void pwgan_infer(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int
   cc.B = B;
   cc.len_add = 2 * pad;
   cc.s[0] = src_of(mel, (long)80 * M_max, M_max, 1, 80, 0);
+  cc.oflow = x3_flag(c);
   cc.pad_mode = 2;
   cc.rep_pad = pad;
   cc.max_q = Lf;
