@@ -1044,17 +1044,18 @@ def test_ge2e_speaker_encoder_matches_reference(tag, proj):
     assert np.abs(cemb - fx[f"{tag}_cemb"]).max() <= 1e-5
 
 
-@pytest.mark.parametrize("proj", [True, False])
-def test_ge2e_layer_pipeline_matches_per_layer_path(proj):
+@pytest.mark.parametrize("proj,nl", [(True, 3), (False, 3), (True, 2), (False, 4), (True, 1)])
+def test_ge2e_layer_pipeline_matches_per_layer_path(proj, nl):
     """The speaker encoder's layer-pipelined launch (B <= 16, encoder.hip ge2e_pipe_kernel, the
     previous layer's Linear folded into W_ih) against the per-layer launches (B > 16 takes them):
-    18 ragged sequences in one call (per-layer) and as two calls of 9 (pipelined), <= 1e-5."""
+    18 ragged sequences in one call (per-layer) and as two calls of 9 (pipelined), <= 1e-5, for
+    1-4 layers (nl x 64 workgroups, one barrier per global step)."""
     from tts_amd import SpeakerEncoder
     from tts_amd.spec import Ge2eConfig, ge2e_spec
     from tts_amd.weights import synth_state_dict
     _dev()
-    m = SpeakerEncoder(40, 256, 768, 3, proj)
-    sd = synth_state_dict(ge2e_spec(Ge2eConfig(use_lstm_with_projection=proj)), 7)
+    m = SpeakerEncoder(40, 256, 768, nl, proj)
+    sd = synth_state_dict(ge2e_spec(Ge2eConfig(num_lstm_layers=nl, use_lstm_with_projection=proj)), 7)
     m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
     m = m.cuda().eval()
     rng = np.random.RandomState(3)
