@@ -860,22 +860,26 @@ __global__ __launch_bounds__(64 * NW, 1) void pw_layer_x3p_kernel(PwLayerArgs a,
       }
       kstep(Zs + ks * PLANE, w2);
     }
-    // x' = (out + b + x) * 0.25 (parallel_wavegan.py:85); skip (+)= s + b
+    // x' = (out + b + x) * 0.25 (parallel_wavegan.py:85); skip (+)= s + b. Buffer stores: the
+    // utterance's rows as the resource, one 32-bit offset per element (the 64-bit flat address
+    // arithmetic per store was a sizeable share of the tile's VALU issue)
+    {
+      const bool outw = wm * 16 * MI < PW_R;  // a wave's rows are all x' rows or all skip rows
+      const __amdgpu_buffer_rsrc_t orr = rsrc_rows((outw ? a.xn : a.skip) + (long)cur.b * 64 * a.Tmax, 64);
 #pragma unroll
-    for (int mi = 0; mi < MI; ++mi) {
+      for (int mi = 0; mi < MI; ++mi) {
 #pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const int R = wm * 16 * MI + mi * 16 + 4 * (lane >> 4) + j;
-        const bool out_row = R < PW_R;
-        const int ch = out_row ? R : R - PW_R;
+        for (int j = 0; j < 4; ++j) {
+          const int R = wm * 16 * MI + mi * 16 + 4 * (lane >> 4) + j;
+          const int row = (outw ? R : R - PW_R) * a.Tmax;
 #pragma unroll
-        for (int ni = 0; ni < 4; ++ni) {
-          const int tt = cur.t0 + nb + ni * 16;
-          if (tt >= cur.T) continue;
-          const float v = x3_value(am[mi][ni][j], ac[mi][ni][j]) + b2s[R];
-          const long i = ((long)cur.b * 64 + ch) * a.Tmax + tt;
-          if (out_row) a.xn[i] = (v + res[mi][j][ni]) * 0.25f;
-          else a.skip[i] = a.first ? v : res[mi][j][ni] + v;
+          for (int ni = 0; ni < 4; ++ni) {
+            const int tt = cur.t0 + nb + ni * 16;
+            if (tt >= cur.T) continue;
+            const float v = x3_value(am[mi][ni][j], ac[mi][ni][j]) + b2s[R];
+            const float o = outw ? (v + res[mi][j][ni]) * 0.25f : (a.first ? v : res[mi][j][ni] + v);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(o), orr, (row + tt) * 4, 0, 0);
+          }
         }
       }
     }
