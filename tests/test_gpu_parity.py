@@ -1071,6 +1071,31 @@ def test_ge2e_layer_pipeline_matches_per_layer_path(proj, nl):
     assert np.abs(full - halves).max() <= 1e-5
 
 
+@pytest.mark.parametrize("proj", [True, False])
+def test_ge2e_layer_pipeline_short_sequences_vs_oracle(proj):
+    """Edge lengths through the layer-pipelined launch: sequences of 1, 2, 3 and 7 frames in one
+    call (the pipeline's T + nl - 1 global steps with most layers idle at the ends), every row
+    against the numpy oracle (oracle/ge2e_np.py, TTS/speaker_encoder/model.py:62-69)."""
+    from oracle.ge2e_np import Ge2eOracle
+    from tts_amd import SpeakerEncoder
+    from tts_amd.spec import Ge2eConfig, ge2e_spec
+    from tts_amd.weights import synth_state_dict
+    _dev()
+    sd = synth_state_dict(ge2e_spec(Ge2eConfig(use_lstm_with_projection=proj)), 21)
+    m = SpeakerEncoder(40, 256, 768, 3, proj)
+    m.load_state_dict({k: torch.from_numpy(v) for k, v in sd.items()})
+    m = m.cuda().eval()
+    go = Ge2eOracle(sd, 3, proj)
+    lens = [1, 2, 3, 7]
+    rng = np.random.RandomState(4)
+    x = np.zeros((4, 7, 40), np.float32)
+    for i, n in enumerate(lens):
+        x[i, :n] = rng.rand(n, 40).astype(np.float32)
+    emb = m.inference(torch.from_numpy(x).cuda(), lengths=lens).cpu().numpy()
+    for i, n in enumerate(lens):
+        assert np.abs(emb[i] - go.inference(x[i, :n])).max() <= 1e-5, (i, n)
+
+
 # --------------------------------------------------------------------------------- Glow-TTS
 @pytest.mark.parametrize("name,enc", [("glow", "gatedconv"), ("glow_tdsep", "time-depth-separable"),
                                       ("glow_tfm", "transformer")])
