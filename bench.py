@@ -174,6 +174,42 @@ def cpu_baseline(tsd, vsd, tcfg, vcfg, ids, steps, r, budget_s):
                       f"{cores} threads (the fastest of the sweep on utterance {j}, {steps[j] * r} frames)"}
 
 
+def rank_shard(world, rank, per_gpu_batch, r):
+    """This rank's share of the global batch (C2 at world 1, C3 above: the 32-utterance LJ profile
+    once per rank) through the product entry point's plan (tts_amd.multigpu.shard_plan: LPT on the
+    decoder step counts, the token count breaking ties, no data-path collective). Returns the global
+    indices of the rank's utterances, their token counts and their profile indices (ids come from
+    synthetic_ids over the profile)."""
+    T_all, M_all, _ = replicated_workload(world, per_gpu_batch)
+    mine = shard_plan([s_ * 1e6 + t_ for s_, t_ in zip(forced_steps(M_all, r), T_all)], world)[rank]
+    n_prof = len(lj_profile()[0])
+    return mine, [T_all[i] for i in mine], [i % n_prof for i in mine], M_all
+
+
+def aggregate(el_s, frames, n, world, device=None):
+    """Whole-job figures of one timed region of ``n`` steps: (ms per step, frames per step summed over
+    the ranks). The time is the slowest rank's (all_reduce MAX), the frames the sum (all_reduce SUM);
+    weak scaling. ``device``: where the reduction tensors live (the rank's GPU under nccl, the CPU
+    under gloo)."""
+    if world > 1:
+        import torch.distributed as dist
+        t = torch.tensor([frames / n], device=device, dtype=torch.float64)
+        m = torch.tensor([el_s], device=device, dtype=torch.float64)
+        dist.all_reduce(m, op=dist.ReduceOp.MAX)
+        dist.all_reduce(t, op=dist.ReduceOp.SUM)
+        el_s, per = float(m.item()), int(round(t.item()))
+    else:
+        per = frames // n
+    return el_s / n * 1000.0, per
+
+
+def bench_config(world, per_gpu_batch, r):
+    """The line's ``config``: C2 at one GPU, C3 (replicas, weak scaling) above."""
+    return {"workload": f"C{2 if world == 1 else 3}: Tacotron2-DDC (r_init=7, r={r}, sigmoid attn) + "
+                        f"MB-MelGAN [8,4,2]x4, {per_gpu_batch} LJ-length utterances per GPU",
+            "global_batch": per_gpu_batch * world, "r": r, "parallelism": f"replicas x{world}"}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -199,15 +235,11 @@ def main():
 
     taco, tsd, voc, vsd, tcfg, vcfg = build_models(dev)
     taco.decoder.verbose = False  # forced lengths end every utterance at max_decoder_steps
-    # the global batch (C3: the 32-utterance profile once per rank) over the ranks through the product
-    # entry point's plan (tts_amd.multigpu: LPT on the decoder step counts, no data-path collective)
-    T_all, M_all, _ = replicated_workload(world, args.per_gpu_batch)
-    # (step count first, the token count breaking ties: copies of one utterance land on different ranks)
-    mine = shard_plan([s_ * 1e6 + t_ for s_, t_ in zip(forced_steps(M_all, args.r), T_all)], world)[rank]
+    # the rank's share of the global batch (rank_shard: tts_amd.multigpu's LPT plan)
+    mine, my_T, my_prof, M_all = rank_shard(world, rank, args.per_gpu_batch, args.r)
     T_prof, M_prof = lj_profile()
     ids = synthetic_ids(T_prof)              # C3 replicates the same 32 utterances
-    my_ids = [ids[i % len(ids)] for i in mine]
-    my_T = [T_all[i] for i in mine]
+    my_ids = [ids[i] for i in my_prof]
     batch, lens = pad_batch(my_ids)
     batch_t = torch.from_numpy(batch).to(dev)
     batch_host = torch.from_numpy(batch).pin_memory()
@@ -260,16 +292,7 @@ def main():
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
-        el = time.perf_counter() - t0
-        if world > 1:
-            t = torch.tensor([el, frames / n], device=dev, dtype=torch.float64)
-            t0_ = torch.tensor([el], device=dev, dtype=torch.float64)
-            dist.all_reduce(t0_, op=dist.ReduceOp.MAX)
-            dist.all_reduce(t, op=dist.ReduceOp.SUM)
-            el, per = float(t0_.item()), int(t[1].item())
-        else:
-            per = frames // n
-        return el / n * 1000.0, per
+        return aggregate(time.perf_counter() - t0, frames, n, world, dev)
 
     from tts_amd._lib import get_engine
     eng = get_engine(dev)
@@ -437,9 +460,7 @@ def main():
         "f32_gemm_ms_per_step": None if f32_ms is None else round(f32_ms, 3),
         "x3_range_fallbacks": fallbacks,
         "data": "synthetic (LJ-profile lengths, RandomState(0) ids, seeded random weights, forced length)",
-        "config": {"workload": f"C{2 if world == 1 else 3}: Tacotron2-DDC (r_init=7, r={r}, sigmoid attn) + "
-                               f"MB-MelGAN [8,4,2]x4, {args.per_gpu_batch} LJ-length utterances per GPU",
-                   "global_batch": args.per_gpu_batch * world, "r": r, "parallelism": f"replicas x{world}"},
+        "config": bench_config(world, args.per_gpu_batch, r),
         "e2e_rtf": ms_step / 1000.0 / audio_s,
         "e2e_rtf_host": m2["host_ms"] / 1000.0 / host_audio,
         "host_ms_per_step": round(m2["host_ms"], 3),

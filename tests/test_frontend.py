@@ -119,8 +119,8 @@ def _test_wav():
 def test_mean_var_scaler_roundtrip(tmp_path):
     """tests/test_audio.py:157-176 (test_scaler): with `stats_path`, melspectrogram() is mean-var
     scaled and _denormalize() inverts it to the un-normalised mel within 1e-4; the stats file is the
-    object array compute_statistics.py writes. The reference's own tests/inputs/scale_stats.npy is a
-    pickle and is not loaded here (numpy's safe loader refuses it), so the stats are recomputed."""
+    object array compute_statistics.py writes, computed here as compute_statistics.py does (the
+    reference's own stats: test_reference_scale_stats_fixture_roundtrip)."""
     path = tmp_path / "scale_stats.npy"
     plain = AudioProcessor(**dict(LJ_AUDIO, signal_norm=False))
     wav = _test_wav()
@@ -141,6 +141,41 @@ def test_mean_var_scaler_roundtrip(tmp_path):
     # the stats were computed with other audio parameters: load_stats asserts (audio.py:174-179)
     with pytest.raises(AssertionError, match="mel_fmin"):
         AudioProcessor(**dict(LJ_AUDIO, mel_fmin=0.0, stats_path=str(path)))
+
+
+def test_reference_scale_stats_fixture_roundtrip(tmp_path):
+    """The reference's own mean-var stats (tests/inputs/scale_stats.npy, decoded statically into
+    tests/golden/scale_stats_ref.npz by make_scale_stats.py: no unpickler runs on the reference
+    file) through this AudioProcessor, as the reference's tests/test_audio.py:157-176 test_scaler
+    runs them: its test_config.json audio section with preemphasis 0 and signal_norm, its
+    example_1.wav; melspectrogram() then _denormalize() returns the un-normalised mel within 1e-4.
+    load_stats' parameter check (audio.py:174-179) passes on the reference's stats_config, and the
+    loader's .npy path (the object array compute_statistics.py writes, here written by this test
+    from the fixture) returns the same stats as the .npz."""
+    from tts_amd.audio import load_stats_file
+    gold = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden", "scale_stats_ref.npz")
+    ref = load_stats_file(gold)
+    with np.load(gold, allow_pickle=False) as z:
+        test_audio = json.loads(str(z["test_audio"]))
+        wav = z["wav_pcm16"].astype(np.float64) / 32768.0  # soundfile.read's float scaling
+        sr = int(z["wav_sr"])
+    assert ref["mel_mean"].shape == (80,) and ref["linear_std"].shape == (513,)
+    assert ref["audio_config"]["num_mels"] == 80 and sr == test_audio["sample_rate"]
+    # the .npy form of the same stats (this test's own file) through the restricted loader
+    npy = tmp_path / "scale_stats.npy"
+    np.save(npy, dict(ref), allow_pickle=True)
+    again = load_stats_file(npy)
+    for k in ("mel_mean", "mel_std", "linear_mean", "linear_std"):
+        assert np.array_equal(again[k], ref[k])
+    assert again["audio_config"] == ref["audio_config"]
+    conf = dict(test_audio, preemphasis=0.0, do_trim_silence=True, signal_norm=True)
+    ap = AudioProcessor(**dict(conf, stats_path=gold))
+    plain = AudioProcessor(**dict(test_audio, preemphasis=0.0, signal_norm=False))
+    mel_reference = plain.melspectrogram(wav)
+    mel_norm = ap.melspectrogram(wav)
+    assert np.allclose(mel_norm, (mel_reference - ref["mel_mean"][:, None]) / ref["mel_std"][:, None])
+    mel_denorm = ap._denormalize(mel_norm)
+    assert abs(mel_reference - mel_denorm).max() < 1e-4
 
 
 def test_stats_loader_refuses_foreign_globals(tmp_path):

@@ -331,6 +331,38 @@ def test_encoder_row_groups_vs_oracle(B):
         assert not out[i, lens[i]:].any(), i
 
 
+@pytest.mark.gpu
+def test_bilstm_row_group_barrier_timeout_raises(monkeypatch):
+    """A grid-barrier timeout in the BiLSTM's second row group (recurrence 3: row group 1, backward;
+    B = 32 runs 2 row groups x 2 directions) is reported by the Tacotron2 call's status read-back:
+    the call raises instead of returning mels built from a half-written encoder output.
+    The test hook TTS_TEST_STALL_LSTM makes one workgroup of that recurrence leave before its second
+    barrier. The next call, without the hook, is correct again."""
+    from oracle.taco_np import TacoOracle
+    from tts_amd.spec import TacotronConfig
+    _dev()
+    cfg = TacotronConfig()
+    _, sd = taco_state_dict(None, seed=4, overrides={}, stop_bias=-1e4, cfg=cfg)
+    m = build_taco(cfg, sd)
+    m.decoder.set_r(2)
+    rs = np.random.RandomState(7)
+    lens = rs.randint(8, 40, size=32)
+    batch = np.zeros((32, int(lens.max())), np.int64)
+    for i, L in enumerate(lens):
+        batch[i, :L] = rs.randint(1, 129, size=L)
+    x = torch.from_numpy(batch).cuda()
+    monkeypatch.setenv("TTS_TEST_STALL_LSTM", "3")
+    with pytest.raises(RuntimeError, match="persistent BiLSTM: grid barrier timed out"):
+        m.inference(x, text_lengths=[int(L) for L in lens], max_decoder_steps=3)
+    monkeypatch.delenv("TTS_TEST_STALL_LSTM")
+    dec, post, align, stop = m.inference(x, text_lengths=[int(L) for L in lens], max_decoder_steps=3)
+    post = post.cpu().numpy()
+    orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
+    for i in (0, 31):
+        _, p, _, _ = orc.inference(batch[i, :lens[i]], 2, 3)
+        assert np.abs(post[i, :len(p)] - p).max() <= MEL_TOL
+
+
 def _check_taco(fx, r, dec, post, align, stop, steps, utts):
     for i in utts:
         k = f"r{r}_u{i}"

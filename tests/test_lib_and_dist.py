@@ -117,6 +117,64 @@ def test_two_rank_sharded_decode_equals_single_process():
         assert np.array_equal(out[i, :len(ref)], ref) and not out[i, len(ref):].any()
 
 
+def _bench_rank_worker(rank, world, port, q):
+    """One rank of bench.py's multi-GPU path on gloo: its shard selection (rank_shard), a stub step
+    loop timed as bench.py times it (barrier, per-rank elapsed time, MAX / SUM aggregation) and the
+    line's config."""
+    import sys
+    import time
+    sys.path.insert(0, ROOT)
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    import bench
+    from tts_amd.workload import forced_steps
+    r, n = 2, 3
+    mine, my_T, my_prof, M_all = bench.rank_shard(world, rank, 32, r)
+    steps = forced_steps([M_all[i] for i in mine], r)
+    dist.barrier()
+    t0 = time.perf_counter()
+    frames = 0
+    for _ in range(n):  # stub step: the rank's mel frames, and a rank-dependent duration
+        time.sleep(0.02 * (rank + 1))
+        frames += sum(st * r for st in steps)
+    dist.barrier()
+    el = time.perf_counter() - t0
+    ms, per = bench.aggregate(el, frames, n, world, torch.device("cpu"))
+    q.put((rank, mine, my_prof, my_T, steps, el, ms, per, bench.bench_config(world, 32, r)))
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2, 4])
+def test_bench_multi_rank_shards_and_aggregation(world):
+    """bench.py at N > 1 (the driver's 8-GPU SCALE run): every rank holds one copy of every profile
+    utterance, the ranks' shards partition the global batch, the line's time is the slowest rank's
+    and its frame count the sum over ranks, and config.global_batch = 32 N."""
+    from tts_amd.workload import forced_steps, lj_profile
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_bench_rank_worker, args=(k, world, port, q)) for k in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted([q.get(timeout=300) for _ in range(world)])
+    for p in procs:
+        p.join(timeout=120)
+        assert p.exitcode == 0
+    T, M = lj_profile()
+    all_idx = sorted(i for _, mine, *_ in res for i in mine)
+    assert all_idx == list(range(32 * world))  # a partition of the global batch
+    per_rank_frames = sum(forced_steps(M, 2)) * 2
+    max_el = max(el for *_, el, _, _, _ in res)
+    for rank, mine, prof, my_T, steps, el, ms, per, cfg in res:
+        assert sorted(prof) == list(range(32)), f"rank {rank} does not hold one copy of each utterance"
+        assert sorted(my_T) == sorted(T) and sum(steps) * 2 == per_rank_frames
+        assert per == world * per_rank_frames
+        assert ms == pytest.approx(max_el / 3 * 1000.0, rel=1e-9)
+        assert cfg["global_batch"] == 32 * world and cfg["parallelism"] == f"replicas x{world}"
+        assert cfg["workload"].startswith("C3")
+
+
 def _pool_factory(seed, device):
     """GpuPool stand-in runner for the CPU suite: the oracle decode, tagged with the worker's device."""
     import sys
@@ -153,6 +211,56 @@ def test_gpu_pool_dispatch_and_gather():
         assert pool.map([]) == []
         with pytest.raises(RuntimeError, match="worker failed"):
             pool.map(items, r=0)  # r = 0 raises inside the workers
+
+
+def _interval_factory(device):
+    """GpuPool stand-in runner that records when each call ran (for the device-lock test)."""
+    import time
+
+    def run(items, hold=0.4):
+        t0 = time.monotonic()
+        if any(x == "die" for x in items):
+            os._exit(3)  # a worker that dies mid-call (GPU fault stand-in)
+        time.sleep(hold)
+        return [(device, os.getpid(), t0, time.monotonic()) for _ in items]
+    return run
+
+
+def test_gpu_pool_serialises_workers_sharing_a_device(tmp_path, monkeypatch):
+    """Two workers on one device label: their runner calls never overlap (per-device inter-process
+    lock, tts_amd.multigpu.DeviceLock); workers on different labels run concurrently."""
+    from tts_amd.multigpu import GpuPool
+    monkeypatch.setenv("TTS_GPU_LOCK_DIR", str(tmp_path))
+    with GpuPool(_interval_factory, devices=[0, 0]) as pool:
+        for _ in range(2):
+            out = pool.map(["a", "b"])
+            (d0, p0, s0, e0), (d1, p1, s1, e1) = out
+            assert d0 == d1 == 0 and p0 != p1
+            assert e0 <= s1 or e1 <= s0, f"calls on one device overlapped: {out}"
+    with GpuPool(_interval_factory, devices=[0, 1]) as pool:
+        out = pool.map(["a", "b"], hold=1.5)
+        (d0, _, s0, e0), (d1, _, s1, e1) = out
+        assert {d0, d1} == {0, 1}
+        assert s1 < e0 and s0 < e1, "workers on different devices were serialised"
+
+
+def test_gpu_pool_dead_worker_and_gpu_parent(monkeypatch, tmp_path):
+    """A worker that dies during map() raises a RuntimeError naming its device and leaves the pool
+    unusable; a parent that has initialised the GPU is refused."""
+    import torch
+    from tts_amd.multigpu import GpuPool
+    monkeypatch.setenv("TTS_GPU_LOCK_DIR", str(tmp_path))
+    pool = GpuPool(_interval_factory, devices=[0, 1])
+    try:
+        with pytest.raises(RuntimeError, match=r"device\(s\) \[\d\] exited"):
+            pool.map(["ok", "die"], hold=0.1)
+        with pytest.raises(RuntimeError, match="unusable"):
+            pool.map(["ok"])
+    finally:
+        pool.close()
+    monkeypatch.setattr(torch.cuda, "is_initialized", lambda: True)
+    with pytest.raises(RuntimeError, match="before this process initialises the GPU"):
+        GpuPool(_interval_factory, devices=[0])
 
 
 def test_library_matches_build_record():

@@ -27,6 +27,20 @@ for (name, grid), c in sorted(vals.items()):
                 out.append(f"{k[3:]} {a[k] / wc:.2f}")
     if "SQ_VALU_MFMA_BUSY_CYCLES" in a and "SQ_BUSY_CYCLES" in a:
         out.append(f"MFMA_BUSY/BUSY {a['SQ_VALU_MFMA_BUSY_CYCLES'] / (a['SQ_BUSY_CYCLES'] * 4 * 4):.2f}")
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in a and "GRBM_GUI_ACTIVE" in a and a["GRBM_GUI_ACTIVE"]:
+        # MfmaUtil as rocprofiler-sdk defines it (sum of per-SIMD busy cycles over GUI-active cycles x
+        # SIMDs); GRBM_GUI_ACTIVE is reported summed over the 8 XCDs, 1024 SIMDs on the chip
+        out.append(f"MfmaUtil {a['SQ_VALU_MFMA_BUSY_CYCLES'] / (a['GRBM_GUI_ACTIVE'] / 8 * 1024):.3f}")
+    # issued MFMA instructions from the MOPS counters (units of 512 FLOP): 16x16x32 f16 = 16384 FLOP,
+    # 16x16x4 f32 = 2048 FLOP
+    if "SQ_INSTS_VALU_MFMA_MOPS_F16" in a:
+        out.append(f"f16 MFMA {a['SQ_INSTS_VALU_MFMA_MOPS_F16'] * 512 / 16384 / 1e6:.3f} M")
+    if "SQ_INSTS_VALU_MFMA_MOPS_F32" in a:
+        out.append(f"f32 MFMA {a['SQ_INSTS_VALU_MFMA_MOPS_F32'] * 512 / 2048 / 1e6:.3f} M")
+    if "SQ_VALU_MFMA_BUSY_CYCLES" in a:
+        out.append(f"MFMA_BUSY {a['SQ_VALU_MFMA_BUSY_CYCLES'] / 1e6:.3f} Mcyc")
+    if "GRBM_GUI_ACTIVE" in a:
+        out.append(f"GUI_ACTIVE {a['GRBM_GUI_ACTIVE'] / 8:.0f} cyc/XCD")
     w = a.get("SQ_WAVES")
     for k in ("SQ_INSTS_VALU", "SQ_INSTS_LDS", "SQ_INSTS_VMEM_RD", "SQ_INSTS_VMEM_WR", "SQ_INSTS_SALU"):
         if k in a and w:

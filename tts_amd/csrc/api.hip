@@ -327,12 +327,14 @@ struct TacoModel {
 };
 
 // Tacotron2 status words (TacoWS::stat on the device, tts_ctx::pinned on the host; one copy after
-// the call): BiLSTM barrier errors (2), persistent-decoder barrier errors (one per launch), the
-// decoder results (done, steps, status per decode row), the range flag, the launches' end steps
+// the call): BiLSTM barrier errors (one per recurrence: 2 directions x up to 2 row groups),
+// persistent-decoder barrier errors (one per launch), the decoder results (done, steps, status per
+// decode row), the range flag, the launches' end steps
 constexpr int PMAX_LAUNCH = 4;  // persistent decoder launches per decode (MT = 4, 3, 2, 1)
-constexpr int TS_ENC = 16, TS_DEC = 18, TS_RES = TS_DEC + PMAX_LAUNCH, TS_FLAG = TS_RES + 3 * BMAX,
+constexpr int ENC_NDOM_MAX = 4;  // BiLSTM recurrences (barrier blocks) per launch
+constexpr int TS_ENC = 16, TS_DEC = TS_ENC + ENC_NDOM_MAX, TS_RES = TS_DEC + PMAX_LAUNCH, TS_FLAG = TS_RES + 3 * BMAX,
               TS_END = TS_FLAG + 1, TS_N = TS_END + PMAX_LAUNCH;
-static_assert(TS_N <= 256, "status words fit the pinned block");
+static_assert(TS_N <= 240, "status words fit the pinned block below check_encoder_barrier's words");
 
 struct TacoWS {
   int B = 0, T_max = 0, S_cap = 0, r = 0, MT = 0;
@@ -1169,7 +1171,7 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
 void check_encoder_barrier(tts_ctx* c) {
   if (!c->tws.enc_persist) return;
   int* pw = c->pinned + 240;  // one error word per recurrence (2 directions x up to 2 row groups)
-  const int nd = std::min(c->tws.enc_ndom, 4);
+  const int nd = std::min(c->tws.enc_ndom, ENC_NDOM_MAX);
   pw[0] = pw[1] = pw[2] = pw[3] = 0;
   const unsigned* words = reinterpret_cast<const unsigned*>(c->tws.lc.p);
   for (int i = 0; i < nd; ++i) HIP_OK(hipMemcpyAsync(&pw[i], words + i * BAR_WORDS + 16, 4, hipMemcpyDeviceToHost, c->s));
@@ -1278,11 +1280,11 @@ __global__ void taco_mlens_kernel(const int* ctl, int B, int r, int* mlens) {
 }
 
 // gather every status word the host checks after a Tacotron2 call into one block (TS_* layout)
-__global__ void taco_status_kernel(const unsigned* enc_bar, const unsigned* dec_bar, int ndec, const int* ctl,
+__global__ void taco_status_kernel(const unsigned* enc_bar, int nenc, const unsigned* dec_bar, int ndec, const int* ctl,
                                    const unsigned* flag, int* st) {
   const int i = threadIdx.x;
   if (i < 3 * BMAX) st[TS_RES + i] = ctl[4 + i];
-  if (i < 2) st[TS_ENC + i] = enc_bar ? (int)enc_bar[i * BAR_WORDS + 16] : 0;
+  if (i < ENC_NDOM_MAX) st[TS_ENC + i] = enc_bar && i < nenc ? (int)enc_bar[i * BAR_WORDS + 16] : 0;
   if (i < PMAX_LAUNCH) {
     st[TS_DEC + i] = dec_bar && i < ndec ? (int)dec_bar[i * BAR_WORDS + 16] : 0;
   }
@@ -1675,14 +1677,14 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   // one host round trip per call: barrier error words, per-row results, range flag, launch steps
   {
     const unsigned* lc = reinterpret_cast<const unsigned*>(W.lc.p);
-    taco_status_kernel<<<1, 256, 0, s>>>(W.enc_persist ? lc : nullptr,
+    taco_status_kernel<<<1, 256, 0, s>>>(W.enc_persist ? lc : nullptr, W.enc_ndom,
                                          persist ? reinterpret_cast<const unsigned*>(W.pbar.p) : nullptr,
                                          c->dec_nlaunch, W.ctl.i(), c->gemm_x3 ? x3_flag(c) : nullptr, W.stat.i());
     HIP_OK(hipGetLastError());
     int* pin = c->pinned;
     HIP_OK(hipMemcpyAsync(pin + TS_ENC, W.stat.i() + TS_ENC, (TS_N - TS_ENC) * 4, hipMemcpyDeviceToHost, s));
     HIP_OK(hipStreamSynchronize(s));
-    TTS_CHECK(!W.enc_persist || (pin[TS_ENC] == 0 && pin[TS_ENC + 1] == 0),
+    TTS_CHECK(!W.enc_persist || (pin[TS_ENC] == 0 && pin[TS_ENC + 1] == 0 && pin[TS_ENC + 2] == 0 && pin[TS_ENC + 3] == 0),
               "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past "
               "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
     TTS_CHECK(!persist || (pin[TS_DEC] == 0 && pin[TS_DEC + 1] == 0 && pin[TS_DEC + 2] == 0 && pin[TS_DEC + 3] == 0),
@@ -2759,6 +2761,8 @@ void glow_encode(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, const 
     cc.oc = T;
     cc.ot = 1;
     cc.epi = 1;
+    // two sources: the fp32 conv (conv_x3 stages one source; this k3 conv over ~T x (H + c_pad)
+    // inputs is a few microseconds of the call either way)
     run_conv(G.dp1, cc, s);
   } else {
     conv(G.dp1, x, H, W.hdp.f(), F, 1);

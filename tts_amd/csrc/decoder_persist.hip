@@ -55,6 +55,33 @@ constexpr int YROWS = 64;    // rows per projection half (independent of the bat
 constexpr int pec_of(int VAR, int MT) { return ((VAR & 8) && !(VAR & 2) && MT <= 2) ? 4 : 0; }
 constexpr int pec_arr(int VAR, int MT) { return pec_of(VAR, MT) > 0 ? pec_of(VAR, MT) : 1; }
 constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = NATT;  // NPQ_: query-projection partials
+// LDS layouts chosen for bank-conflict-free access (64 banks x 4 B; ds_read_b32 / ds_write_b32 bank
+// = dword index mod 32 within a 32-lane group, ds_read_b128 = mod 64 within a 16-lane group):
+// * RS: row stride of the wave-partial reduction scratch [wave][row][RS]. Writers put row
+//   4 (lane >> 4) + j, column lane & 15 (rows r and r + 4 in one 32-lane group: 20 * 4 = 80 = 16 mod
+//   32, disjoint halves); the LSTM cells read row tid >> 2 (8 rows per group), column 4 q + (tid & 3):
+//   20 m mod 32 = {0, 20, 8, 28, 16, 4, 24, 12} + 0..3, disjoint. Stride 17 gave 2-way conflicts on
+//   the cell reads.
+// * WCLD: row stride of the folded location filter Wcomb [64 taps][WCLD]: lanes 0-15 read tap j,
+//   lanes 16-31 tap j + 1 of the same 16 dims; WCLD = 16 mod 32 puts them on disjoint banks (128
+//   put both halves on the same 16 banks: 2-way).
+// * split-f16 weight / operand fragments in LDS as [k-step][hi 64 lanes | lo 64 lanes] planes: a
+//   lane's 16-byte read is contiguous with its neighbours' (the interleaved [lane][hi | lo] form
+//   strides lanes 32 B apart: 2-way on every ds_read_b128 / ds_write_b128).
+#ifndef TTS_RS
+#define TTS_RS 20
+#endif
+#ifndef TTS_WCLD
+#define TTS_WCLD 144
+#endif
+#ifndef TTS_X3_PLANES
+#define TTS_X3_PLANES 1
+#endif
+constexpr int RS = TTS_RS, WCLD = TTS_WCLD;
+// LDS index (in 16-byte units) of the hi (h = 0) / lo (h = 1) half of lane `lane`'s split fragment of k-step ks
+__device__ __forceinline__ int x3i(int ks, int lane, int h) {
+  return TTS_X3_PLANES ? (ks * 128 + h * 64 + lane) : ((ks * 64 + lane) * 2 + h);
+}
 }  // namespace
 
 // Opaque copies of lane / wave indices, taken at the start of each phase: without them the
@@ -70,33 +97,33 @@ __device__ __forceinline__ int opaque_s(int v) {
 }
 constexpr int ACT_AUX = 16;  // sc1; measured: plain / sc0 / sc0|sc1 loads are no faster
 
-// partial sums of one wave's MT accumulators into LDS [wave][m][17]
+// partial sums of one wave's MT accumulators into LDS [wave][m][RS]
 template <int MT>
 __device__ __forceinline__ void acc_to_lds(float* part, int w, int lane, const f32x4 (&acc)[MT]) {
   constexpr int Bp = MT * 16;
-  float* p = part + w * Bp * 17;
+  float* p = part + w * Bp * RS;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
+    for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * RS + (lane & 15)] = acc[mt][j];
 }
-// chunk c (m-tiles CM c .. CM c + CM - 1) of a wave's MT accumulators into LDS [wave][CM * 16][17]:
+// chunk c (m-tiles CM c .. CM c + CM - 1) of a wave's MT accumulators into LDS [wave][CM * 16][RS]:
 // reductions over the waves go in chunks of at most 2 m-tiles (32 rows, the scratch's size), so
 // MT = 3, 4 (48 / 64 rows) reuse the MT = 2 scratch; rows past MT stay stale and are not read
 template <int MT, int CM>
 __device__ __forceinline__ void acc_chunk_to_lds(float* part, int w, int lane, const f32x4 (&acc)[MT], int c) {
-  float* p = part + w * CM * 16 * 17;
+  float* p = part + w * CM * 16 * RS;
 #pragma unroll
   for (int mt = 0; mt < CM; ++mt)
     if (c * CM + mt < MT)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[c * CM + mt][j];
+      for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * RS + (lane & 15)] = acc[c * CM + mt][j];
 }
 template <int KS, int Bp>
 __device__ __forceinline__ float lds_sum(const float* part, int m, int n) {
-  float s = part[m * 17 + n];
+  float s = part[m * RS + n];
 #pragma unroll
-  for (int w = 1; w < KS; ++w) s += part[(w * Bp + m) * 17 + n];
+  for (int w = 1; w < KS; ++w) s += part[(w * Bp + m) * RS + n];
   return s;
 }
 
@@ -181,7 +208,7 @@ __device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* A
     const int ci = j >= LOCK_ ? 1 : 0;
     const int k = j - LOCK_ * ci;
     const bool valid = j < 2 * LOCK_;
-    const float w = wcomb[j * ADIM_ + a];
+    const float w = wcomb[j * WCLD + a];
 #pragma unroll
     for (int mt = 0; mt < 2; ++mt) {
       const float x = valid ? Aw[ci * 64 + 16 * mt + (lane & 15) + k] : 0.f;
@@ -887,8 +914,8 @@ __device__ __forceinline__ void gemm_seg2(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], 
 // ------------------------------------------------------------------ the persistent kernel
 // LDS: [att-pre weights 96 x 1 KiB][Wcomb 64 x 128][scratch: GEMM reduction + hs | attention]
 constexpr size_t P_LDS_APRE = 96 * 64 * 16;
-constexpr size_t P_LDS_WC = 64 * 128 * 4;
-constexpr size_t P_LDS_SCRATCH = 8 * 32 * 17 * 4 + 64 * 17 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
+constexpr size_t P_LDS_WC = 64 * WCLD * 4;
+constexpr size_t P_LDS_SCRATCH = 8 * 32 * RS * 4 + 64 * 17 * 4;  // red0 | hs; >= attention scratch (~2.5K floats)
 constexpr int PDEF_MAXIT = 8;  // attention items per workgroup the deferred alignment pass keeps
 constexpr size_t P_LDS_EKEEP = PDEF_MAXIT * (32 + 1) * 4;
 constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH + P_LDS_EKEEP;
@@ -913,10 +940,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   constexpr int JR = (X3P && MT > 2) ? 4 : 2;    // projection jobs per tile (row blocks / K halves)
   const DecDev& D = P.D;
   f32x4* Wap = smem4;                                              // [96][64]
-  float* wcomb = reinterpret_cast<float*>(smem4) + 96 * 64 * 4;    // [64][128]
-  float* scr = wcomb + 64 * 128;
-  float* red0 = scr;                   // [8][CB][17]
-  float* hs = red0 + 8 * 32 * 17;      // [Bp][17]
+  float* wcomb = reinterpret_cast<float*>(smem4) + 96 * 64 * 4;    // [64][WCLD]
+  float* scr = wcomb + 64 * WCLD;
+  float* red0 = scr;                   // [8][CB][RS]
+  float* hs = red0 + 8 * 32 * RS;      // [Bp][17]
   float* ekeep0 = scr + P_LDS_SCRATCH / 4;  // [PDEF_MAXIT][PTC + 1]: deferred alignment pass
   const int g = blockIdx.x, tid0 = threadIdx.x, lane0 = tid0 & 63;
   const int wave0 = __builtin_amdgcn_readfirstlane(tid0 >> 6);
@@ -928,9 +955,12 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     const f32x4* src = reinterpret_cast<const f32x4*>(P.apre_w) + (long)g * 96 * 64;
     // split-f16 variant: the same bytes hold split B fragments [48 k-steps][64 lanes][hi | lo]
     const f32x4* srcx = reinterpret_cast<const f32x4*>(P.apre_x3) + (long)g * 96 * 64;
-    for (int i = tid; i < 96 * 64; i += PT) Wap[i] = X3P ? srcx[i] : src[i];
+    for (int i = tid; i < 96 * 64; i += PT) {
+      if (X3P) Wap[x3i(i >> 7, (i >> 1) & 63, i & 1)] = srcx[i];
+      else Wap[i] = src[i];
+    }
     if (g >= IW0)  // attention_rnn workgroups use this area as P3 staging instead
-      for (int i = tid; i < 64 * 128; i += PT) wcomb[i] = P.Wcomb[i];
+      for (int i = tid; i < 64 * 128; i += PT) wcomb[(i >> 7) * WCLD + (i & 127)] = P.Wcomb[i];
   }
   // decoder_rnn weights of this wave: K = [h_att 64 chunks | ctx 32 | h_dec 64]; wave w keeps
   // h_att chunks 8w..8w+7 (wd[0..7]), ctx chunks 4w..4w+3 (wd[8..11]), h_dec chunks 8w..8w+7
@@ -960,8 +990,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   auto wdx_f = [&](int base) { return [&, base](int k, h8& hi, h8& lo) { hi = wdx[base + k][0], lo = wdx[base + k][1]; }; };
   auto wap_f = [&](int ks0) {
     return [&, ks0](int k, h8& hi, h8& lo) {
-      hi = Wapx[((ks0 + k) * 64 + lane) * 2];
-      lo = Wapx[((ks0 + k) * 64 + lane) * 2 + 1];
+      hi = Wapx[x3i(ks0 + k, lane, 0)];
+      lo = Wapx[x3i(ks0 + k, lane, 1)];
     };
   };
   // epilogue constants: decoder_rnn biases of this thread's (row, unit) item, attention_rnn
@@ -1089,15 +1119,15 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           for (int q = 0; q < 4; ++q) acc = MFMA16(x[h][q], h ? w2b[q] : w2[q], acc);
         }
       }
-      float* p = red0 + wave * 16 * 17;  // [wave][16 rows][17]
+      float* p = red0 + wave * 16 * RS;  // [wave][16 rows][RS]
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[(4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[j];
+      for (int j = 0; j < 4; ++j) p[(4 * (lane >> 4) + j) * RS + (lane & 15)] = acc[j];
       lds_barrier();
       if (tid < 256) {
         const int mm = tid >> 4, n = tid & 15;
-        float v = red0[mm * 17 + n];
+        float v = red0[mm * RS + n];
 #pragma unroll
-        for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * 17 + n];
+        for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * RS + n];
         if (P.pre2_b) v += P.pre2_b[tl2 * 16 + n];  // BN prenet layer-2 bias
         stc_quad(P.pb, (int)frag_idx(mt * 16 + mm, tl2 * 16 + n, 256), v);
       }
@@ -1229,8 +1259,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
             bad |= !(mx < F16_RANGE);
             h8 hi, lo;
             split8(v, hi, lo);
-            xs[(((mt - ps * CM) * 8 + wave) * 64 + lane) * 2] = hi;
-            xs[(((mt - ps * CM) * 8 + wave) * 64 + lane) * 2 + 1] = lo;
+            xs[x3i((mt - ps * CM) * 8 + wave, lane, 0)] = hi;
+            xs[x3i((mt - ps * CM) * 8 + wave, lane, 1)] = lo;
           }
           lds_barrier();
           PTRACE(13);
@@ -1240,8 +1270,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
             for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt) {
               const int ks = 4 * (wave & 1) + i;
-              xh[mt - ps * CM] = xs[(((mt - ps * CM) * 8 + ks) * 64 + lane) * 2];
-              xl[mt - ps * CM] = xs[(((mt - ps * CM) * 8 + ks) * 64 + lane) * 2 + 1];
+              xh[mt - ps * CM] = xs[x3i((mt - ps * CM) * 8 + ks, lane, 0)];
+              xl[mt - ps * CM] = xs[x3i((mt - ps * CM) * 8 + ks, lane, 1)];
             }
 #pragma unroll
             for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt)
@@ -1288,13 +1318,13 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       PTRACE(10);
 #pragma unroll
       for (int ck = 0; ck < NCK; ++ck) {
-        acc_chunk_to_lds<MT, CM>(red0 + (wave >> 1) * 2 * CB * 17, wave & 1, lane, acc, ck);
+        acc_chunk_to_lds<MT, CM>(red0 + (wave >> 1) * 2 * CB * RS, wave & 1, lane, acc, ck);
         lds_barrier();
         if (tid < 4 * CB * 4) {
           const int gl = tid / (CB * 4), rem = tid % (CB * 4);
           const int m = ck * CB + (rem >> 2), u = rem & 3;
           const int tile = 4 * g + gl;
-          const float* pg = red0 + gl * 2 * CB * 17;
+          const float* pg = red0 + gl * 2 * CB * RS;
           if (m < Bp) {
             float pre[4];
 #pragma unroll
@@ -1503,15 +1533,15 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         split_x3_step(y[i][0], xh, xl);
         mfma_x3(xh, xl, wpx[i][0], wpx[i][1], am, ac);
       }
-      float* p = red0 + wave * 16 * 17;  // [wave][16 rows][17]
+      float* p = red0 + wave * 16 * RS;  // [wave][16 rows][RS]
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[(4 * (lane >> 4) + j) * 17 + (lane & 15)] = x3_value(am[j], ac[j]);
+      for (int j = 0; j < 4; ++j) p[(4 * (lane >> 4) + j) * RS + (lane & 15)] = x3_value(am[j], ac[j]);
       lds_barrier();
       if (tid < 256) {
         const int mm = tid >> 4, n = tid & 15;
-        float v = red0[mm * 17 + n];
+        float v = red0[mm * RS + n];
 #pragma unroll
-        for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * 17 + n];
+        for (int w = 1; w < NWV; ++w) v += red0[(w * 16 + mm) * RS + n];
         stc_quad(P.ypart, (mtb * 16 + mm) * YP + (pj / JR) * 16 + n, v);
       }
       lds_barrier();

@@ -124,7 +124,7 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
                                                            const uint16_t* __restrict__ Whh16,
                                                            const float* __restrict__ Gin, const int* lens,
                                                            int T_max, int B, float* hbuf, float* __restrict__ out,
-                                                           unsigned* bar) {
+                                                           unsigned* bar, int stall) {
   constexpr int Bp = MT * 16;
   constexpr int NT = H / 4;                   // gate tiles per direction
   constexpr int NW = LSTM_NW;
@@ -164,6 +164,9 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
 #pragma unroll
   for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(0) * G + q * 4];
   for (int step = 0; step < T_max; ++step) {
+    // test hook (TTS_TEST_STALL_LSTM=<recurrence>): one workgroup of that recurrence leaves before
+    // its second barrier, so the others time out and set that recurrence's error word
+    if (step == 1 && dom == stall && tl == 0) return;
     const float* hi = hbuf + (size_t)(step & 1) * RG * NDIR * Bp * H + (long)dom * Bp * H;
     float* ho = hbuf + (size_t)((step + 1) & 1) * RG * NDIR * Bp * H + (long)dom * Bp * H;
     const int t = tpos(step);
@@ -264,8 +267,10 @@ static int launch_lstm_persist_t(const float* Gin, const float* Whh, const uint1
   const int MT = MT0 / RG, Bp = MT * 16;
   HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * RG * NDIR * Bp * H * 4, s));
   arm_barrier(bar, RG * NDIR, s);
+  const char* st = std::getenv("TTS_TEST_STALL_LSTM");
+  int stall = st ? std::atoi(st) : -1;
   void* args[] = {(void*)&Whh, (void*)&Whh16, (void*)&Gin, (void*)&lens, (void*)&T_max,
-                  (void*)&B,   (void*)&hbuf,  (void*)&out, (void*)&bar};
+                  (void*)&B,   (void*)&hbuf,  (void*)&out, (void*)&bar, (void*)&stall};
 #define LPK(mt, x) (const void*)lstm_persist_kernel<mt, H, NDIR, x>
   static const void* const fns[2][4] = {{LPK(1, false), LPK(2, false), LPK(3, false), LPK(4, false)},
                                         {LPK(1, true), LPK(2, true), LPK(3, true), LPK(4, true)}};

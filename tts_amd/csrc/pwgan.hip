@@ -900,7 +900,11 @@ void launch_pw_layer_x3(const float* x, const float* c, float* xn, float* skip, 
     const char* e = std::getenv("TTS_PWGAN_TILE");
     return e ? std::atoi(e) : 0;
   }();
-  if (B <= 64 && h_lens && var != 1) {  // persistent, weights in registers (TTS_PWGAN_TILE=1: the per-tile kernel)
+  // the persistent kernel addresses a row block of the (B, 80, Tmax) features with 32-bit buffer
+  // offsets: utterances past 2^31 bytes per row block (~26 k frames at hop 256) take the per-tile
+  // kernel, whose offsets are 64-bit
+  const bool off32 = (long)PW_A * Tmax * 4 < (1L << 31);
+  if (B <= 64 && h_lens && var != 1 && off32) {  // persistent, weights in registers (TTS_PWGAN_TILE=1: the per-tile kernel)
     long ntiles = 0;
     for (int b = 0; b < B; ++b) ntiles += ((long)(h_lens[b] + len_add) * hop + 63) / 64;
     TTS_CHECK(ntiles < (1L << 30), "pwgan: too many tiles");
@@ -917,7 +921,7 @@ void launch_pw_layer_x3(const float* x, const float* c, float* xn, float* skip, 
     HIP_OK(hipGetLastError());
     return;
   }
-  // per-tile kernel (B > 64, or TTS_PWGAN_TILE=1): one 4-wave workgroup per tile of 64 positions
+  // per-tile kernel (B > 64, very long utterances, or TTS_PWGAN_TILE=1): one 4-wave workgroup per tile of 64 positions
   constexpr int WN = 1;
   const dim3 grid((Tmax + 64 * WN - 1) / (64 * WN), B);
   pw_layer_x3_kernel<WN><<<grid, 256 * WN, 0, st>>>(a, W1x, W2x, oflow);

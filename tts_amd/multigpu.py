@@ -15,6 +15,10 @@ utterance in it, ``workload.lpt_shards``). Two ways to run the shards:
 """
 
 import multiprocessing as mp
+import os
+import queue
+import sys
+import time
 import traceback
 from typing import Callable, List, Optional, Sequence
 
@@ -56,8 +60,43 @@ def run_sharded(runner: Callable[[list], list], items: Sequence, costs: Sequence
     return [merged[i] for i in range(len(items))], mine
 
 
+def device_lock_path(device) -> str:
+    """Lock file that serialises this library's runner calls on one GPU across processes
+    (``TTS_GPU_LOCK_DIR``, default the temp directory)."""
+    import tempfile
+    d = os.environ.get("TTS_GPU_LOCK_DIR") or tempfile.gettempdir()
+    return os.path.join(d, f"tts_amd_gpu{device}.lock")
+
+
+class DeviceLock:
+    """Inter-process exclusive lock on one device label (``fcntl.flock`` on ``device_lock_path``).
+
+    The persistent decoder and BiLSTM launches hold every CU of their GPU for the whole call and
+    meet at grid barriers: two such launches from different processes on one GPU can leave part of
+    each grid waiting for CUs the other holds, and the barrier gives up after
+    TTS_BARRIER_TIMEOUT_MS. Workers that share a device therefore run their calls
+    one at a time under this lock."""
+
+    def __init__(self, device):
+        self.path = device_lock_path(device)
+        self._fd = None
+
+    def __enter__(self):
+        import fcntl
+        self._fd = os.open(self.path, os.O_RDWR | os.O_CREAT, 0o666)
+        fcntl.flock(self._fd, fcntl.LOCK_EX)
+        return self
+
+    def __exit__(self, *exc):
+        import fcntl
+        fcntl.flock(self._fd, fcntl.LOCK_UN)
+        os.close(self._fd)
+        self._fd = None
+
+
 def _pool_worker(factory, device, inq, outq):
-    """Worker process: build the runner for ``device`` once, then serve shards until None."""
+    """Worker process: build the runner for ``device`` once, then serve shards until None. Every
+    runner call holds the device's inter-process lock (``DeviceLock``)."""
     try:
         runner = factory(device)
         outq.put(("ready", device, None))
@@ -70,7 +109,9 @@ def _pool_worker(factory, device, inq, outq):
             break
         job, idx, items, kw = msg
         try:
-            outq.put(("done", job, (idx, runner(items, **kw))))
+            with DeviceLock(device):
+                res = runner(items, **kw)
+            outq.put(("done", job, (idx, res)))
         except Exception:
             outq.put(("error", job, traceback.format_exc()))
 
@@ -79,11 +120,20 @@ class GpuPool:
     """One worker process per device. ``factory(device)`` (picklable: a module-level function or a
     functools.partial of one) builds the per-device runner inside the worker; the runner maps a list
     of items to a list of results. Create the pool before this process touches the GPU: workers are
-    started with the 'spawn' method and initialise their own device."""
+    started with the 'spawn' method and initialise their own device (a GPU-initialised parent is
+    refused). A device may be listed more than once: its workers' calls are serialised by a
+    per-device inter-process lock (``DeviceLock``), so their grid-barrier launches never share the
+    GPU at the same time."""
+
+    POLL_S = 0.5  # how often map() checks that its workers are alive while it waits
 
     def __init__(self, factory: Callable, devices: Sequence[int], start_timeout: float = 600.0):
         if not devices:
             raise ValueError("GpuPool needs at least one device")
+        torch = sys.modules.get("torch")
+        if torch is not None and torch.cuda.is_initialized():
+            raise RuntimeError("GpuPool must be created before this process initialises the GPU "
+                               "(spawned workers initialise their own device)")
         ctx = mp.get_context("spawn")
         self.devices = list(devices)
         self._out = ctx.Queue()
@@ -93,9 +143,19 @@ class GpuPool:
         for p in self._procs:
             p.start()
         self._job = 0
+        self._broken = None
         ready, errors = 0, []
+        deadline = time.monotonic() + start_timeout
         while ready + len(errors) < len(self._procs):
-            kind, dev, payload = self._out.get(timeout=start_timeout)
+            try:
+                kind, dev, payload = self._out.get(timeout=self.POLL_S)
+            except queue.Empty:
+                dead = self._dead()
+                if dead or time.monotonic() > deadline:
+                    self.close()
+                    raise RuntimeError("GpuPool worker failed to start: " +
+                                       (f"worker for device(s) {dead} exited" if dead else "timed out"))
+                continue
             if kind == "ready":
                 ready += 1
             else:
@@ -104,9 +164,16 @@ class GpuPool:
             self.close()
             raise RuntimeError("GpuPool worker failed to start:\n" + "\n".join(errors))
 
+    def _dead(self) -> List[int]:
+        return [d for d, p in zip(self.devices, self._procs) if not p.is_alive()]
+
     def map(self, items: Sequence, costs: Optional[Sequence[float]] = None, timeout: float = 3600.0, **kw) -> list:
         """Results for ``items`` in input order; shards planned by LPT on ``costs`` (default: equal
-        costs). Keyword arguments go to every runner call."""
+        costs). Keyword arguments go to every runner call. A worker that dies, or a call past
+        ``timeout`` seconds, raises and leaves the pool unusable (results of an abandoned call
+        could still arrive)."""
+        if self._broken:
+            raise RuntimeError(f"GpuPool is unusable: {self._broken}")
         n = len(items)
         if n == 0:
             return []
@@ -121,10 +188,23 @@ class GpuPool:
                 sent += 1
         out = [None] * n
         errors = []
-        for _ in range(sent):
-            kind, j, payload = self._out.get(timeout=timeout)
-            if j != job:
-                raise RuntimeError("GpuPool: result of another job")
+        got = 0
+        deadline = time.monotonic() + timeout
+        while got < sent:
+            try:
+                kind, j, payload = self._out.get(timeout=self.POLL_S)
+            except queue.Empty:
+                dead = self._dead()
+                if dead:
+                    self._broken = f"worker for device(s) {dead} exited"
+                    raise RuntimeError(f"GpuPool: {self._broken} during map()")
+                if time.monotonic() > deadline:
+                    self._broken = f"map() timed out after {timeout} s"
+                    raise RuntimeError(f"GpuPool: {self._broken}")
+                continue
+            if j != job:  # a result of an earlier call that raised before it arrived
+                continue
+            got += 1
             if kind == "error":
                 errors.append(payload)
                 continue
