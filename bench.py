@@ -64,6 +64,17 @@ def pipeline_bound_ms(T, steps, r, peak_tflops=F32_PEAK_TFLOPS):
     return (dec + other) * 1e3, dec * 1e3
 
 
+def latest_profile(name):
+    """The newest record ``profiles/r<NN>/<name>`` (the current round's measurement of this tree
+    once it exists), else ``profiles/<name>``; None if neither exists."""
+    import glob
+    rounds = sorted(glob.glob(os.path.join(ROOT, "profiles", "r[0-9][0-9]", name)), reverse=True)
+    if rounds:
+        return rounds[0]
+    flat = os.path.join(ROOT, "profiles", name)
+    return flat if os.path.exists(flat) else None
+
+
 def build_models(device, seed=0):
     tcfg = TacotronConfig()
     tsd = synth_state_dict(tacotron2_spec(tcfg), seed)
@@ -156,8 +167,8 @@ def cpu_baseline(tsd, vsd, tcfg, vcfg, ids, steps, r, budget_s):
     el = t_taco + t_voc
     audio = frames * HOP / SAMPLE_RATE
     calib = None  # this restatement timed beside the imported reference (build container, same weights)
-    cpath = os.path.join(ROOT, "profiles", "r03", f"cpu_baseline_check_r{r}.json")
-    if os.path.exists(cpath):
+    cpath = latest_profile(f"cpu_baseline_check_r{r}.json")
+    if cpath:
         try:
             cj = json.load(open(cpath))
             calib = {"port_over_reference_e2e": cj["aten_port_over_reference_e2e"],
@@ -373,11 +384,12 @@ def main():
         flops = row_steps * flop_row + att_flops
         achieved = flops / (ms0 * 1e-3) / 1e12
         step_ms = ms0 / max(st0, 1)
-        traffic = None
-        pmc = os.path.join(ROOT, "profiles", "persist_pmc.json")
-        if os.path.exists(pmc):
+        traffic, traffic_src = None, None
+        pmc = latest_profile("persist_pmc.json")
+        if pmc:
             try:
                 traffic = json.load(open(pmc)).get("hbm_bytes_per_launch")
+                traffic_src = os.path.relpath(pmc, ROOT)
             except Exception:
                 traffic = None
         # split-f16 mode: the decoder's GEMM parts run 3 f16 MFMAs per fp32 product, so the
@@ -389,8 +401,8 @@ def main():
         # sizes and no arithmetic (profiles/r04/chain_floor.json). achieved / peak stay the MFMA
         # figures (algorithmic FLOPs / launch time against the split-f16 ceiling)
         floor = None
-        fpath = os.path.join(ROOT, "profiles", "r04", "chain_floor.json")
-        if os.path.exists(fpath):
+        fpath = latest_profile("chain_floor.json")
+        if fpath:
             try:
                 floor = json.load(open(fpath))
             except Exception:
@@ -400,7 +412,7 @@ def main():
                 "bound": "latency", "compute_bound": "mfma",
                 "achieved": round(achieved, 2), "peak": peak, "unit": "TFLOP/s",
                 "frac": round(achieved / peak, 4), "frac_vs_fp32_mfma_peak": round(achieved / F32_PEAK_TFLOPS, 4),
-                "traffic": traffic,
+                "traffic": traffic, "traffic_source": traffic_src,
                 "avg_launch_us": round(ms0 * 1000.0, 1), "algorithmic_flops": flops,
                 "launch_steps": st0, "launches": [[round(m_, 3), s_] for m_, s_ in launches]}
         if floor:

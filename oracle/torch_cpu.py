@@ -176,3 +176,117 @@ class MelganTorchCPU:
             x = F.conv_transpose1d(x, updown * N, stride=N)
             x = F.conv1d(x, self.G, padding=(self.G.shape[-1] - 1) // 2)
         return x.reshape(-1).numpy()
+
+
+class PwganTorchCPU:
+    """ParallelWaveGAN generator inference (config C4's vocoder) at B = 1, float32 ATen on the CPU:
+    the same op sequence as ``oracle/pwgan_np.py`` (which it is checked against) with conv1d /
+    conv2d doing the work, fast enough to check every row of a 64-row batch.
+
+    * ``TTS/vocoder/models/parallel_wavegan_generator.py:90-125``  replicate pad, first_conv on the
+      noise, upsample, residual blocks, skip sum * sqrt(1 / layers), ReLU-conv-ReLU-conv
+    * ``TTS/vocoder/layers/upsample.py:5-101``  ConvUpsample: conv_in (no bias), per factor s a
+      nearest stretch then a (1, 2s + 1) Conv2d with zero padding (0, s), no bias
+    * ``TTS/vocoder/layers/parallel_wavegan.py:56-87``  dilated conv + conv1x1_aux, tanh * sigmoid
+      gate, conv1x1_skip / conv1x1_out, (out + residual) * sqrt(0.5) ** 2 = 0.25 as the oracle folds it
+    """
+
+    def __init__(self, sd, cfg, device="cpu"):
+        """``device``: where PyTorch runs these fp32 ops. The GPU tests may put this reference on the
+        GPU (PyTorch's own ROCm kernels, independent of libttship) to check all 64 rows of the C4
+        batch in seconds; it is pinned to the reference fixtures on the CPU (test_oracle_golden)."""
+        from oracle.pwgan_np import fold_weight_norm
+        self.dev = torch.device(device)
+        self.w = {k: _t(v).to(self.dev) for k, v in fold_weight_norm(sd).items()}
+        self.c = cfg
+
+    def _aux(self, mel):
+        """replicate pad + ConvUpsample of one utterance: (80, M) -> (1, 80, T)."""
+        w, cfg = self.w, self.c
+        p = cfg.inference_padding
+        c = _t(mel).to(self.dev)[None]
+        if p:
+            c = F.pad(c, (p, p), mode="replicate")
+        c = F.conv1d(c, w["upsample_net.conv_in.weight"])
+        c = c[:, None]                                                         # (1, 1, 80, L)
+        for i, s in enumerate(cfg.upsample_factors):
+            c = F.interpolate(c, scale_factor=(1, s), mode="nearest")
+            c = F.conv2d(c, w[f"upsample_net.upsample.up_layers.{2 * i + 1}.weight"], padding=(0, s))
+        return c[:, 0]                                                         # (1, 80, T)
+
+    def inference_batch(self, mels, noises, chunk=1 << 20):
+        """Many utterances at once, each exactly as its own B = 1 call: the rows sit in one time axis
+        separated by zero gaps of the largest dilation, and the residual stream is re-zeroed in the
+        gaps after every layer, so every dilated tap past a row's end reads the zeros of B = 1 zero
+        padding. The residual blocks then run as (128 x 272) x columns GEMMs over column chunks.
+        mels: [(80, M_i)], noises: [(T_i,)] -> [waveform (T_i,)] numpy float32."""
+        w, cfg = self.w, self.c
+        G = max(cfg.dilation(i) for i in range(cfg.num_res_blocks)) * ((cfg.kernel_size - 1) // 2)
+        with torch.no_grad():
+            aux = [self._aux(m)[0] for m in mels]
+            starts, pos = [], G
+            for a in aux:
+                starts.append(pos)
+                pos += a.shape[1] + G
+            N = pos
+            c = torch.zeros(cfg.aux_channels, N, device=self.dev)
+            x = torch.zeros(cfg.res_channels, N, device=self.dev)
+            mask = torch.zeros(1, N, device=self.dev)
+            fw, fb = w["first_conv.weight"].reshape(-1, 1), w["first_conv.bias"].reshape(-1, 1)
+            for a, nz, s0 in zip(aux, noises, starts):
+                n = a.shape[1]
+                assert len(nz) == n, "noise length != upsampled length"
+                c[:, s0:s0 + n] = a
+                x[:, s0:s0 + n] = fw * _t(nz).to(self.dev)[None] + fb
+                mask[:, s0:s0 + n] = 1.0
+            skips = torch.zeros(cfg.skip_channels, N, device=self.dev)
+            H = cfg.gate_channels // 2
+            for i in range(cfg.num_res_blocks):
+                q = f"conv_layers.{i}."
+                d = cfg.dilation(i)
+                W = w[q + "conv.weight"]                                      # (128, 64, 3): taps t-d, t, t+d
+                Wc = torch.cat([W[:, :, k] for k in range(cfg.kernel_size)], 1)
+                Wa, b = w[q + "conv1x1_aux.weight"][:, :, 0], w[q + "conv.bias"].reshape(-1, 1)
+                Ws, bs = w[q + "conv1x1_skip.weight"][:, :, 0], w[q + "conv1x1_skip.bias"].reshape(-1, 1)
+                Wo, bo = w[q + "conv1x1_out.weight"][:, :, 0], w[q + "conv1x1_out.bias"].reshape(-1, 1)
+                xn = torch.zeros_like(x)
+                for s0 in range(G, N - G, chunk):
+                    e = min(s0 + chunk, N - G)
+                    X3 = torch.cat([x[:, s0 - d:e - d], x[:, s0:e], x[:, s0 + d:e + d]], 0)
+                    a = torch.addmm(b, Wc, X3) + Wa @ c[:, s0:e]
+                    z = torch.tanh(a[:H]) * torch.sigmoid(a[H:])
+                    skips[:, s0:e] += torch.addmm(bs, Ws, z)
+                    xn[:, s0:e] = (torch.addmm(bo, Wo, z) + x[:, s0:e]) * 0.25
+                x = xn * mask
+            outs = []
+            w1, b1 = w["last_conv_layers.1.weight"][:, :, 0], w["last_conv_layers.1.bias"].reshape(-1, 1)
+            w3, b3 = w["last_conv_layers.3.weight"][:, :, 0], w["last_conv_layers.3.bias"].reshape(-1, 1)
+            for a, s0 in zip(aux, starts):
+                n = a.shape[1]
+                h = torch.relu(skips[:, s0:s0 + n] * (1.0 / cfg.num_res_blocks) ** 0.5)
+                h = torch.relu(torch.addmm(b1, w1, h))
+                outs.append(torch.addmm(b3, w3, h)[0].cpu().numpy())
+        return outs
+
+    def inference(self, mel, noise):
+        """mel (80, M), noise (T,) with T = (M + 2 pad) * 256 -> waveform (T,) numpy float32."""
+        w, cfg = self.w, self.c
+        with torch.no_grad():
+            c = self._aux(mel)                                                 # (1, 80, T)
+            x = F.conv1d(_t(noise).to(self.dev)[None, None], w["first_conv.weight"], w["first_conv.bias"])
+            skips = 0
+            H = cfg.gate_channels // 2
+            for i in range(cfg.num_res_blocks):
+                q = f"conv_layers.{i}."
+                d = cfg.dilation(i)
+                a = F.conv1d(x, w[q + "conv.weight"], w[q + "conv.bias"], padding=(cfg.kernel_size - 1) // 2 * d,
+                             dilation=d)
+                a = a + F.conv1d(c, w[q + "conv1x1_aux.weight"])
+                z = torch.tanh(a[:, :H]) * torch.sigmoid(a[:, H:])
+                s = F.conv1d(z, w[q + "conv1x1_skip.weight"], w[q + "conv1x1_skip.bias"])
+                x = (F.conv1d(z, w[q + "conv1x1_out.weight"], w[q + "conv1x1_out.bias"]) + x) * 0.25
+                skips = skips + s
+            h = torch.relu(skips * (1.0 / cfg.num_res_blocks) ** 0.5)
+            h = torch.relu(F.conv1d(h, w["last_conv_layers.1.weight"], w["last_conv_layers.1.bias"]))
+            y = F.conv1d(h, w["last_conv_layers.3.weight"], w["last_conv_layers.3.bias"])
+        return y[0, 0].cpu().numpy()

@@ -216,6 +216,34 @@ def test_pwgan_oracle_matches_reference():
         assert np.abs(y - fx[f"M{M}_wav"][0, 0]).max() <= 2e-6
 
 
+def test_torch_pwgan_reference_matches_reference_and_numpy_oracle():
+    """oracle/torch_cpu.py PwganTorchCPU (the ATen form the C4 GPU test checks all 64 rows with): its
+    batched form against the reference's own ParallelWaveganGenerator.inference fixtures (M = 5 and
+    11, inference_padding 2) and, on a ragged 3-row batch at padding 0, each row against its own
+    B = 1 call and the numpy oracle."""
+    import dataclasses
+    from oracle.pwgan_np import PwganOracle
+    from oracle.torch_cpu import PwganTorchCPU
+    from tts_amd.spec import PwganConfig, pwgan_spec
+    from tts_amd.weights import synth_state_dict
+    fx = load_fixture("pwgan")
+    cfg = PwganConfig()
+    sd = synth_state_dict(pwgan_spec(cfg), int(fx["seed"]))
+    ys = PwganTorchCPU(sd, cfg).inference_batch([fx["M5_mel"][0], fx["M11_mel"][0]],
+                                                [fx["M5_noise"][0, 0], fx["M11_noise"][0, 0]])
+    for M, y in zip((5, 11), ys):
+        assert y.shape == fx[f"M{M}_wav"][0, 0].shape
+        assert np.abs(y - fx[f"M{M}_wav"][0, 0]).max() <= 2e-6
+    c0 = dataclasses.replace(cfg, inference_padding=0)
+    pt, po = PwganTorchCPU(sd, c0), PwganOracle(sd, c0)
+    rs = np.random.RandomState(0)
+    mels = [rs.randn(80, m).astype(np.float32) for m in (9, 3, 14)]
+    noises = [rs.randn(m.shape[1] * 256).astype(np.float32) for m in mels]
+    for m, n, y in zip(mels, noises, pt.inference_batch(mels, noises, chunk=1000)):
+        assert np.abs(y - pt.inference(m, n)).max() <= 1e-6
+        assert np.abs(y - po.inference(m, n)).max() <= 2e-6
+
+
 @pytest.mark.parametrize("r", [2, 1])
 def test_torch_cpu_baseline_tacotron2_matches_reference(r):
     """bench.py's cpu_baseline (oracle/torch_cpu.py, the ATen op sequence) against the reference."""

@@ -5,7 +5,7 @@ oracle's host-CPU number on the GPU box can be read against the reference's. Bui
 
     PYTHONPATH=/root/reference:/root/repo python tools/cpu_baseline_check.py [--threads 8] [--r 2]
 
-Writes profiles/r03/cpu_baseline_check_r{r}.json.
+Writes profiles/<round>/cpu_baseline_check_r{r}.json (--round, default r05).
 """
 import argparse
 import json
@@ -31,6 +31,7 @@ def main():
     ap.add_argument("--threads", type=int, default=8)
     ap.add_argument("--r", type=int, default=2)
     ap.add_argument("--n", type=int, default=32, help="utterances (file order)")
+    ap.add_argument("--round", default="r05", help="profiles/ subdirectory the record goes to")
     args = ap.parse_args()
     from threadpoolctl import threadpool_limits
     from TTS.tts.models.tacotron2 import Tacotron2
@@ -132,7 +133,7 @@ def main():
            "oracle_over_reference_tacotron2": round(res["oracle"]["tacotron2_frames_per_s"]
                                                     / res["reference"]["tacotron2_frames_per_s"], 3),
            "oracle_over_reference_e2e": round(res["oracle"]["e2e_frames_per_s"] / res["reference"]["e2e_frames_per_s"], 3)}
-    path = os.path.join(ROOT, "profiles", "r03", f"cpu_baseline_check_r{r}.json")
+    path = os.path.join(ROOT, "profiles", args.round, f"cpu_baseline_check_r{r}.json")
     json.dump(out, open(path, "w"), indent=1)
     print(json.dumps(out))
 

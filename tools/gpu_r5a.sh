@@ -5,7 +5,8 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-step() { local name=$1; shift; echo "== $name $(date +%T)"; "$@"; local rc=$?; echo "== $name rc=$rc"; return $rc; }
+exec 3>&1
+step() { local name=$1; shift; echo "== $name $(date +%T)" >&3; "$@"; local rc=$?; echo "== $name rc=$rc" >&3; return $rc; }
 bl() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['ms_per_step'], d['decoder_step_us'], d['tacotron2_ms'], d['vocoder_ms'], d['roofline']['launches'])" $1; }
 step tests timeout -k 10 400 python3 -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/a_tests.log 2>&1 || { tail -30 gpurun_out/a_tests.log; exit 1; }
 tail -2 gpurun_out/a_tests.log

@@ -46,6 +46,10 @@ def main():
         "hbm_bytes_per_launch": int(2 * f_kb * 1024 + w_kb * 1024),
         "correction": "FETCH_SIZE x2 (gfx950 half-count of 16-B/lane reads); Infinity-Cache hits are counted",
     }
+    info = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tts_amd", "build_info.json")
+    if os.path.exists(info):  # which build of the sources the counted library was
+        b = json.load(open(info))
+        out["library_sha256"], out["sources_sha256"] = b.get("library_sha256"), b.get("sources_sha256")
     json.dump(out, open(sys.argv[3], "w"), indent=1)
     print(json.dumps(out))
 

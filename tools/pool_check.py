@@ -32,6 +32,7 @@ def main(argv):
     synth = Synthesizer(conf)
     try:
         assert synth.pool is not None and len(synth.pool.devices) == len(devices)
+        assert synth.tts_model is None and synth.vocoder_model is None  # the models live in the workers
         cfg, sd, mcfg, msd = T._synth_models()
         to, vo = TacoOracle(sd, cfg.attn_norm, cfg.r), melgan_oracle(mcfg, msd)
         sens = ["Hello world.", "This is a longer test of the sharded path, with 2 numbers!", "Short one?",

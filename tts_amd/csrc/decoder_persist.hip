@@ -169,14 +169,16 @@ __device__ __forceinline__ float wave64_sum(float v) {
 // t0 + 16 (i >> 2) + 4 (lane >> 4) + (i & 3), attention dim 16 wave + (lane & 15). Sums
 // loc + penc before the query is added: (pq + (loc + penc)) instead of the reference's
 // ((pq + loc) + penc), a one-ulp reassociation inside the tanh argument.
-__device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* Aw, const float* wcomb, float (&L)[8]) {
+// T: the utterance's length (D.lens[b], read by the caller: for a workgroup's first item once per
+// launch, so that the window loads below do not wait for it)
+__device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, int T, float* Aw, const float* wcomb,
+                                         float (&L)[8]) {
   const DecDev& D = P.D;
   const int t0 = ch * PTC;
   const int tid = opaque_v(threadIdx.x);
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int a = 16 * wave + (lane & 15);
-  const int T = D.lens[b];
   const int Tm1 = max(T - 1, 0);
   float aw;
   {
@@ -223,7 +225,7 @@ __device__ __forceinline__ void attn_loc(const PArgs& P, int b, int ch, float* A
 // ekeep: (deferred alignment pass) LDS slot [32 energies | valid flag] of this item, kept until P6;
 // null: the last arriver runs the alignment pass itself (decoder variants, many items per workgroup)
 template <int MT, int VAR>
-__device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, float* sm, const float* wcomb,
+__device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch, int Tb, float* sm, const float* wcomb,
                                            int* is_last, float (&L)[8], bool haveL,
                                            f32x4 (&evc)[pec_arr(VAR, MT)], bool load_ev, float* ekeep) {
   constexpr int PEC = pec_of(VAR, MT);
@@ -240,23 +242,25 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   float* sv = esum + 8 * TC;    // [TC] energies
   float* sw = sv + TC;          // [TC] normalised weights
   float* swf = sw + TC;         // [TC] forward-attention weights
-  if (!haveL) attn_loc(P, b, ch, Aw, wcomb, L);  // items beyond a workgroup's first
+  if (!haveL) attn_loc(P, b, ch, Tb, Aw, wcomb, L);  // items beyond a workgroup's first
   const int tid = opaque_v(threadIdx.x);
   const int lane = tid & 63;
   const int wave = __builtin_amdgcn_readfirstlane(tid >> 6);  // attention dims 16 wave .. 16 wave + 15
   const int a = 16 * wave + (lane & 15);                       // this lane's dim in the MFMA output
-  const int T = D.lens[b];
-  const int Tm1 = max(T - 1, 0);
   // ---- independent loads first (clamped indices), in the order they are consumed: vmcnt is an
-  //      in-order counter, so waiting for an early load does not wait for the later ones ----
-  const int dn = ldci(D.done + b);
-  __builtin_amdgcn_sched_barrier(0);
+  //      in-order counter, so waiting for an early load does not wait for the later ones. The
+  //      query partials (the phase's critical hand-off) go out before anything whose value is
+  //      needed to form an address: reading the utterance length first put a full load round
+  //      trip (~0.5 us) in front of them ----
   const int a4 = tid & 31, pg = tid >> 5;  // query partials: 16-byte loads, dims 4 a4 .. 4 a4 + 3
   f32x4 pp[NPT];
 #pragma unroll
   for (int i = 0; i < NPT; ++i) pp[i] = ldc4(P.pq, ((((pg * NPT + i) * Bp + b) * ADIM_) + 4 * a4) * 4);
+  const int dn = ldci(D.done + b);
   const float va = P.v[a];
   __builtin_amdgcn_sched_barrier(0);
+  const int T = Tb;
+  const int Tm1 = max(T - 1, 0);
   ATRACE(0);
   if (t0 >= T || dn) return;  // workgroup-uniform
   {
@@ -1023,6 +1027,9 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   __syncthreads();
 
   unsigned gen = 0;
+  // the first attention item's utterance length, constant over the launch
+  const int it_first = g - IW0;
+  const int T_first = (it_first >= 0 && it_first < D.B * P.nchmax) ? D.lens[it_first / P.nchmax] : 0;
   float Lr[8];  // location features of the first attention item (attn_loc in P1, used in P4)
   f32x4 evc[pec_arr(VAR, MT)];  // encoder rows of the first attention item (loaded on its first step)
   const int t_first = D.ctl->base;
@@ -1137,21 +1144,25 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     // final); items sit on workgroups IW0.. so that they miss the prenet workgroups
     const int it0 = g - IW0;
     if (!GRAVES && it0 >= 0 && it0 < D.B * P.nchmax)
-      attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, scr + 16 * ADIM_, wcomb, Lr);
+      attn_loc(P, it0 / P.nchmax, it0 % P.nchmax, T_first, scr + 16 * ADIM_, wcomb, Lr);
     // stop decision: an attention_rnn workgroup that is not a prenet one (MT <= 2), or the last
     // item workgroup once every attention_rnn workgroup runs a prenet job (MT = 3, 4)
     if (g == (MT <= 2 ? IW0 - 1 : PW - 1)) {
       int dn = 1;
       if (tid < D.B) {
         const int m = tid;
+        // every input of the decision in one round trip (the logit's loads used to wait for the
+        // done flag's)
         dn = ldci(D.done + m);
+        const float y0 = ldc(P.ypart + (long)m * YP), y1 = X3P ? 0.f : ldc(P.ypart + (long)(YROWS + m) * YP);
+        const float yb = pjb1(m, 0);
+        const int msteps = D.max_steps[m];
         if (t >= 1 && !dn) {
-          const float logit = ldc(P.ypart + (long)m * YP) + (X3P ? 0.f : ldc(P.ypart + (long)(YROWS + m) * YP)) +
-                              pjb1(m, 0);
+          const float logit = y0 + y1 + yb;
           const float sg = sigm(logit);
           if (t - 1 < D.S_cap) D.stop_out[(long)m * D.S_cap + (t - 1)] = sg;
           const bool st = (sg > P.thr) && (t - 1) > 0;
-          if (st || t >= D.max_steps[m]) {
+          if (st || t >= msteps) {
             stci(D.done + m, 1);
             stci(D.steps + m, t);
             stci(D.status + m, st ? 1 : 2);
@@ -1207,22 +1218,32 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     }
     if (!gsync_wait(P.bar, gen, &sflag)) return;
     PTRACE(2);
-    {
-      const int all_done = ldci(&D.ctl->all_done), act = ldci(&D.ctl->active_tiles);
-      if (all_done || act < MT || t > D.S_cap + 1) {
+    tid = opaque_v(tid0);
+    lane = opaque_v(lane0);
+    wave = opaque_s(wave0);
+    // loop exit: rows all done, the batch tile shrank (the next launch takes over), or past S_cap.
+    // The exit words are a coherent load round trip (~0.5 us) after the barrier; the split-f16
+    // attention_rnn workgroups (P3's critical path) evaluate them only after their first staging
+    // pass, so that round trip overlaps their operand loads instead of preceding them (nothing
+    // before that point writes anything outside LDS)
+    const int ex_done = ldci(&D.ctl->all_done), ex_act = ldci(&D.ctl->active_tiles);
+    // (the words pass through opaque copies at each test, so the compiler cannot hoist their
+    // scalar conversion, and with it the wait for the load, above the operand loads)
+    auto p3_exit = [&]() {
+      const int done = opaque_v(ex_done), act = opaque_v(ex_act);
+      if (done || act < MT || t > D.S_cap + 1) {
         write_frames(t - 1, 0, PW);
         if (g == 0 && tid == 0) {
           D.ctl->base = t;
           if (P.base_out) *P.base_out = t;
         }
-        return;
+        return true;
       }
-    }
+      return false;
+    };
+    if (!(X3P && g < NATT) && p3_exit()) return;
     // ======== P3: attention_rnn (prenet part) + cell + query partials (workgroups 0 .. NATT-1)
     //            || frames(t-1) + the decoder_rnn h_dec part (item workgroups) ========
-    tid = opaque_v(tid0);
-    lane = opaque_v(lane0);
-    wave = opaque_s(wave0);
     if (g < NATT) {
       // relu(prenet output) staged once per workgroup in LDS (the Wcomb area: attention_rnn
       // workgroups have no attention item); wave w loads k-chunks 2w, 2w+1
@@ -1244,11 +1265,18 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
         for (int ps = 0; ps < NCK; ++ps) {
           if (ps > 0) lds_barrier();  // the previous pass's operand reads are done
+          f32x4 xv[CM][2];
 #pragma unroll
           for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt) {
             const int c = mt * 16 + 2 * wave + (lane >> 5);
-            const f32x4 x0 = ldc4(P.pb, (c * 64 + l1) * 16);
-            const f32x4 x1 = ldc4(P.pb, (c * 64 + l1 + 16) * 16);
+            xv[mt - ps * CM][0] = ldc4(P.pb, (c * 64 + l1) * 16);
+            xv[mt - ps * CM][1] = ldc4(P.pb, (c * 64 + l1 + 16) * 16);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+          if (ps == 0 && p3_exit()) return;  // workgroup-uniform; the operand loads are in flight
+#pragma unroll
+          for (int mt = ps * CM; mt < min(MT, ps * CM + CM); ++mt) {
+            const f32x4 x0 = xv[mt - ps * CM][0], x1 = xv[mt - ps * CM][1];
             float v[8];
             float mx = 0.f;
 #pragma unroll
@@ -1421,8 +1449,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
             if (tid == 0) ek[PTC] = 0.f;  // set by the item when its utterance is still decoding
           }
           if constexpr (GRAVES) graves_item<MT>(P, t, it / P.nchmax, it % P.nchmax, scr, &is_last);
-          else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, scr, wcomb, &is_last, Lr, it < PW - IW0,
-                                   evc, nitems > PW - IW0 || t == t_first, ek);
+          else pattn_item<MT, VAR>(P, t, it / P.nchmax, it % P.nchmax, it < PW - IW0 ? T_first : D.lens[it / P.nchmax],
+                                   scr, wcomb, &is_last, Lr, it < PW - IW0, evc, nitems > PW - IW0 || t == t_first, ek);
           lds_barrier();
         }
         // split-f16: the h_att part runs at the start of P5 instead (h_att is still in place), off

@@ -10,6 +10,12 @@
 #include "gsync.h"
 #include "split16.h"
 
+// row stride of the LDS gate-partial reductions [wave][row][LRS]: writers put rows r and r + 4 of a
+// 32-lane group 80 = 16 (mod 32) banks apart, the cell threads read rows m = tid / 4 (8 per group)
+// at columns 4 q + (tid & 3): 20 m mod 32 = {0, 20, 8, 28, 16, 4, 24, 12} + 0..3, no two alike
+// (stride 17 put 2 lanes on one bank: 2-way conflicts on every read of the reduction)
+constexpr int LRS = 20;
+
 __global__ __launch_bounds__(256) void embed_gather_kernel(const int64_t* __restrict__ ids, int T_max,
                                                            const float* __restrict__ table, int num_rows,
                                                            int D, const int* lens,
@@ -47,7 +53,7 @@ __global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restric
                                                           float* __restrict__ c, float* __restrict__ out) {
   constexpr int Bp = MT * 16;
   constexpr int H = 256, NKC = H / 16, KPW = NKC / 4;  // 4 k-chunks per wave
-  __shared__ float part[4 * Bp * 17];
+  __shared__ float part[4 * Bp * LRS];
   const int dir = blockIdx.x >> 6, tl = blockIdx.x & 63;
   const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const f32x4* Wv = reinterpret_cast<const f32x4*>(Whh) + ((long)(dir * 64 + tl) * NKC + wave * KPW) * 64 + lane;
@@ -79,18 +85,18 @@ __global__ __launch_bounds__(256) void bilstm_step_kernel(const float* __restric
     for (int s4 = 0; s4 < 4; ++s4)
 #pragma unroll
       for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[k][mt][s4], w[k][s4], acc[mt]);
-  float* p = part + wave * Bp * 17;
+  float* p = part + wave * Bp * LRS;
 #pragma unroll
   for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-    for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
+    for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * LRS + (lane & 15)] = acc[mt][j];
   __syncthreads();
   if (!valid) return;
   float pre[4];
 #pragma unroll
   for (int q = 0; q < 4; ++q) {
     const int n = q * 4 + u;
-    pre[q] = part[m * 17 + n] + part[(Bp + m) * 17 + n] + part[(2 * Bp + m) * 17 + n] + part[(3 * Bp + m) * 17 + n] +
+    pre[q] = part[m * LRS + n] + part[(Bp + m) * LRS + n] + part[(2 * Bp + m) * LRS + n] + part[(3 * Bp + m) * LRS + n] +
              gin[q];
   }
   const float ig = 1.f / (1.f + expf(-pre[0]));
@@ -131,7 +137,7 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
   constexpr int NKC = H / 16, KPW = NKC / NW;  // k-chunks, per wave
   constexpr int G = NDIR * 4 * H, O = NDIR * H;
   static_assert(NKC % NW == 0 && KPW % 2 == 0 && NT % 8 == 0, "LSTM geometry");
-  __shared__ float part[NW * Bp * 17];
+  __shared__ float part[NW * Bp * LRS];
   __shared__ int sflag;
   const int RG = gridDim.x / (NDIR * NT);      // row groups (the launcher sizes the grid)
   const int rg = blockIdx.x / (NDIR * NT);
@@ -216,20 +222,20 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
 #pragma unroll
           for (int mt = 0; mt < MT; ++mt) acc[mt] = MFMA16(x[k][mt][s4], w[k][s4], acc[mt]);
     }
-    float* p = part + wave * Bp * 17;
+    float* p = part + wave * Bp * LRS;
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt)
 #pragma unroll
-      for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * 17 + (lane & 15)] = acc[mt][j];
+      for (int j = 0; j < 4; ++j) p[(mt * 16 + 4 * (lane >> 4) + j) * LRS + (lane & 15)] = acc[mt][j];
     lds_barrier();
     if (row && step < Tm) {
       float pre[4];
 #pragma unroll
       for (int q = 0; q < 4; ++q) {
         const int n = q * 4 + u;
-        float sum = part[m * 17 + n];
+        float sum = part[m * LRS + n];
 #pragma unroll
-        for (int w = 1; w < NW; ++w) sum += part[(w * Bp + m) * 17 + n];
+        for (int w = 1; w < NW; ++w) sum += part[(w * Bp + m) * LRS + n];
         pre[q] = sum + gin[q];
       }
       cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
@@ -349,7 +355,7 @@ __device__ __forceinline__ T pick4(T v0, T v1, T v2, T v3, int i) {  // wave-uni
 
 __global__ __launch_bounds__(64 * GP_NW) void ge2e_pipe_kernel(GePipeArgs a) {
   constexpr int H = 768, KSH = H / 32;  // 24 k-steps per 768-wide operand
-  __shared__ float part[GP_NW][3][16 * 17];
+  __shared__ float part[GP_NW][3][16 * 17];  // (stride 17: see LRS; this kernel reads 3 tiles per row group)
   __shared__ int sflag;
   const int l = blockIdx.x / GP_TILES, tile = blockIdx.x % GP_TILES;
   const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);

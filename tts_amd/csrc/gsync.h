@@ -32,6 +32,7 @@
 #include <cstdlib>
 #include <map>
 #include <mutex>
+#include <utility>
 
 constexpr int BAR_TMO = 48;  // word of the barrier block holding the wait limit (s_memrealtime ticks)
 // words per barrier block: 0 global counter, 16 error word, 32 go word, BAR_TMO wait limit, then up
@@ -72,21 +73,21 @@ inline bool gsync_count_ok(unsigned n) { return n > 0 && n % (n >= 256 ? 16u : 8
 // written), so the plain launch is the default. TTS_COOP_LAUNCH=1 restores it.
 inline void launch_resident(const void* f, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
   static std::mutex mu;
-  static std::map<const void*, int> fits;  // kernel -> workgroups the device holds at once
+  static std::map<std::pair<const void*, int>, int> fits;  // (kernel, device) -> workgroups it holds at once
   static const bool coop = [] {
     const char* e = std::getenv("TTS_COOP_LAUNCH");
     return e && std::atoi(e) != 0;
   }();
-  int cap = 0;
+  int cap = 0, dev = 0;
+  HIP_OK(hipGetDevice(&dev));
   {
     std::lock_guard<std::mutex> lk(mu);
-    auto it = fits.find(f);
+    auto it = fits.find({f, dev});
     if (it == fits.end()) {
-      int dev = 0, cus = 0, nb = 0;
-      HIP_OK(hipGetDevice(&dev));
+      int cus = 0, nb = 0;
       HIP_OK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev));
       HIP_OK(hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, f, (int)(block.x * block.y * block.z), lds));
-      it = fits.emplace(f, nb * cus).first;
+      it = fits.emplace(std::make_pair(f, dev), nb * cus).first;
     }
     cap = it->second;
   }

@@ -49,20 +49,25 @@ class Synthesizer:
         if devices is None and int(config.get("num_gpus") or 1) > 1:
             devices = list(range(min(int(config["num_gpus"]), torch.cuda.device_count())))
         if self.use_cuda and devices is not None and len(devices) > 1:
-            # one worker per GPU, started before this process makes any GPU call; the models here
-            # stay on the host (text front end, audio processor and shapes only)
+            # one worker per GPU, started before this process makes any GPU call; every worker loads
+            # the models, this process keeps the text front end and the audio processor only
             self.pool = GpuPool(functools.partial(_pool_synthesizer, dict(config), phonemize), devices)
             self.use_cuda = False
         if self.use_cuda:
             assert torch.cuda.is_available(), "CUDA is not availabe on this machine."
-        self.load_tts(config["tts_checkpoint"], config["tts_config"], self.use_cuda)
-        if config.get("vocoder_checkpoint"):
-            self.load_vocoder(config["vocoder_checkpoint"], config["vocoder_config"], self.use_cuda)
+        self.tts_model = None
+        if self.pool is not None:
+            self.load_tts_config(config["tts_config"])
+        else:
+            self.load_tts(config["tts_checkpoint"], config["tts_config"], self.use_cuda)
+            if config.get("vocoder_checkpoint"):
+                self.load_vocoder(config["vocoder_checkpoint"], config["vocoder_config"], self.use_cuda)
         if config.get("wavernn_lib_path"):
             raise NotImplementedError("WaveRNN is outside the MI355X hot path (SURVEY.md §8f)")
 
-    def load_tts(self, tts_checkpoint, tts_config, use_cuda):
-        """synthesizer.py:44-82"""
+    def load_tts_config(self, tts_config):
+        """The config half of synthesizer.py:44-67: model config, audio processor, symbol tables,
+        speaker mapping (what the text front end and the output stage need)."""
         self.tts_config = load_config(tts_config) if isinstance(tts_config, str) else tts_config
         self.use_phonemes = self.tts_config["use_phonemes"]
         self.ap = AudioProcessor(**self.tts_config["audio"])
@@ -83,7 +88,12 @@ class Synthesizer:
             except FileNotFoundError:
                 self.tts_speakers = {}
             num_speakers = len(self.tts_speakers)
-        self.tts_model = setup_model(self.input_size, num_speakers=num_speakers, c=self.tts_config)
+        self.num_speakers = num_speakers
+
+    def load_tts(self, tts_checkpoint, tts_config, use_cuda):
+        """synthesizer.py:44-82"""
+        self.load_tts_config(tts_config)
+        self.tts_model = setup_model(self.input_size, num_speakers=self.num_speakers, c=self.tts_config)
         cp = torch.load(tts_checkpoint, map_location=torch.device("cpu"), weights_only=True)
         self.tts_model.load_state_dict(cp["model"])
         if use_cuda:
