@@ -38,10 +38,17 @@ def tanh_f(x, s):
     return np.copysign(np.where(ax < f32(0.25), small, big), x).astype(f32)
 
 
+def tanh_e(x, s):  # the attention energies' form: no small-argument polynomial
+    ax = np.abs(x).astype(f32)
+    e = exp2_hw(f32(-2.8853900817779268) * ax, s)
+    return np.copysign(((f32(1) - e) * rcp_hw(f32(1) + e, -s)).astype(f32), x).astype(f32)
+
+
 def main():
     x = np.concatenate([np.linspace(-30, 30, 2_000_001), np.linspace(-0.3, 0.3, 600_001)]).astype(f32)
     xd = x.astype(np.float64)
-    for name, fn, ref in (("sigm_f", sigm_f, 1 / (1 + np.exp(-xd))), ("tanh_f", tanh_f, np.tanh(xd))):
+    for name, fn, ref in (("sigm_f", sigm_f, 1 / (1 + np.exp(-xd))), ("tanh_f", tanh_f, np.tanh(xd)),
+                          ("tanh_e", tanh_e, np.tanh(xd))):
         err = max(np.abs(fn(x, s).astype(np.float64) - ref).max() for s in (-1, 1))
         libm = np.abs((1 / (1 + np.exp(-x)) if name == "sigm_f" else np.tanh(x)).astype(np.float64) - ref).max()
         print(f"{name}: max |error| {err:.2e} (numpy float32 libm: {libm:.2e})")

@@ -1,19 +1,20 @@
 #!/bin/bash
-# GPU tests, then an A/B of the bench on the same box: ENV_A vs ENV_B (environment assignments),
-# alternating, each run under its own time limit; then the decoder phase trace of the B setting.
-#   bash tools/gpu_ab.sh "TTS_ALIGN_IN_P4=1" ""
+# Same-box A/B of tools/var/lib_<name>.so variants against the in-tree library on the C2 bench,
+# after the decoder / encoder GPU tests of the in-tree library. Usage: tools/gpu_ab.sh <rounds> <name>...
 set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
-A=$1; B=$2
-timeout -k 10 700 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/t.log 2>&1; rc=$?
-tail -3 gpurun_out/t.log; [ $rc = 0 ] || exit $rc
-for i in 1 2; do
-  for tag in A B; do
-    envs=$([ $tag = A ] && echo "$A" || echo "$B")
-    env $envs timeout -k 10 200 python bench.py --no-cpu-baseline --f32-steps 0 --r1-steps 0 --steps 10 > gpurun_out/ab_${tag}$i.json 2>gpurun_out/ab_${tag}$i.err || exit 1
-    python -c "import json,sys; d=json.load(open('gpurun_out/ab_${tag}$i.json')); print('$tag$i', d['ms_per_step'], d['decoder_step_us'], d['tacotron2_ms'], d['vocoder_ms'], d['roofline']['launches'])"
+export TMPDIR=/tmp
+rounds=$1; shift
+timeout -k 10 400 python3 -u -m pytest -x -q --timeout 150 --timeout-method thread tests/test_gpu_parity.py -m gpu \
+  -k "tacotron2 or decoder or encoder or bilstm or bench_workload or synthesizer" > gpurun_out/ab_tests.log 2>&1 || { tail -30 gpurun_out/ab_tests.log; exit 1; }
+tail -1 gpurun_out/ab_tests.log
+bl() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['ms_per_step'], d['decoder_step_us'], d['tacotron2_ms'], d['vocoder_ms'], d['roofline']['launches'])" $1; }
+for i in $(seq 1 $rounds); do
+  for v in "$@" new; do
+    lib=$PWD/tts_amd/libttship.so; [ $v != new ] && lib=$PWD/tools/var/lib_$v.so
+    TTSHIP_LIB=$lib timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
+    echo "$v run $i: $(bl gpurun_out/ab_$v.json)"
   done
 done
-env $B TTS_PTRACE=gpurun_out/pt.bin timeout -k 10 150 python bench.py --steps 1 --warmup 1 --no-cpu-baseline --f32-steps 0 --r1-steps 0 > /dev/null 2>gpurun_out/pt.err &&
-python tools/ptrace.py gpurun_out/pt.bin
+TTS_PTRACE=gpurun_out/ab_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/ab_pt.err && python3 tools/ptrace.py gpurun_out/ab_pt.bin > gpurun_out/ab_ptrace.txt && head -14 gpurun_out/ab_ptrace.txt

@@ -6,6 +6,7 @@
 //   kernel            per wave                                          expected pipe share
 //   cal_f16_full      N x v_mfma_f32_16x16x32_f16, 4 independent accs   1.0  (one wave per SIMD)
 //   cal_f16_half      N x (MFMA + ~16 cycles of dependent VALU)         ~0.5
+//   cal_f16k16_full   N x v_mfma_f32_16x16x16_f16, 4 independent accs  1.0 (its cycles per MFMA)
 //   cal_f32_full      N x v_mfma_f32_16x16x4_f32, 4 independent accs    1.0
 //
 // Grid: 256 workgroups x 256 threads (4 waves: one per SIMD on every CU). Each kernel writes its
@@ -63,6 +64,22 @@ __global__ __launch_bounds__(256) void cal_f16_half(float* out, float seed) {
   out[blockIdx.x * 256 + threadIdx.x] = c[0] + c[1] + c[2] + c[3] + x;
 }
 
+// the K = 16 f16 MFMA (half the work of the K = 32 form): does it take half the cycles on gfx950?
+typedef _Float16 h4 __attribute__((ext_vector_type(4)));
+__global__ __launch_bounds__(256) void cal_f16k16_full(float* out, float seed) {
+  h4 a, b;
+  for (int i = 0; i < 4; ++i) a[i] = (_Float16)(seed * (threadIdx.x + i)), b[i] = (_Float16)(seed - i);
+  f32x4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
+  for (int i = 0; i < N / 4; ++i) {
+    c0 = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c0, 0, 0, 0);
+    c1 = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c1, 0, 0, 0);
+    c2 = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c2, 0, 0, 0);
+    c3 = __builtin_amdgcn_mfma_f32_16x16x16f16(a, b, c3, 0, 0, 0);
+  }
+  const f32x4 s = c0 + c1 + c2 + c3;
+  out[blockIdx.x * 256 + threadIdx.x] = s[0] + s[1] + s[2] + s[3];
+}
+
 __global__ __launch_bounds__(256) void cal_f32_full(float* out, float seed) {
   const float a = seed * threadIdx.x, b = seed - 1.f;
   f32x4 c0 = {0, 0, 0, 0}, c1 = c0, c2 = c0, c3 = c0;
@@ -89,16 +106,17 @@ int main() {
     double flop_per_mfma;
   } ks[] = {{"cal_f16_full", cal_f16_full, 16.0 * 16 * 32 * 2},
             {"cal_f16_half", cal_f16_half, 16.0 * 16 * 32 * 2},
+            {"cal_f16k16_full", cal_f16k16_full, 16.0 * 16 * 16 * 2},
             {"cal_f32_full", cal_f32_full, 16.0 * 16 * 4 * 2}};
   for (const K& k : ks) {
-    for (int rep = 0; rep < 3; ++rep) {
+    for (int rep = 0; rep < 12; ++rep) {
       HIP_OK(hipEventRecord(e0));
       hipLaunchKernelGGL(k.f, dim3(256), dim3(256), 0, 0, out, 0.001f);
       HIP_OK(hipEventRecord(e1));
       HIP_OK(hipEventSynchronize(e1));
       float ms = 0.f;
       HIP_OK(hipEventElapsedTime(&ms, e0, e1));
-      if (rep == 2)
+      if (rep == 11)
         std::printf("{\"kernel\": \"%s\", \"mfma_per_launch\": %ld, \"flop_per_launch\": %.6e, \"ms\": %.4f, "
                     "\"tflops\": %.1f}\n",
                     k.name, waves * N, waves * N * k.flop_per_mfma, ms, waves * N * k.flop_per_mfma / ms * 1e-9);

@@ -80,6 +80,15 @@ __device__ __forceinline__ float tanh_f(float x) {
   return __builtin_copysignf(ax < 0.25f ? small : big, x);
 }
 
+// tanh for the attention energies: the same form without the small-argument polynomial. Near 0,
+// (1 - e) / (1 + e) loses relative accuracy but not absolute: its error stays below ~1.5e-7 over the
+// whole range (tools/fast_math_err.py), the size that matters in e = v . tanh(..), a sum of 128
+// such terms. Half the instructions of tanh_f on the attention items' VALU-bound energy stage.
+__device__ __forceinline__ float tanh_e(float x) {
+  const float e = __builtin_amdgcn_exp2f(-2.8853900817779268f * __builtin_fabsf(x));  // exp(-2|x|)
+  return __builtin_copysignf((1.f - e) * __builtin_amdgcn_rcpf(1.f + e), x);
+}
+
 // ---------------------------------------------------------------------------------------
 // Generic fp32 MFMA Conv1d (implicit GEMM): out[b][co][q*out_mul+ph] =
 //   epi( sum_{ci,tap} W[co][ci][tap] * in_act(src[b][ci][pad_map(q + tap*dil - pad_left[ph])]) )

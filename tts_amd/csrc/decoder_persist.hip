@@ -305,7 +305,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
   {
     float z[8];
 #pragma unroll
-    for (int i = 0; i < 8; ++i) z[i] = row16_sum(tanh_f(pqa + L[i]) * va);
+    for (int i = 0; i < 8; ++i) z[i] = row16_sum(tanh_e(pqa + L[i]) * va);
     if ((lane & 15) == 0) {
 #pragma unroll
       for (int i = 0; i < 8; ++i) esum[wave * TC + 16 * (i >> 2) + 4 * (lane >> 4) + (i & 3)] = z[i];
