@@ -17,4 +17,4 @@ for i in $(seq 1 $rounds); do
     echo "$v run $i: $(bl gpurun_out/ab_$v.json)"
   done
 done
-TTS_PTRACE=gpurun_out/ab_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/ab_pt.err && python3 tools/ptrace.py gpurun_out/ab_pt.bin > gpurun_out/ab_ptrace.txt && head -14 gpurun_out/ab_ptrace.txt
+TTSHIP_LIB=$PWD/tools/var/lib_trace.so TTS_PTRACE=gpurun_out/ab_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/ab_pt.err && python3 tools/ptrace.py gpurun_out/ab_pt.bin > gpurun_out/ab_ptrace.txt && head -14 gpurun_out/ab_ptrace.txt

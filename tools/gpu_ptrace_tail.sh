@@ -6,7 +6,7 @@ cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 for cfg in "0 100" "1 340"; do
   set -- $cfg
-  TTS_PTRACE=gpurun_out/pt$1.bin TTS_PTRACE_LAUNCH=$1 TTS_PTRACE_T0=$2 timeout -k 10 150 python bench.py --steps 1 --warmup 1 \
+  TTSHIP_LIB=$PWD/tools/var/lib_trace.so TTS_PTRACE=gpurun_out/pt$1.bin TTS_PTRACE_LAUNCH=$1 TTS_PTRACE_T0=$2 timeout -k 10 150 python bench.py --steps 1 --warmup 1 \
     --no-cpu-baseline --f32-steps 0 --r1-steps 0 > /dev/null 2>gpurun_out/pt$1.err || exit 1
   echo "== launch $1 from step $2"; python tools/ptrace.py gpurun_out/pt$1.bin | head -12
 done

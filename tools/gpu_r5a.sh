@@ -25,5 +25,5 @@ for v in old new; do
     --kernel-trace -d gpurun_out/a_pmc_$v -o run --output-format csv -- python3 bench.py $ARGS > gpurun_out/a_pmc_$v.log 2>&1 || exit 1
   echo "PMC $v:"; python3 tools/pmc_kernels.py gpurun_out/a_pmc_$v | grep persist_decoder
 done
-TTS_PTRACE=gpurun_out/a_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/a_pt.err && python3 tools/ptrace.py gpurun_out/a_pt.bin > gpurun_out/a_ptrace.txt; cat gpurun_out/a_ptrace.txt | head -8
+TTSHIP_LIB=$PWD/tools/var/lib_trace.so TTS_PTRACE=gpurun_out/a_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/a_pt.err && python3 tools/ptrace.py gpurun_out/a_pt.bin > gpurun_out/a_ptrace.txt; cat gpurun_out/a_ptrace.txt | head -8
 step cal ./tools/mfma_cal.sh; cat gpurun_out/mfma_cal.txt

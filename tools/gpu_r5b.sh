@@ -20,7 +20,7 @@ for i in 1 2 3; do  # same-box A/B: tools/var/lib_<v>.so (earlier decoders) agai
     echo "$v run $i: $(bl gpurun_out/b_ab_$v.json)"
   done
 done
-TTS_PTRACE=gpurun_out/b_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/b_pt.err && python3 tools/ptrace.py gpurun_out/b_pt.bin > gpurun_out/b_ptrace.txt; head -12 gpurun_out/b_ptrace.txt
+TTSHIP_LIB=$PWD/tools/var/lib_trace.so TTS_PTRACE=gpurun_out/b_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/b_pt.err && python3 tools/ptrace.py gpurun_out/b_pt.bin > gpurun_out/b_ptrace.txt; head -12 gpurun_out/b_ptrace.txt
 rm -rf gpurun_out/b_prof
 step prof timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/b_prof -o run --output-format csv -- python3 bench.py --steps 2 --warmup 1 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > gpurun_out/b_prof.log 2>&1 || exit 1
 step pmc ./tools/pmc_bench.sh || exit 1

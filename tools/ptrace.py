@@ -42,6 +42,18 @@ g14 = [np.median([(a[s][14] - a[s][4]).astype(float) / 100.0 for s in range(7) i
 if g14 is not None:
     print("P4 GEMM waves done (median WG, us after release): %.2f" % g14[0])
 
+if a[:, 15, NATT:].min() > 0:  # item workgroups' P4 entry stamps (15: path taken, 14: first item call)
+    s15 = np.median([np.median((a[s][15][NATT:] - a[s][4][NATT:]).astype(float) / 100.0) for s in range(7)])
+    s14 = np.median([np.median((a[s][14][NATT:] - a[s][4][NATT:]).astype(float) / 100.0) for s in range(7)])
+    print("P4 item workgroups after their own release (median, us): item path %.2f, first item call %.2f" % (s15, s14))
+    if at is not None:
+        own = []
+        for s in range(3):
+            for i in range(256 - NATT):
+                if at[s][i][0] > 0:
+                    own.append((at[s][i][0] - a[s][4][NATT + i]) / 100.0)
+        print("P4 items: loads issued %.2f us after their own release (median)" % np.median(own))
+
 if at is not None:
     # attention items: stamps 0 start (after loads), 1 query summed, 2 location conv, 3 energies,
     # 4 energy reduction, 5 partials published, 6 ticket, 7 combine done (last arriver only)

@@ -1480,6 +1480,8 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   // TTS_PTRACE=<file>: phase timestamps of 8 steps from step TTS_PTRACE_T0 (default 100)
   static DevBuf trace_buf;
   const char* tr = std::getenv("TTS_PTRACE");
+  TTS_CHECK(!tr || persist_trace_built(), "TTS_PTRACE needs a library built with -DTTS_PHASE_TRACE "
+                                          "(tools/build_variants.sh trace -DTTS_PHASE_TRACE; TTSHIP_LIB=tools/var/lib_trace.so)");
   if (tr) {
     trace_buf.ensure((size_t)8 * 24 * 256 * 8);
     HIP_OK(hipMemsetAsync(trace_buf.p, 0, (size_t)8 * 24 * 256 * 8, s));

@@ -186,6 +186,7 @@ struct PArgs {
 bool persist_supported(int device);
 int persist_attn_tc();  // attention positions per work item (sizes the chunk-partial buffers)
 bool persist_defer_ok(int nitems);  // the deferred alignment pass has room for this many items
+bool persist_trace_built();          // phase stamps compiled in (-DTTS_PHASE_TRACE)
 // arm: zero the barrier block first (false: the caller armed it, e.g. in its state fill)
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm = true);
 

@@ -160,9 +160,17 @@ __device__ __forceinline__ float wave64_sum(float v) {
 // (folded in double at load; read from LDS), slid over the alpha window in registers.
 
 // attention item timestamps (P.atrace, optional): [8 steps][256 items][8]
+// The phase / item stamps are compiled in only with -DTTS_PHASE_TRACE (tools/build_variants.sh,
+// TTS_PTRACE=<file> with TTSHIP_LIB pointing at that build): in the default build their conditions
+// and pointers held ~10 SGPRs across the step loop, in a kernel whose SGPRs already spill to VGPR
+// lanes, and every phase start paid the lane reads and writes
+#ifdef TTS_PHASE_TRACE
 #define ATRACE(k)                                                                             \
   if (P.atrace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                         \
   P.atrace[(((long)(t - P.trace_t0) * PW + b * P.nchmax + ch) * 8) + (k)] = __builtin_amdgcn_s_memrealtime()
+#else
+#define ATRACE(k)
+#endif
 
 // Location features of item (b, ch) for this step, computed one phase early (P1, from the alpha /
 // alpha_cum the previous step's combine wrote): L[i] = location term + processed input at position
@@ -926,9 +934,13 @@ constexpr size_t P_LDS = P_LDS_APRE + P_LDS_WC + P_LDS_SCRATCH + P_LDS_EKEEP;
 
 // phase timestamps of every workgroup for 8 steps (P.trace, optional): [step][16][256]
 // (0-9 phase boundaries, 10-15 points inside P5)
+#ifdef TTS_PHASE_TRACE
 #define PTRACE(k)                                                                              \
   if (P.trace && threadIdx.x == 0 && (unsigned)(t - P.trace_t0) < 8u)                          \
   P.trace[((long)(t - P.trace_t0) * 16 + (k)) * PW + blockIdx.x] = __builtin_amdgcn_s_memrealtime()
+#else
+#define PTRACE(k)
+#endif
 
 template <int MT, int VAR>
 __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
@@ -1441,8 +1453,10 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       // (no co-issue with the attention's VALU work on the other wave), so under the item they
       // only lengthen the attention chain; after it they overlap the other items' tails.
       if (g >= IW0) {  // items, then the decoder_rnn h_att part (attention_rnn's waits for P6)
+        PTRACE(15);
         const int nitems = D.B * P.nchmax;
         for (int it = g - IW0, k = 0; it < nitems; it += PW - IW0, ++k) {
+          if (k == 0) PTRACE(14);
           float* ek = nullptr;
           if (DEFER && P.defer_align) {
             ek = ekeep0 + k * (PTC + 1);
@@ -1648,6 +1662,11 @@ bool persist_supported(int device) {
 }
 
 int persist_attn_tc() { return PTC; }
+#ifdef TTS_PHASE_TRACE
+bool persist_trace_built() { return true; }
+#else
+bool persist_trace_built() { return false; }
+#endif
 bool persist_defer_ok(int nitems) { return nitems <= (PW - IW0) * PDEF_MAXIT; }
 
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
