@@ -122,7 +122,12 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         if (i >= T.L) i = 2 * (T.L - 1) - i;
         i = i < 0 ? 0 : (i >= T.L ? T.L - 1 : i);
       }
-      const int c0 = min(32 * ch + 8 * min(sg[j], 3), C - 8);
+      // the channel octet passes through an opaque copy: otherwise the compiler hoists c0 * Ls of
+      // every chunk out of the tile loop, and at C = 192 (168 VGPRs for 12 waves) spills them; each
+      // scratch reload then came with a vmcnt(0) that drained the weight ring's prefetches
+      int g8 = min(sg[j], 3);
+      asm volatile("" : "+v"(g8));
+      const int c0 = min(32 * ch + 8 * g8, C - 8);
       const int vo = (c0 * a.Ls + i) * 4;  // per-lane offset; the 8 channel rows are SGPR offsets
 #pragma unroll
       for (int c = 0; c < 8; ++c)
