@@ -38,6 +38,16 @@
 
 namespace {
 constexpr int PW = 256, PT = 512, NWV = 8;
+// the step's grid barriers: gsync.h's flag barrier (one store per arrival, workgroup 0 releases);
+// -DTTS_BAR_COUNTERS builds the counter form for A/B
+#ifdef TTS_BAR_COUNTERS
+#define BAR_ARRIVE gsync_arrive
+#define BAR_WAIT gsync_wait
+#else
+static_assert(PW <= 256, "gflag barrier: one flag word per workgroup, 256 at most");
+#define BAR_ARRIVE gflag_arrive
+#define BAR_WAIT gflag_wait
+#endif
 constexpr int DEC_NC = 20;   // 160 k-chunks / 8 waves
 constexpr int ATTP_NC = 8;   // 4 tiles x 16 chunks / 8 waves
 constexpr int PJ_NC = 6;     // 48 / 8
@@ -1192,7 +1202,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
     }
     PTRACE(1);
-    gsync_arrive(P.bar, gen);
+    BAR_ARRIVE(P.bar, gen);
     // P3 operands that are already final: its epilogue's gate addends (written by P5 of the
     // previous step), c_att, the query-projection weights
     float ga[NCK][4], ca[NCK], wq[4];
@@ -1228,7 +1238,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
       for (int i = 0; i < ATTP_NC; ++i) wa[i] = src[(long)i * 64];
     }
-    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    if (!BAR_WAIT(P.bar, gen, &sflag)) return;
     PTRACE(2);
     tid = opaque_v(tid0);
     lane = opaque_v(lane0);
@@ -1410,8 +1420,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       write_frames(t - 1, NATT, PW - NATT);
     }
     PTRACE(3);
-    gsync_arrive(P.bar, gen);
-    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    BAR_ARRIVE(P.bar, gen);
+    if (!BAR_WAIT(P.bar, gen, &sflag)) return;
     if constexpr (GRAVES) {
       // ======== P3g: N_a hidden = relu(W1 h_att + b1), 16 units per workgroup IW0 .. IW0+63 ========
       tid = opaque_v(tid0);
@@ -1440,8 +1450,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           lds_barrier();
         }
       }
-      gsync_arrive(P.bar, gen);
-      if (!gsync_wait(P.bar, gen, &sflag)) return;
+      BAR_ARRIVE(P.bar, gen);
+      if (!BAR_WAIT(P.bar, gen, &sflag)) return;
     }
     PTRACE(4);
     // ======== P4: attention || the h_att parts of decoder_rnn and attention_rnn ========
@@ -1481,12 +1491,12 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
     }
     PTRACE(5);
-    gsync_arrive(P.bar, gen);
+    BAR_ARRIVE(P.bar, gen);
     // P5 epilogue operand (own tile's c_dec), fetched during the barrier
     float cd[NCK];
 #pragma unroll
     for (int c = 0; c < NCK; ++c) cd[c] = P.cdec[(long)min(c * CB + (tid >> 2), Bp - 1) * 1024 + g * 4 + (tid & 3)];
-    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    if (!BAR_WAIT(P.bar, gen, &sflag)) return;
     PTRACE(6);
     // ======== P5: ctx parts, then the decoder_rnn cell (tile g) and the next step's
     //            attention_rnn ctx/h part (tile g, + biases) ========
@@ -1534,7 +1544,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       for (int mt = 0; mt < MT; ++mt) accd[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
     PTRACE(7);
-    gsync_arrive(P.bar, gen);
+    BAR_ARRIVE(P.bar, gen);
     // projection weights for P6 (half pj & 1 of job tile pj >> 1, 6 k-chunks per wave)
     f32x4 wp[X3P ? 1 : PJ_NC];
     h8 wpx[X3P ? PJ_NC : 1][2];  // split-f16: the whole K for 16 rows, k-steps 6 wave .. + 5
@@ -1551,7 +1561,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         for (int i = 0; i < PJ_NC; ++i) wp[i] = src[(long)i * 64];
       }
     }
-    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    if (!BAR_WAIT(P.bar, gen, &sflag)) return;
     PTRACE(8);
     // ======== P6: projection halves (workgroups PJ_WG0 ..) || attention_rnn h_att part (items) ========
     tid = opaque_v(tid0);
@@ -1648,8 +1658,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
       }
     }
     PTRACE(9);
-    gsync_arrive(P.bar, gen);
-    if (!gsync_wait(P.bar, gen, &sflag)) return;
+    BAR_ARRIVE(P.bar, gen);
+    if (!BAR_WAIT(P.bar, gen, &sflag)) return;
   }
 }
 
