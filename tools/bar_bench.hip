@@ -36,6 +36,100 @@ __device__ __forceinline__ bool poll_flags(const unsigned* flags, unsigned gen) 
   }
 }
 
+// ring polling: 4 loads in flight, issued SL x 64 clocks apart, the oldest checked as the next is issued
+__device__ __forceinline__ bool flags_ok(f32x4 v, unsigned gen) {
+  bool ok = true;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ok = ok && __float_as_uint(v[j]) >= gen;
+  return __all(ok);
+}
+template <int SL>
+__device__ __forceinline__ bool poll_flags_ring(const unsigned* flags, unsigned gen) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const float* f = reinterpret_cast<const float*>(flags);
+  const int off = (int)threadIdx.x * 16;
+  f32x4 a = ldc4(f, off);
+  if (SL) __builtin_amdgcn_s_sleep(SL);
+  f32x4 b = ldc4(f, off);
+  if (SL) __builtin_amdgcn_s_sleep(SL);
+  f32x4 c = ldc4(f, off);
+  if (SL) __builtin_amdgcn_s_sleep(SL);
+  while (true) {
+    f32x4 d = ldc4(f, off);
+    if (flags_ok(a, gen)) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    a = ldc4(f, off);
+    if (flags_ok(b, gen)) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    b = ldc4(f, off);
+    if (flags_ok(c, gen)) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    c = ldc4(f, off);
+    if (flags_ok(d, gen)) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) return false;
+  }
+}
+template <int SL>
+__device__ __forceinline__ bool go_ring(const unsigned* go, unsigned gen) {
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  auto ld = [&]() { return __hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT); };
+  unsigned a = ld();
+  if (SL) __builtin_amdgcn_s_sleep(SL);
+  unsigned b = ld();
+  if (SL) __builtin_amdgcn_s_sleep(SL);
+  unsigned c = ld();
+  if (SL) __builtin_amdgcn_s_sleep(SL);
+  while (true) {
+    unsigned d = ld();
+    if (a >= gen) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    a = ld();
+    if (b >= gen) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    b = ld();
+    if (c >= gen) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    c = ld();
+    if (d >= gen) return true;
+    if (SL) __builtin_amdgcn_s_sleep(SL);
+    if (__builtin_amdgcn_s_memrealtime() - t0 > 20000000ull) return false;
+  }
+}
+
+template <int SL>
+__global__ __launch_bounds__(512) void ring_kernel(unsigned* bar, unsigned* flags, float* data, int iters, int hand,
+                                                   float* out) {
+  __shared__ int flag;
+  unsigned gen = 0;
+  f32x4 acc = {0, 0, 0, 0};
+  for (int i = 0; i < iters; ++i) {
+    if (hand && threadIdx.x < 64) stc4(data, (blockIdx.x * 64 + threadIdx.x) * 16, acc + (float)i);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    ++gen;
+    if (threadIdx.x == 0) stci(reinterpret_cast<int*>(flags) + blockIdx.x, (int)gen);
+    if (blockIdx.x == 0) {
+      if (threadIdx.x < 64) {
+        const bool good = poll_flags_ring<SL>(flags, gen);
+        if (good && threadIdx.x < 8) stci(reinterpret_cast<int*>(bar) + 32 + 64 * threadIdx.x, (int)gen);
+        if (threadIdx.x == 0) {
+          flag = good;
+          if (!good) atomicOr(&g_err, 1u);
+        }
+      }
+    } else if (threadIdx.x == 0) {
+      const bool good = go_ring<SL>(bar + 32 + 64 * (blockIdx.x % 8), gen);
+      flag = good;
+      if (!good) atomicOr(&g_err, 1u);
+    }
+    lds_barrier();
+    if (!flag) return;
+    if (hand && threadIdx.x < 64) acc += ldc4(data, (((blockIdx.x * 37 + i + 1) & 255) * 64 + threadIdx.x) * 16);
+  }
+  if (threadIdx.x < 64) out[blockIdx.x * 64 + threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3];
+}
+
 __global__ __launch_bounds__(512) void bar_kernel(unsigned* bar, unsigned* flags, float* data, int iters, int mode,
                                                   float* out, int ncp) {
   __shared__ int flag;
@@ -134,5 +228,30 @@ int main(int argc, char** argv) {
                 names[mode & 7], mode >> 3, ncp, best * 1000.f / iters, err | berr);
     if (err | berr) return 1;
   }
+  const void* rk[] = {(const void*)ring_kernel<0>, (const void*)ring_kernel<1>, (const void*)ring_kernel<2>,
+                      (const void*)ring_kernel<4>};
+  const int sls[] = {0, 1, 2, 4};
+  for (int hand = 0; hand < 2; ++hand)
+    for (int k = 0; k < 4; ++k) {
+      float best = 1e30f;
+      for (int rep = 0; rep < 5; ++rep) {
+        HIP_OK(hipMemset(bar, 0, 64 * 64 * 4));
+        HIP_OK(hipMemset(flags, 0, 256 * 4));
+        int it = iters, hd = hand;
+        void* args[] = {&bar, &flags, &data, &it, &hd, &out};
+        HIP_OK(hipEventRecord(e0));
+        HIP_OK(hipLaunchKernel(rk[k], dim3(256), dim3(512), args, 0, 0));
+        HIP_OK(hipEventRecord(e1));
+        HIP_OK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+      }
+      unsigned err = 0;
+      HIP_OK(hipMemcpyFromSymbol(&err, HIP_SYMBOL(g_err), 4));
+      std::printf("{\"form\": \"flags, wg0 ring-polls + 8 go copies, ring polls\", \"sleep\": %d, \"handoff\": %d, "
+                  "\"us_per_barrier\": %.3f, \"err\": %u}\n", sls[k], hand, best * 1000.f / iters, err);
+      if (err) return 1;
+    }
   return 0;
 }

@@ -136,7 +136,7 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
   constexpr int NW = LSTM_NW;
   constexpr int NKC = H / 16, KPW = NKC / NW;  // k-chunks, per wave
   constexpr int G = NDIR * 4 * H, O = NDIR * H;
-  static_assert(NKC % NW == 0 && KPW % 2 == 0 && NT % 8 == 0, "LSTM geometry");
+  static_assert(NKC % NW == 0 && KPW % 2 == 0 && NT % 8 == 0 && NT <= 256, "LSTM geometry (gflag groups of <= 256)");
   __shared__ float part[NW * Bp * LRS];
   __shared__ int sflag;
   const int RG = gridDim.x / (NDIR * NT);      // row groups (the launcher sizes the grid)
@@ -245,10 +245,18 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
     }
     if (step + 1 < T_max) {  // directions and row groups are independent: one barrier each
       unsigned* db = bar + dom * BAR_WORDS;
+#ifdef TTS_BAR_COUNTERS
       gsync_arrive(db, gen, NT);
+#else
+      gflag_arrive(db, gen, tl);  // the recurrence's NT workgroups, released by its tile 0
+#endif
 #pragma unroll
       for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(step + 1) * G + q * 4];
+#ifdef TTS_BAR_COUNTERS
       if (!gsync_wait(db, gen, &sflag)) return;
+#else
+      if (!gflag_wait(db, gen, &sflag, NT, tl)) return;
+#endif
     }
   }
 }
@@ -450,9 +458,9 @@ __global__ __launch_bounds__(64 * GP_NW) void ge2e_pipe_kernel(GePipeArgs a) {
       }
     }
     if (s + 1 < S) {
-      gsync_arrive(a.bar, gen);
+      gflag_arrive(a.bar, gen);
       if (l == 0) load_gin(t + 1);
-      if (!gsync_wait(a.bar, gen, &sflag)) return;
+      if (!gflag_wait(a.bar, gen, &sflag)) return;
     }
   }
 }

@@ -1,4 +1,4 @@
-// Agent-coherent access helpers and the hierarchical grid barrier shared by the persistent kernels
+// Agent-coherent access helpers and the grid barriers (counter and flag forms) shared by the persistent kernels
 // (decoder_persist.hip, the BiLSTM in encoder.hip).
 //
 // Memory model: cross-workgroup data is written with agent-scope relaxed atomic stores (sc1:
@@ -178,18 +178,23 @@ __device__ __forceinline__ void gsync_arrive(unsigned* bar, unsigned& gen, unsig
 // The memory-model argument is gsync's: the stores before the arrival are drained sc1 stores.
 constexpr int BAR_FLAGS = 512;  // words 512 .. 767 of the barrier block
 constexpr int BAR_NGO = 8;
-__device__ __forceinline__ void gflag_arrive(unsigned* bar, unsigned& gen) {
+// A barrier over a group of n workgroups (default the grid): idx = the workgroup's index in the
+// group (default blockIdx.x), n <= 256; the group's index-0 workgroup releases it.
+__device__ __forceinline__ void gflag_arrive(unsigned* bar, unsigned& gen, int idx = -1) {
   asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   __syncthreads();
   ++gen;
-  if (threadIdx.x == 0) __hip_atomic_store(bar + BAR_FLAGS + blockIdx.x, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (idx < 0) idx = (int)blockIdx.x;
+  if (threadIdx.x == 0) __hip_atomic_store(bar + BAR_FLAGS + idx, gen, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
-__device__ __forceinline__ bool gflag_wait(unsigned* bar, unsigned gen, int* flag) {
+__device__ __forceinline__ bool gflag_wait(unsigned* bar, unsigned gen, int* flag, int n = 0, int idx = -1) {
   const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
-  if (blockIdx.x == 0) {
+  if (idx < 0) idx = (int)blockIdx.x;
+  if (n <= 0) n = (int)gridDim.x;
+  if (idx == 0) {
     if (threadIdx.x < 64) {
       const unsigned long long tmo = bar[BAR_TMO];
-      const int n = (int)gridDim.x, w0 = 4 * (int)threadIdx.x;
+      const int w0 = 4 * (int)threadIdx.x;
       bool good = true;
       while (true) {
         const f32x4 v = ldc4(reinterpret_cast<const float*>(bar + BAR_FLAGS), w0 * 4);
@@ -211,7 +216,7 @@ __device__ __forceinline__ bool gflag_wait(unsigned* bar, unsigned gen, int* fla
     }
   } else if (threadIdx.x == 0) {
     const unsigned long long tmo = bar[BAR_TMO];
-    const unsigned* go = bar + 32 + 64 * (blockIdx.x % BAR_NGO);
+    const unsigned* go = bar + 32 + 64 * (idx % BAR_NGO);
     int good = 1;
     while (__hip_atomic_load(go, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) < gen) {
       if (__builtin_amdgcn_s_memrealtime() - t0 > tmo) {
