@@ -11,7 +11,8 @@
 //   staging   32 input channels x (TQ + 2d) positions of lrelu(x), reflect-padded per utterance,
 //             split into hi / lo f16 and stored position-major ([pos][32 hi | 32 lo | 16 pad]):
 //             one lane's B operand (8 consecutive channels of one position) is one ds_read_b128,
-//             and the 160-byte row stride keeps those reads bank-conflict free for any tap offset.
+//             and the 160-byte row stride keeps those reads bank-conflict free for any tap offset
+//             (16-byte chunks swizzled per row for the stores, split16.h lds_rsw).
 //             The centre positions' raw x (shortcut input) go split into HX. Two LDS buffers and
 //             two register sets: chunk c+2's global loads are in flight during chunk c's MFMAs.
 //   phase 1   h = Wd . X over K = 3 taps x C channels (3 MFMAs per product), weights (A operand,
@@ -68,6 +69,11 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   const int wm = wave / WN, wn = wave % WN;
   const int nb = wn * 16 * NI + (lane & 15);  // this lane's position (B column) for ni = 0
   const int kg = 8 * (lane >> 4);             // this lane's k offset inside a k-step
+  // swizzled (split16.h lds_rsw) k offsets of this lane's rows: HX rows nb + 16 i, X rows
+  // nb + 16 i + kq d (tap kq)
+  const int lsw = lds_rsw(lane & 15);
+  const int kgsw = kg ^ lsw;
+  const int kgx[3] = {kgsw, kg ^ lds_rsw((lane & 15) + d), kg ^ lds_rsw((lane & 15) + 2 * d)};
   const int mt0 = wm * MI;
   bool bad = false;   // staged inputs: ordered compare (catches NaN)
   float vmax = 0.f;   // h values: running max of |h| (split16.h absmax4)
@@ -152,13 +158,15 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         for (int c = 0; c < 8; ++c) lv[c] = lrelu_x3(v[c]);
         h8 hi, lo;
         split8(lv, hi, lo);
-        *reinterpret_cast<h8*>(X + row * XR + 8 * g) = hi;
-        *reinterpret_cast<h8*>(X + row * XR + 32 + 8 * g) = lo;
+        const int sx = (8 * g) ^ lds_rsw(row);
+        *reinterpret_cast<h8*>(X + row * XR + sx) = hi;
+        *reinterpret_cast<h8*>(X + row * XR + 32 + sx) = lo;
         const int p = row - d;
         if (real && p >= 0 && p < TQ) {  // raw x of the centre positions: the shortcut's operand
           split8(v, hi, lo);
-          *reinterpret_cast<h8*>(HX + p * HR + C + 32 * ch + 8 * g) = hi;
-          *reinterpret_cast<h8*>(HX + p * HR + 3 * C + 32 * ch + 8 * g) = lo;
+          const int hx = C + 32 * ch + ((8 * g) ^ lds_rsw(p));
+          *reinterpret_cast<h8*>(HX + p * HR + hx) = hi;
+          *reinterpret_cast<h8*>(HX + p * HR + 2 * C + hx) = lo;
         }
       }
     }
@@ -240,7 +248,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         h8 bh[NI], bl[NI];
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          const _Float16* p = X + (nb + ni * 16 + kq * d) * XR + kg;
+          const _Float16* p = X + (nb + ni * 16 + kq * d) * XR + kgx[kq];
           bh[ni] = *reinterpret_cast<const h8*>(p);
           bl[ni] = *reinterpret_cast<const h8*>(p + 32);
         }
@@ -261,7 +269,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     // lrelu(h + b_d), split, into HX[pos][0:C) (hi) and HX[pos][2C:3C) (lo)
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi) {
-      const int co = (mt0 + mi) * 16 + 4 * (lane >> 4);
+      const int co = ((mt0 + mi) * 16 + 4 * (lane >> 4)) ^ lsw;
       const f32x4 bd{bdv[mi][0], bdv[mi][1], bdv[mi][2], bdv[mi][3]};
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) {
@@ -291,7 +299,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         h8 bh[NI], bl[NI];
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          const _Float16* p = HX + (nb + ni * 16) * HR + kc * 32 + kg;
+          const _Float16* p = HX + (nb + ni * 16) * HR + kc * 32 + kgsw;
           bh[ni] = *reinterpret_cast<const h8*>(p);
           bl[ni] = *reinterpret_cast<const h8*>(p + 2 * C);
         }

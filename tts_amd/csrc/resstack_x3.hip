@@ -7,7 +7,8 @@
 // Block 3 (dilation 27: a 27-position halo per side would cost more recompute than its traffic)
 // stays on resblock_x3_kernel.
 //
-// LDS rows (position-major, row r <-> position q0 - OFF + r, ROWS = TQ + 2 OFF):
+// LDS rows (position-major, row r <-> position q0 - OFF + r, ROWS = TQ + 2 OFF; 16-byte chunks
+// swizzled per row, split16.h lds_rsw):
 //   XL  lrelu(x_k) split: [C hi | C lo | 16 pad] -- the phase-1 operand (3 taps read each row)
 //   HX  [lrelu(h) hi | x_k hi | lrelu(h) lo | x_k lo | 16 pad] -- the phase-2 operand, as resblock_x3
 // Per block: phase 1 h = Wd . XL over 3 taps (rows reflected at the utterance ends), epilogue
@@ -101,6 +102,9 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
   const int wm = wave / WN, wn = wave % WN;
   const int kg = 8 * (lane >> 4);
   const int co = wm * 16 + 4 * (lane >> 4);  // first of this lane's 4 output channels
+  // rows nt * 16 + (lane & 15) (epilogues, phase 2): the swizzled channel / k offsets
+  const int lsw = lds_rsw(lane & 15);
+  const int cosw = co ^ lsw, kgsw = kg ^ lsw;
   bool bad = false;   // staged inputs: ordered compare (catches NaN)
   float vmax = 0.f;   // produced values: running max of |v| (split16.h absmax4)
   int t = blockIdx.x;
@@ -219,11 +223,12 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
       bad |= !(mx < F16_RANGE);
       h8 hi, lo;
       split8(lv, hi, lo);
-      _Float16* xl = XL + srow[j] * XLR + 8 * sg[j];
+      const int sx = (8 * sg[j]) ^ lds_rsw(srow[j]);
+      _Float16* xl = XL + srow[j] * XLR + sx;
       *reinterpret_cast<h8*>(xl) = hi;
       *reinterpret_cast<h8*>(xl + C) = lo;
       split8(v, hi, lo);
-      _Float16* hx = HX + srow[j] * HR + C + 8 * sg[j];
+      _Float16* hx = HX + srow[j] * HR + C + sx;
       *reinterpret_cast<h8*>(hx) = hi;
       *reinterpret_cast<h8*>(hx + 2 * C) = lo;
     }
@@ -314,13 +319,14 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
         const int p = P0 + r;
         const bool in = p >= 0 && p < T.L;
         const f32x2_ x2{in ? v[ph] : 0.f, in ? v[2 + ph] : 0.f};
+        const int cs = co0 ^ lds_rsw(r);
         h2_ hi, lo;
         split2(x2, hi, lo);
-        *reinterpret_cast<h2_*>(HX + r * HR + C + co0) = hi;
-        *reinterpret_cast<h2_*>(HX + r * HR + 3 * C + co0) = lo;
+        *reinterpret_cast<h2_*>(HX + r * HR + C + cs) = hi;
+        *reinterpret_cast<h2_*>(HX + r * HR + 3 * C + cs) = lo;
         split2(f32x2_{lrelu_s(x2[0]), lrelu_s(x2[1])}, hi, lo);
-        *reinterpret_cast<h2_*>(XL + r * XLR + co0) = hi;
-        *reinterpret_cast<h2_*>(XL + r * XLR + C + co0) = lo;
+        *reinterpret_cast<h2_*>(XL + r * XLR + cs) = hi;
+        *reinterpret_cast<h2_*>(XL + r * XLR + C + cs) = lo;
       }
     }
     lds_barrier();
@@ -390,7 +396,7 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
           for (int ni = 0; ni < NI; ++ni) {
             // unconditional: an inactive slot reads a clamped row and its result is dropped;
             // C = 48's chunk-1 channels >= 48 read finite neighbours that meet zero weights
-            const _Float16* p = XL + trow[ni][kq] * XLR + 32 * ch + kg;
+            const _Float16* p = XL + trow[ni][kq] * XLR + 32 * ch + (kg ^ lds_rsw(trow[ni][kq]));
             bh[ni] = RS_LD(p);
             bl[ni] = RS_LD(p + C);
           }
@@ -415,8 +421,8 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
           vmax = absmax4(vmax, v);
           h4 hi, lo;
           split4(v, hi, lo);
-          *reinterpret_cast<h4*>(HX + r * HR + co) = hi;
-          *reinterpret_cast<h4*>(HX + r * HR + 2 * C + co) = lo;
+          *reinterpret_cast<h4*>(HX + r * HR + cosw) = hi;
+          *reinterpret_cast<h4*>(HX + r * HR + 2 * C + cosw) = lo;
           am[ni] = ac[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
         }
       }
@@ -431,7 +437,7 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
           {
-            const _Float16* p = HX + (min(nt[ni], ROWS / 16 - 1) * 16 + (lane & 15)) * HR + kc * 32 + kg;
+            const _Float16* p = HX + (min(nt[ni], ROWS / 16 - 1) * 16 + (lane & 15)) * HR + kc * 32 + kgsw;
             bh[ni] = RS_LD(p);
             bl[ni] = RS_LD(p + 2 * C);
           }
@@ -462,10 +468,10 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
           h4 xh, xlo, lh, llo;
           split4(v, xh, xlo);
           split4(lrelu4(v), lh, llo);
-          *reinterpret_cast<h4*>(XL + r * XLR + co) = lh;
-          *reinterpret_cast<h4*>(XL + r * XLR + C + co) = llo;
-          *reinterpret_cast<h4*>(HX + r * HR + C + co) = xh;
-          *reinterpret_cast<h4*>(HX + r * HR + 3 * C + co) = xlo;
+          *reinterpret_cast<h4*>(XL + r * XLR + cosw) = lh;
+          *reinterpret_cast<h4*>(XL + r * XLR + C + cosw) = llo;
+          *reinterpret_cast<h4*>(HX + r * HR + C + cosw) = xh;
+          *reinterpret_cast<h4*>(HX + r * HR + 3 * C + cosw) = xlo;
         }
         lds_barrier();
         RS_STAMP(4 * bi + 4);

@@ -153,4 +153,18 @@ __device__ __forceinline__ float absmax4(float mx, const f32x4& v) {
   return fmaxf(fmaxf(mx, fmaxf(__builtin_fabsf(v[0]), __builtin_fabsf(v[1]))),
                fmaxf(__builtin_fabsf(v[2]), __builtin_fabsf(v[3])));
 }
+// LDS row swizzle of the position-major split-f16 tiles (resblock_x3 / resstack_x3): the 16-byte
+// chunks of row r swap pairwise when bit 2 of r is set (an XOR of this value on the half offset
+// within the row). Row strides there are 8 mod 16 dwords, which keeps the B-operand ds_read_b128 of
+// 16 consecutive rows conflict-free with or without it; the swizzle takes the epilogues' 8-byte
+// stores of 16 consecutive rows (banks mod 32) from 4-way to 2-way and the staging's 16-byte stores
+// of 8 consecutive rows from 2-way to conflict-free. Every access of a tile's halves goes through
+// it; offsets that are multiples of 16 halves (C, 2C, 32 ch) commute with the XOR.
+__device__ __forceinline__ int lds_rsw(int r) {
+#ifdef TTS_NO_LDS_SWZ  // A/B builds: the unswizzled layout
+  return 0 * r;
+#else
+  return ((r >> 2) & 1) << 3;
+#endif
+}
 #endif
