@@ -228,6 +228,41 @@ int main(int argc, char** argv) {
                 names[mode & 7], mode >> 3, ncp, best * 1000.f / iters, err | berr);
     if (err | berr) return 1;
   }
+  // placement: the flag barrier (mode 6, 8 go copies) on barrier blocks at different offsets of one
+  // 64 MiB allocation (8 KiB steps, then 2 MiB steps): does the block's physical place matter?
+  {
+    unsigned* big;
+    HIP_OK(hipMalloc(&big, 64u << 20));
+    auto run_at = [&](size_t off_bytes, int hand) {
+      unsigned* b = big + off_bytes / 4;
+      unsigned* fl = b + 16 * 64;  // flags after the 64 go-copy lines (words 0 .. 1023)
+      float best = 1e30f;
+      for (int rep = 0; rep < 3; ++rep) {
+        HIP_OK(hipMemset(b, 0, 64 * 64 * 4 + 1024));
+        const unsigned tmo = 20000000u;
+        for (int k = 0; k < 8; ++k) HIP_OK(hipMemcpy(b + 64 * k + BAR_TMO, &tmo, 4, hipMemcpyHostToDevice));
+        int it = iters / 2, md = 6 + 8 * hand, nc = 8;
+        HIP_OK(hipEventRecord(e0));
+        hipLaunchKernelGGL(bar_kernel, dim3(256), dim3(512), 0, 0, b, fl, data, it, md, out, nc);
+        HIP_OK(hipEventRecord(e1));
+        HIP_OK(hipEventSynchronize(e1));
+        float ms = 0.f;
+        HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+        best = ms < best ? ms : best;
+      }
+      return best * 1000.f / (iters / 2);
+    };
+    for (int hand = 0; hand < 2; ++hand) {
+      std::printf("{\"placement\": \"8KiB steps\", \"handoff\": %d, \"us\": [", hand);
+      for (int k = 0; k < 16; ++k) std::printf("%s%.3f", k ? ", " : "", run_at((size_t)k * 4096 * 2, hand));
+      std::printf("]}\n{\"placement\": \"2MiB steps\", \"handoff\": %d, \"us\": [", hand);
+      for (int k = 0; k < 16; ++k) std::printf("%s%.3f", k ? ", " : "", run_at((size_t)k * (2u << 20) + 8192 * 17, hand));
+      std::printf("]}\n");
+    }
+    unsigned err = 0;
+    HIP_OK(hipMemcpyFromSymbol(&err, HIP_SYMBOL(g_err), 4));
+    if (err) return 1;
+  }
   const void* rk[] = {(const void*)ring_kernel<0>, (const void*)ring_kernel<1>, (const void*)ring_kernel<2>,
                       (const void*)ring_kernel<4>};
   const int sls[] = {0, 1, 2, 4};

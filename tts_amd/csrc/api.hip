@@ -331,6 +331,7 @@ struct TacoModel {
 // persistent-decoder barrier errors (one per launch), the decoder results (done, steps, status per
 // decode row), the range flag, the launches' end steps
 constexpr int PMAX_LAUNCH = 4;  // persistent decoder launches per decode (MT = 4, 3, 2, 1)
+constexpr int PBAR_CAND = 16;   // candidate barrier blocks timed for them
 constexpr int ENC_NDOM_MAX = 4;  // BiLSTM recurrences (barrier blocks) per launch
 constexpr int TS_ENC = 16, TS_DEC = TS_ENC + ENC_NDOM_MAX, TS_RES = TS_DEC + PMAX_LAUNCH, TS_FLAG = TS_RES + 3 * BMAX,
               TS_END = TS_FLAG + 1, TS_N = TS_END + PMAX_LAUNCH;
@@ -347,6 +348,10 @@ struct TacoWS {
   DevBuf ids, post, map;       // rows in decode order (longest first); map = [perm | inverse]
   DevBuf stat;                 // status words for the host, laid out as tts_ctx::pinned (TS_*)
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
+  // the decoder launches' barrier blocks: PBAR_CAND candidates in pbar, the PMAX_LAUNCH fastest
+  // picked once per allocation (pick_barrier_blocks)
+  int pslot[PMAX_LAUNCH] = {0, 1, 2, 3};
+  const void* pslot_base = nullptr;
   DevBuf anorm;                // persistent decoder: per-utterance attention normaliser (deferred alignment)
   DevBuf spk, spkid, spkb;     // speaker vectors (decode order), per-row biases [Bp][NSPK]
   DevBuf win_idx, fwd_u, apf;  // windowing argmax, transition probability, forward chunk sums
@@ -896,7 +901,11 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<int>(W.map, 2 * BMAX, g);
   grow<int>(W.stat, 256, g);
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
-  grow<unsigned>(W.pbar, PMAX_LAUNCH * BAR_WORDS, g);  // one barrier block per persistent launch (MT = 4 .. 1)
+  grow<unsigned>(W.pbar, PBAR_CAND * BAR_WORDS, g);  // candidate barrier blocks, one picked per launch (MT = 4 .. 1)
+  if (W.pslot_base != W.pbar.p && persist_supported(c->device)) {
+    pick_barrier_blocks(reinterpret_cast<unsigned*>(W.pbar.p), PBAR_CAND, PMAX_LAUNCH, W.pslot, c->s);
+    W.pslot_base = W.pbar.p;
+  }
   grow<float>(W.anorm, (size_t)2 * BMAX, g);
   grow<float>(W.spk, (size_t)64 * 1024, g);
   grow<int>(W.win_idx, 64, g);
@@ -1280,13 +1289,16 @@ __global__ void taco_mlens_kernel(const int* ctl, int B, int r, int* mlens) {
 }
 
 // gather every status word the host checks after a Tacotron2 call into one block (TS_* layout)
-__global__ void taco_status_kernel(const unsigned* enc_bar, int nenc, const unsigned* dec_bar, int ndec, const int* ctl,
-                                   const unsigned* flag, int* st) {
+struct DecSlots {
+  int v[PMAX_LAUNCH];
+};
+__global__ void taco_status_kernel(const unsigned* enc_bar, int nenc, const unsigned* dec_bar, DecSlots dslot, int ndec,
+                                   const int* ctl, const unsigned* flag, int* st) {
   const int i = threadIdx.x;
   if (i < 3 * BMAX) st[TS_RES + i] = ctl[4 + i];
   if (i < ENC_NDOM_MAX) st[TS_ENC + i] = enc_bar && i < nenc ? (int)enc_bar[i * BAR_WORDS + 16] : 0;
   if (i < PMAX_LAUNCH) {
-    st[TS_DEC + i] = dec_bar && i < ndec ? (int)dec_bar[i * BAR_WORDS + 16] : 0;
+    st[TS_DEC + i] = dec_bar && i < ndec ? (int)dec_bar[dslot.v[i] * BAR_WORDS + 16] : 0;
   }
   if (i == 0) st[TS_FLAG] = flag ? (int)*flag : 0;
 }
@@ -1497,15 +1509,19 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   }();
   unsigned long long* const trace_p = a.trace;
   unsigned long long* const atrace_p = a.atrace;
+  static const bool xdiag = std::getenv("TTS_DIAG_XCC") != nullptr;
+  static DevBuf xdiag_buf;
+  if (xdiag) xdiag_buf.ensure((size_t)PMAX_LAUNCH * 256 * 4);
   HIP_OK(hipEventRecord(c->ev_dec[0], s));
   c->dec_nlaunch = 0;
   for (int mt = W.MT; mt >= 1; --mt) {
     const int li = W.MT - mt;  // launch index: its barrier block (armed in taco_infer's state fill)
-    a.bar = reinterpret_cast<unsigned*>(W.pbar.p) + BAR_WORDS * li;
+    a.bar = reinterpret_cast<unsigned*>(W.pbar.p) + BAR_WORDS * W.pslot[li];
     a.base_out = W.stat.i() + TS_END + li;
     a.D = make_dev(c, std::min(W.B, 16 * mt));
     a.trace = li == trace_li ? trace_p : nullptr;
     a.atrace = li == trace_li ? atrace_p : nullptr;
+    a.diag = xdiag ? static_cast<unsigned*>(xdiag_buf.p) + 256 * li : nullptr;
     launch_persist_decoder(a, mt, s, false);
     if (tr && li == trace_li) {  // one launch is traced
       HIP_OK(hipStreamSynchronize(s));
@@ -1521,6 +1537,19 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     }
     const int i = c->dec_nlaunch++;
     HIP_OK(hipEventRecord(c->ev_dec[i + 1], s));
+  }
+  a.diag = nullptr;
+  if (xdiag) {  // TTS_DIAG_XCC: print each launch's workgroup -> XCD map and the hand-off addresses
+    HIP_OK(hipStreamSynchronize(s));
+    std::vector<unsigned> h((size_t)PMAX_LAUNCH * 256);
+    HIP_OK(hipMemcpy(h.data(), xdiag_buf.p, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int li = 0; li < c->dec_nlaunch; ++li) {
+      std::fprintf(stderr, "TTS_DIAG_XCC launch %d: wg0 xcc %u, wg0..15:", li, h[li * 256]);
+      for (int k = 0; k < 16; ++k) std::fprintf(stderr, " %u", h[li * 256 + k]);
+      std::fprintf(stderr, "\n");
+    }
+    std::fprintf(stderr, "TTS_DIAG_XCC addresses: bar %p pq %p hatt %p ctx %p hdec0 %p pb %p\n", (void*)W.pbar.p,
+                 (void*)a.pq, (void*)a.hatt, (void*)a.ctx, (void*)a.hdec0, (void*)a.pb);
   }
 }
 
@@ -1623,7 +1652,8 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     f.add(W.stop.p, (size_t)B * S_cap * 4);
     f.add(W.acnt.p, BMAX * sizeof(unsigned));
     f.add(W.post.p, (size_t)B * S_cap * r * 80 * 4);
-    if (persist) add_barrier_fills(f, reinterpret_cast<unsigned*>(W.pbar.p), W.MT);
+    if (persist)
+      for (int li = 0; li < W.MT; ++li) add_barrier_fills(f, reinterpret_cast<unsigned*>(W.pbar.p) + BAR_WORDS * W.pslot[li], 1);
     launch_fills(f, s);
   }
   bcast_rows_kernel<<<256, 256, 0, s>>>(M.att_bias.f(), 4096, W.gatt.f(), Bp);
@@ -1681,7 +1711,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     const unsigned* lc = reinterpret_cast<const unsigned*>(W.lc.p);
     taco_status_kernel<<<1, 256, 0, s>>>(W.enc_persist ? lc : nullptr, W.enc_ndom,
                                          persist ? reinterpret_cast<const unsigned*>(W.pbar.p) : nullptr,
-                                         c->dec_nlaunch, W.ctl.i(), c->gemm_x3 ? x3_flag(c) : nullptr, W.stat.i());
+                                         DecSlots{{W.pslot[0], W.pslot[1], W.pslot[2], W.pslot[3]}}, c->dec_nlaunch, W.ctl.i(), c->gemm_x3 ? x3_flag(c) : nullptr, W.stat.i());
     HIP_OK(hipGetLastError());
     int* pin = c->pinned;
     HIP_OK(hipMemcpyAsync(pin + TS_ENC, W.stat.i() + TS_ENC, (TS_N - TS_ENC) * 4, hipMemcpyDeviceToHost, s));

@@ -180,6 +180,7 @@ struct PArgs {
   unsigned long long* trace;   // optional phase timestamps [8 steps][10][256] (TTS_PTRACE)
   unsigned long long* atrace;  // optional attention-item timestamps [8 steps][256][8]
   int trace_t0;
+  unsigned* diag;  // optional (TTS_DIAG_XCC): the XCC id of every workgroup, written at launch
   DecDev D;
 };
 
@@ -187,6 +188,9 @@ bool persist_supported(int device);
 int persist_attn_tc();  // attention positions per work item (sizes the chunk-partial buffers)
 bool persist_defer_ok(int nitems);  // the deferred alignment pass has room for this many items
 bool persist_trace_built();          // phase stamps compiled in (-DTTS_PHASE_TRACE)
+// time the flag barrier on `ncand` candidate blocks (BAR_WORDS apart from pool) and return the
+// `nwant` fastest in slot[] (TTS_BAR_CALIBRATE=0: slots 0 .. nwant-1); one decoder grid per block
+void pick_barrier_blocks(unsigned* pool, int ncand, int nwant, int* slot, hipStream_t s);
 // arm: zero the barrier block first (false: the caller armed it, e.g. in its state fill)
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm = true);
 

@@ -34,7 +34,10 @@
 #include "gsync.h"
 #include "split16.h"
 
+#include <algorithm>
+#include <cstdio>
 #include <type_traits>
+#include <vector>
 
 namespace {
 constexpr int PW = 256, PT = 512, NWV = 8;
@@ -1054,6 +1057,11 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   const int T_first = (it_first >= 0 && it_first < D.B * P.nchmax) ? D.lens[it_first / P.nchmax] : 0;
   float Lr[8];  // location features of the first attention item (attn_loc in P1, used in P4)
   f32x4 evc[pec_arr(VAR, MT)];  // encoder rows of the first attention item (loaded on its first step)
+  if (P.diag && tid0 == 0) {  // placement diagnostics: which XCD this workgroup runs on
+    unsigned xcc;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+    stci(reinterpret_cast<int*>(P.diag) + blockIdx.x, (int)(xcc & 15u));
+  }
   const int t_first = D.ctl->base;
   int t = t_first;
   const int pj_jobs = (X3P && MT > 2 ? 4 : 2) * P.ntj;
@@ -1672,6 +1680,63 @@ bool persist_supported(int device) {
 }
 
 int persist_attn_tc() { return PTC; }
+
+// ---- barrier-block placement (tools/bar_bench.hip placement sweep): the same flag barrier costs
+// 1.53-1.58 or 1.78-1.92 us depending on where its 4 KiB block lies (alternating with address bit 13
+// at 8 KiB steps; 2.15 against 2.32 us with a hand-off), i.e. on which memory stack the words sit
+// relative to the releasing workgroup's XCD. The decoder saw it as a per-process 25.8 / 27.2 us
+// step. Candidate blocks are timed once per workspace and the fastest serve the launches.
+namespace {
+__global__ __launch_bounds__(PT) void gflag_cal_kernel(unsigned* bar, int iters) {
+  __shared__ int flag;
+  unsigned gen = 0;
+  for (int i = 0; i < iters; ++i) {
+    gflag_arrive(bar, gen);
+    if (!gflag_wait(bar, gen, &flag)) return;
+  }
+}
+}  // namespace
+
+void pick_barrier_blocks(unsigned* pool, int ncand, int nwant, int* slot, hipStream_t s) {
+  for (int i = 0; i < nwant; ++i) slot[i] = i;
+  const char* e = std::getenv("TTS_BAR_CALIBRATE");
+  if ((e && std::atoi(e) == 0) || ncand <= nwant) return;
+  const void* f = (const void*)gflag_cal_kernel;
+  ensure_dyn_lds(f, (int)P_LDS);  // one workgroup per CU, as the decoder
+  hipEvent_t e0, e1;
+  HIP_OK(hipEventCreate(&e0));
+  HIP_OK(hipEventCreate(&e1));
+  std::vector<std::pair<float, int>> t;
+  int iters = 200;
+  for (int k = 0; k < ncand; ++k) {
+    unsigned* b = pool + (size_t)k * BAR_WORDS;
+    float best = 1e30f;
+    for (int rep = 0; rep < 2; ++rep) {
+      arm_barrier(b, 1, s);
+      void* args[] = {&b, &iters};
+      HIP_OK(hipEventRecord(e0, s));
+      launch_resident(f, dim3(PW), dim3(PT), args, P_LDS, s);
+      HIP_OK(hipEventRecord(e1, s));
+      HIP_OK(hipEventSynchronize(e1));
+      float ms = 0.f;
+      HIP_OK(hipEventElapsedTime(&ms, e0, e1));
+      best = std::min(best, ms);
+    }
+    unsigned err = 0;
+    HIP_OK(hipMemcpy(&err, b + 16, 4, hipMemcpyDeviceToHost));
+    TTS_CHECK(err == 0, "barrier calibration: grid barrier timed out (workgroups not co-resident)");
+    t.push_back({best, k});
+  }
+  HIP_OK(hipEventDestroy(e0));
+  HIP_OK(hipEventDestroy(e1));
+  std::stable_sort(t.begin(), t.end());
+  for (int i = 0; i < nwant; ++i) slot[i] = t[i].second;
+  if (std::getenv("TTS_DIAG_XCC")) {
+    std::fprintf(stderr, "TTS_DIAG_XCC barrier blocks (us per barrier):");
+    for (auto& x : t) std::fprintf(stderr, " %d:%.3f", x.second, x.first * 1000.f / iters);
+    std::fprintf(stderr, "\n");
+  }
+}
 #ifdef TTS_PHASE_TRACE
 bool persist_trace_built() { return true; }
 #else
