@@ -61,6 +61,8 @@ if at is not None:
     for s in range(3):
         p4start = a[s][4].min()
         items = [i for i in range(256) if at[s][i][0] > 0]
+        if not items:
+            continue
         d = np.array([[(at[s][i][k] - p4start) / 100.0 if at[s][i][k] > 0 else np.nan for k in range(8)]
                       for i in items])
         print(f"step {s}: {len(items)} items; stamp times after P4 release (us): median / max")
