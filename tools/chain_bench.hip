@@ -6,6 +6,13 @@
 // Not part of the library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/chain_bench.hip -o tools/chain_bench
 #include "../tts_amd/csrc/gsync.h"
+// -DCB_FLAG: the flag barrier the decoder runs since round 5 (gsync.h gflag_*) in place of the
+// counter form; argv[2] picks the barrier block among 16 of one allocation (its placement matters,
+// DESIGN.md 4.1d)
+#ifdef CB_FLAG
+#define gsync_arrive(b, g) gflag_arrive(b, g)
+#define gsync_wait(b, g, f) gflag_wait(b, g, f)
+#endif
 
 #include <cstdio>
 #include <cstring>
@@ -314,7 +321,9 @@ int main(int argc, char** argv) {
   a.hd1 = alloc(8 * S_HD);
   a.alpha = alloc(NB * 256);
   a.sink = alloc(PW);
-  HIP_OK(hipMalloc(&a.bar, BAR_WORDS * 4));
+  unsigned* bar_pool;
+  HIP_OK(hipMalloc(&bar_pool, 16 * BAR_WORDS * 4));
+  a.bar = bar_pool + (argc > 2 ? std::atoi(argv[2]) % 16 : 0) * BAR_WORDS;
   HIP_OK(hipMalloc(&a.ctr, 16384 * 4));
   HIP_OK(hipMalloc(&a.err, 4));
   const int steps = 400;

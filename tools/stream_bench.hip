@@ -8,6 +8,9 @@
 //   mode 3: two k-steps of loads ahead (mode 0 order)
 //   mode 4: mode 0 without the rewrite (the block stays valid in every XCD's L2)
 //   mode 5: mode 0 with plain loads (not a valid hand-off: L1 may serve stale lines; timing only)
+//   mode 6: mode 0, and wave 0 of each workgroup first touches its 1/32 share of the block's lines
+//           (workgroups g and g + 8 k share an XCD: share (g / 8) % 32), so that each XCD's L2
+//           requests all of the block at once instead of line by line behind the k-steps
 // Every workgroup rewrites its 1/256 of the block before each barrier, so the lines the next pass
 // reads were last written by another XCD (as the decoder's hand-offs).
 // Not part of the library:
@@ -36,8 +39,17 @@ __global__ __launch_bounds__(512) void stream_kernel(unsigned* bar, float* act, 
   const int rot = MODE == 1 ? (int)(blockIdx.x / 8) % NKS : 0;
   f32x4 acc = {0, 0, 0, 0};
   for (int it = 0; it < iters; ++it) {
-    if (MODE == 0 || MODE == 1 || MODE == 4 || MODE == 5) {
+    if (MODE == 0 || MODE == 1 || MODE == 4 || MODE == 5 || MODE == 6) {
       constexpr int AUX = MODE == 5 ? 0 : 16;
+      if (MODE == 6 && wave == 0) {
+        // 1536 lines of 128 B; this workgroup's share: lines sh + 32 i, i < 48; lane L of load j
+        // reads 16 B of line sh + 32 (8 j + L / 8) (8 lanes per line)
+        const int sh = (int)(blockIdx.x / 8) % 32;
+        f32x4 t = {0, 0, 0, 0};
+#pragma unroll
+        for (int j = 0; j < 6; ++j) t += ldc4(act, ((sh + 32 * (8 * j + lane / 8)) * 128) + (lane & 7) * 16);
+        acc += t * 1e-30f;
+      }
       f32x4 x[2][4];
       ld_step<AUX>(x[0], act, wave, rot, lane);
 #pragma unroll
@@ -81,11 +93,12 @@ int main(int argc, char** argv) {
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   const void* ks[] = {(const void*)stream_kernel<0>, (const void*)stream_kernel<1>, (const void*)stream_kernel<2>,
-                      (const void*)stream_kernel<3>, (const void*)stream_kernel<4>, (const void*)stream_kernel<5>};
+                      (const void*)stream_kernel<3>, (const void*)stream_kernel<4>, (const void*)stream_kernel<5>,
+                      (const void*)stream_kernel<6>};
   const char* names[] = {"same order", "rotated start per XCD slot", "barriers only", "two k-steps ahead",
-                         "no rewrite (L2-valid block)", "plain loads (timing only)"};
+                         "no rewrite (L2-valid block)", "plain loads (timing only)", "XCD-shared line touch first"};
   for (int rep = 0; rep < 2; ++rep)
-    for (int m = 0; m < 6; ++m) {
+    for (int m = 0; m < 7; ++m) {
       float best = 1e30f;
       for (int r = 0; r < 3; ++r) {
         HIP_OK(hipMemset(bar, 0, BAR_WORDS * 4));
