@@ -5,7 +5,7 @@ set -o pipefail
 cd "$(dirname "$0")/.."
 mkdir -p gpurun_out
 export TMPDIR=/tmp
-for i in 1 2; do
+for i in 1 2 3; do
   for v in "$@" new; do
     lib=$PWD/tts_amd/libttship.so; [ $v != new ] && lib=$PWD/tools/var/lib_$v.so
     rm -rf gpurun_out/l_prof

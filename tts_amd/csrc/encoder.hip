@@ -245,14 +245,18 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
     }
     if (step + 1 < T_max) {  // directions and row groups are independent: one barrier each
       unsigned* db = bar + dom * BAR_WORDS;
-#ifdef TTS_BAR_COUNTERS
+      // the recurrence's NT workgroups: counter form (tools/group_bar_bench.hip, 4 groups of 64
+      // with the 16 KB h exchange: 2.41-2.51 us per step against 2.51-2.64 for the flag form,
+      // which wins on the full 256-workgroup grid; the BiLSTM kernel itself reads the same with
+      // either, 531 / 528 us); -DTTS_LSTM_BAR_FLAGS builds the flag form
+#ifndef TTS_LSTM_BAR_FLAGS
       gsync_arrive(db, gen, NT);
 #else
-      gflag_arrive(db, gen, tl);  // the recurrence's NT workgroups, released by its tile 0
+      gflag_arrive(db, gen, tl);
 #endif
 #pragma unroll
       for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(step + 1) * G + q * 4];
-#ifdef TTS_BAR_COUNTERS
+#ifndef TTS_LSTM_BAR_FLAGS
       if (!gsync_wait(db, gen, &sflag)) return;
 #else
       if (!gflag_wait(db, gen, &sflag, NT, tl)) return;
