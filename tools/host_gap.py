@@ -1,63 +1,105 @@
-"""Host time inside one bench step (the device-resident C2 step of bench.py): where the host spends
-the Tacotron2 -> MB-MelGAN hand-over. Wall-clock stamps around the library calls, cProfile of a
-few steps, top functions by own time.
-
-    python tools/host_gap.py
-"""
-import cProfile
+"""Host-side intervals of the C2 bench step: where the ~0.25 ms between the end of
+the Tacotron2 kernels and the start of the vocoder's goes. Wraps the engine's C-ABI calls with
+perf_counter stamps and reports medians over N steps:
+  taco_c      the tts_taco_infer call (enqueue, the GPU work, the status read-back)
+  py_between  from its return to the tts_melgan_infer_strided call (Python: Tacotron2.inference's
+              post-processing, bench's one_step, MultibandMelganGenerator.inference's checks)
+  voc_c       the vocoder call (enqueue, GPU work, range-flag read-back)
+Not part of the library: python tools/host_gap.py [steps]"""
 import os
-import pstats
 import sys
 import time
 
 import numpy as np
 import torch
 
-ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-sys.path.insert(0, ROOT)
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import bench  # noqa: E402
+from tts_amd._lib import get_engine  # noqa: E402
 from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids  # noqa: E402
 
 
 def main():
+    n = int(sys.argv[1]) if len(sys.argv) > 1 else 10
     dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
     taco, _, voc, _, _, _ = bench.build_models(dev)
     taco.decoder.verbose = False
-    T, M = lj_profile()
-    ids = synthetic_ids(T)
-    batch, lens = pad_batch(ids)
-    x = torch.from_numpy(batch).to(dev)
     taco.decoder.set_r(2)
-    steps = forced_steps(M, 2)
+    T_prof, M_prof = lj_profile()
+    batch, lens = pad_batch(synthetic_ids(T_prof))
+    batch_t = torch.from_numpy(batch).to(dev)
+    steps = forced_steps(M_prof, 2)
+    eng = get_engine(dev)
+    stamps = {}
+    orig_t, orig_v = eng.taco_infer, eng.melgan_infer
 
-    def step(stamps=None):
-        t0 = time.perf_counter()
-        _, post, _, _ = taco.inference(x, text_lengths=lens, max_decoder_steps=steps)
-        t1 = time.perf_counter()
-        wav = voc.inference(post.transpose(1, 2), lengths=taco.last_mel_lengths)
-        t2 = time.perf_counter()
+    def taco_w(*a, **k):
+        stamps["t0"] = time.perf_counter()
+        out = orig_t(*a, **k)
+        stamps["t1"] = time.perf_counter()
+        return out
+
+    def voc_w(*a, **k):
+        stamps["v0"] = time.perf_counter()
+        out = orig_v(*a, **k)
+        stamps["v1"] = time.perf_counter()
+        return out
+
+    eng.taco_infer, eng.melgan_infer = taco_w, voc_w
+    rec = []
+    for i in range(n + 2):
         torch.cuda.synchronize()
-        t3 = time.perf_counter()
-        if stamps is not None:
-            stamps.append((t1 - t0, t2 - t1, t3 - t2))
-        return wav
+        s0 = time.perf_counter()
+        _, post, _, _ = taco.inference(batch_t, text_lengths=lens, max_decoder_steps=steps)
+        wav = voc.inference(post.transpose(1, 2), lengths=taco.last_mel_lengths)
+        torch.cuda.synchronize()
+        s1 = time.perf_counter()
+        if i >= 2:
+            rec.append([(stamps["t0"] - s0) * 1e6, (stamps["t1"] - stamps["t0"]) * 1e6,
+                        (stamps["v0"] - stamps["t1"]) * 1e6, (stamps["v1"] - stamps["v0"]) * 1e6,
+                        (s1 - stamps["v1"]) * 1e6, (s1 - s0) * 1e6])
+    med = np.median(np.array(rec), axis=0)
+    names = ["py_before_taco", "taco_c", "py_between", "voc_c", "py_after", "step"]
+    print("{" + ", ".join(f'"{k}_us": {v:.1f}' for k, v in zip(names, med)) + "}")
+    del wav
 
-    for _ in range(3):
+
+
+
+def profile(n=10):
+    """cProfile of n steps' host code (the C calls show as two leaf entries)."""
+    import cProfile
+    import pstats
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    taco, _, voc, _, _, _ = bench.build_models(dev)
+    taco.decoder.verbose = False
+    taco.decoder.set_r(2)
+    T_prof, M_prof = lj_profile()
+    batch, lens = pad_batch(synthetic_ids(T_prof))
+    batch_t = torch.from_numpy(batch).to(dev)
+    steps = forced_steps(M_prof, 2)
+
+    def step():
+        _, post, _, _ = taco.inference(batch_t, text_lengths=lens, max_decoder_steps=steps)
+        return voc.inference(post.transpose(1, 2), lengths=taco.last_mel_lengths)
+
+    for _ in range(2):
         step()
-    st = []
-    for _ in range(10):
-        step(st)
-    a = np.array(st) * 1e3
-    print("per step (ms, median of 10): taco call %.3f  voc call (enqueue) %.3f  voc drain %.3f" %
-          tuple(np.median(a, 0)))
+    torch.cuda.synchronize()
     pr = cProfile.Profile()
     pr.enable()
-    for _ in range(5):
+    for _ in range(n):
         step()
+    torch.cuda.synchronize()
     pr.disable()
-    ps = pstats.Stats(pr).sort_stats("tottime")
-    ps.print_stats(25)
+    st = pstats.Stats(pr)
+    st.sort_stats("tottime").print_stats(35)
 
 
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[2] == "prof":
+        profile(int(sys.argv[1]))
+    else:
+        main()
