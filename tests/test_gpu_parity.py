@@ -1051,6 +1051,30 @@ def test_mbmelgan_fused_convtranspose_bit_identical(tmp_path):
     assert outs[0].shape == outs[1].shape and np.array_equal(outs[0], outs[1])
 
 
+@pytest.mark.gpu
+def test_decoder_barrier_block_calibration_bit_identical(tmp_path):
+    """The persistent decoder's barrier blocks are picked by timing 16 candidates once per workspace
+    (decoder_persist.hip pick_barrier_blocks); where the barrier words live must not change a bit of
+    the outputs. Calibrated (with TTS_DIAG_XCC=1 the timings are printed) against the blocks taken in
+    order (TTS_BAR_CALIBRATE=0), in child processes (both switches are read once per process),
+    through tools/taco_dump.py on 12 LJ-length utterances of the bench model."""
+    import subprocess
+    import sys
+    _dev()
+    outs = []
+    for cal in ("0", "1"):
+        path = str(tmp_path / f"t{cal}.npz")
+        env = dict(os.environ, TTS_BAR_CALIBRATE=cal, TTS_DIAG_XCC="1")
+        r = subprocess.run([sys.executable, os.path.join(ROOT, "tools", "taco_dump.py"), path], env=env,
+                           capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-2000:]
+        calibrated = "barrier blocks (us per barrier)" in r.stderr
+        assert calibrated == (cal == "1"), r.stderr[-2000:]
+        outs.append(np.load(path))
+    for k in ("dec", "post", "align", "stop", "steps"):
+        assert np.array_equal(outs[0][k], outs[1][k]), k
+
+
 # --------------------------------------------------------------------- GE2E speaker encoder
 @pytest.mark.parametrize("tag,proj", [("proj", True), ("noproj", False)])
 def test_ge2e_speaker_encoder_matches_reference(tag, proj):
