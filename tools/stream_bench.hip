@@ -11,6 +11,10 @@
 //   mode 6: mode 0, and wave 0 of each workgroup first touches its 1/32 share of the block's lines
 //           (workgroups g and g + 8 k share an XCD: share (g / 8) % 32), so that each XCD's L2
 //           requests all of the block at once instead of line by line behind the k-steps
+//   mode 7: rewrite, barrier, each XCD's workgroups touch the whole block (full 128-byte lines,
+//           8 lanes x 16 B each, 1/32 of the lines per workgroup), barrier, then mode 0's stream
+//   mode 8: as mode 7 with one 4-byte load per line
+//   mode 9: as mode 7 without the touch (its baseline: two barriers per iteration)
 // Every workgroup rewrites its 1/256 of the block before each barrier, so the lines the next pass
 // reads were last written by another XCD (as the decoder's hand-offs).
 // Not part of the library:
@@ -39,7 +43,20 @@ __global__ __launch_bounds__(512) void stream_kernel(unsigned* bar, float* act, 
   const int rot = MODE == 1 ? (int)(blockIdx.x / 8) % NKS : 0;
   f32x4 acc = {0, 0, 0, 0};
   for (int it = 0; it < iters; ++it) {
-    if (MODE == 0 || MODE == 1 || MODE == 4 || MODE == 5 || MODE == 6) {
+    if (MODE >= 7) {  // rewrite, barrier, touch (or not), barrier; the stream below
+      if (threadIdx.x < 48) stc4(act, (blockIdx.x * 48 + threadIdx.x) * 16, acc * 1e-30f);
+      gflag_arrive(bar, gen);
+      if (!gflag_wait(bar, gen, &flag)) return;
+      const int sh = (int)(blockIdx.x / 8) % 32;  // 1536 lines, 48 per workgroup of an XCD
+      if (MODE == 7 && wave < 6) {                // 6 waves x 8 lines x 8 lanes x 16 B
+        const f32x4 t = ldc4(act, ((sh + 32 * (8 * wave + lane / 8)) * 128) + (lane & 7) * 16);
+        acc += t * 1e-30f;
+      }
+      if (MODE == 8 && wave == 0 && lane < 48) acc[0] += ldc(act + (sh + 32 * lane) * 32) * 1e-30f;
+      gflag_arrive(bar, gen);
+      if (!gflag_wait(bar, gen, &flag)) return;
+    }
+    if (MODE == 0 || MODE == 1 || MODE == 4 || MODE == 5 || MODE == 6 || MODE >= 7) {
       constexpr int AUX = MODE == 5 ? 0 : 16;
       if (MODE == 6 && wave == 0) {
         // 1536 lines of 128 B; this workgroup's share: lines sh + 32 i, i < 48; lane L of load j
@@ -74,7 +91,7 @@ __global__ __launch_bounds__(512) void stream_kernel(unsigned* bar, float* act, 
       }
     }
     // producers: every workgroup rewrites its 768-byte slice of the block (sc1), as P3 / P4 do
-    if (MODE != 2 && MODE != 4 && threadIdx.x < 48) stc4(act, (blockIdx.x * 48 + threadIdx.x) * 16, acc * 1e-30f);
+    if (MODE != 2 && MODE != 4 && MODE < 7 && threadIdx.x < 48) stc4(act, (blockIdx.x * 48 + threadIdx.x) * 16, acc * 1e-30f);
     gflag_arrive(bar, gen);
     if (!gflag_wait(bar, gen, &flag)) return;
   }
@@ -94,11 +111,14 @@ int main(int argc, char** argv) {
   HIP_OK(hipEventCreate(&e1));
   const void* ks[] = {(const void*)stream_kernel<0>, (const void*)stream_kernel<1>, (const void*)stream_kernel<2>,
                       (const void*)stream_kernel<3>, (const void*)stream_kernel<4>, (const void*)stream_kernel<5>,
-                      (const void*)stream_kernel<6>};
+                      (const void*)stream_kernel<6>, (const void*)stream_kernel<7>, (const void*)stream_kernel<8>,
+                      (const void*)stream_kernel<9>};
   const char* names[] = {"same order", "rotated start per XCD slot", "barriers only", "two k-steps ahead",
-                         "no rewrite (L2-valid block)", "plain loads (timing only)", "XCD-shared line touch first"};
+                         "no rewrite (L2-valid block)", "plain loads (timing only)", "XCD-shared line touch first",
+                         "touch full lines one barrier ahead", "touch one dword per line one barrier ahead",
+                         "two barriers, no touch (baseline of 7 / 8)"};
   for (int rep = 0; rep < 2; ++rep)
-    for (int m = 0; m < 7; ++m) {
+    for (int m = 0; m < 10; ++m) {
       float best = 1e30f;
       for (int r = 0; r < 3; ++r) {
         HIP_OK(hipMemset(bar, 0, BAR_WORDS * 4));
