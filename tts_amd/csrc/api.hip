@@ -1890,6 +1890,18 @@ static bool stack_fuse_on() {
   }();
   return on;
 }
+// the C = 96 stack in one launch: off by default since round 5 (TTS_STACK_FUSE96=1 turns it on).
+// Same-box A/B over 4 bench runs each (profiles/r05/v17_stack96_ab.txt): vocoder 2.958 ms fused
+// against 2.922 ms with blocks 0-2 as three resblock_x3 launches; the stack kernel's halo
+// recompute (up to 24 extra rows per 96-position tile) now costs more than the two HBM round trips
+// of x it saves at this width, while at C = 48 (with the fused ConvTranspose) fusing still wins
+static bool stack_fuse96_on() {
+  static const bool on = [] {
+    const char* e = std::getenv("TTS_STACK_FUSE96");
+    return e && std::atoi(e) != 0;
+  }();
+  return on;
+}
 // the last upsample's ConvTranspose inside the C = 48 stack kernel (resstack_x3.hip CTU = 2);
 // TTS_CT_FUSE=0 keeps the separate conv_x3 launch
 static bool ct_fuse_on() {
@@ -1966,6 +1978,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   auto stack3 = [&](size_t i, int Cs, long Lss, int muls, const float* xs, float* ys, const ConvLayer* ct,
                     const float* xin, int Cin, long Lin) {
     if (!(cc.oflow && G.nres >= 3 && stack_fuse_on() && G.rb_wd16[i * G.nres].p)) return false;
+    if (Cs == 96 && !stack_fuse96_on()) return false;
     int dil[3];
     for (int k = 0; k < 3; ++k) dil[k] = G.dconv[i * G.nres + k].dil;
     if (!resstack_x3_supported(Cs, dil, 3)) return false;
