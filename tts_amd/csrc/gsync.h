@@ -1,5 +1,5 @@
 // Agent-coherent access helpers and the grid barriers (counter and flag forms) shared by the persistent kernels
-// (decoder_persist.hip, the BiLSTM in encoder.hip).
+// (decoder_persist.hip, the BiLSTM and GE2E pipeline in encoder.hip).
 //
 // Memory model: cross-workgroup data is written with agent-scope relaxed atomic stores (sc1:
 // write-through past the per-XCD L2) and read with agent-scope loads (sc1, L1 bypass); every wave
@@ -176,6 +176,10 @@ __device__ __forceinline__ void gsync_arrive(unsigned* bar, unsigned& gen, unsig
 // barrier against 1.84 us for gsync_arrive / gsync_wait, 2.10 against 2.45 us with a 1 KB hand-off
 // around it. Every workgroup polling the array itself is slower (2.7 us: 256 pollers on 8 lines).
 // The memory-model argument is gsync's: the stores before the arrival are drained sc1 stores.
+// Users: the persistent decoder and the GE2E layer pipeline (whole grids). The BiLSTM's 64-workgroup
+// recurrences keep gsync (tools/group_bar_bench.hip: counters 0.1 us per step ahead at that size).
+// The block's physical place changes the cost (1.50-2.08 us per barrier): the decoder times
+// candidate blocks once per workspace (decoder_persist.hip pick_barrier_blocks).
 constexpr int BAR_FLAGS = 512;  // words 512 .. 767 of the barrier block
 constexpr int BAR_NGO = 8;
 // A barrier over a group of n workgroups (default the grid): idx = the workgroup's index in the
