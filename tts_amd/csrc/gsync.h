@@ -36,7 +36,8 @@
 
 constexpr int BAR_TMO = 48;  // word of the barrier block holding the wait limit (s_memrealtime ticks)
 // words per barrier block: 0 global counter, 16 error word, 32 go word, BAR_TMO wait limit, then up
-// to 16 first-level counters on their own 128-byte lines (words 64 + 32 c)
+// to 16 first-level counters on their own 128-byte lines (words 64 + 32 c); the flag form uses the
+// error word, the wait limit, go words 32 + 64 k (k < BAR_NGO) and arrival flags at BAR_FLAGS
 constexpr int BAR_WORDS = 1024;
 
 // entries zeroing `nblk` barrier blocks and writing their wait limit, for a caller's fill
