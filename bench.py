@@ -398,7 +398,8 @@ def main():
         # what the step actually hits is the latency of its hand-off chain (5 phases per step, each
         # separated by a grid barrier, each starting with a coherent load of what the previous one
         # published): tools/chain_bench.hip runs that chain with the decoder's roles and hand-off
-        # sizes and no arithmetic (profiles/r04/chain_floor.json). achieved / peak stay the MFMA
+        # sizes and no arithmetic (the newest profiles/rNN/chain_floor.json; round 5 re-ran it with the
+        # flag barrier the kernel now uses). achieved / peak stay the MFMA
         # figures (algorithmic FLOPs / launch time against the split-f16 ceiling)
         floor = None
         fpath = latest_profile("chain_floor.json")
