@@ -130,6 +130,25 @@ __global__ __launch_bounds__(512) void ring_kernel(unsigned* bar, unsigned* flag
   if (threadIdx.x < 64) out[blockIdx.x * 64 + threadIdx.x] = acc[0] + acc[1] + acc[2] + acc[3];
 }
 
+// atomic round trip from each XCD to candidate 4 KiB blocks: workgroup w (one per XCD) chases
+// dependent agent-scope atomics through word 32 of block c; out[w][c] = ticks (100 MHz) for NCH loads, out[w][NC] = XCC id
+constexpr int LAT_NC = 64, LAT_NCH = 64;
+__global__ void lat_kernel(unsigned* pool, unsigned* out) {
+  if (threadIdx.x != 0) return;
+  unsigned xcc;
+  asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(xcc));
+  for (int c = 0; c < LAT_NC; ++c) {
+    const unsigned* p = pool + (size_t)c * 1024 + 32;
+    unsigned v = __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // warm
+    const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+    for (int i = 0; i < LAT_NCH; ++i)  // atomics: performed past the XCD's L2 (a load would hit in it)
+      v = __hip_atomic_fetch_add(const_cast<unsigned*>(p) + (v & 1), 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+    out[blockIdx.x * (LAT_NC + 1) + c] = (unsigned)(t1 - t0) + (v & 1);
+  }
+  out[blockIdx.x * (LAT_NC + 1) + LAT_NC] = xcc & 15u;
+}
+
 __global__ __launch_bounds__(512) void bar_kernel(unsigned* bar, unsigned* flags, float* data, int iters, int mode,
                                                   float* out, int ncp) {
   __shared__ int flag;
@@ -227,6 +246,23 @@ int main(int argc, char** argv) {
     std::printf("{\"mode\": %d, \"form\": \"%s\", \"handoff\": %d, \"go_copies\": %d, \"us_per_barrier\": %.3f, \"err\": %u}\n", mode,
                 names[mode & 7], mode >> 3, ncp, best * 1000.f / iters, err | berr);
     if (err | berr) return 1;
+  }
+  {  // load latency matrix (XCD x candidate block)
+    unsigned *pool, *lat;
+    HIP_OK(hipMalloc(&pool, (size_t)LAT_NC * 4096));
+    HIP_OK(hipMemset(pool, 0, (size_t)LAT_NC * 4096));
+    HIP_OK(hipMalloc(&lat, 8 * (LAT_NC + 1) * 4));
+    std::vector<unsigned> h(8 * (LAT_NC + 1));
+    for (int rep = 0; rep < 2; ++rep) {
+      hipLaunchKernelGGL(lat_kernel, dim3(8), dim3(64), 0, 0, pool, lat);
+      HIP_OK(hipDeviceSynchronize());
+    }
+    HIP_OK(hipMemcpy(h.data(), lat, h.size() * 4, hipMemcpyDeviceToHost));
+    for (int w = 0; w < 8; ++w) {
+      std::printf("{\"lat_xcc\": %u, \"ns_per_load\": [", h[w * (LAT_NC + 1) + LAT_NC]);
+      for (int c = 0; c < LAT_NC; ++c) std::printf("%s%.0f", c ? ", " : "", h[w * (LAT_NC + 1) + c] * 10.0 / LAT_NCH);
+      std::printf("]}\n");
+    }
   }
   // placement: the flag barrier (mode 6, 8 go copies) on barrier blocks at different offsets of one
   // 64 MiB allocation (8 KiB steps, then 2 MiB steps): does the block's physical place matter?

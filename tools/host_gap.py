@@ -95,7 +95,9 @@ def profile(n=10):
     torch.cuda.synchronize()
     pr.disable()
     st = pstats.Stats(pr)
-    st.sort_stats("tottime").print_stats(35)
+    rows = sorted(((v[2], v[3], v[1], k) for k, v in st.stats.items()), reverse=True)[:40]
+    for tt, ct, nc, k in rows:
+        print(f"{tt * 1e6 / n:9.1f} us/step self {ct * 1e6 / n:10.1f} us/step cum {nc / n:5.1f} calls  {k[0].split('/')[-1]}:{k[1]}({k[2]})")
 
 
 if __name__ == "__main__":
