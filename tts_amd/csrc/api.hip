@@ -488,6 +488,7 @@ struct tts_ctx {
   bool flag_read = false; // the entry point already fetched the range flag into pinned[12]
   int dec_end[PMAX_LAUNCH] = {};  // step index after each persistent launch of the last decode
   int dec_path = 0;       // last decode: 0 = step graphs, 1 = persistent kernel
+  bool dec_presplit = false;  // last persistent decode published h_att / ctx / h_dec pre-split
   // GEMM arithmetic: true = split-f16 MFMA kernels where built (fp32-accurate, split16.h), false =
   // fp32 MFMA everywhere (tts_set_gemm_mode; TTS_GEMM=f32 in the environment starts a context so)
   bool gemm_x3 = true;
@@ -1262,19 +1263,28 @@ __global__ void taco_setup_kernel(TacoSetup a, int* map, int* lens, int* ctl) {
   }
 }
 
+// element (m, k) of a fragment-order activation; ps: published pre-split (decoder_persist.hip
+// stc_quad_x3: the f16 hi / lo halves of k & ~3 .. + 3 as [hi 4 | lo 4] in their 16 bytes), read back
+// as hi + 2^-11 lo, the value the decoder's split-f16 GEMMs consumed
+__device__ __forceinline__ float frag_value(const float* p, int m, int k, int K, int ps) {
+  if (!ps) return p[frag_idx(m, k, K)];
+  const _Float16* q = reinterpret_cast<const _Float16*>(p + frag_idx(m, k & ~3, K));
+  return (float)q[k & 3] + (float)q[4 + (k & 3)] * SPLIT_INV;
+}
+
 // decoder state in the caller's row order (tts_taco_decoder_state): fragment-order activations
 // (h_att, h_dec, ctx) and row-major cells / attention rows of decode row inv[b] -> row b
 __global__ void taco_state_kernel(const float* hatt, const float* catt, const float* hdec, const float* cdec,
                                   const float* ctx, const float* alpha, const float* acum, const int* inv, int T_max,
-                                  float* o_ha, float* o_ca, float* o_hd, float* o_cd, float* o_ctx, float* o_al,
-                                  float* o_ac) {
+                                  int ps, float* o_ha, float* o_ca, float* o_hd, float* o_cd, float* o_ctx,
+                                  float* o_al, float* o_ac) {
   const int b = blockIdx.y, m = inv[b];
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < 1024; k += gridDim.x * blockDim.x) {
-    if (o_ha) o_ha[(long)b * 1024 + k] = hatt[frag_idx(m, k, 1024)];
+    if (o_ha) o_ha[(long)b * 1024 + k] = frag_value(hatt, m, k, 1024, ps);
     if (o_ca) o_ca[(long)b * 1024 + k] = catt[(long)m * 1024 + k];
-    if (o_hd) o_hd[(long)b * 1024 + k] = hdec[frag_idx(m, k, 1024)];
+    if (o_hd) o_hd[(long)b * 1024 + k] = frag_value(hdec, m, k, 1024, ps);
     if (o_cd) o_cd[(long)b * 1024 + k] = cdec[(long)m * 1024 + k];
-    if (o_ctx && k < 512) o_ctx[(long)b * 512 + k] = ctx[frag_idx(m, k, 512)];
+    if (o_ctx && k < 512) o_ctx[(long)b * 512 + k] = frag_value(ctx, m, k, 512, ps);
   }
   for (int k = blockIdx.x * blockDim.x + threadIdx.x; k < T_max; k += gridDim.x * blockDim.x) {
     if (o_al) o_al[(long)b * T_max + k] = alpha[(long)m * T_max + k];
@@ -1514,6 +1524,7 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   if (xdiag) xdiag_buf.ensure((size_t)PMAX_LAUNCH * 256 * 4);
   HIP_OK(hipEventRecord(c->ev_dec[0], s));
   c->dec_nlaunch = 0;
+  c->dec_presplit = persist_presplit(a);
   for (int mt = W.MT; mt >= 1; --mt) {
     const int li = W.MT - mt;  // launch index: its barrier block (armed in taco_infer's state fill)
     a.bar = reinterpret_cast<unsigned*>(W.pbar.p) + BAR_WORDS * W.pslot[li];
@@ -3271,7 +3282,7 @@ int tts_taco_decoder_state(tts_ctx* c, int B, int T_max, float* d_att_h, float* 
     enter(c, stream);
     taco_state_kernel<<<dim3(4, c->last_B), 256, 0, c->s>>>(W.hatt.f(), W.catt.f(), hdec, W.cdec.f(), W.ctx.f(),
                                                             W.alpha.f(), W.acum.f(), W.map.i() + BMAX, c->last_T,
-                                                            d_att_h, d_att_c, d_dec_h, d_dec_c, d_context, d_alpha,
+                                                            c->dec_presplit ? 1 : 0, d_att_h, d_att_c, d_dec_h, d_dec_c, d_context, d_alpha,
                                                             d_alpha_cum);
     HIP_OK(hipGetLastError());
     leave(c, stream);

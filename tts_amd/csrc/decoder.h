@@ -193,6 +193,8 @@ bool persist_trace_built();          // phase stamps compiled in (-DTTS_PHASE_TR
 void pick_barrier_blocks(unsigned* pool, int ncand, int nwant, int* slot, hipStream_t s);
 // arm: zero the barrier block first (false: the caller armed it, e.g. in its state fill)
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm = true);
+// whether that launch publishes h_att / ctx / h_dec pre-split (decoder_persist.hip presplit_of)
+bool persist_presplit(const PArgs& a);
 
 void launch_skinny(const SkArgs& a, const DecDev& d, int jstep, int NT, int KS, hipStream_t s);
 // prenet layer 1 + layer 2 in one launch (16 workgroups) plus the stop workgroup

@@ -67,6 +67,36 @@ constexpr int YROWS = 64;    // rows per projection half (independent of the bat
 // sizes the (unused) array of the latter
 constexpr int pec_of(int VAR, int MT) { return ((VAR & 8) && !(VAR & 2) && MT <= 2) ? 4 : 0; }
 constexpr int pec_arr(int VAR, int MT) { return pec_of(VAR, MT) > 0 ? pec_of(VAR, MT) : 1; }
+// pre-split hand-offs (VAR 8: location attention, every decoder GEMM on the split-f16 MFMA): h_att,
+// ctx and h_dec are published as their f16 hi / lo halves, [hi 0..3 | lo 0..3] in the 16 bytes a
+// fragment quad takes in fp32, so the streaming consumers feed the loads to the MFMA without
+// splitting (the split is done once, by the producer; tools/payload_bench.hip mode 3: 0.42 us less
+// per streamed 192 KB block). The variants with fp32 readers of these buffers keep fp32.
+#ifdef TTS_NO_PRESPLIT
+constexpr bool presplit_of(int) { return false; }
+#else
+constexpr bool presplit_of(int VAR) { return VAR == 8; }
+#endif
+// stc_quad's pre-split form: lanes 4 q .. 4 q + 3 hold the 4 consecutive k of one row; lane 4 q
+// stores their hi halves then their lo halves (split_fast, as split8 on the consumer would)
+__device__ __forceinline__ void stc_quad_x3(float* base, int e, float v) {
+  _Float16 hi, lo;
+  split_fast(v, hi, lo);
+  const int p = (int)((unsigned)__builtin_bit_cast(unsigned short, hi) |
+                      ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16));
+  const unsigned p0 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0x00, 0xf, 0xf, true),
+                 p1 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0x55, 0xf, 0xf, true),
+                 p2 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0xAA, 0xf, 0xf, true),
+                 p3 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0xFF, 0xf, 0xf, true);
+  const f32x4 q = {__uint_as_float((p0 & 0xffffu) | (p1 << 16)), __uint_as_float((p2 & 0xffffu) | (p3 << 16)),
+                   __uint_as_float((p0 >> 16) | (p1 & 0xffff0000u)), __uint_as_float((p2 >> 16) | (p3 & 0xffff0000u))};
+  if ((threadIdx.x & 3) == 0) stc4(base, e * 4, q);
+}
+template <bool PS>
+__device__ __forceinline__ void stc_quad_h(float* base, int e, float v) {
+  if constexpr (PS) stc_quad_x3(base, e, v);
+  else stc_quad(base, e, v);
+}
 constexpr int LOCK_ = 31, ADIM_ = 128, NPQ_ = NATT;  // NPQ_: query-projection partials
 // LDS layouts chosen for bank-conflict-free access (64 banks x 4 B; ds_read_b32 / ds_write_b32 bank
 // = dword index mod 32 within a 32-lane group, ds_read_b128 = mod 64 within a 16-lane group):
@@ -478,7 +508,7 @@ __device__ __forceinline__ void pattn_item(const PArgs& P, int t, int b, int ch,
     }
   }
   float ctx_v = cx / ((FWD && P.fwd) ? Fz : S);
-  stc_quad(P.ctx, (int)frag_idx(b, tid, 512), ctx_v);
+  stc_quad_h<presplit_of(VAR)>(P.ctx, (int)frag_idx(b, tid, 512), ctx_v);
   ATRACE(7);
   if (ekeep) {  // deferred alignment pass: publish the normaliser, the items finish in P6
     if (tid == 0) {
@@ -773,11 +803,18 @@ __device__ __forceinline__ void ld_x3_step(f32x4 (&x)[MT][2], const float* base,
     x[mt][1] = ldc4<ACT_AUX>(base, (c * 64 + l1 + 16) * 16);
   }
 }
+// PS: the chunk was published pre-split (stc_quad_x3): x[0] holds k 0..3 as [hi | lo], x[1] k 4..7
+template <bool PS>
 __device__ __forceinline__ void split_x3_step(const f32x4 (&x)[2], h8& xh, h8& xl) {
-  const float v[8] = {x[0][0], x[0][1], x[0][2], x[0][3], x[1][0], x[1][1], x[1][2], x[1][3]};
-  split8(v, xh, xl);
+  if constexpr (PS) {
+    xh = __builtin_bit_cast(h8, (f32x4{x[0][0], x[0][1], x[1][0], x[1][1]}));
+    xl = __builtin_bit_cast(h8, (f32x4{x[0][2], x[0][3], x[1][2], x[1][3]}));
+  } else {
+    const float v[8] = {x[0][0], x[0][1], x[0][2], x[0][3], x[1][0], x[1][1], x[1][2], x[1][3]};
+    split8(v, xh, xl);
+  }
 }
-template <int MT, int NKS, class WF>
+template <int MT, int NKS, bool PS = false, class WF>
 __device__ __forceinline__ void gemm_x3(f32x4 (&acc)[MT], const float* base, int nk, int ks0, int lane, WF wf) {
   f32x4 x[2][MT][2];
   ld_x3_step<MT>(x[0], base, nk, ks0, lane);
@@ -792,7 +829,7 @@ __device__ __forceinline__ void gemm_x3(f32x4 (&acc)[MT], const float* base, int
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       h8 xh, xl;
-      split_x3_step(x[k & 1][mt], xh, xl);
+      split_x3_step<PS>(x[k & 1][mt], xh, xl);
       mfma_x3(xh, xl, bh, bl, am[mt], ac[mt]);
     }
   }
@@ -801,7 +838,7 @@ __device__ __forceinline__ void gemm_x3(f32x4 (&acc)[MT], const float* base, int
 #pragma unroll
     for (int j = 0; j < 4; ++j) acc[mt][j] += x3_value(am[mt][j], ac[mt][j]);
 }
-template <int MT, int NKS, class WF1, class WF2>
+template <int MT, int NKS, bool PS = false, class WF1, class WF2>
 __device__ __forceinline__ void gemm_x3_pair(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* base, int nk, int ks0,
                                              int lane, WF1 wf1, WF2 wf2) {
   f32x4 x[2][MT][2];
@@ -818,7 +855,7 @@ __device__ __forceinline__ void gemm_x3_pair(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       h8 xh, xl;
-      split_x3_step(x[k & 1][mt], xh, xl);
+      split_x3_step<PS>(x[k & 1][mt], xh, xl);
       mfma_x3(xh, xl, b1h, b1l, am1[mt], ac1[mt]);
       mfma_x3(xh, xl, b2h, b2l, am2[mt], ac2[mt]);
     }
@@ -836,7 +873,7 @@ __device__ __forceinline__ void gemm_x3_pair(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT
 // wa1 / wa2) then the ctx parts (NKC k-steps from `c`, weights wc1 / wc2) of both LSTMs, one
 // pipeline: every activation chunk is read once and the first ctx k-step's loads are in flight
 // under the last h_att k-step
-template <int MT, int NKA, int NKC, class WA1, class WA2, class WC1, class WC2>
+template <int MT, int NKA, int NKC, bool PS = false, class WA1, class WA2, class WC1, class WC2>
 __device__ __forceinline__ void gemm_x3_hatt_ctx(f32x4 (&acc1)[MT], f32x4 (&acc2)[MT], const float* a, int nka,
                                                  int ksa, const float* c, int nkc, int ksc, int lane, WA1 wa1,
                                                  WA2 wa2, WC1 wc1, WC2 wc2) {
@@ -859,7 +896,7 @@ __device__ __forceinline__ void gemm_x3_hatt_ctx(f32x4 (&acc1)[MT], f32x4 (&acc2
 #pragma unroll
     for (int mt = 0; mt < MT; ++mt) {
       h8 xh, xl;
-      split_x3_step(x[k & 1][mt], xh, xl);
+      split_x3_step<PS>(x[k & 1][mt], xh, xl);
       mfma_x3(xh, xl, b1h, b1l, am1[mt], ac1[mt]);
       mfma_x3(xh, xl, b2h, b2l, am2[mt], ac2[mt]);
     }
@@ -960,6 +997,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   constexpr bool GRAVES = (VAR & 4) != 0;  // Graves attention replaces the location-sensitive one
   constexpr bool X3P = (VAR & 8) != 0;     // P3's attention_rnn prenet part on the split-f16 MFMA
   constexpr bool DEFER = (VAR & 7) == 0;   // plain location attention: alignment pass deferred to P6
+  constexpr bool PS = presplit_of(VAR);    // h_att, ctx, h_dec published pre-split
   extern __shared__ __attribute__((aligned(16))) f32x4 smem4[];
   __shared__ int sflag, is_last;
   constexpr int Bp = MT * 16;
@@ -1082,7 +1120,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   for (int mt = 0; mt < MT; ++mt) accd[mt] = acca[mt] = f32x4{0.f, 0.f, 0.f, 0.f};
   auto dec_hdec_part = [&](const float* hd) {
     if constexpr (X3P)
-      X3_PASSES(MT, (gemm_x3<NM, 4>(msub<MO, NM>(accd), hd + MO * 64 * 256, 64, 4 * wave, lane, wdx_f(6))));
+      X3_PASSES(MT, (gemm_x3<NM, 4, PS>(msub<MO, NM>(accd), hd + MO * 64 * 256, 64, 4 * wave, lane, wdx_f(6))));
     else gemm_seg<MT, 8, 4>(accd, hd, 64, 8 * wave, lane, [&](int i) { return wd[12 + i]; });
   };
   // attention_rnn ctx/h tile g complete: reduce over the waves, add the biases, publish the next
@@ -1391,7 +1429,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
             const float c = sigm_f(pre[1]) * ca[ck] + sigm_f(pre[0]) * tanh_f(pre[2]);
             const float h = sigm_f(pre[3]) * tanh_f(c);
             P.catt[ci] = c;
-            stc_quad(P.hatt, (int)frag_idx(m, tile * 4 + u, 1024), h);
+            stc_quad_h<PS>(P.hatt, (int)frag_idx(m, tile * 4 + u, 1024), h);
             hs[m * 17 + gl * 4 + u] = h;
           }
         }
@@ -1490,7 +1528,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
         if constexpr (!X3P) gemm_seg<MT, 8, 2>(accd, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; });
       } else {  // no item: both h_att parts and the decoder_rnn h_dec part
         if constexpr (X3P)
-          X3_PASSES(MT, (gemm_x3_pair<NM, 4>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.hatt + MO * 64 * 256, 64,
+          X3_PASSES(MT, (gemm_x3_pair<NM, 4, PS>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.hatt + MO * 64 * 256, 64,
                                              4 * wave, lane, wdx_f(0), wap_f(16 + 4 * wave))));
         else
           gemm_seg2<MT, 8, 2>(accd, acca, P.hatt, 64, 8 * wave, lane, [&](int i) { return wd[i]; },
@@ -1514,11 +1552,11 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     {
       if constexpr (X3P) {
         if (g >= IW0)  // + both h_att parts (moved here from P4 / P6: h_att read once per step)
-          X3_PASSES(MT, (gemm_x3_hatt_ctx<NM, 4, 2>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.hatt + MO * 64 * 256, 64,
+          X3_PASSES(MT, (gemm_x3_hatt_ctx<NM, 4, 2, PS>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.hatt + MO * 64 * 256, 64,
                                                     4 * wave, P.ctx + MO * 32 * 256, 32, 2 * wave, lane, wdx_f(0),
                                                     wap_f(16 + 4 * wave), wdx_f(4), wap_f(2 * wave))));
         else
-          X3_PASSES(MT, (gemm_x3_pair<NM, 2>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.ctx + MO * 32 * 256, 32,
+          X3_PASSES(MT, (gemm_x3_pair<NM, 2, PS>(msub<MO, NM>(accd), msub<MO, NM>(acca), P.ctx + MO * 32 * 256, 32,
                                              2 * wave, lane, wdx_f(4), wap_f(2 * wave))));
       }
       else
@@ -1543,7 +1581,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
           const float c = sigm_f(pre[1]) * cd[ck] + sigm_f(pre[0]) * tanh_f(pre[2]);
           const float h = sigm_f(pre[3]) * tanh_f(c);
           P.cdec[ci] = c;
-          stc_quad(hd_nxt, (int)frag_idx(m, g * 4 + u, 1024), h);
+          stc_quad_h<PS>(hd_nxt, (int)frag_idx(m, g * 4 + u, 1024), h);
         }
         lds_barrier();
       }
@@ -1590,7 +1628,7 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
 #pragma unroll
       for (int i = 0; i < PJ_NC; ++i) {
         h8 xh, xl;
-        split_x3_step(y[i][0], xh, xl);
+        split_x3_step<PS>(y[i][0], xh, xl);
         mfma_x3(xh, xl, wpx[i][0], wpx[i][1], am, ac);
       }
       float* p = red0 + wave * 16 * RS;  // [wave][16 rows][RS]
@@ -1744,6 +1782,11 @@ bool persist_trace_built() { return false; }
 #endif
 bool persist_defer_ok(int nitems) { return nitems <= (PW - IW0) * PDEF_MAXIT; }
 
+static int persist_var(const PArgs& a) {
+  return (a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0)) | (a.attp_x3 ? 8 : 0);
+}
+bool persist_presplit(const PArgs& a) { return presplit_of(persist_var(a)); }
+
 void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
   TTS_CHECK(MT >= 1 && MT <= 4, "persistent decoder: MT must be in [1, 4]");
   TTS_CHECK(PJ_WG0 + a.ntj * (MT > 2 ? 4 : 2) <= PW && a.ntj >= 17, "persistent decoder: projection job count");
@@ -1754,7 +1797,7 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
   // (bit 2: Graves attention, exclusive of the others); bit 3: split-f16 P3 (attp_x3 given)
   TTS_CHECK(!a.attp_x3 || (a.x3flag && a.dec_x3 && a.apre_x3 && a.pj_x3),
             "persistent decoder: split-f16 weights incomplete or without a range flag");
-  const int var = (a.gK > 0 ? 4 : (a.win ? 1 : 0) | (a.fwd ? 2 : 0)) | (a.attp_x3 ? 8 : 0);
+  const int var = persist_var(a);
 #define PDK(mt, v) (const void*)persist_decoder_kernel<mt, v>
 #define PDK_ROW(mt) \
   {PDK(mt, 0), PDK(mt, 1), PDK(mt, 2), PDK(mt, 3), PDK(mt, 4), nullptr, nullptr, nullptr, PDK(mt, 8), PDK(mt, 9), \
