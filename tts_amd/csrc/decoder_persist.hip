@@ -77,21 +77,6 @@ constexpr bool presplit_of(int) { return false; }
 #else
 constexpr bool presplit_of(int VAR) { return VAR == 8; }
 #endif
-// stc_quad's pre-split form: lanes 4 q .. 4 q + 3 hold the 4 consecutive k of one row; lane 4 q
-// stores their hi halves then their lo halves (split_fast, as split8 on the consumer would)
-__device__ __forceinline__ void stc_quad_x3(float* base, int e, float v) {
-  _Float16 hi, lo;
-  split_fast(v, hi, lo);
-  const int p = (int)((unsigned)__builtin_bit_cast(unsigned short, hi) |
-                      ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16));
-  const unsigned p0 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0x00, 0xf, 0xf, true),
-                 p1 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0x55, 0xf, 0xf, true),
-                 p2 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0xAA, 0xf, 0xf, true),
-                 p3 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0xFF, 0xf, 0xf, true);
-  const f32x4 q = {__uint_as_float((p0 & 0xffffu) | (p1 << 16)), __uint_as_float((p2 & 0xffffu) | (p3 << 16)),
-                   __uint_as_float((p0 >> 16) | (p1 & 0xffff0000u)), __uint_as_float((p2 >> 16) | (p3 & 0xffff0000u))};
-  if ((threadIdx.x & 3) == 0) stc4(base, e * 4, q);
-}
 template <bool PS>
 __device__ __forceinline__ void stc_quad_h(float* base, int e, float v) {
   if constexpr (PS) stc_quad_x3(base, e, v);

@@ -199,10 +199,10 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
       for (int k = 0; k < KSW; ++k)
 #pragma unroll
         for (int mt = 0; mt < MT; ++mt) {
-          const float v[8] = {x[k][mt][0][0], x[k][mt][0][1], x[k][mt][0][2], x[k][mt][0][3],
-                              x[k][mt][1][0], x[k][mt][1][1], x[k][mt][1][2], x[k][mt][1][3]};
-          h8 xh, xl;
-          split8(v, xh, xl);
+          // h was published pre-split (stc_quad_x3): k 0..3 as [hi | lo] in x[..][0], k 4..7 in x[..][1]
+          const f32x4 &a = x[k][mt][0], &b = x[k][mt][1];
+          const h8 xh = __builtin_bit_cast(h8, (f32x4{a[0], a[1], b[0], b[1]}));
+          const h8 xl = __builtin_bit_cast(h8, (f32x4{a[2], a[3], b[2], b[3]}));
           mfma_x3(xh, xl, wx[k][0], wx[k][1], am[mt], ac[mt]);
         }
 #pragma unroll
@@ -240,7 +240,9 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
       }
       cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
       const float hn = sigm_f(pre[3]) * tanh_f(cst);
-      stc_quad(ho, (int)frag_idx(m, tl * 4 + u, H), hn);  // lanes u = 0..3 of a quad: one 16-byte store
+      // lanes u = 0..3 of a quad: one 16-byte store (split-f16: pre-split, the consumers' MFMA operands)
+      if constexpr (X3) stc_quad_x3(ho, (int)frag_idx(m, tl * 4 + u, H), hn);
+      else stc_quad(ho, (int)frag_idx(m, tl * 4 + u, H), hn);
       out[((long)ma * T_max + t) * O + dir * H + tl * 4 + u] = hn;
     }
     if (step + 1 < T_max) {  // directions and row groups are independent: one barrier each

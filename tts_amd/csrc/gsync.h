@@ -28,6 +28,7 @@
 // by another queue on the same GPU does not trip it.
 #pragma once
 #include "common.h"
+#include "split16.h"
 
 #include <cstdlib>
 #include <map>
@@ -139,6 +140,22 @@ __device__ __forceinline__ void stc_quad(float* base, int e, float v) {
                    __int_as_float(__builtin_amdgcn_mov_dpp(b, 0xFF, 0xf, 0xf, true))};  // (3,3,3,3)
   if ((threadIdx.x & 3) == 0) stc4(base, e * 4, q);
 #endif
+}
+// stc_quad's pre-split form (the persistent decoder's and the BiLSTM's split-f16 hand-offs): lanes
+// 4 q .. 4 q + 3 hold 4 consecutive k of one row; lane 4 q stores their f16 hi halves then their lo
+// halves, [hi 0..3 | lo 0..3] in the 16 bytes (split_fast: the bits split8 on the consumer gives)
+__device__ __forceinline__ void stc_quad_x3(float* base, int e, float v) {
+  _Float16 hi, lo;
+  split_fast(v, hi, lo);
+  const int p = (int)((unsigned)__builtin_bit_cast(unsigned short, hi) |
+                      ((unsigned)__builtin_bit_cast(unsigned short, lo) << 16));
+  const unsigned p0 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0x00, 0xf, 0xf, true),
+                 p1 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0x55, 0xf, 0xf, true),
+                 p2 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0xAA, 0xf, 0xf, true),
+                 p3 = (unsigned)__builtin_amdgcn_mov_dpp(p, 0xFF, 0xf, 0xf, true);
+  const f32x4 q = {__uint_as_float((p0 & 0xffffu) | (p1 << 16)), __uint_as_float((p2 & 0xffffu) | (p3 << 16)),
+                   __uint_as_float((p0 >> 16) | (p1 & 0xffff0000u)), __uint_as_float((p2 >> 16) | (p3 & 0xffff0000u))};
+  if ((threadIdx.x & 3) == 0) stc4(base, e * 4, q);
 }
 
 // LDS-only workgroup barrier: unlike __syncthreads() (whose workgroup-scope fences wait for every
