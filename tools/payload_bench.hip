@@ -8,6 +8,8 @@
 //   mode 2: barriers and rewrites only
 //   mode 3: the fp32 block's bytes published pre-split ([hi 4 | lo 4] per 16 bytes): the f16 MFMA
 //           operands come straight from the loads, no split on the consumer
+//   mode 4: as 3 with the halves laid out so that each 16-byte load is one whole operand (the hi
+//           of 8 k in one slot, their lo in the other): no operand moves either
 // Not part of the library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/payload_bench.hip -o tools/payload_bench
 #include "../tts_amd/csrc/gsync.h"
@@ -41,6 +43,12 @@ __global__ __launch_bounds__(512) void payload_kernel(unsigned* bar, float* act,
 #pragma unroll
       for (int k = 0; k < NKS; ++k) {
         if (k + 1 < NKS) ld(x[(k + 1) & 1], k + 1);
+        if constexpr (MODE == 4) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h)
+            mfma_x3(wh, wl, __builtin_bit_cast(h8, x[k & 1][2 * h]), __builtin_bit_cast(h8, x[k & 1][2 * h + 1]), am, ac);
+          continue;
+        }
         if constexpr (MODE == 3) {
 #pragma unroll
           for (int h = 0; h < 2; ++h) {
@@ -105,14 +113,14 @@ int main(int argc, char** argv) {
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   const void* ks[] = {(const void*)payload_kernel<0>, (const void*)payload_kernel<1>, (const void*)payload_kernel<2>,
-                      (const void*)payload_kernel<3>};
+                      (const void*)payload_kernel<3>, (const void*)payload_kernel<4>};
   const char* names[] = {"fp32 payload (192 KB)", "24-bit payload (144 KB) + unpack", "barriers + rewrites only",
-                         "pre-split payload (192 KB, no consumer split)"};
+                         "pre-split payload (192 KB, no consumer split)", "pre-split, whole-operand slots (no moves)"};
   // the fastest of 4 barrier-block placements, then 2 passes over the modes
   int best_slot = 0;
   float best_t = 1e30f;
   for (int pass = 0; pass < 3; ++pass)
-    for (int m = (pass == 0 ? 2 : 0); m < 4; ++m) {
+    for (int m = (pass == 0 ? 2 : 0); m < 5; ++m) {
       for (int slot = 0; slot < (pass == 0 ? 4 : 1); ++slot) {
         unsigned* bar = pool + (pass == 0 ? slot : best_slot) * BAR_WORDS;
         float best = 1e30f;
