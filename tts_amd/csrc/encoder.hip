@@ -348,7 +348,7 @@ void launch_bilstm(const float* Gin, const float* Whh, const int* lens, int T_ma
 // combine through LDS; thread (m, unit) keeps the cell state. Split-f16 only (|h| <= 1, weights
 // range-checked at pack time), B <= 16.
 //   w16  : per layer [192 m-tiles][NKS k-steps][64][16] (split16.h pack_split_a), NKS = 24 / 48
-//   hbuf : [2 ping-pong][nl][16 x 768] fragment order (zeroed by the launcher)
+//   hbuf : [2 ping-pong][nl][16 x 768] fragment order, pre-split (stc_quad_x3; zeroed by the launcher)
 //   out  : (B, T_max, 768), the last layer's h
 struct GePipeArgs {
   const uint16_t* w16[4];
@@ -433,10 +433,9 @@ __global__ __launch_bounds__(64 * GP_NW) void ge2e_pipe_kernel(GePipeArgs a) {
 #pragma unroll
       for (int j = 0; j < 6; ++j)
         if (j < KS) {
-          const float v[8] = {x[j][0][0], x[j][0][1], x[j][0][2], x[j][0][3],
-                              x[j][1][0], x[j][1][1], x[j][1][2], x[j][1][3]};
-          h8 xh, xl;
-          split8(v, xh, xl);
+          // published pre-split (stc_quad_x3): k 0..3 as [hi | lo] in x[j][0], k 4..7 in x[j][1]
+          const h8 xh = __builtin_bit_cast(h8, (f32x4{x[j][0][0], x[j][0][1], x[j][1][0], x[j][1][1]}));
+          const h8 xl = __builtin_bit_cast(h8, (f32x4{x[j][0][2], x[j][0][3], x[j][1][2], x[j][1][3]}));
 #pragma unroll
           for (int mi = 0; mi < 3; ++mi) mfma_x3(xh, xl, w[j][mi][0], w[j][mi][1], am[mi], ac[mi]);
         }
@@ -459,7 +458,7 @@ __global__ __launch_bounds__(64 * GP_NW) void ge2e_pipe_kernel(GePipeArgs a) {
         cst = sigm_f(pre[1]) * cst + sigm_f(pre[0]) * tanh_f(pre[2]);
         const float hn = sigm_f(pre[3]) * tanh_f(cst);
         float* ho = a.hbuf + ((size_t)((s + 1) & 1) * a.nl + l) * slab;
-        stc_quad(ho, (int)frag_idx(m, unit, H), hn);  // a quad = 4 units of one row: one 16-byte store
+        stc_quad_x3(ho, (int)frag_idx(m, unit, H), hn);  // a quad = 4 units of one row: one 16-byte store, pre-split
         if (l == a.nl - 1) a.out[((long)m * a.T_max + t) * H + unit] = hn;
       }
     }
