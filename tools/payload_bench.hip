@@ -10,6 +10,8 @@
 //           operands come straight from the loads, no split on the consumer
 //   mode 4: as 3 with the halves laid out so that each 16-byte load is one whole operand (the hi
 //           of 8 k in one slot, their lo in the other): no operand moves either
+//   mode 5: mode 3's layout read with 8-byte loads straight into the operand halves (hi of k 0..3
+//           and of k 4..7 into one operand, their lo into the other): no moves, twice the loads
 // Not part of the library:
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 tools/payload_bench.hip -o tools/payload_bench
 #include "../tts_amd/csrc/gsync.h"
@@ -39,10 +41,39 @@ __global__ __launch_bounds__(512) void payload_kernel(unsigned* bar, float* act,
 #pragma unroll
         for (int j = 0; j < NLD; ++j) d[j] = ldc4(act, wave * NKS * STEP + k * STEP + (j * 64 + lane) * 16);
       };
-      ld(x[0], 0);
+      // mode 5: y[buf][2 h] = hi operand, y[buf][2 h + 1] = lo operand of pair h, from 8-byte loads
+      f32x4 y[2][NLD];
+      auto ld5 = [&](f32x4 (&d)[NLD], int k) {
+#pragma unroll
+        for (int h = 0; h < 2; ++h) {
+          const int o0 = wave * NKS * STEP + k * STEP + ((2 * h) * 64 + lane) * 16;
+          const int o1 = wave * NKS * STEP + k * STEP + ((2 * h + 1) * 64 + lane) * 16;
+          const __amdgpu_buffer_rsrc_t r = __builtin_amdgcn_make_buffer_rsrc((void*)act, 0, 0x7fffffff, 0x00020000);
+          typedef unsigned u2 __attribute__((ext_vector_type(2)));
+          const u2 a0 = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(r, o0, 0, 16));
+          const u2 b0 = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(r, o1, 0, 16));
+          const u2 a1 = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(r, o0 + 8, 0, 16));
+          const u2 b1 = __builtin_bit_cast(u2, __builtin_amdgcn_raw_buffer_load_b64(r, o1 + 8, 0, 16));
+          d[2 * h] = f32x4{__uint_as_float(a0[0]), __uint_as_float(a0[1]), __uint_as_float(b0[0]), __uint_as_float(b0[1])};
+          d[2 * h + 1] = f32x4{__uint_as_float(a1[0]), __uint_as_float(a1[1]), __uint_as_float(b1[0]), __uint_as_float(b1[1])};
+        }
+      };
+      if constexpr (MODE == 5) ld5(y[0], 0);
+      else ld(x[0], 0);
 #pragma unroll
       for (int k = 0; k < NKS; ++k) {
-        if (k + 1 < NKS) ld(x[(k + 1) & 1], k + 1);
+        if (k + 1 < NKS) {
+          if constexpr (MODE == 5) ld5(y[(k + 1) & 1], k + 1);
+          else ld(x[(k + 1) & 1], k + 1);
+        }
+        if constexpr (MODE == 5) {
+#pragma unroll
+          for (int h = 0; h < 2; ++h) {
+            const f32x4 a = y[k & 1][2 * h], b = y[k & 1][2 * h + 1];
+            mfma_x3(wh, wl, __builtin_bit_cast(h8, a), __builtin_bit_cast(h8, b), am, ac);
+          }
+          continue;
+        }
         if constexpr (MODE == 4) {
 #pragma unroll
           for (int h = 0; h < 2; ++h)
@@ -113,14 +144,16 @@ int main(int argc, char** argv) {
   HIP_OK(hipEventCreate(&e0));
   HIP_OK(hipEventCreate(&e1));
   const void* ks[] = {(const void*)payload_kernel<0>, (const void*)payload_kernel<1>, (const void*)payload_kernel<2>,
-                      (const void*)payload_kernel<3>, (const void*)payload_kernel<4>};
+                      (const void*)payload_kernel<3>, (const void*)payload_kernel<4>,
+                      (const void*)payload_kernel<5>};
   const char* names[] = {"fp32 payload (192 KB)", "24-bit payload (144 KB) + unpack", "barriers + rewrites only",
-                         "pre-split payload (192 KB, no consumer split)", "pre-split, whole-operand slots (no moves)"};
+                         "pre-split payload (192 KB, no consumer split)", "pre-split, whole-operand slots (no moves)",
+                         "pre-split, 8-byte loads into the operands (no moves)"};
   // the fastest of 4 barrier-block placements, then 2 passes over the modes
   int best_slot = 0;
   float best_t = 1e30f;
   for (int pass = 0; pass < 3; ++pass)
-    for (int m = (pass == 0 ? 2 : 0); m < 5; ++m) {
+    for (int m = (pass == 0 ? 2 : 0); m < 6; ++m) {
       for (int slot = 0; slot < (pass == 0 ? 4 : 1); ++slot) {
         unsigned* bar = pool + (pass == 0 ? slot : best_slot) * BAR_WORDS;
         float best = 1e30f;
