@@ -10,7 +10,9 @@ pipeline over all ranks, ids and waveforms resident in HBM (r = 2). Extra fields
 Tacotron2-only frames/s, end-to-end RTF, ``e2e_rtf_host`` (ids on the host -> per-utterance
 waveforms on the host), the r = 1 run (``r1``), and ``roofline.pipeline_frac`` =
 SURVEY 8d's whole-pipeline bound / measured.
-Launch for N > 1: python -m torch.distributed.run --nproc-per-node N bench.py --gpus N
+Launch for N > 1: ``python bench.py --gpus N`` starts N ranks itself (torch.distributed.run as a
+child process, before any GPU call; launch_plan), or run it as the ranks of
+``python -m torch.distributed.run --nproc-per-node N bench.py --gpus N`` (WORLD_SIZE must equal N).
 """
 
 import argparse
@@ -221,7 +223,38 @@ def bench_config(world, per_gpu_batch, r):
             "global_batch": per_gpu_batch * world, "r": r, "parallelism": f"replicas x{world}"}
 
 
-def main():
+def free_port():
+    import socket
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s_:
+        s_.bind(("127.0.0.1", 0))
+        return s_.getsockname()[1]
+
+
+def launch_plan(gpus, env, argv):
+    """What ``python bench.py --gpus N`` must do before anything touches a GPU (one process per GPU,
+    as TTS/bin/distribute.py:41-65 starts one training process per GPU):
+    * no WORLD_SIZE and N > 1: start N ranks under torch.distributed.run as a CHILD process (never
+      exec) with the same arguments, and exit with its return code -> returns that command;
+    * WORLD_SIZE set (already a rank of a launcher) and equal to N, or N == 1 with no WORLD_SIZE:
+      run in this process -> returns None;
+    * WORLD_SIZE set and different from N: refused (SystemExit with a message, status 2)."""
+    ws = env.get("WORLD_SIZE")
+    if ws is not None:
+        if int(ws) != gpus:
+            raise SystemExit(f"bench.py: --gpus {gpus} but WORLD_SIZE={ws}; launch N ranks with "
+                             f"--gpus N (or drop --gpus and let bench.py start them)")
+        return None
+    if gpus < 1:
+        raise SystemExit(f"bench.py: --gpus must be >= 1 (got {gpus})")
+    if gpus == 1:
+        return None
+    return [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={gpus}",
+            "--master-addr", "127.0.0.1", "--master-port", str(env.get("MASTER_PORT") or free_port()),
+            os.path.abspath(__file__)] + list(argv)
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=5)
@@ -233,11 +266,24 @@ def main():
     ap.add_argument("--kernel-iters", type=int, default=50)
     ap.add_argument("--f32-steps", type=int, default=3, help="steps re-timed with fp32-MFMA GEMMs only (0: skip)")
     ap.add_argument("--r1-steps", type=int, default=3, help="steps timed at r=1 as extra fields (0: skip)")
-    args = ap.parse_args()
+    ap.add_argument("--plan-only", action="store_true",
+                    help="print this rank's shard of the global batch as one JSON line and exit (no GPU)")
+    args = ap.parse_args(argv)
+
+    # before any torch.cuda call (not even device_count): become the launcher of N ranks if asked
+    cmd = launch_plan(args.gpus, os.environ, argv)
+    if cmd is not None:
+        import subprocess
+        return subprocess.call(cmd)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.plan_only:
+        mine, my_T, _, _ = rank_shard(world, rank, args.per_gpu_batch, args.r)
+        print(json.dumps({"rank": rank, "world": world, "local_rank": local, "shard": [int(i) for i in mine],
+                          "tokens": [int(t_) for t_ in my_T]}), flush=True)
+        return 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
@@ -461,6 +507,7 @@ def main():
         "value": round(value, 1),
         "unit": "mel-frames/s",
         "n_gpus": world,
+        "rccl_world": dist.get_world_size() if world > 1 else 1,
         "steps": args.steps,
         "warmup": args.warmup,
         "ms_per_step": round(ms_step, 3),
@@ -494,7 +541,8 @@ def main():
     if world > 1:
         dist.barrier()
         dist.destroy_process_group()
+    return 0
 
 
 if __name__ == "__main__":
-    main()
+    sys.exit(main())

@@ -175,6 +175,50 @@ def test_bench_multi_rank_shards_and_aggregation(world):
         assert cfg["workload"].startswith("C3")
 
 
+def test_bench_launch_decision():
+    """`python bench.py --gpus N` (the driver's command form): with no WORLD_SIZE and N > 1 it
+    becomes the launcher of N ranks (torch.distributed.run as a child, same arguments); inside a
+    launcher's rank it runs itself; a WORLD_SIZE that differs from --gpus is refused."""
+    import sys
+    sys.path.insert(0, ROOT)
+    import bench
+    argv = ["--gpus", "2", "--steps", "3", "--no-cpu-baseline"]
+    cmd = bench.launch_plan(2, {}, argv)
+    assert cmd[:3] == [sys.executable, "-m", "torch.distributed.run"]
+    assert "--nproc-per-node=2" in cmd and cmd[cmd.index("--master-addr") + 1] == "127.0.0.1"
+    assert cmd[-len(argv) - 1] == os.path.join(ROOT, "bench.py") and cmd[-len(argv):] == argv
+    assert bench.launch_plan(2, {"MASTER_PORT": "29511"}, argv)[cmd.index("--master-port") + 1] == "29511"
+    assert bench.launch_plan(1, {}, ["--gpus", "1"]) is None
+    assert bench.launch_plan(8, {"WORLD_SIZE": "8"}, argv) is None
+    assert bench.launch_plan(1, {"WORLD_SIZE": "1"}, argv) is None
+    with pytest.raises(SystemExit, match="WORLD_SIZE=4"):
+        bench.launch_plan(2, {"WORLD_SIZE": "4"}, argv)
+    with pytest.raises(SystemExit):
+        bench.launch_plan(0, {}, argv)
+
+
+def test_bench_gpus_2_starts_two_ranks_plan_only():
+    """End to end on the CPU: `python bench.py --gpus 2 --plan-only` from a process with no
+    WORLD_SIZE starts two ranks under torch.distributed.run; each prints its own shard of the
+    64-utterance C3 batch before touching a GPU, and the shards partition it."""
+    import json
+    import subprocess
+    import sys
+    env = {k: v for k, v in os.environ.items() if k not in ("WORLD_SIZE", "RANK", "LOCAL_RANK", "MASTER_PORT")}
+    env["OMP_NUM_THREADS"] = "1"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plan-only"],
+                         env=env, capture_output=True, text=True, timeout=600)
+    assert out.returncode == 0, out.stderr[-2000:]
+    lines = [json.loads(ln) for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert sorted(d["rank"] for d in lines) == [0, 1] and all(d["world"] == 2 for d in lines)
+    assert sorted(i for d in lines for i in d["shard"]) == list(range(64))
+    # a mismatched launcher is refused with a nonzero status
+    env["WORLD_SIZE"] = "3"
+    bad = subprocess.run([sys.executable, os.path.join(ROOT, "bench.py"), "--gpus", "2", "--plan-only"],
+                         env=env, capture_output=True, text=True, timeout=600)
+    assert bad.returncode != 0 and "WORLD_SIZE=3" in bad.stderr
+
+
 def _pool_factory(seed, device):
     """GpuPool stand-in runner for the CPU suite: the oracle decode, tagged with the worker's device."""
     import sys
