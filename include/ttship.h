@@ -124,7 +124,11 @@ int tts_taco_postnet(tts_ctx* ctx, const float* d_dec, const int32_t* h_lens, in
    (B, T_max). Rows that stopped before the call's last step hold the state the batched decode left
    in them, not their own final state: compare rows that ran the call's full step count. Any output
    pointer may be NULL (skipped). B and T_max size the caller's buffers and must equal the last
-   decode's batch and encoder length (an error otherwise, nothing written). */
+   decode's batch and encoder length (an error otherwise, nothing written). In split-f16 mode
+   (tts_set_gemm_mode 1) the persistent decoder publishes attention_rnn h, decoder_rnn h and the
+   context pre-split as f16 hi / lo halves; those three outputs are rebuilt as hi + 2^-11 lo, the
+   value the next step's GEMMs consume (about 22 significant bits, within ~2^-22 relative of the
+   fp32 value), not the unrounded fp32 state. The cell states and attention weights are fp32. */
 int tts_taco_decoder_state(tts_ctx* ctx, int B, int T_max, float* d_att_h, float* d_att_c, float* d_dec_h,
                            float* d_dec_c, float* d_context, float* d_alpha, float* d_alpha_cum, void* stream);
 
@@ -222,6 +226,11 @@ int tts_decoder_stats(tts_ctx* ctx, int* path, int* nlaunch, float* ms, int* ste
    how many calls fell back to fp32. */
 int tts_set_gemm_mode(tts_ctx* ctx, int mode);
 int tts_gemm_mode(tts_ctx* ctx, int* mode, int64_t* fallbacks);
+
+/* Test hook (process-wide, off by default): recurrence >= 0 makes one workgroup of that persistent
+   BiLSTM recurrence leave before its second grid barrier, so the others time out and the next
+   Tacotron2 call reports the encoder barrier error; -1 turns it off. Only tests call it. */
+int tts_test_stall_lstm(int recurrence);
 
 #ifdef __cplusplus
 }

@@ -336,7 +336,7 @@ def test_bilstm_row_group_barrier_timeout_raises(monkeypatch):
     """A grid-barrier timeout in the BiLSTM's second row group (recurrence 3: row group 1, backward;
     B = 32 runs 2 row groups x 2 directions) is reported by the Tacotron2 call's status read-back:
     the call raises instead of returning mels built from a half-written encoder output.
-    The test hook TTS_TEST_STALL_LSTM makes one workgroup of that recurrence leave before its second
+    The test hook tts_test_stall_lstm (a C-ABI call, no environment variable) makes one workgroup of that recurrence leave before its second
     barrier. The next call, without the hook, is correct again."""
     from oracle.taco_np import TacoOracle
     from tts_amd.spec import TacotronConfig
@@ -351,10 +351,14 @@ def test_bilstm_row_group_barrier_timeout_raises(monkeypatch):
     for i, L in enumerate(lens):
         batch[i, :L] = rs.randint(1, 129, size=L)
     x = torch.from_numpy(batch).cuda()
-    monkeypatch.setenv("TTS_TEST_STALL_LSTM", "3")
-    with pytest.raises(RuntimeError, match="persistent BiLSTM: grid barrier timed out"):
-        m.inference(x, text_lengths=[int(L) for L in lens], max_decoder_steps=3)
-    monkeypatch.delenv("TTS_TEST_STALL_LSTM")
+    from tts_amd._lib import load_library
+    lib = load_library()
+    lib.tts_test_stall_lstm(3)
+    try:
+        with pytest.raises(RuntimeError, match="persistent BiLSTM: grid barrier timed out"):
+            m.inference(x, text_lengths=[int(L) for L in lens], max_decoder_steps=3)
+    finally:
+        lib.tts_test_stall_lstm(-1)
     dec, post, align, stop = m.inference(x, text_lengths=[int(L) for L in lens], max_decoder_steps=3)
     post = post.cpu().numpy()
     orc = TacoOracle(sd, cfg.attn_norm, cfg.r)
@@ -1625,6 +1629,58 @@ def test_bench_workload_full_size_vs_oracle():
     print(f"32 utterances, worst mel error {worst:.2e}, worst waveform error {worst_w:.2e}")
 
 
+def test_bench_workload_full_size_r1_vs_oracle():
+    """The bench line's r = 1 run at its full length (bench.py `r1`: the same 32 LJ-profile
+    utterances, forced lengths of up to 857 decoder steps, one frame per step as the
+    Decoder.inference loop of layers/tacotron2.py:354-369 runs it at r = 1), every utterance against
+    the oracle at B = 1: mel L-inf within 1e-4 (north_star), every step's alignment argmax identical,
+    and the two longest rows' MB-MelGAN waveforms (from the bench's batched vocoder call) within
+    WAV_TOL of the oracle chain."""
+    import bench
+    from oracle.melgan_np import MelganOracle
+    from oracle.taco_np import TacoOracle
+    from tts_amd.pqmf import pqmf_filters
+    from tts_amd.spec import melgan_layers
+    from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids
+    dev = _dev()
+    taco, tsd, voc, vsd, tcfg, vcfg = bench.build_models(dev)
+    r = 1
+    taco.decoder.set_r(r)
+    taco.decoder.verbose = False
+    T_prof, M_prof = lj_profile()
+    ids = synthetic_ids(T_prof)
+    steps = forced_steps(M_prof, r)
+    assert max(steps) >= 850
+    batch, lens = pad_batch(ids)
+    with torch.no_grad():
+        _, post, align, _ = taco.inference(torch.from_numpy(batch).to(dev), text_lengths=lens,
+                                           max_decoder_steps=steps)
+        assert list(taco.last_steps) == list(steps)
+        wavb = voc.inference(post.transpose(1, 2), lengths=taco.last_mel_lengths).cpu().numpy()
+    taco.decoder.set_r(tcfg.r)
+    post, align = post.cpu().numpy(), align.cpu().numpy()
+    to = TacoOracle(tsd, tcfg.attn_norm, tcfg.r)
+    longest = set(np.argsort(steps)[-2:].tolist())
+    vo = MelganOracle(vsd, melgan_layers(vcfg), pqmf_filters()[1])
+    worst = worst_w = 0.0
+    for i in range(len(ids)):
+        L, S = len(ids[i]), steps[i]
+        _, p, a, _ = to.inference(ids[i], r, S)
+        assert p.shape[0] == S
+        err = float(np.abs(post[i, :S] - p).max())
+        worst = max(worst, err)
+        assert err <= MEL_TOL, (i, L, S, err)
+        assert (align[i, :S, :L].argmax(1) == a.argmax(1)).all(), i
+        if i in longest:
+            ref = vo.inference(p.T, pad=0).reshape(-1)
+            werr = float(np.abs(wavb[i, 0, :ref.size] - ref).max())
+            worst_w = max(worst_w, werr)
+            assert werr <= WAV_TOL, (i, werr)
+            assert not wavb[i, 0, ref.size:].any(), i
+    print(f"r=1, 32 utterances ({sum(steps)} row-steps, {max(steps)} max), worst mel error {worst:.2e}, "
+          f"worst waveform error (2 longest) {worst_w:.2e}")
+
+
 def test_glow_lj_batch_full_size_vs_oracle():
     """Glow-TTS on tools/glow_bench.py's workload at full size (32 LJ-profile utterances, 3346
     tokens, ~19 k frames, seed-3 weights), every utterance against the oracle at B = 1: y_lengths and
@@ -1819,6 +1875,11 @@ def test_c4_glow_pwgan_batch64_vs_oracle():
     ref_np = PwganOracle(psd, pcfg).inference(rows_mel[i0], rows_noise[i0])
     ref_cpu = PwganTorchCPU(psd, pcfg).inference(rows_mel[i0], rows_noise[i0])
     assert np.abs(refs[i0] - ref_np).max() <= 2e-6 and np.abs(refs[i0] - ref_cpu).max() <= 2e-6
+    # the longest row (the persistent kernel's last tiles) against the same reference on the CPU
+    i1 = int(order[-1])
+    ref_cpu1 = PwganTorchCPU(psd, pcfg).inference(rows_mel[i1], rows_noise[i1])
+    assert np.abs(refs[i1] - ref_cpu1).max() <= 2e-6
+    assert np.abs(wav[i1, 0, :mlens[i1] * 256] - ref_cpu1).max() <= WAV_TOL
     worst_w, wrow = 0.0, -1
     for i in range(B):
         n = mlens[i] * 256

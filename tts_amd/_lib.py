@@ -71,6 +71,7 @@ SIGNATURES = [
     ("tts_time_decoder_kernel", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, _c_f_p]),
     ("tts_decoder_stats", ctypes.c_int, [_vp, _c_i_p, _c_i_p, _c_f_p, _c_i_p]),
     ("tts_set_gemm_mode", ctypes.c_int, [_vp, ctypes.c_int]),
+    ("tts_test_stall_lstm", ctypes.c_int, [ctypes.c_int]),
     ("tts_gemm_mode", ctypes.c_int, [_vp, _c_i_p, _c_i64_p]),
 ]
 

@@ -352,10 +352,12 @@ struct TacoWS {
   // picked once per allocation (pick_barrier_blocks)
   int pslot[PMAX_LAUNCH] = {0, 1, 2, 3};
   const void* pslot_base = nullptr;
+  bool pslot_cal = false;      // pslot timed (after enter(), on the first persistent decode of these blocks)
   DevBuf anorm;                // persistent decoder: per-utterance attention normaliser (deferred alignment)
   DevBuf spk, spkid, spkb;     // speaker vectors (decode order), per-row biases [Bp][NSPK]
   DevBuf win_idx, fwd_u, apf;  // windowing argmax, transition probability, forward chunk sums
   DevBuf gh, gmu;              // Graves: N_a hidden (32 x 1024), mixture means (64 x 16)
+  DevBuf trace, xdiag;         // TTS_PTRACE / TTS_DIAG_XCC diagnostics, on this context's device
   bool enc_persist = false;    // the last encoder ran the persistent BiLSTM (lc = its barrier words)
   int enc_ndom = 0;            // its recurrences (directions x row groups), one barrier block each
   // one CHUNK-step graph per batch-tile count MT' <= MT (the batch tile shrinks as the
@@ -903,9 +905,10 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<int>(W.stat, 256, g);
   grow<float>(W.ypart, (size_t)2 * 64 * (1 + 5 * c->taco.r_init + 16) * 16, g);
   grow<unsigned>(W.pbar, PBAR_CAND * BAR_WORDS, g);  // candidate barrier blocks, one picked per launch (MT = 4 .. 1)
-  if (W.pslot_base != W.pbar.p && persist_supported(c->device)) {
-    pick_barrier_blocks(reinterpret_cast<unsigned*>(W.pbar.p), PBAR_CAND, PMAX_LAUNCH, W.pslot, c->s);
+  if (W.pslot_base != W.pbar.p) {  // new candidate blocks: calibrated lazily by the first persistent decode
+    for (int i = 0; i < PMAX_LAUNCH; ++i) W.pslot[i] = i;
     W.pslot_base = W.pbar.p;
+    W.pslot_cal = false;
   }
   grow<float>(W.anorm, (size_t)2 * BMAX, g);
   grow<float>(W.spk, (size_t)64 * 1024, g);
@@ -1500,7 +1503,7 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   a.thr = thr;
   a.bar = reinterpret_cast<unsigned*>(W.pbar.p);
   // TTS_PTRACE=<file>: phase timestamps of 8 steps from step TTS_PTRACE_T0 (default 100)
-  static DevBuf trace_buf;
+  DevBuf& trace_buf = W.trace;
   const char* tr = std::getenv("TTS_PTRACE");
   TTS_CHECK(!tr || persist_trace_built(), "TTS_PTRACE needs a library built with -DTTS_PHASE_TRACE "
                                           "(tools/build_variants.sh trace -DTTS_PHASE_TRACE; TTSHIP_LIB=tools/var/lib_trace.so)");
@@ -1520,7 +1523,7 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   unsigned long long* const trace_p = a.trace;
   unsigned long long* const atrace_p = a.atrace;
   static const bool xdiag = std::getenv("TTS_DIAG_XCC") != nullptr;
-  static DevBuf xdiag_buf;
+  DevBuf& xdiag_buf = W.xdiag;
   if (xdiag) xdiag_buf.ensure((size_t)PMAX_LAUNCH * 256 * 4);
   HIP_OK(hipEventRecord(c->ev_dec[0], s));
   c->dec_nlaunch = 0;
@@ -1647,6 +1650,10 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   // decoder state
   const int Bp = W.MT * 16;
   const bool persist = use_persistent(c);
+  if (persist && !W.pslot_cal) {  // ordered after the caller's work (enter above) and this call's encoder
+    pick_barrier_blocks(reinterpret_cast<unsigned*>(W.pbar.p), PBAR_CAND, PMAX_LAUNCH, W.pslot, s);
+    W.pslot_cal = true;
+  }
   {
     FillList f;  // decoder state and outputs zeroed in one launch (the postnet output too)
     f.add(W.catt.p, (size_t)Bp * 1024 * 4);
@@ -3487,6 +3494,11 @@ int tts_set_gemm_mode(tts_ctx* c, int mode) {
     TTS_CHECK(mode == 0 || mode == 1, "gemm mode must be 0 (fp32) or 1 (split-f16)");
     c->gemm_x3 = mode == 1;
   });
+}
+
+int tts_test_stall_lstm(int recurrence) {
+  g_test_stall_lstm.store(recurrence < 0 ? -1 : recurrence);
+  return 0;
 }
 
 int tts_gemm_mode(tts_ctx* c, int* mode, int64_t* fallbacks) {

@@ -1,6 +1,7 @@
 // Shared definitions for the ttship HIP library (gfx950 / CDNA4 only).
 #pragma once
 #include <hip/hip_runtime.h>
+#include <atomic>
 #include <cstdint>
 #include <mutex>
 #include <set>
@@ -253,3 +254,6 @@ void launch_out_conv1(const float* x, long xb, long xc, int C, const float* W, c
 bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, const float* bo, const float* G,
                      int N, int taps, const int* lens, int len_add, int L_mul, int maxL, int B, float* y, long yb,
                      hipStream_t s);
+// test hook of the persistent BiLSTM (tts_test_stall_lstm): recurrence to stall, -1 = off
+extern std::atomic<int> g_test_stall_lstm;
+

@@ -170,7 +170,7 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
 #pragma unroll
   for (int q = 0; q < 4; ++q) gin[q] = gbase[(long)tpos(0) * G + q * 4];
   for (int step = 0; step < T_max; ++step) {
-    // test hook (TTS_TEST_STALL_LSTM=<recurrence>): one workgroup of that recurrence leaves before
+    // test hook (tts_test_stall_lstm(<recurrence>)): one workgroup of that recurrence leaves before
     // its second barrier, so the others time out and set that recurrence's error word
     if (step == 1 && dom == stall && tl == 0) return;
     const float* hi = hbuf + (size_t)(step & 1) * RG * NDIR * Bp * H + (long)dom * Bp * H;
@@ -269,6 +269,8 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
 
 // returns the number of recurrences launched (row groups x directions, each with its own barrier
 // block), 0 when a cooperative launch is unavailable
+std::atomic<int> g_test_stall_lstm{-1};
+
 template <int H, int NDIR>
 static int launch_lstm_persist_t(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
                                  int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
@@ -287,8 +289,7 @@ static int launch_lstm_persist_t(const float* Gin, const float* Whh, const uint1
   const int MT = MT0 / RG, Bp = MT * 16;
   HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * RG * NDIR * Bp * H * 4, s));
   arm_barrier(bar, RG * NDIR, s);
-  const char* st = std::getenv("TTS_TEST_STALL_LSTM");
-  int stall = st ? std::atoi(st) : -1;
+  int stall = g_test_stall_lstm.load();  // test hook (tts_test_stall_lstm), -1 in production
   void* args[] = {(void*)&Whh, (void*)&Whh16, (void*)&Gin, (void*)&lens, (void*)&T_max,
                   (void*)&B,   (void*)&hbuf,  (void*)&out, (void*)&bar, (void*)&stall};
 #define LPK(mt, x) (const void*)lstm_persist_kernel<mt, H, NDIR, x>
