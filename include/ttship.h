@@ -23,6 +23,8 @@
  *   tts_melgan_infer_strided      <- the same on a (B, M, C) tensor viewed as (B, C, M) (no transposed copy)
  *   tts_melgan_generator          <- MelganGenerator.layers(c) (melgan_generator.py:28-81)
  *   tts_pqmf_synthesis            <- PQMF.synthesis (TTS/vocoder/layers/pqmf.py:51-56)
+ *   tts_taco_mbmelgan_infer       <- Tacotron2.inference then MultibandMelganGenerator.inference on its
+ *                                    postnet output (TTS/server/synthesizer.py:150-159), one call
  *
  * Conventions: every function returns 0 on success and nonzero on failure; the message is
  * available from tts_last_error() (thread-local). Pointers prefixed d_ are device (HIP) memory
@@ -226,6 +228,22 @@ int tts_decoder_stats(tts_ctx* ctx, int* path, int* nlaunch, float* ms, int* ste
    how many calls fell back to fp32. */
 int tts_set_gemm_mode(tts_ctx* ctx, int mode);
 int tts_gemm_mode(tts_ctx* ctx, int* mode, int64_t* fallbacks);
+
+/* Tacotron2.inference then MultibandMelganGenerator.inference on its postnet output in ONE call
+   (TTS/server/synthesizer.py:150-159 runs the two back to back, the mel lengths passing through
+   Python): the decoded lengths h_steps[b] * r go from the decode's status words straight to the
+   vocoder launches, which read d_post in place (frame-major). Arguments as tts_taco_infer_spk
+   (d_spk_ids / d_spk_emb may both be NULL: single-speaker model) plus the vocoder's inference
+   padding `pad` and d_wav, which must hold B * hop * (S_cap * r + 2 pad) floats (hop = 4 x the
+   product of the upsample factors). On return its first B * hop * (M + 2 pad) floats, M = r *
+   max(h_steps), are the (B, 1, hop * (M + 2 pad)) waveform batch: bit-identical to
+   tts_melgan_infer_strided on d_post viewed as (B, 80, M) with strides (S_cap r 80, 1, 80) and
+   lengths h_steps * r. One split-f16 range scope covers both models (an overflow re-runs the
+   whole call in fp32). */
+int tts_taco_mbmelgan_infer(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                            const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
+                            const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
+                            int pad, float* d_wav, int32_t* h_steps, int32_t* h_status, void* stream);
 
 /* Test hook (process-wide, off by default): recurrence >= 0 makes one workgroup of that persistent
    BiLSTM recurrence leave before its second grid barrier, so the others time out and the next

@@ -1629,6 +1629,35 @@ def test_bench_workload_full_size_vs_oracle():
     print(f"32 utterances, worst mel error {worst:.2e}, worst waveform error {worst_w:.2e}")
 
 
+@pytest.mark.parametrize("pad", [0, 2])
+def test_fused_taco_mbmelgan_equals_two_calls(pad):
+    """Tacotron2.inference_vocoded (tts_taco_mbmelgan_infer: the decode's lengths handed to the
+    vocoder inside the library) against the reference's call pair, Tacotron2.inference then
+    MultibandMelganGenerator.inference(postnet.transpose(1, 2), lengths) (server/synthesizer.py:
+    150-159): every output bit-identical, ragged forced lengths over the 32-row LJ batch (steps cut
+    to a quarter), inference padding 0 and 2; the per-row lengths on the model agree too."""
+    import bench
+    from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids
+    dev = _dev()
+    taco, tsd, voc, vsd, tcfg, vcfg = bench.build_models(dev)
+    voc.inference_padding = pad
+    taco.decoder.verbose = False
+    T_prof, M_prof = lj_profile()
+    ids = synthetic_ids(T_prof)
+    steps = [max(3, s_ // 4) for s_ in forced_steps(M_prof, 2)]
+    batch, lens = pad_batch(ids)
+    x = torch.from_numpy(batch).to(dev)
+    with torch.no_grad():
+        a = taco.inference(x, text_lengths=lens, max_decoder_steps=steps)
+        ml = taco.last_mel_lengths.copy()
+        wa = voc.inference(a[1].transpose(1, 2), lengths=ml)
+        b = taco.inference_vocoded(x, voc, text_lengths=lens, max_decoder_steps=steps)
+    assert list(taco.last_mel_lengths) == list(ml) == [2 * s_ for s_ in steps]
+    for u, v in zip(a + (wa,), b):
+        assert u.shape == v.shape and torch.equal(u, v)
+    assert wa.shape[-1] == voc.hop * (max(ml) + 2 * pad)
+
+
 def test_bench_workload_full_size_r1_vs_oracle():
     """The bench line's r = 1 run at its full length (bench.py `r1`: the same 32 LJ-profile
     utterances, forced lengths of up to 857 decoder steps, one frame per step as the

@@ -38,6 +38,9 @@ SIGNATURES = [
     ("tts_taco_infer_spk", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int, _c_int_p,
                                           ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp, _vp, _c_int_p,
                                           _c_int_p, _vp]),
+    ("tts_taco_mbmelgan_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                               _c_int_p, ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
+                                               _vp, ctypes.c_int, _vp, _c_int_p, _c_int_p, _vp]),
     ("tts_taco_speaker_dim", ctypes.c_int, [_vp, _c_i_p, _c_i_p]),
     ("tts_taco_set_options", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_taco_encoder", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
@@ -180,6 +183,23 @@ class Engine:
                                                float(stop_threshold), sid, semb, _ptr(dec), _ptr(post),
                                                _ptr(align), _ptr(stop), steps.ctypes.data_as(_c_int_p),
                                                status.ctypes.data_as(_c_int_p), _stream(ids.device)))
+        return steps, status
+
+    def taco_mbmelgan_infer(self, ids, lens, r, max_steps, S_cap, stop_threshold, dec, post, align, stop, pad, wav,
+                            speaker_ids=None, speaker_embeddings=None):
+        """Tacotron2 decode and MB-MelGAN on its postnet output in one library call
+        (tts_taco_mbmelgan_infer); ``wav`` holds B * hop * (S_cap * r + 2 pad) floats."""
+        B, T = ids.shape
+        lens_a, lens_p = _i32(lens)
+        ms_a, ms_p = _i32(max_steps)
+        steps = np.zeros(B, np.int32)
+        status = np.zeros(B, np.int32)
+        sid = None if speaker_ids is None else _ptr(speaker_ids)
+        semb = None if speaker_embeddings is None else _ptr(speaker_embeddings)
+        _check(self.lib.tts_taco_mbmelgan_infer(self.h, _ptr(ids), lens_p, B, T, r, ms_p, S_cap, float(stop_threshold),
+                                                sid, semb, _ptr(dec), _ptr(post), _ptr(align), _ptr(stop), int(pad),
+                                                _ptr(wav), steps.ctypes.data_as(_c_int_p),
+                                                status.ctypes.data_as(_c_int_p), _stream(ids.device)))
         return steps, status
 
     def taco_speaker_dim(self):

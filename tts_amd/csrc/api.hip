@@ -3429,6 +3429,31 @@ int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, 
   });
 }
 
+// MultibandMelganGenerator.inference body on c->s: generator, output conv and PQMF synthesis into
+// d_wav (B, 1, hop * (M_max + 2 pad)), rows zero past their own length
+static void mbmelgan_body(tts_ctx* c, const float* d_mel, const int64_t* mel_strides, const int32_t* h_lens, int B,
+                          int M_max, int pad, float* d_wav) {
+  auto& G = c->mg;
+  int up = 1;
+  for (int u : G.ups) up *= u;
+  const long Ls = (long)(M_max + 2 * pad) * up;
+  HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
+  const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
+  if (fused) {
+    GenTail t;
+    run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t, mel_strides);
+    TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
+    TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
+                              G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
+              "fused output/PQMF shape not covered");
+  } else {
+    c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
+    run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s, nullptr, mel_strides);
+    launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
+                          2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
+  }
+}
+
 static int melgan_infer_impl(tts_ctx* c, const float* d_mel, const int64_t* mel_strides, const int32_t* h_lens, int B,
                       int M_max, int pad, float* d_wav, void* stream) {
   return guarded_ctx(c, [&] {
@@ -3438,27 +3463,42 @@ static int melgan_infer_impl(tts_ctx* c, const float* d_mel, const int64_t* mel_
     TTS_CHECK(G.ready && G.pqmf, "melgan (with PQMF) not finalized");
     DeviceGuard g(c->device);
     enter(c, stream);
-    with_x3_fallback(c, [&] {
-      int up = 1;
-      for (int u : G.ups) up *= u;
-      const long Ls = (long)(M_max + 2 * pad) * up;
-      HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
-      const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
-      if (fused) {
-        GenTail t;
-        run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t, mel_strides);
-        TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
-        TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
-                                  G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
-                  "fused output/PQMF shape not covered");
-      } else {
-        c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
-        run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s, nullptr, mel_strides);
-        launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
-                              2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
-      }
-    });
+    with_x3_fallback(c, [&] { mbmelgan_body(c, d_mel, mel_strides, h_lens, B, M_max, pad, d_wav); });
     leave(c, stream);
+  });
+}
+
+int tts_taco_mbmelgan_infer(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                            const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
+                            const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
+                            int pad, float* d_wav, int32_t* h_steps, int32_t* h_status, void* stream) {
+  return guarded_ctx(c, [&] {
+    TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && d_wav && h_steps &&
+                  h_status,
+              "null argument");
+    TTS_CHECK(pad >= 0, "pad >= 0");
+    TTS_CHECK(c->mg.ready && c->mg.pqmf, "melgan (with PQMF) not finalized");
+    TTS_CHECK(c->mg.in_ch == 80, "vocoder input channels must be the decoder's 80 mel channels");
+    DeviceGuard g(c->device);
+    std::vector<int32_t> mlens(B);
+    // one range-flag scope over both models: a split-f16 overflow anywhere re-runs the whole call
+    // in fp32 (decode included), as the two separate calls would each have done
+    with_x3_fallback(c, [&] {
+      taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+                 h_status, stream, d_spk_ids, d_spk_emb);
+      if (c->gemm_x3 && c->flag_read && c->pinned[12]) return;  // the decode overflowed: re-run it all
+      c->flag_read = false;  // the vocoder raises the same flag: with_x3_fallback reads it after it
+      // the decoded lengths go from the decode's status words (already on the host) straight to
+      // the vocoder, whose input is the postnet output read in place, frame-major
+      int S = 0;
+      for (int b = 0; b < B; ++b) {
+        S = std::max(S, (int)h_steps[b]);
+        mlens[b] = h_steps[b] * r;
+      }
+      const int64_t st[3] = {(int64_t)S_cap * r * 80, 1, 80};
+      mbmelgan_body(c, d_post, st, mlens.data(), B, S * r, pad, d_wav);
+      leave(c, stream);
+    });
   });
 }
 

@@ -27,6 +27,7 @@ from .audio import AudioProcessor, wav_bytes
 from .factories import load_config, setup_generator, setup_model
 from .glow_tts import GlowTts
 from .multigpu import GpuPool
+from .vocoder import MultibandMelganGenerator
 from .text import make_symbols, phonemes, split_into_sentences, symbols, text_to_seqvec
 
 
@@ -137,6 +138,7 @@ class Synthesizer:
         for i, q in enumerate(seqs):
             batch[i, :len(q)] = q
         with torch.no_grad():
+            wav = None
             if isinstance(self.tts_model, GlowTts):  # synthesis.py:60-66
                 y = self.tts_model.inference(torch.from_numpy(batch).to(dev), lens)[0]
                 post = y.transpose(1, 2)
@@ -144,11 +146,17 @@ class Synthesizer:
                 mel_lens = [2 * (int(m) // 2) for m in self.tts_model.last_y_lengths]
             else:
                 spk = None if speaker_id is None else torch.full((len(seqs),), int(speaker_id), dtype=torch.long)
-                _, post, _, _ = self.tts_model.inference(torch.from_numpy(batch).to(dev), text_lengths=lens,
-                                                         speaker_ids=spk)
+                ids = torch.from_numpy(batch).to(dev)
+                if isinstance(self.vocoder_model, MultibandMelganGenerator):
+                    # both models in one library call (tts_taco_mbmelgan_infer), same waveforms
+                    _, post, _, _, wav = self.tts_model.inference_vocoded(ids, self.vocoder_model, text_lengths=lens,
+                                                                          speaker_ids=spk)
+                else:
+                    _, post, _, _ = self.tts_model.inference(ids, text_lengths=lens, speaker_ids=spk)
                 mel_lens = [int(m) for m in self.tts_model.last_mel_lengths]
             if self.vocoder_model is not None:
-                wav = self.vocoder_model.inference(post.transpose(1, 2), lengths=mel_lens)
+                if wav is None:
+                    wav = self.vocoder_model.inference(post.transpose(1, 2), lengths=mel_lens)
                 hop = wav.shape[-1] // post.shape[1]
                 wav = wav.reshape(len(seqs), -1).cpu().numpy()
                 return [wav[i, :mel_lens[i] * hop] for i in range(len(seqs))]

@@ -151,11 +151,9 @@ class Tacotron2(nn.Module):
                               self.cfg.forward_attn_mask)
             eng.taco_key = key
 
-    @torch.no_grad()
-    def inference(self, text, speaker_ids=None, style_mel=None, speaker_embeddings=None,
-                  text_lengths: Optional[Sequence[int]] = None, max_decoder_steps=None):
-        if style_mel is not None:
-            raise NotImplementedError("GST style conditioning is not implemented (SURVEY.md §8f)")
+    def _prepare(self, text, speaker_ids, speaker_embeddings, text_lengths, max_decoder_steps):
+        """Arguments of one inference call, checked and placed: (device, engine, ids, lengths, per-row
+        max steps, r, speaker ids / embeddings, rows per library call)."""
         dev = self.embedding.weight.device
         eng = get_engine(dev)
         text = torch.as_tensor(text).to(dev, torch.int64)
@@ -176,6 +174,22 @@ class Tacotron2(nn.Module):
         variant = self.cfg.prenet_type == "bn" or self.cfg.windowing or self.cfg.forward_attn or \
             self.cfg.attn_type == "graves"
         limit = BATCH_LIMIT if self.num_speakers <= 1 and not variant else SPEAKER_BATCH_LIMIT
+        return dev, eng, text, lens, ms, r, spk_ids, spk_emb, limit
+
+    @staticmethod
+    def _buffers(nb, S_cap, r, Tn, dev):
+        dec = torch.empty(nb, S_cap * r, 80, device=dev, dtype=torch.float32)
+        return (dec, torch.empty_like(dec), torch.empty(nb, S_cap, Tn, device=dev, dtype=torch.float32),
+                torch.empty(nb, S_cap, device=dev, dtype=torch.float32))
+
+    @torch.no_grad()
+    def inference(self, text, speaker_ids=None, style_mel=None, speaker_embeddings=None,
+                  text_lengths: Optional[Sequence[int]] = None, max_decoder_steps=None):
+        if style_mel is not None:
+            raise NotImplementedError("GST style conditioning is not implemented (SURVEY.md §8f)")
+        dev, eng, text, lens, ms, r, spk_ids, spk_emb, limit = self._prepare(
+            text, speaker_ids, speaker_embeddings, text_lengths, max_decoder_steps)
+        B = text.shape[0]
         outs = []
         with eng.lock:
             self._sync(eng)
@@ -184,16 +198,18 @@ class Tacotron2(nn.Module):
                 Tn = int(lens[b0:b1].max())
                 sub = text[b0:b1, :Tn].contiguous()
                 S_cap = int(ms[b0:b1].max())
-                nb = b1 - b0
-                dec = torch.empty(nb, S_cap * r, 80, device=dev, dtype=torch.float32)
-                post = torch.empty_like(dec)
-                align = torch.empty(nb, S_cap, Tn, device=dev, dtype=torch.float32)
-                stop = torch.empty(nb, S_cap, device=dev, dtype=torch.float32)
+                dec, post, align, stop = self._buffers(b1 - b0, S_cap, r, Tn, dev)
                 steps, status = eng.taco_infer(
                     sub, lens[b0:b1], r, ms[b0:b1], S_cap, self.decoder.stop_threshold, dec, post, align, stop,
                     speaker_ids=None if spk_ids is None else spk_ids[b0:b1].contiguous(),
                     speaker_embeddings=None if spk_emb is None else spk_emb[b0:b1].contiguous())
                 outs.append((dec, post, align, stop, steps, status))
+        return self._assemble(outs, text.shape, lens, r, dev)
+
+    def _assemble(self, outs, shape, lens, r, dev):
+        """The library calls' outputs as the reference's (B, M, 80) x 2, (B, S, T), (B, S, 1), and the
+        per-row lengths on ``self`` (last_steps, last_mel_lengths, last_status)."""
+        B, T = shape
         steps = np.concatenate([o[4] for o in outs])
         status = np.concatenate([o[5] for o in outs])
         if getattr(self.decoder, "verbose", True):  # reference behaviour (tacotron2.py:365); bench.py mutes it
@@ -227,6 +243,43 @@ class Tacotron2(nn.Module):
         self.last_status = status
         self._last_call = (B, int(lens.max()), len(outs))
         return dec, post, align, stop[:, :, None]
+
+    @torch.no_grad()
+    def inference_vocoded(self, text, vocoder, speaker_ids=None, speaker_embeddings=None,
+                          text_lengths: Optional[Sequence[int]] = None, max_decoder_steps=None):
+        """``inference`` followed by ``vocoder.inference(postnet_outputs.transpose(1, 2),
+        lengths=last_mel_lengths)`` -- the pair TTS/server/synthesizer.py:150-159 runs -- in one
+        library call when ``vocoder`` is a MultibandMelganGenerator on the same device and the batch
+        fits one decode (tts_taco_mbmelgan_infer: the decoded lengths go from the decode's status
+        words straight to the vocoder, no Python between the models); otherwise the two calls.
+        Returns (decoder_outputs, postnet_outputs, alignments, stop_tokens, waveforms (B, 1, hop *
+        (M + 2 pad))), bit-identical to the two calls either way."""
+        from .vocoder import MultibandMelganGenerator
+        dev, eng, text, lens, ms, r, spk_ids, spk_emb, limit = self._prepare(
+            text, speaker_ids, speaker_embeddings, text_lengths, max_decoder_steps)
+        B = text.shape[0]
+        vdev = vocoder.layers._modules["1"].bias.device if isinstance(vocoder, MultibandMelganGenerator) else None
+        if vdev != dev or B > limit or vocoder.cfg.in_channels != 80:
+            dec, post, align, stop = self.inference(text, speaker_ids=speaker_ids, speaker_embeddings=speaker_embeddings,
+                                                    text_lengths=lens, max_decoder_steps=ms)
+            wav = vocoder.inference(post.transpose(1, 2), lengths=self.last_mel_lengths)
+            return dec, post, align, stop, wav
+        pad = int(vocoder.inference_padding)
+        Tn = int(lens.max())
+        sub = text[:, :Tn].contiguous()
+        S_cap = int(ms.max())
+        dec, post, align, stop = self._buffers(B, S_cap, r, Tn, dev)
+        hop = vocoder.hop
+        wbuf = torch.empty(B * hop * (S_cap * r + 2 * pad), device=dev, dtype=torch.float32)
+        with eng.lock:
+            self._sync(eng)
+            vocoder._sync(eng)
+            steps, status = eng.taco_mbmelgan_infer(sub, lens, r, ms, S_cap, self.decoder.stop_threshold, dec, post,
+                                                    align, stop, pad, wbuf, speaker_ids=spk_ids,
+                                                    speaker_embeddings=spk_emb)
+        res = self._assemble([(dec, post, align, stop, steps, status)], text.shape, lens, r, dev)
+        L = hop * (int(steps.max()) * r + 2 * pad)
+        return res + (wbuf[:B * L].view(B, 1, L),)
 
     @torch.no_grad()
     def decoder_state(self):
