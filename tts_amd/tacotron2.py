@@ -177,7 +177,7 @@ class Tacotron2(nn.Module):
         return dev, eng, text, lens, ms, r, spk_ids, spk_emb, limit
 
     @staticmethod
-    def _buffers(nb, S_cap, r, Tn, dev):
+    def _out_tensors(nb, S_cap, r, Tn, dev):
         dec = torch.empty(nb, S_cap * r, 80, device=dev, dtype=torch.float32)
         return (dec, torch.empty_like(dec), torch.empty(nb, S_cap, Tn, device=dev, dtype=torch.float32),
                 torch.empty(nb, S_cap, device=dev, dtype=torch.float32))
@@ -198,7 +198,7 @@ class Tacotron2(nn.Module):
                 Tn = int(lens[b0:b1].max())
                 sub = text[b0:b1, :Tn].contiguous()
                 S_cap = int(ms[b0:b1].max())
-                dec, post, align, stop = self._buffers(b1 - b0, S_cap, r, Tn, dev)
+                dec, post, align, stop = self._out_tensors(b1 - b0, S_cap, r, Tn, dev)
                 steps, status = eng.taco_infer(
                     sub, lens[b0:b1], r, ms[b0:b1], S_cap, self.decoder.stop_threshold, dec, post, align, stop,
                     speaker_ids=None if spk_ids is None else spk_ids[b0:b1].contiguous(),
@@ -268,7 +268,7 @@ class Tacotron2(nn.Module):
         Tn = int(lens.max())
         sub = text[:, :Tn].contiguous()
         S_cap = int(ms.max())
-        dec, post, align, stop = self._buffers(B, S_cap, r, Tn, dev)
+        dec, post, align, stop = self._out_tensors(B, S_cap, r, Tn, dev)
         hop = vocoder.hop
         wbuf = torch.empty(B * hop * (S_cap * r + 2 * pad), device=dev, dtype=torch.float32)
         with eng.lock:
