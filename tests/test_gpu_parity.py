@@ -1641,6 +1641,7 @@ def test_fused_taco_mbmelgan_equals_two_calls(pad):
     dev = _dev()
     taco, tsd, voc, vsd, tcfg, vcfg = bench.build_models(dev)
     voc.inference_padding = pad
+    taco.decoder.set_r(2)
     taco.decoder.verbose = False
     T_prof, M_prof = lj_profile()
     ids = synthetic_ids(T_prof)

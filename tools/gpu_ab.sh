@@ -1,5 +1,5 @@
 #!/bin/bash
-# Same-box A/B of tools/var/lib_<name>.so variants against the in-tree library on the C2 bench,
+# Same-box A/B of tools/ab/lib_<name>.so variants against the in-tree library on the C2 bench,
 # after the decoder / encoder GPU tests of the in-tree library. Usage: tools/gpu_ab.sh <rounds> <name>...
 set -o pipefail
 cd "$(dirname "$0")/.."
@@ -12,9 +12,11 @@ tail -1 gpurun_out/ab_tests.log
 bl() { python3 -c "import json,sys; d=json.loads(open(sys.argv[1]).read().strip().splitlines()[-1]); print(d['ms_per_step'], d['decoder_step_us'], d['tacotron2_ms'], d['vocoder_ms'], d['roofline']['launches'])" $1; }
 for i in $(seq 1 $rounds); do
   for v in "$@" new; do
-    lib=$PWD/tts_amd/libttship.so; [ $v != new ] && lib=$PWD/tools/var/lib_$v.so
+    lib=$PWD/tts_amd/libttship.so; [ $v != new ] && lib=$PWD/tools/ab/lib_$v.so
     TTSHIP_LIB=$lib timeout -k 10 200 python3 bench.py --steps 10 --warmup 2 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > gpurun_out/ab_$v.json 2>/dev/null || exit 1
     echo "$v run $i: $(bl gpurun_out/ab_$v.json)"
   done
 done
-TTSHIP_LIB=$PWD/tools/var/lib_trace.so TTS_PTRACE=gpurun_out/ab_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/ab_pt.err && python3 tools/ptrace.py gpurun_out/ab_pt.bin > gpurun_out/ab_ptrace.txt && head -14 gpurun_out/ab_ptrace.txt
+if [ -f tools/var/lib_trace.so ]; then
+  TTSHIP_LIB=$PWD/tools/var/lib_trace.so TTS_PTRACE=gpurun_out/ab_pt.bin timeout -k 10 120 python3 bench.py --steps 1 --warmup 0 --no-cpu-baseline --r1-steps 0 --f32-steps 0 > /dev/null 2>gpurun_out/ab_pt.err && python3 tools/ptrace.py gpurun_out/ab_pt.bin > gpurun_out/ab_ptrace.txt && head -14 gpurun_out/ab_ptrace.txt
+fi

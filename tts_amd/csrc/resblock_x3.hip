@@ -24,6 +24,21 @@
 
 #include <algorithm>
 
+// bottleneck probes for tools/rbx3_bench.hip only (results are wrong in these builds):
+// RB_NO_WLOAD (the weight ring is loaded once and never refilled), RB_NO_LDS (MFMAs on register
+// operands instead of the LDS reads), RB_NO_MFMA (operand traffic only), RB_NO_XLOAD (tiles staged
+// from stale registers: no activation loads after the first tile)
+#ifdef RB_NO_LDS
+#define RB_LD(ptr) (ring[0][0][1])
+#else
+#define RB_LD(ptr) (*reinterpret_cast<const h8*>(ptr))
+#endif
+#ifdef RB_NO_MFMA
+#define RB_MMA(ah, al, bh, bl, am, ac) ((am)[0] += (float)(bh)[0] + (float)(bl)[7])
+#else
+#define RB_MMA(ah, al, bh, bl, am, ac) mfma_x3(ah, al, bh, bl, am, ac)
+#endif
+
 namespace {
 constexpr int X3_DMAX = 27;   // largest dilation (3^3, num_res_blocks <= 4)
 constexpr int XR = 80;        // staging row, halves: 32 hi | 32 lo | 16 pad (160 B)
@@ -117,6 +132,9 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   }
   float st[2][SPT][8];
   auto stage_load = [&](const RbTile& T, float (&sr)[SPT][8], int ch) {
+#ifdef RB_NO_XLOAD
+    if (T.q0 + T.b + ch > 0 || blockIdx.x > 0) return;
+#endif
     const __amdgpu_buffer_rsrc_t xr = rsrc(a.x + (long)T.b * a.sb);  // one utterance: < 2^31 bytes
     const int i0 = T.q0 - d;
     const bool interior = i0 >= 0 && i0 + ROWS <= T.L;
@@ -180,6 +198,9 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   const int wlo = lane * 32;
   h8 ring[R][MI][2];
   auto wload = [&](h8 (&r)[MI][2], int seq) {
+#ifdef RB_NO_WLOAD
+    if (seq >= R) return;
+#endif
     if (seq >= NTOT) seq -= NTOT;
     const bool p1 = seq < NK1;
     const __amdgpu_buffer_rsrc_t wr = p1 ? wdr : wfr;
@@ -249,14 +270,14 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
           const _Float16* p = X + (nb + ni * 16 + kq * d) * XR + kgx[kq];
-          bh[ni] = *reinterpret_cast<const h8*>(p);
-          bl[ni] = *reinterpret_cast<const h8*>(p + 32);
+          bh[ni] = RB_LD(p);
+          bl[ni] = RB_LD(p + 32);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) mfma_x3(ring[sl][mi][0], ring[sl][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
+          for (int ni = 0; ni < NI; ++ni) RB_MMA(ring[sl][mi][0], ring[sl][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
         wload(ring[sl], ch * 3 + kq + R);
         __builtin_amdgcn_sched_barrier(0);
       }
@@ -300,14 +321,14 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
           const _Float16* p = HX + (nb + ni * 16) * HR + kc * 32 + kgsw;
-          bh[ni] = *reinterpret_cast<const h8*>(p);
-          bl[ni] = *reinterpret_cast<const h8*>(p + 2 * C);
+          bh[ni] = RB_LD(p);
+          bl[ni] = RB_LD(p + 2 * C);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
-          for (int ni = 0; ni < NI; ++ni) mfma_x3(bh[ni], bl[ni], ring[u][mi][0], ring[u][mi][1], am[mi][ni], ac[mi][ni]);
+          for (int ni = 0; ni < NI; ++ni) RB_MMA(bh[ni], bl[ni], ring[u][mi][0], ring[u][mi][1], am[mi][ni], ac[mi][ni]);
         wload(ring[u], NK1 + kc + R);  // past NK2: the next tile's phase-1 weights
       }
     }
