@@ -1093,8 +1093,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
   // prenet layer-2 weight chunks of this wave
   // (workgroups 0-31: tile g & 15, k-chunks wave and 8 + wave: the whole K for 16 batch rows,
   // so P3 reads one pb copy)
-  const f32x4 w2 = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + wave) * 64 + lane];
-  const f32x4 w2b = reinterpret_cast<const f32x4*>(P.pre2_w)[((long)(g & 15) * 16 + 8 + wave) * 64 + lane];
+  // are loaded per step at P1's start beside its hand-off loads (L2 hits): kept in registers for the
+  // whole launch they held 8 VGPRs through P5's k-loop, where the kernel spilled to scratch
   // partial sums of this workgroup's decoder_rnn tile (accd) and attention_rnn ctx/h tile (acca),
   // accumulated across phases. Attention-item workgroups (g >= IW0): accd h_dec part in P3, h_att
   // part in P4 after the item, ctx part in P5; acca ctx part in P5, h_att part + epilogue in P6.
@@ -1155,6 +1155,8 @@ __global__ __launch_bounds__(PT) void persist_decoder_kernel(PArgs P) {
     if (g < 16 * MT) {  // prenet layer 2: tile g & 15, batch rows 16 (g >> 4) .. + 15, whole K
       const int tl2 = g & 15, mt = g >> 4;
       f32x4 acc = f32x4{0.f, 0.f, 0.f, 0.f};
+      const f32x4* w2p = reinterpret_cast<const f32x4*>(P.pre2_w) + ((long)tl2 * 16 + wave) * 64 + lane;
+      const f32x4 w2 = w2p[0], w2b = w2p[8 * 64];
       // t = 0: the prenet input is the zero go-frame: layer 1 gives relu(b1') (BN prenet) or 0
       if (t > 0 || P.pre1_b0) {
         f32x4 x[2];
