@@ -11,24 +11,29 @@
 
 #include <cstdio>
 
-constexpr int NT = 64, NG = 4;
+#ifndef GB_NT
+#define GB_NT 64
+#endif
+// NT workgroups per group (64: the encoder BiLSTM's 4 hidden units per workgroup; 16 / 32: 16 / 8
+// units per workgroup), 16 KB of h per group either way (FPW floats published per workgroup)
+constexpr int NT = GB_NT, NG = 4, FPW = 4096 / NT;
 
 template <int MODE>
 __global__ __launch_bounds__(256) void group_kernel(unsigned* bars, float* h, int steps, float* out) {
   __shared__ int flag;
   const int dom = blockIdx.x / NT, tl = blockIdx.x % NT;
   unsigned* bar = bars + dom * BAR_WORDS;
-  float* hd = h + (size_t)dom * 2 * NT * 64;  // [2 step parities][64 workgroups][64 floats]
+  float* hd = h + (size_t)dom * 2 * 4096;  // [2 step parities][NT workgroups][FPW floats]
   unsigned gen = 0;
   f32x4 acc = {0, 0, 0, 0};
   const int lane = threadIdx.x & 63;
   for (int s = 0; s < steps; ++s) {
-    const float* hi = hd + (s & 1) * NT * 64;
-    float* ho = hd + ((s + 1) & 1) * NT * 64;
+    const float* hi = hd + (s & 1) * 4096;
+    float* ho = hd + ((s + 1) & 1) * 4096;
     // read the group's whole h (16 KB): 256 threads x 4 x 16 B
 #pragma unroll
-    for (int j = 0; j < 4; ++j) acc += ldc4(hi, ((j * 256 + threadIdx.x) * 16) % (NT * 256));
-    if (threadIdx.x < 16) stc4(ho, (tl * 16 + threadIdx.x) * 16, acc * 0.5f);
+    for (int j = 0; j < 4; ++j) acc += ldc4(hi, ((j * 256 + threadIdx.x) * 16) % 16384);
+    if (threadIdx.x < FPW / 4) stc4(ho, (tl * (FPW / 4) + threadIdx.x) * 16, acc * 0.5f);
     if (s + 1 == steps) break;
     if (MODE == 0) {
       gflag_arrive(bar, gen, tl);
@@ -43,7 +48,7 @@ __global__ __launch_bounds__(256) void group_kernel(unsigned* bars, float* h, in
         bool good = true;
         while (true) {
           bool ok = true;
-          if (lane < 16) {
+          if (lane < NT / 4) {
             const f32x4 v = ldc4(reinterpret_cast<const float*>(bar + BAR_FLAGS), lane * 16);
 #pragma unroll
             for (int j = 0; j < 4; ++j) ok = ok && __float_as_uint(v[j]) >= gen;
@@ -71,8 +76,8 @@ int main(int argc, char** argv) {
   unsigned* pool;
   float *h, *out;
   HIP_OK(hipMalloc(&pool, (size_t)16 * NG * BAR_WORDS * 4));
-  HIP_OK(hipMalloc(&h, (size_t)NG * 2 * NT * 64 * 4));
-  HIP_OK(hipMemset(h, 0, (size_t)NG * 2 * NT * 64 * 4));
+  HIP_OK(hipMalloc(&h, (size_t)NG * 2 * 4096 * 4));
+  HIP_OK(hipMemset(h, 0, (size_t)NG * 2 * 4096 * 4));
   HIP_OK(hipMalloc(&out, 256 * 256 * 4));
   hipEvent_t e0, e1;
   HIP_OK(hipEventCreate(&e0));
@@ -91,7 +96,7 @@ int main(int argc, char** argv) {
         int st = steps;
         void* args[] = {&bars, &h, &st, &out};
         HIP_OK(hipEventRecord(e0));
-        HIP_OK(hipLaunchKernel(ks[m], dim3(256), dim3(256), args, 96 * 1024, 0));  // LDS: one workgroup per CU
+        HIP_OK(hipLaunchKernel(ks[m], dim3(NG * NT), dim3(256), args, 96 * 1024, 0));  // LDS: one workgroup per CU
         HIP_OK(hipEventRecord(e1));
         HIP_OK(hipEventSynchronize(e1));
         float ms = 0.f;

@@ -226,9 +226,6 @@ int main(int argc, char** argv) {
     }
     timeit("fp32", [&] { launch_resblock(a, C, S); });
     timeit("split-f16 (library tile)", [&] { launch_resblock_x3(a, kM, C, S); });
-    if (C == 192) timeit("x3 old (all waves stage)", [&] { launch_rbx3<192, 64, 12, 1, 3>(a, kM, S); });
-    if (C == 96) timeit("x3 old (all waves stage)", [&] { launch_rbx3<96, 128, 6, 2, 3>(a, kM, S); });
-    if (C == 48) timeit("x3 old (all waves stage)", [&] { launch_rbx3<48, 192, 3, 4, 3>(a, kM, S); });
     if (C == 192) {
       timeit("x3 TQ64 12x1", [&] { launch_rbx3<192, 64, 12, 1, 3>(a, kM, S); });
       timeit("x3 TQ48 12x1 (NI3)", [&] { launch_rbx3<192, 48, 12, 1, 3>(a, kM, S); });

@@ -80,12 +80,15 @@ int main(int argc, char** argv) {
   StackArgs sa{};
   ResArgs ra[3]{};
   for (int k = 0; k < 3; ++k) {
-    std::vector<uint16_t> wd16, wf16;
-    pack_resblock_x3(rnd((size_t)C * C * 3, 0.08f, 11u + k), rnd((size_t)C * 2 * C, 0.08f, 21u + k), C, wd16, wf16);
+    std::vector<uint16_t> wd16, wf16, wd16p;
+    const std::vector<float> wd = rnd((size_t)C * C * 3, 0.08f, 11u + k);
+    pack_resblock_x3(wd, rnd((size_t)C * 2 * C, 0.08f, 21u + k), C, wd16, wf16);
     const float* bd = dup(rnd(C, 0.1f, 31u + k));
     const float* bf = dup(rnd(C, 0.1f, 41u + k));
     sa.dil[k] = dil[k];
-    sa.wd16[k] = dup(wd16);
+    const void* wd_plain = dup(wd16);
+    if (C % 32 == 16) pack_resblock_x3p(wd, C, wd16p);  // the stack's packed phase-1 order
+    sa.wd16[k] = C % 32 == 16 ? dup(wd16p) : wd_plain;
     sa.wf16[k] = dup(wf16);
     sa.bd[k] = bd;
     sa.bf[k] = bf;
@@ -98,7 +101,7 @@ int main(int argc, char** argv) {
     r.dil = dil[k];
     r.bd = bd;
     r.bf = bf;
-    r.Wd16 = sa.wd16[k];
+    r.Wd16 = wd_plain;
     r.Wf16 = sa.wf16[k];
     r.oflow = of;
     r.max_q = (Mmax + 2 * pad) * mul;

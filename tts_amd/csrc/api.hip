@@ -377,6 +377,7 @@ struct MelganModel {
   std::vector<ConvLayer> convTm;  // phase-merged split-f16 form (conv_x3.hip merged_u), W16 only
   std::vector<ConvLayer> dconv, fused;  // [stage*nres + block]
   std::vector<DevBuf> rb_wd16, rb_wf16;  // split-f16 block weights (resblock_x3.hip), empty if C unsupported
+  std::vector<DevBuf> rb_wd16p;          // phase-1 weights in the packed order (C % 32 == 16), for resstack_x3
   DevBuf G;
   DevBuf out_w, out_b;  // conv_out as [c][k][o] for the fused output + PQMF kernel
   int C_last = 0;
@@ -1804,6 +1805,8 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
   G.rb_wf16.clear();
   G.rb_wd16.resize((size_t)n_up * nres);
   G.rb_wf16.resize((size_t)n_up * nres);
+  G.rb_wd16p.clear();
+  G.rb_wd16p.resize((size_t)n_up * nres);
   int pl3[8] = {3}, pl0[8] = {0};
   {
     auto w = wn_weight(m, "layers.1", {base, in_ch, 7});
@@ -1867,6 +1870,10 @@ void melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32_t*
         pack_resblock_x3(wd, Wf, C, wd16, wf16);
         G.rb_wd16[(size_t)i * nres + bk].upload(wd16);
         G.rb_wf16[(size_t)i * nres + bk].upload(wf16);
+        if (C % 32 == 16) {
+          pack_resblock_x3p(wd, C, wd16);
+          G.rb_wd16p[(size_t)i * nres + bk].upload(wd16);
+        }
       }
     }
     idx += 3;
@@ -2011,7 +2018,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     sa.mul = muls;
     for (int k = 0; k < 3; ++k) {
       sa.dil[k] = dil[k];
-      sa.wd16[k] = G.rb_wd16[i * G.nres + k].p;
+      sa.wd16[k] = Cs % 32 == 16 ? G.rb_wd16p[i * G.nres + k].p : G.rb_wd16[i * G.nres + k].p;
       sa.wf16[k] = G.rb_wf16[i * G.nres + k].p;
       sa.bd[k] = G.dconv[i * G.nres + k].bias.f();
       sa.bf[k] = G.fused[i * G.nres + k].bias.f();

@@ -217,9 +217,12 @@ bool resblock_x3_supported(int C);
 void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t s);
 void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf, int C,
                       std::vector<uint16_t>& wd16, std::vector<uint16_t>& wf16);
+// phase-1 weights in resstack_x3's packed order for C % 32 == 16 (C = 48: 5 k-steps, not 6)
+void pack_resblock_x3p(const std::vector<float>& wd, int C, std::vector<uint16_t>& wd16);
 
 // Blocks 0-2 of a ResidualStack fused per time tile (resstack_x3.hip), split-f16 weights in the
-// pack_resblock_x3 layout; y = block2(block1(block0(x)))
+// pack_resblock_x3 layout (phase 1 in the pack_resblock_x3p order when C % 32 == 16);
+// y = block2(block1(block0(x)))
 struct StackArgs {
   const float* x;
   float* y;

@@ -28,7 +28,10 @@
 // bottleneck probes for tools/rbx3_bench.hip only (results are wrong in these builds):
 // RB_NO_WLOAD (the weight ring is loaded once and never refilled), RB_NO_LDS (MFMAs on register
 // operands instead of the LDS reads), RB_NO_MFMA (operand traffic only), RB_NO_XLOAD (tiles staged
-// from stale registers: no activation loads after the first tile)
+// from stale registers: no activation loads after the first tile). Every probe also makes the MFMA
+// operands repeat from tile to tile, which lets the chip clock higher (DVFS, MI355X_MICROARCH.md):
+// their speedups (profiles/r06/v3_rb_probes.txt) overstate the removed resource's share; loader
+// waves that took the HBM staging off the MFMA waves measured no faster (v4_rb_ws_rejected.txt)
 #ifdef RB_NO_LDS
 #define RB_LD(ptr) (ring[0][0][1])
 #else
@@ -373,335 +376,6 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   if (bad || !(vmax < F16_RANGE)) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
 }
 
-// ---- warp-specialised form (round 6): the same tile, LDS layout and arithmetic, with the HBM
-// staging moved to NLW loader waves. vmcnt is an in-order counter: in resblock_x3_kernel every wave
-// issues both the tile's HBM staging loads (~1.5-2 us under load) and its weight-ring loads (L2,
-// waited for R k-steps after issue), so the first weight wait behind a staging batch waited for
-// the HBM loads too (RB_NO_XLOAD probe, profiles/r06/v3_rb_probes.txt: 14-27 % of the launch).
-// Here the MFMA waves issue only weight loads; the loader waves load, split and store the staged
-// chunks and the shortcut operand between the same workgroup barriers, S register sets ahead
-// (2 sets; with an odd chunk count they trade places at each tile boundary). The MFMA waves keep the kernel's 16-wave budget of 128 VGPRs without the staging
-// registers. Products and their order are those of resblock_x3_kernel: bit-identical outputs.
-constexpr int RB_NLW = 4;
-typedef unsigned v4u_ __attribute__((ext_vector_type(4)));
-template <int C, int TQ, int WM, int WN, int R>
-__global__ __launch_bounds__(64 * (WM * WN + RB_NLW)) void resblock_x3w_kernel(ResArgs a, int ntiles, bool vec) {
-  constexpr int NMW = WM * WN;
-  constexpr int LTHR = 64 * RB_NLW;
-  constexpr int MI = C / 16 / WM;
-  constexpr int NI = TQ / 16 / WN;
-  static_assert(MI * 16 * WM == C && NI * 16 * WN == TQ, "tile split");
-  constexpr int NCH = (C + 31) / 32;
-  constexpr int NK1 = 3 * NCH;
-  constexpr int NK2 = 2 * C / 32;
-  constexpr int NTOT = NK1 + NK2;
-  static_assert(NK2 * 32 == 2 * C && NK1 % R == 0 && NK2 % R == 0, "weight ring: R must divide both phases");
-  constexpr int HR = 4 * C + 16;
-  constexpr int NG2 = NI > 3 ? 2 : NI;                                   // n-tiles per operand group
-  static_assert(NI % NG2 == 0, "n-tile groups");
-  constexpr int S = NCH > 1 ? 2 : 1;                                    // loader register sets
-  constexpr int LPT = (4 * (TQ + 2 * X3_DMAX) + LTHR - 1) / LTHR;       // staging items per loader thread
-  extern __shared__ __attribute__((aligned(16))) _Float16 sh[];
-
-  int t = blockIdx.x;
-  const int d = a.dil;
-  const int ROWS = TQ + 2 * d;
-  _Float16* X0 = sh;
-  _Float16* X1 = sh + ROWS * XR;
-  _Float16* HX = sh + 2 * ROWS * XR;
-
-  const int tid = threadIdx.x;
-  const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const bool loader = wave >= NMW;  // wave-uniform role
-  bool bad = false;
-  float vmax = 0.f;
-
-  __shared__ int tcum[65], tlen[64];
-  __shared__ float sbd[C], sbf[C];  // biases: LDS reads in the epilogues (a global load there would
-                                    // wait behind the weight ring; registers for them spilled)
-  for (int i = tid; i < C; i += 64 * (NMW + RB_NLW)) {
-    sbd[i] = a.bd[i];
-    sbf[i] = a.bf[i];
-  }
-  if (wave == 0) {
-    const int L = lane < a.B ? (a.lens[lane] + a.len_add) * a.mul : 0;
-    const int n = (L + TQ - 1) / TQ;
-    int v = n;
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-      const int y = __shfl_up(v, o, 64);
-      if (lane >= o) v += y;
-    }
-    tcum[lane] = v - n;
-    tlen[lane] = L;
-    if (lane == 63) tcum[64] = v;
-  }
-  lds_barrier();
-  auto tile_of = [&](int i) {
-    const bool hit = lane < a.B && tcum[lane] <= i && i < tcum[lane + 1];
-    const unsigned long long m = __ballot(hit);
-    const int b = __builtin_amdgcn_readfirstlane(m ? __ffsll((long long)m) - 1 : 0);
-    RbTile r;
-    r.b = b;
-    r.q0 = __builtin_amdgcn_readfirstlane((i - tcum[b]) * TQ);
-    r.L = __builtin_amdgcn_readfirstlane(tlen[b]);
-    return r;
-  };
-  if (t >= ntiles) return;  // workgroup-uniform
-  RbTile cur = tile_of(t);
-  RbTile nxt = t + (int)gridDim.x < ntiles ? tile_of(t + gridDim.x) : cur;
-
-  if (loader) {
-    // ================= loader waves: staging of lrelu(x) (phase-1 operand) and x (shortcut) =========
-    const int ltid = tid - 64 * NMW;
-    int srow[LPT], sg[LPT];
-#pragma unroll
-    for (int j = 0; j < LPT; ++j) {
-      const int e = ltid + LTHR * j;
-      sg[j] = e / ROWS;
-      srow[j] = e - sg[j] * ROWS;
-    }
-    float st[S][LPT][8];
-    // chunk ch of tile T into register set `set` (compile-time); loads issued unconditionally
-    // (clamped), so the waits below count them
-    auto stage_load = [&](const RbTile& T, float (&sr)[LPT][8], int ch) {
-#ifdef RB_NO_XLOAD
-      if (T.q0 + T.b + ch > 0 || blockIdx.x > 0) return;
-#endif
-      const __amdgpu_buffer_rsrc_t xr = rsrc(a.x + (long)T.b * a.sb);
-      const int i0 = T.q0 - d;
-      const bool interior = i0 >= 0 && i0 + ROWS <= T.L;
-#pragma unroll
-      for (int j = 0; j < LPT; ++j) {
-        int i = i0 + min(srow[j], ROWS - 1);
-        if (!interior) {
-          if (i < 0) i = -i;
-          if (i >= T.L) i = 2 * (T.L - 1) - i;
-          i = i < 0 ? 0 : (i >= T.L ? T.L - 1 : i);
-        }
-        int g8 = min(sg[j], 3);
-        asm volatile("" : "+v"(g8));
-        const int c0 = min(32 * ch + 8 * g8, C - 8);
-        const int vo = (c0 * a.Ls + i) * 4;
-#pragma unroll
-        for (int c = 0; c < 8; ++c)
-          sr[j][c] = __uint_as_float(__builtin_amdgcn_raw_buffer_load_b32(xr, vo, c * a.Ls * 4, 0));
-      }
-    };
-    auto stage_store = [&](_Float16* X, const float (&sr)[LPT][8], int ch) {
-#pragma unroll
-      for (int j = 0; j < LPT; ++j) {
-        const int g = sg[j], row = srow[j];
-        if (g < 4) {
-          const bool real = 32 * ch + 8 * g < C;
-          float v[8], mx = 0.f;
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            v[c] = real ? sr[j][c] : 0.f;
-            mx = fmaxf(mx, __builtin_fabsf(v[c]));
-          }
-          bad |= !(mx < F16_RANGE);
-          float lv[8];
-#pragma unroll
-          for (int c = 0; c < 8; ++c) lv[c] = lrelu_x3(v[c]);
-          h8 hi, lo;
-          split8(lv, hi, lo);
-          const int sx = (8 * g) ^ lds_rsw(row);
-          *reinterpret_cast<h8*>(X + row * XR + sx) = hi;
-          *reinterpret_cast<h8*>(X + row * XR + 32 + sx) = lo;
-          const int p = row - d;
-          if (real && p >= 0 && p < TQ) {
-            split8(v, hi, lo);
-            const int hx = C + 32 * ch + ((8 * g) ^ lds_rsw(p));
-            *reinterpret_cast<h8*>(HX + p * HR + hx) = hi;
-            *reinterpret_cast<h8*>(HX + p * HR + 2 * C + hx) = lo;
-          }
-        }
-      }
-    };
-    // after storing chunk c of cur from set c % S: chunk c + S goes into that set (cur, or the
-    // next tile's chunk c + S - NCH)
-    auto refill = [&](int c) __attribute__((always_inline)) {
-      const int cn = c + S;
-      if (cn < NCH) stage_load(cur, st[c % S], cn);
-      else stage_load(nxt, st[c % S], cn - NCH);
-    };
-#pragma unroll
-    for (int c = 0; c < S; ++c) stage_load(cur, st[c], c);
-    stage_store(X0, st[0], 0);
-    refill(0);
-    lds_barrier();
-    for (;;) {
-      const int tn = t + gridDim.x;
-      const bool more = tn < ntiles;
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-        if (ch + 1 < NCH) {  // during chunk ch's MFMAs: chunk ch + 1 into the buffer chunk ch - 1 used
-          stage_store(((ch + 1) & 1) ? X1 : X0, st[(ch + 1) % S], ch + 1);
-          refill(ch + 1);
-        }
-        lds_barrier();
-      }
-      lds_barrier();  // epilogue: h into HX
-      if (!more) break;
-      lds_barrier();  // every wave is done with this tile's X / HX
-      t = tn;
-      cur = nxt;
-      nxt = t + (int)gridDim.x < ntiles ? tile_of(t + gridDim.x) : cur;
-      if constexpr (S == 2 && NCH % 2 == 1) {  // odd chunk count: the new tile's chunk 0 sits in set 1
-#pragma unroll
-        for (int j = 0; j < LPT; ++j)
-#pragma unroll
-          for (int c = 0; c < 8; ++c) {
-            const float x_ = st[0][j][c];
-            st[0][j][c] = st[1][j][c];
-            st[1][j][c] = x_;
-          }
-      }
-      stage_store(X0, st[0], 0);
-      refill(0);
-      lds_barrier();
-    }
-  } else {
-    // ================= MFMA waves: resblock_x3_kernel's phases without the staging ===============
-    const int wm = wave / WN, wn = wave % WN;
-    const int nb = wn * 16 * NI + (lane & 15);
-    const int kg = 8 * (lane >> 4);
-    const int lsw = lds_rsw(lane & 15);
-    const int kgsw = kg ^ lsw;
-    const int kgx[3] = {kgsw, kg ^ lds_rsw((lane & 15) + d), kg ^ lds_rsw((lane & 15) + 2 * d)};
-    const int mt0 = wm * MI;
-    const __amdgpu_buffer_rsrc_t wdr = rsrc(a.Wd16), wfr = rsrc(a.Wf16);
-    const int wlo = lane * 32;
-    h8 ring[R][MI][2];
-    auto wload = [&](h8 (&r)[MI][2], int seq) {
-#ifdef RB_NO_WLOAD
-      if (seq >= R) return;
-#endif
-      if (seq >= NTOT) seq -= NTOT;
-      const bool p1 = seq < NK1;
-      const __amdgpu_buffer_rsrc_t wr = p1 ? wdr : wfr;
-      const int nk = p1 ? NK1 : NK2;
-      const int ks = p1 ? seq : seq - NK1;
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int so = ((mt0 + mi) * nk + ks) * 2048;
-        r[mi][0] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo, so, 0));
-        r[mi][1] = __builtin_bit_cast(h8, __builtin_amdgcn_raw_buffer_load_b128(wr, wlo + 16, so, 0));
-      }
-    };
-#pragma unroll
-    for (int u = 0; u < R; ++u) wload(ring[u], u);
-    lds_barrier();  // chunk 0 staged
-    f32x4 am[MI][NI], ac[MI][NI];
-    for (;;) {
-      const int tn = t + gridDim.x;
-      const bool more = tn < ntiles;
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-#pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
-        const _Float16* X = (ch & 1) ? X1 : X0;
-#pragma unroll
-        for (int kq = 0; kq < 3; ++kq) {
-          const int sl = (ch * 3 + kq) % R;
-          // the n-tiles in groups of NG2 (B operands of one group live at a time: register budget)
-#pragma unroll
-          for (int n0 = 0; n0 < NI; n0 += NG2) {
-            h8 bh[NG2], bl[NG2];
-#pragma unroll
-            for (int i = 0; i < NG2; ++i) {
-              const _Float16* p = X + (nb + (n0 + i) * 16 + kq * d) * XR + kgx[kq];
-              bh[i] = RB_LD(p);
-              bl[i] = RB_LD(p + 32);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-              for (int i = 0; i < NG2; ++i)
-                RB_MMA(ring[sl][mi][0], ring[sl][mi][1], bh[i], bl[i], am[mi][n0 + i], ac[mi][n0 + i]);
-          }
-          wload(ring[sl], ch * 3 + kq + R);
-          __builtin_amdgcn_sched_barrier(0);
-        }
-        lds_barrier();
-      }
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int co = ((mt0 + mi) * 16 + 4 * (lane >> 4)) ^ lsw;
-        const f32x4 bd = *reinterpret_cast<const f32x4*>(sbd + (mt0 + mi) * 16 + 4 * (lane >> 4));
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const f32x4 v = lrelu4(x3_value4(am[mi][ni], ac[mi][ni], bd));
-          vmax = absmax4(vmax, v);
-          h4 hi, lo;
-          split4(v, hi, lo);
-          const int p = nb + ni * 16;
-          *reinterpret_cast<h4*>(HX + p * HR + co) = hi;
-          *reinterpret_cast<h4*>(HX + p * HR + 2 * C + co) = lo;
-          am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
-        }
-      }
-      lds_barrier();
-#pragma unroll
-      for (int k0 = 0; k0 < NK2; k0 += R) {
-#pragma unroll
-        for (int u = 0; u < R; ++u) {
-          const int kc = k0 + u;
-#pragma unroll
-          for (int n0 = 0; n0 < NI; n0 += NG2) {
-            h8 bh[NG2], bl[NG2];
-#pragma unroll
-            for (int i = 0; i < NG2; ++i) {
-              const _Float16* p = HX + (nb + (n0 + i) * 16) * HR + kc * 32 + kgsw;
-              bh[i] = RB_LD(p);
-              bl[i] = RB_LD(p + 2 * C);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int mi = 0; mi < MI; ++mi)
-#pragma unroll
-              for (int i = 0; i < NG2; ++i)
-                RB_MMA(bh[i], bl[i], ring[u][mi][0], ring[u][mi][1], am[mi][n0 + i], ac[mi][n0 + i]);
-          }
-          wload(ring[u], NK1 + kc + R);
-        }
-      }
-      // output rows through a buffer resource of the utterance (SGPRs) and 32-bit lane offsets
-      const __amdgpu_buffer_rsrc_t yr = rsrc(a.y + (long)cur.b * a.sb);
-#pragma unroll
-      for (int mi = 0; mi < MI; ++mi) {
-        const int co = (mt0 + mi) * 16 + (lane & 15);
-        const float bf1 = sbf[co];
-        const f32x4 bf{bf1, bf1, bf1, bf1};
-#pragma unroll
-        for (int ni = 0; ni < NI; ++ni) {
-          const f32x4 v = x3_value4(am[mi][ni], ac[mi][ni], bf);
-          const int q = cur.q0 + wn * 16 * NI + ni * 16 + 4 * (lane >> 4);
-          const int off = (co * a.Ls + q) * 4;
-          if (vec && q + 3 < cur.L) {
-            __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(v4u_, v), yr, off, 0, 0);
-          } else {
-#pragma unroll
-            for (int j = 0; j < 4; ++j)
-              if (q + j < cur.L) __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(v[j]), yr, off + 4 * j, 0, 0);
-          }
-        }
-      }
-      if (!more) break;
-      lds_barrier();
-      t = tn;
-      cur = nxt;
-      nxt = t + (int)gridDim.x < ntiles ? tile_of(t + gridDim.x) : cur;
-      lds_barrier();  // the loaders staged the new tile's chunk 0
-    }
-  }
-  if (bad || !(vmax < F16_RANGE)) __hip_atomic_fetch_or(a.oflow, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-}
-
 // one resident workgroup per CU (the LDS tile allows no more), each looping over tiles; the
 // dynamic LDS leaves 1 KiB of the CU's 160 KiB for the kernel's static tile tables
 constexpr int RB_DYN_LDS = 159 * 1024;
@@ -721,22 +395,6 @@ static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   resblock_x3_kernel<C, TQ, WM, WN, R><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles, vec);
 }
 
-template <int C, int TQ, int WM, int WN, int R>
-static void launch_rbx3w(const ResArgs& a, const int* h_lens, hipStream_t s) {
-  const int ROWS = TQ + 2 * a.dil;
-  const size_t lds = ((size_t)2 * ROWS * XR + (size_t)TQ * (4 * C + 16)) * 2;
-  ensure_dyn_lds((const void*)resblock_x3w_kernel<C, TQ, WM, WN, R>, RB_DYN_LDS);
-  const int ncu = device_cu_count();
-  TTS_CHECK(lds <= RB_DYN_LDS, "resblock_x3w: LDS tile too large");
-  long ntiles = 0;
-  for (int b = 0; b < a.B; ++b) ntiles += ((long)(h_lens[b] + a.len_add) * a.mul + TQ - 1) / TQ;
-  TTS_CHECK(ntiles < (1L << 30), "resblock_x3w: too many tiles");
-  if (ntiles == 0) return;
-  const int grid = (int)std::min<long>(ntiles, ncu);
-  const bool vec = a.Ls % 4 == 0 && a.sb % 4 == 0 && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
-  resblock_x3w_kernel<C, TQ, WM, WN, R><<<grid, 64 * (WM * WN + RB_NLW), lds, s>>>(a, (int)ntiles, vec);
-}
-
 bool resblock_x3_supported(int C) { return C == 256 || C == 192 || C == 128 || C == 96 || C == 64 || C == 48 || C == 32; }
 
 // host packing of one block's split weights: Wd (C, C, 3) [co][ci][k] and Wf (C, 2C) [co][k]
@@ -750,31 +408,41 @@ void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf
   wf16 = pack_split_a(C / 16, 2 * C / 32, [&](int m, int k) -> float { return wf[(size_t)m * 2 * C + k]; });
 }
 
+// the phase-1 weights in resstack_x3's packed k-step order for a half last chunk (C % 32 == 16):
+// full chunks as pack_resblock_x3 (k-step 3 ch + tap), then the half chunk's 2 octets x 3 taps in
+// 2 k-steps: k-step 3K lane groups 0-1 tap 0 / 2-3 tap 1, k-step 3K + 1 groups 0-1 tap 2 / 2-3 zero
+// (group g reads channel octet 4 (K) + (g & 1), i.e. channels 32 K + 8 (g & 1) + j)
+void pack_resblock_x3p(const std::vector<float>& wd, int C, std::vector<uint16_t>& wd16) {
+  TTS_CHECK(C % 32 == 16, "pack_resblock_x3p: half last chunk only");
+  const int K = C / 32;  // full chunks
+  wd16 = pack_split_a(C / 16, 3 * K + 2, [&](int m, int k) -> float {
+    const int step = k / 32, g = (k % 32) / 8, j = k % 8;
+    int kq, ci;
+    if (step < 3 * K) {
+      kq = step % 3;
+      ci = 32 * (step / 3) + 8 * g + j;
+    } else if (step == 3 * K) {
+      kq = g >> 1;
+      ci = 32 * K + 8 * (g & 1) + j;
+    } else {
+      if (g >= 2) return 0.f;
+      kq = 2;
+      ci = 32 * K + 8 * g + j;
+    }
+    return wd[((size_t)m * C + ci) * 3 + kq];
+  });
+}
+
 void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t s) {
   TTS_CHECK(a.dil >= 1 && a.dil <= X3_DMAX, "resblock: dilation must be in [1, 27] (num_res_blocks <= 4)");
   TTS_CHECK(a.Wd16 && a.Wf16 && a.oflow, "resblock_x3: split weights / overflow flag missing");
   TTS_CHECK(a.B <= 64, "resblock_x3: at most 64 utterances per call");
   if (a.max_q <= 0 || a.B <= 0) return;
-  // TTS_RB_WS=1: the warp-specialised form at the MB-MelGAN stages (under evaluation); default:
-  // the round-5 kernel (every wave stages)
-  static const bool ws = [] {
-    const char* e = std::getenv("TTS_RB_WS");
-    return e && std::atoi(e) != 0;
-  }();
   switch (C) {
-    // tiles from tools/rbx3_bench.hip (C2 shapes): 12 MFMA waves, one m-tile (or two) per wave
-    case 192:
-      if (ws) launch_rbx3w<192, 64, 12, 1, 3>(a, h_lens, s);
-      else launch_rbx3<192, 64, 12, 1, 3>(a, h_lens, s);
-      break;
-    case 96:
-      if (ws) launch_rbx3w<96, 128, 6, 2, 3>(a, h_lens, s);
-      else launch_rbx3<96, 128, 6, 2, 3>(a, h_lens, s);  // round 3: 4 blocks 926 -> 879 us
-      break;
-    case 48:
-      if (ws) launch_rbx3w<48, 192, 3, 4, 3>(a, h_lens, s);
-      else launch_rbx3<48, 192, 3, 4, 3>(a, h_lens, s);
-      break;
+    // tiles from tools/rbx3_bench.hip (C2 shapes): 12 waves, one m-tile (or two) per wave
+    case 192: launch_rbx3<192, 64, 12, 1, 3>(a, h_lens, s); break;
+    case 96: launch_rbx3<96, 128, 6, 2, 3>(a, h_lens, s); break;  // round 3: 4 blocks 926 -> 879 us
+    case 48: launch_rbx3<48, 192, 3, 4, 3>(a, h_lens, s); break;
     // full-band MelGAN stages (base 512): tiles sized to the 159 KB LDS budget, 8 waves
     case 256: launch_rbx3<256, 32, 8, 1, 4>(a, h_lens, s); break;
     case 128: launch_rbx3<128, 64, 8, 1, 4>(a, h_lens, s); break;

@@ -21,6 +21,7 @@
 #include "split16.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace {
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc_s(const void* p) {
@@ -72,18 +73,26 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
   constexpr int ROWS = TQ + 2 * OFF;
   static_assert(ROWS % 16 == 0 && ROWS / 16 <= WN * NI, "n-tiles per wave group");
   constexpr int NCH = (C + 31) / 32;  // phase-1 chunks of 32 input channels
-  constexpr int NK1 = 3 * NCH, NK2 = 2 * C / 32, NKB = NK1 + NK2;
-  constexpr int R = 3;  // weight ring: divides both phases, so a k-step's slot is fixed
-  static_assert(NK2 * 32 == 2 * C && NK1 % R == 0 && NK2 % R == 0, "weight ring");
+  // phase-1 k-steps: 3 taps per full chunk; a half chunk (C % 32 == 16: C = 48) packs its 2 channel
+  // octets x 3 taps into 2 k-steps instead of 3 (pack_resblock_x3p; k-step 3K: taps 0 | 1 by lane
+  // group pair, 3K + 1: tap 2 | zero weights), 5 k-steps instead of 6 at C = 48
+  constexpr bool HALF = C % 32 == 16;
+  constexpr int NK1 = HALF ? 3 * (NCH - 1) + 2 : 3 * NCH, NK2 = 2 * C / 32, NKB = NK1 + NK2;
+  constexpr int R = 3;  // weight ring; the blocks are unrolled, so a k-step's slot is the compile-time
+                        // (its index in the tile's weight sequence) % R
+  static_assert(NK2 * 32 == 2 * C && (C % 32 == 0 || HALF), "weight ring / channel chunks");
   // XL row stride 2C + 16 halves (C = 48: 56 dwords): the 16 lanes of each ds_read_b128 group
   // (16 consecutive rows, two k-octets) land on distinct banks
   constexpr int XLR = 2 * C + 16;
   constexpr int HR = 4 * C + 16;
   constexpr int NG = C / 8;  // channel octets of a staged row
-  // fused ConvTranspose geometry: CIN input channels in CROWS staged rows of CRS halves (stride
-  // 100 dwords: the 16 rows of a ds_read_b128 group on distinct banks); CMT m-tiles of merged rows,
-  // CNT n-tiles of input columns, CKS k-steps (32 channels x 2 taps)
-  constexpr int CIN = 2 * C, NGI = CIN / 8, CROWS = 128, CRS = 2 * CIN + 8;
+  // fused ConvTranspose geometry: CIN input channels in CROWS staged rows of CRS halves; CMT m-tiles
+  // of merged rows, CNT n-tiles of input columns, CKS k-steps (32 channels x 2 taps). Row stride
+  // 104 dwords (8 mod 16, as XL / HX): the B-operand ds_read_b128 is conflict-free in each of the
+  // instruction's four lane groups ({0-3, 12-15, 20-27}, ...: rows 0-3 and 12-15 at k-group 0 beside
+  // rows 4-11 at k-group 1). Round 5's 100-dword stride kept 16 consecutive rows on distinct banks
+  // but put every group's two k-groups 2-way on the same banks (PMC LDS_conflict 0.29).
+  constexpr int CIN = 2 * C, NGI = CIN / 8, CROWS = 128, CRS = 2 * CIN + 16;
   constexpr int CMT = CTU ? C * CTU / 16 : 1, CNT = CROWS / 16, CKS = CIN / 32 * 2;
   static_assert(CTU == 0 || (C == 48 && CTU == 2 && ROWS / 2 + 2 <= CROWS && CROWS * CRS <= ROWS * (2 * C + 16) &&
                              WM * WN == 2 * CMT && CNT == 2 * NI),
@@ -248,7 +257,8 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
   h8 ring[R][2];
   // CTU: the fused ConvTranspose is "block -1" of every tile, CKS k-steps of this wave's merged-row
   // m-tile (wave % CMT) ahead of block 0 in the ring sequence (CKS % R == 0 keeps slots fixed)
-  static_assert(CTU == 0 || CKS % R == 0, "weight ring over the fused ConvTranspose");
+  constexpr int SEQ0 = CTU ? CKS : 0;  // index of block 0's first k-step in the tile's weight sequence
+  static_assert((SEQ0 + NB * NKB) % R == 0, "weight ring: a tile's weight sequence must be a multiple of R");
   auto wload = [&](h8 (&r)[2], int blk, int s) {  // s: k-step within block blk (compile-time)
     if (CTU && blk < 0) {
       const __amdgpu_buffer_rsrc_t wr = rsrc_s(a.ct16);
@@ -353,7 +363,9 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
     // one ResidualStack block; the last is peeled (a second inlined copy) so that the next tile's
     // staging loads are issued on a path the compiler sees whole: its vmcnt waits for the weight
     // ring then count them instead of draining them
-    auto block = [&](const int bi, const bool last) __attribute__((always_inline)) {
+    auto block = [&](auto BI, const bool last) __attribute__((always_inline)) {
+      constexpr int bi = decltype(BI)::value;
+      constexpr int g0 = SEQ0 + bi * NKB;  // weight-sequence index of this block's k-step 0
       const int d = pick3(a.dil[0], a.dil[1], a.dil[2], bi), E = pick3(a.ext[0], a.ext[1], a.ext[2], bi);
       const int vlo = max(OFF - E, -base), vhi = min(OFF + TQ + E, cur.L - base);
       const int tlo = vlo >> 4, thi = (vhi + 15) >> 4;
@@ -387,26 +399,33 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) am[ni] = ac[ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-      for (int ch = 0; ch < NCH; ++ch) {
+      for (int s = 0; s < NK1; ++s) {
+        const int ch = HALF && s >= 3 * (NCH - 1) ? NCH - 1 : s / 3;
+        h8 bh[NI], bl[NI];
 #pragma unroll
-        for (int kq = 0; kq < 3; ++kq) {
-          const int s = ch * 3 + kq;
-          h8 bh[NI], bl[NI];
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni) {
-            // unconditional: an inactive slot reads a clamped row and its result is dropped;
-            // C = 48's chunk-1 channels >= 48 read finite neighbours that meet zero weights
-            const _Float16* p = XL + trow[ni][kq] * XLR + 32 * ch + (kg ^ lds_rsw(trow[ni][kq]));
-            bh[ni] = RS_LD(p);
-            bl[ni] = RS_LD(p + C);
+        for (int ni = 0; ni < NI; ++ni) {
+          // unconditional: an inactive slot reads a clamped row and its result is dropped
+          int r, col;
+          if (!HALF || s < 3 * (NCH - 1)) {  // full chunk ch, tap s % 3, the lane's k octet kg
+            r = trow[ni][s % 3];
+            col = 32 * ch + kg;
+          } else {  // half chunk: lane-group pair gp = lane >> 5 picks the tap, octet 4 + (lane >> 4 & 1)
+            const int gp = lane >> 5;
+            r = s == 3 * (NCH - 1) ? (gp ? trow[ni][1] : trow[ni][0]) : trow[ni][2];
+            col = 32 * ch + 8 * ((lane >> 4) & 1);  // the second lane-group pair of the last
+                                                     // k-step reads these finite halves against
+                                                     // zero weights
           }
-          RS_SB();
-#pragma unroll
-          for (int ni = 0; ni < NI; ++ni)
-            RS_MMA(ring[s % R][0], ring[s % R][1], bh[ni], bl[ni], am[ni], ac[ni]);
-          wnext(ring[s % R], bi, s);
-          RS_SB();
+          const _Float16* p = XL + r * XLR + (col ^ lds_rsw(r));
+          bh[ni] = RS_LD(p);
+          bl[ni] = RS_LD(p + C);
         }
+        RS_SB();
+#pragma unroll
+        for (int ni = 0; ni < NI; ++ni)
+          RS_MMA(ring[(g0 + s) % R][0], ring[(g0 + s) % R][1], bh[ni], bl[ni], am[ni], ac[ni]);
+        wnext(ring[(g0 + s) % R], bi, s);
+        RS_SB();
       }
       // lrelu(h + b_d) into HX's h columns; rows outside [vlo, vhi) as zeros
       {
@@ -446,10 +465,10 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni)
           if (last)  // transposed (D = HX^T . Wf^T): the stores below write 4 positions of one channel
-            RS_MMA(bh[ni], bl[ni], ring[s % R][0], ring[s % R][1], am[ni], ac[ni]);
+            RS_MMA(bh[ni], bl[ni], ring[(g0 + s) % R][0], ring[(g0 + s) % R][1], am[ni], ac[ni]);
           else
-            RS_MMA(ring[s % R][0], ring[s % R][1], bh[ni], bl[ni], am[ni], ac[ni]);
-        wnext(ring[s % R], bi, s);
+            RS_MMA(ring[(g0 + s) % R][0], ring[(g0 + s) % R][1], bh[ni], bl[ni], am[ni], ac[ni]);
+        wnext(ring[(g0 + s) % R], bi, s);
         RS_SB();
       }
       const f32x4 bf = *reinterpret_cast<const f32x4*>(bias[bi][1] + co);
@@ -500,8 +519,10 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
         }
       }
     };
-    for (int bi = 0; bi < NB - 1; ++bi) block(bi, false);
-    block(NB - 1, true);
+    static_assert(NB == 3, "three fused blocks");
+    block(std::integral_constant<int, 0>{}, false);
+    block(std::integral_constant<int, 1>{}, false);
+    block(std::integral_constant<int, 2>{}, true);
     if (!more) break;
     RS_STAMP(14);
     lds_barrier();  // every wave is done with this tile's XL / HX
