@@ -1,5 +1,6 @@
 """Timeline of the last headline step in a rocprofv3 kernel trace: per-kernel start, gap to the
-previous kernel's end and duration, then span vs busy time.
+previous kernel's end and duration, then span vs busy time, and the idle time between the previous
+step's last kernel (out_pqmf) and this step's first (taco_setup).
   python tools/step_gaps.py gpurun_out/prof/run_kernel_trace.csv [--all]"""
 import csv
 import sys
@@ -8,11 +9,14 @@ rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Time
 idx = [i for i, r in enumerate(rows) if "persist_decoder_kernel<2, 8>" in r["Kernel_Name"]]
 i0 = idx[-1]
 j = i0
-while "embed_gather" not in rows[j]["Kernel_Name"]:
+while "taco_setup_kernel" not in rows[j]["Kernel_Name"]:
     j -= 1
 k = i0
 while k + 1 < len(rows) and "out_pqmf" not in rows[k]["Kernel_Name"]:
     k += 1
+p = j - 1
+while p > 0 and "out_pqmf" not in rows[p]["Kernel_Name"]:
+    p -= 1
 t0 = int(rows[j]["Start_Timestamp"])
 prev = t0
 busy = 0
@@ -20,7 +24,10 @@ show = "--all" in sys.argv
 for r in rows[j:k + 1]:
     s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
     busy += e - s
-    if show or s - prev > 2000 or e - s < 20000:
+    if show or s - prev > 2000 or e - s > 100000:
         print(f"{(s - t0) / 1e3:9.1f} gap={(s - prev) / 1e3:7.1f} dur={(e - s) / 1e3:8.1f}  {r['Kernel_Name'][:70]}")
     prev = max(prev, e)
-print(f"span {(prev - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, idle {(prev - t0 - busy) / 1e3:.1f} us")
+print(f"span {(prev - t0) / 1e3:.1f} us, busy {busy / 1e3:.1f} us, idle inside the step {(prev - t0 - busy) / 1e3:.1f} us")
+if p > 0:
+    print(f"previous step's out_pqmf end -> this step's taco_setup start: "
+          f"{(t0 - int(rows[p]['End_Timestamp'])) / 1e3:.1f} us")
