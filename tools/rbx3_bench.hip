@@ -51,6 +51,7 @@ static T* dup(const std::vector<T>& h) {
 }
 
 static double lrelu_d(double v) { return v >= 0 ? v : 0.2 * v; }
+static int g_variant = 0;  // check(): 0 the library tile, 1..3 the CPB sweep variants
 
 // CPU block on utterance b: x (C, Ls) -> y (C, L)
 static void cpu_block(const float* x, int C, int Ls, int L, int d, const std::vector<float>& wd,
@@ -105,7 +106,10 @@ static int check(int C, int d, float xscale) {
   a.oflow = dup(std::vector<unsigned>(1, 0));
   a.max_q = 301;
   a.B = B;
-  launch_resblock_x3(a, lens, C, S);
+  if (g_variant == 1) launch_rbx3<192, 48, 12, 1, 3, 2>(a, lens, S);
+  else if (g_variant == 2) launch_rbx3<192, 48, 12, 1, 3, 3>(a, lens, S);
+  else if (g_variant == 3) launch_rbx3<96, 64, 6, 1, 3, 3>(a, lens, S);
+  else launch_resblock_x3(a, lens, C, S);
   HIP_OK(hipStreamSynchronize(S));
   std::vector<float> y((size_t)B * C * Ls);
   HIP_OK(hipMemcpy(y.data(), a.y, y.size() * 4, hipMemcpyDeviceToHost));
@@ -140,6 +144,15 @@ int main(int argc, char** argv) {
     for (int d : {1, 9, 27}) fails += check(C, d, 1.f);
   for (int C : {32, 64, 128, 256}) fails += check(C, 3, 1.f);  // the full-band MelGAN stages
   fails += check(96, 3, 1e-3f);
+  // CPB variants (several chunks per barrier): bit-identical to the library tile by construction;
+  // checked against the CPU block like it
+  g_variant = 1;
+  for (int d : {1, 27}) fails += check(192, d, 1.f);
+  g_variant = 2;
+  for (int d : {1, 27}) fails += check(192, d, 1.f);
+  g_variant = 3;
+  for (int d : {1, 27}) fails += check(96, d, 1.f);
+  g_variant = 0;
   fails += check(96, 3, 1e5f);  // out of the f16 range: must raise the flag
   }
   int* lens;
@@ -233,12 +246,16 @@ int main(int argc, char** argv) {
       timeit("x3 TQ64 4x2 (MI3 NI2)", [&] { launch_rbx3<192, 64, 4, 2, 3>(a, kM, S); });
       timeit("x3 TQ64 4x1 (MI3 NI4)", [&] { launch_rbx3<192, 64, 4, 1, 3>(a, kM, S); });
       timeit("x3 TQ64 6x2 (MI2 NI2)", [&] { launch_rbx3<192, 64, 6, 2, 3>(a, kM, S); });
+      timeit("x3 TQ48 12x1 CPB2", [&] { launch_rbx3<192, 48, 12, 1, 3, 2>(a, kM, S); });
+      timeit("x3 TQ48 12x1 CPB3", [&] { launch_rbx3<192, 48, 12, 1, 3, 3>(a, kM, S); });
     } else if (C == 96) {
       timeit("x3 TQ128 6x2", [&] { launch_rbx3<96, 128, 6, 2, 3>(a, kM, S); });
       timeit("x3 TQ96 6x2 (NI3)", [&] { launch_rbx3<96, 96, 6, 2, 3>(a, kM, S); });
       timeit("x3 TQ64 6x2 (NI2)", [&] { launch_rbx3<96, 64, 6, 2, 3>(a, kM, S); });
       timeit("x3 TQ96 2x2 (MI3 NI3)", [&] { launch_rbx3<96, 96, 2, 2, 3>(a, kM, S); });
       timeit("x3 TQ128 2x4 (MI3 NI2)", [&] { launch_rbx3<96, 128, 2, 4, 3>(a, kM, S); });
+      timeit("x3 TQ64 6x2 CPB3 (NI2)", [&] { launch_rbx3<96, 64, 6, 2, 3, 3>(a, kM, S); });
+      timeit("x3 TQ64 6x1 CPB3 (NI4)", [&] { launch_rbx3<96, 64, 6, 1, 3, 3>(a, kM, S); });
     } else {
       timeit("x3 TQ128 3x4", [&] { launch_rbx3<48, 128, 3, 4, 3>(a, kM, S); });
       timeit("x3 TQ192 3x4 (NI3)", [&] { launch_rbx3<48, 192, 3, 4, 3>(a, kM, S); });

@@ -45,7 +45,6 @@
 
 namespace {
 constexpr int X3_DMAX = 27;   // largest dilation (3^3, num_res_blocks <= 4)
-constexpr int XR = 80;        // staging row, halves: 32 hi | 32 lo | 16 pad (160 B)
 
 __device__ __forceinline__ __amdgpu_buffer_rsrc_t rsrc(const void* p) {
   return __builtin_amdgcn_make_buffer_rsrc(const_cast<void*>(p), 0, 0x7fffffff, 0x00020000);
@@ -58,7 +57,11 @@ struct RbTile {
   int b, q0, L;
 };
 
-template <int C, int TQ, int WM, int WN, int R>
+// CPB (round 6): channel chunks of 32 staged per barrier interval. The staging row holds CPB chunks
+// ([32 CPB hi | 32 CPB lo | 16 pad]: a stride of 8 mod 16 dwords, conflict-free as the 1-chunk row),
+// so phase 1 runs 3 CPB k-steps between barriers instead of 3; the weights keep their k-step order
+// (chunk-major, tap-minor), so results are bit-identical for every CPB.
+template <int C, int TQ, int WM, int WN, int R, int CPB = 1>
 __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, int ntiles, bool vec) {
   constexpr int NTHR = 64 * WM * WN;
   constexpr int MI = C / 16 / WM;
@@ -66,6 +69,10 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   static_assert(MI * 16 * WM == C && NI * 16 * WN == TQ, "tile split");
   constexpr int NCH = (C + 31) / 32;     // staging chunks of 32 input channels (C = 48: 16 zero channels)
   constexpr int NK1 = 3 * NCH;           // phase-1 k-steps: (chunk, tap)
+  constexpr int W32 = 32 * CPB;          // channels staged per barrier interval ("super-chunk")
+  constexpr int NSC = NCH / CPB;         // super-chunks
+  constexpr int XRW = 2 * W32 + 16;      // staging row, halves
+  static_assert(NSC * CPB == NCH && (CPB == 1 || C % W32 == 0), "chunks per barrier");
   constexpr int NK2 = 2 * C / 32;        // phase-2 k-steps
   constexpr int NTOT = NK1 + NK2;        // weight sequence of one tile (the ring runs on across tiles)
   // R-slot weight ring: k-step s of a tile's sequence uses slot s % R, so R must divide both
@@ -73,15 +80,16 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   // C = 256 / 128: 4; C = 64 / 32: 2 / 1)
   static_assert(NK2 * 32 == 2 * C && NK1 % R == 0 && NK2 % R == 0, "weight ring: R must divide both phases");
   constexpr int HR = 4 * C + 16;         // HX row, halves: 2C hi | 2C lo | 16 pad (8C + 32 bytes)
-  constexpr int SPT = (4 * (TQ + 2 * X3_DMAX) + NTHR - 1) / NTHR;  // staging items (8 channels x 1 pos) per thread
+  constexpr int NO = 4 * CPB;  // channel octets per staged row
+  constexpr int SPT = (NO * (TQ + 2 * X3_DMAX) + NTHR - 1) / NTHR;  // staging items (8 channels x 1 pos) per thread
   extern __shared__ __attribute__((aligned(16))) _Float16 sh[];
 
   int t = blockIdx.x;
   const int d = a.dil;
   const int ROWS = TQ + 2 * d;
   _Float16* X0 = sh;
-  _Float16* X1 = sh + ROWS * XR;
-  _Float16* HX = sh + 2 * ROWS * XR;
+  _Float16* X1 = sh + ROWS * XRW;
+  _Float16* HX = sh + 2 * ROWS * XRW;
 
   const int tid = threadIdx.x;
   const int lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -153,9 +161,9 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
       // the channel octet passes through an opaque copy: otherwise the compiler hoists c0 * Ls of
       // every chunk out of the tile loop, and at C = 192 (168 VGPRs for 12 waves) spills them; each
       // scratch reload then came with a vmcnt(0) that drained the weight ring's prefetches
-      int g8 = min(sg[j], 3);
+      int g8 = min(sg[j], NO - 1);
       asm volatile("" : "+v"(g8));
-      const int c0 = min(32 * ch + 8 * g8, C - 8);
+      const int c0 = min(W32 * ch + 8 * g8, C - 8);
       const int vo = (c0 * a.Ls + i) * 4;  // per-lane offset; the 8 channel rows are SGPR offsets
 #pragma unroll
       for (int c = 0; c < 8; ++c)
@@ -166,8 +174,8 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 #pragma unroll
     for (int j = 0; j < SPT; ++j) {
       const int g = sg[j], row = srow[j];
-      if (g < 4) {
-        const bool real = 32 * ch + 8 * g < C;  // C = 48: the second chunk's upper half is zero
+      if (g < NO) {
+        const bool real = W32 * ch + 8 * g < C;  // C = 48: the second chunk's upper half is zero
         float v[8], mx = 0.f;
 #pragma unroll
         for (int c = 0; c < 8; ++c) {
@@ -181,12 +189,12 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
         h8 hi, lo;
         split8(lv, hi, lo);
         const int sx = (8 * g) ^ lds_rsw(row);
-        *reinterpret_cast<h8*>(X + row * XR + sx) = hi;
-        *reinterpret_cast<h8*>(X + row * XR + 32 + sx) = lo;
+        *reinterpret_cast<h8*>(X + row * XRW + sx) = hi;
+        *reinterpret_cast<h8*>(X + row * XRW + W32 + sx) = lo;
         const int p = row - d;
         if (real && p >= 0 && p < TQ) {  // raw x of the centre positions: the shortcut's operand
           split8(v, hi, lo);
-          const int hx = C + 32 * ch + ((8 * g) ^ lds_rsw(p));
+          const int hx = C + W32 * ch + ((8 * g) ^ lds_rsw(p));
           *reinterpret_cast<h8*>(HX + p * HR + hx) = hi;
           *reinterpret_cast<h8*>(HX + p * HR + 2 * C + hx) = lo;
         }
@@ -226,15 +234,15 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
   stage_load(cur, st[0], 0);
 #pragma unroll
   for (int u = 0; u < R; ++u) wload(ring[u], u);
-  if (NCH > 1) stage_load(cur, st[1], 1);
+  if (NSC > 1) stage_load(cur, st[1], 1);
   stage_store(X0, st[0], 0);
-  if (NCH > 2) stage_load(cur, st[0], 2);
+  if (NSC > 2) stage_load(cur, st[0], 2);
   lds_barrier();
   f32x4 am[MI][NI], ac[MI][NI];
   // EARLY (an even chunk count): the next tile's chunk k loads into the register set this tile's
   // chunk NCH - 2 + k vacates, i.e. during phase 1, a whole tile ahead of its use; with an odd
   // count the set parity would flip every tile, so those loads wait for phase 2
-  constexpr bool EARLY = NCH % 2 == 0;
+  constexpr bool EARLY = NSC % 2 == 0;
   // per-channel biases, loaded once (a load inside the tile loop would be the youngest in the
   // vmcnt order and make its wait drain every prefetch)
   float bdv[MI][4], bfv[MI];
@@ -258,36 +266,37 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     const RbTile nxt = more ? tile_of(tn) : cur;
     // the prefetch loads are issued unconditionally (a last tile re-loads itself): vmcnt is an
     // in-order counter, and a conditional load makes the compiler wait for everything (vmcnt(0))
-    if (EARLY && NCH == 2) stage_load(nxt, st[0], 0);
+    if (EARLY && NSC == 2) stage_load(nxt, st[0], 0);
     // ---------------- phase 1: h = Wd . lrelu(x) ----------------
 #pragma unroll
     for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
       for (int ni = 0; ni < NI; ++ni) am[mi][ni] = ac[mi][ni] = f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-    for (int ch = 0; ch < NCH; ++ch) {
+    for (int ch = 0; ch < NSC; ++ch) {
       const _Float16* X = (ch & 1) ? X1 : X0;
 #pragma unroll
-      for (int kq = 0; kq < 3; ++kq) {
-        const int sl = (ch * 3 + kq) % R;  // compile-time after unrolling
+      for (int jk = 0; jk < 3 * CPB; ++jk) {
+        const int jc = jk / 3, kq = jk % 3;                // chunk jc of the super-chunk, tap kq
+        const int sl = ((ch * CPB + jc) * 3 + kq) % R;     // compile-time after unrolling
         h8 bh[NI], bl[NI];
 #pragma unroll
         for (int ni = 0; ni < NI; ++ni) {
-          const _Float16* p = X + (nb + ni * 16 + kq * d) * XR + kgx[kq];
+          const _Float16* p = X + (nb + ni * 16 + kq * d) * XRW + 32 * jc + kgx[kq];
           bh[ni] = RB_LD(p);
-          bl[ni] = RB_LD(p + 32);
+          bl[ni] = RB_LD(p + W32);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
         for (int mi = 0; mi < MI; ++mi)
 #pragma unroll
           for (int ni = 0; ni < NI; ++ni) RB_MMA(ring[sl][mi][0], ring[sl][mi][1], bh[ni], bl[ni], am[mi][ni], ac[mi][ni]);
-        wload(ring[sl], ch * 3 + kq + R);
+        wload(ring[sl], (ch * CPB + jc) * 3 + kq + R);
         __builtin_amdgcn_sched_barrier(0);
       }
-      if (ch + 1 < NCH) stage_store((ch & 1) ? X0 : X1, st[(ch + 1) & 1], ch + 1);
-      if (ch + 3 < NCH) stage_load(cur, st[(ch + 1) & 1], ch + 3);
-      else if (EARLY && ch + 3 - NCH < 2) stage_load(nxt, st[(ch + 1) & 1], ch + 3 - NCH);
+      if (ch + 1 < NSC) stage_store((ch & 1) ? X0 : X1, st[(ch + 1) & 1], ch + 1);
+      if (ch + 3 < NSC) stage_load(cur, st[(ch + 1) & 1], ch + 3);
+      else if (EARLY && ch + 3 - NSC < 2) stage_load(nxt, st[(ch + 1) & 1], ch + 3 - NSC);
       lds_barrier();
     }
     RB_STAMP(1);
@@ -312,7 +321,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     // odd chunk count: the next tile's first two chunks load during phase 2
     if (!EARLY) {
       stage_load(nxt, st[0], 0);
-      if (NCH > 1) stage_load(nxt, st[1], 1);
+      if (NSC > 1) stage_load(nxt, st[1], 1);
     }
     RB_STAMP(2);
     // ---------------- phase 2: y = [W1 | Wsc] . [lrelu(h); x] ----------------
@@ -366,7 +375,7 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     cur = nxt;
     t = tn;
     stage_store(X0, st[0], 0);
-    if (NCH > 2) stage_load(cur, st[0], 2);
+    if (NSC > 2) stage_load(cur, st[0], 2);
     lds_barrier();
 #ifdef RB_TRACE
     ++it;
@@ -379,11 +388,11 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
 // one resident workgroup per CU (the LDS tile allows no more), each looping over tiles; the
 // dynamic LDS leaves 1 KiB of the CU's 160 KiB for the kernel's static tile tables
 constexpr int RB_DYN_LDS = 159 * 1024;
-template <int C, int TQ, int WM, int WN, int R>
+template <int C, int TQ, int WM, int WN, int R, int CPB = 1>
 static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   const int ROWS = TQ + 2 * a.dil;
-  const size_t lds = ((size_t)2 * ROWS * XR + (size_t)TQ * (4 * C + 16)) * 2;
-  ensure_dyn_lds((const void*)resblock_x3_kernel<C, TQ, WM, WN, R>, RB_DYN_LDS);
+  const size_t lds = ((size_t)2 * ROWS * (64 * CPB + 16) + (size_t)TQ * (4 * C + 16)) * 2;
+  ensure_dyn_lds((const void*)resblock_x3_kernel<C, TQ, WM, WN, R, CPB>, RB_DYN_LDS);
   const int ncu = device_cu_count();
   TTS_CHECK(lds <= RB_DYN_LDS, "resblock_x3: LDS tile too large");
   long ntiles = 0;
@@ -392,7 +401,7 @@ static void launch_rbx3(const ResArgs& a, const int* h_lens, hipStream_t s) {
   if (ntiles == 0) return;
   const int grid = (int)std::min<long>(ntiles, ncu);
   const bool vec = a.Ls % 4 == 0 && a.sb % 4 == 0 && (reinterpret_cast<uintptr_t>(a.y) & 15) == 0;
-  resblock_x3_kernel<C, TQ, WM, WN, R><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles, vec);
+  resblock_x3_kernel<C, TQ, WM, WN, R, CPB><<<grid, 64 * WM * WN, lds, s>>>(a, (int)ntiles, vec);
 }
 
 bool resblock_x3_supported(int C) { return C == 256 || C == 192 || C == 128 || C == 96 || C == 64 || C == 48 || C == 32; }
