@@ -25,6 +25,8 @@
  *   tts_pqmf_synthesis            <- PQMF.synthesis (TTS/vocoder/layers/pqmf.py:51-56)
  *   tts_taco_mbmelgan_infer       <- Tacotron2.inference then MultibandMelganGenerator.inference on its
  *                                    postnet output (TTS/server/synthesizer.py:150-159), one call
+ *   tts_taco_mbmelgan_submit/finish <- the same, returning once the decode's results are on the host
+ *                                    (the vocoder still running), completed by finish
  *
  * Conventions: every function returns 0 on success and nonzero on failure; the message is
  * available from tts_last_error() (thread-local). Pointers prefixed d_ are device (HIP) memory
@@ -238,12 +240,30 @@ int tts_gemm_mode(tts_ctx* ctx, int* mode, int64_t* fallbacks);
    product of the upsample factors). On return its first B * hop * (M + 2 pad) floats, M = r *
    max(h_steps), are the (B, 1, hop * (M + 2 pad)) waveform batch: bit-identical to
    tts_melgan_infer_strided on d_post viewed as (B, 80, M) with strides (S_cap r 80, 1, 80) and
-   lengths h_steps * r. One split-f16 range scope covers both models (an overflow re-runs the
-   whole call in fp32). */
+   lengths h_steps * r. The vocoder is launched on the decoded lengths as the decode leaves them on
+   the device (rows shorter than the vocoder's reflection pads fail the call), before the host
+   reads the decode's status words. Split-f16 range scopes as the two calls: a decode overflow
+   re-runs decode and vocoder in fp32, a vocoder overflow the vocoder alone. Returns with the
+   call's work done. */
 int tts_taco_mbmelgan_infer(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
                             const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
                             const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
                             int pad, float* d_wav, int32_t* h_steps, int32_t* h_status, void* stream);
+
+/* tts_taco_mbmelgan_infer in two halves, so that a caller can queue the next batch while this
+   one's vocoder runs. submit returns when h_steps / h_status are filled and hands out *h_ticket:
+   the decode's outputs are done and later work on `stream` is ordered after them, while the
+   vocoder may still be running on the library's stream. finish(ticket, stream) waits for that
+   vocoder and, if its split-f16 operands left the f16 range, runs it again on the fp32 kernels;
+   then d_wav is final and later work on `stream` is ordered after it. Until finish, the caller
+   must leave d_post and d_wav untouched and must not read d_wav. At most 4 submissions are outstanding per context: a fifth submit finishes the oldest
+   first. finish on a ticket that is already complete returns 0. */
+int tts_taco_mbmelgan_submit(tts_ctx* ctx, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                             const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
+                             const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
+                             int pad, float* d_wav, int32_t* h_steps, int32_t* h_status, int64_t* h_ticket,
+                             void* stream);
+int tts_taco_mbmelgan_finish(tts_ctx* ctx, int64_t ticket, void* stream);
 
 /* Test hook (process-wide, off by default): recurrence >= 0 makes one workgroup of that persistent
    BiLSTM recurrence leave before its second grid barrier, so the others time out and the next

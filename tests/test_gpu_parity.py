@@ -1659,6 +1659,79 @@ def test_fused_taco_mbmelgan_equals_two_calls(pad):
     assert wa.shape[-1] == voc.hop * (max(ml) + 2 * pad)
 
 
+def test_fused_submit_pipelined_and_short_decode():
+    """The fused call's two halves (tts_taco_mbmelgan_submit / _finish) with the host one batch
+    ahead, as bench.py times it: two batches with different ragged forced lengths submitted back to
+    back, then both finished; each batch bit-identical to its two-call form. Then the vocoder
+    launched on device-side lengths below the S_cap bound (S_cap = max steps + 7: the waveform rows
+    are packed back to hop (M + 2 pad) samples apart), blocking and submitted; and a decode whose
+    rows stop at step 2 (stop threshold -1, r = 1: 2 mel frames, shorter than ReflectionPad1d(3)
+    allows) fails the call with the vocoder's length message, the context usable afterwards."""
+    import bench
+    from tts_amd._lib import get_engine
+    from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids
+    dev = _dev()
+    taco, tsd, voc, vsd, tcfg, vcfg = bench.build_models(dev)
+    taco.decoder.set_r(2)
+    taco.decoder.verbose = False
+    T_prof, M_prof = lj_profile()
+    ids = synthetic_ids(T_prof)
+    batch, lens = pad_batch(ids)
+    x = torch.from_numpy(batch).to(dev)
+    full = forced_steps(M_prof, 2)
+    steps_a = [max(3, s_ // 5) for s_ in full]
+    steps_b = [max(3, s_ // 7) for s_ in full][::-1]
+
+    def two_calls(steps):
+        a = taco.inference(x, text_lengths=lens, max_decoder_steps=steps)
+        return a + (voc.inference(a[1].transpose(1, 2), lengths=taco.last_mel_lengths.copy()),)
+
+    with torch.no_grad():
+        ref_a, ref_b = two_calls(steps_a), two_calls(steps_b)
+        fa = taco.inference_vocoded_submit(x, voc, text_lengths=lens, max_decoder_steps=steps_a)
+        fb = taco.inference_vocoded_submit(x, voc, text_lengths=lens, max_decoder_steps=steps_b)
+        got_a, got_b = fa.result(), fb.result()
+        assert fa.result() is not None  # finishing twice is harmless
+    for ref, got in ((ref_a, got_a), (ref_b, got_b)):
+        for u, v in zip(ref, got):
+            assert u.shape == v.shape and torch.equal(u, v)
+
+    # S_cap above the decoded steps: rows packed after the vocoder, blocking and submitted
+    eng = get_engine(dev)
+    Tn, B, r, pad = int(max(lens)), len(ids), 2, int(voc.inference_padding)
+    S_cap = max(steps_a) + 7
+    sub = x[:, :Tn].contiguous()
+    for submit in (False, True):
+        dec, post, align, stop = taco._out_tensors(B, S_cap, r, Tn, dev)
+        wbuf = torch.full((B * voc.hop * (S_cap * r + 2 * pad),), float("nan"), device=dev)
+        args = (sub, lens, r, np.asarray(steps_a), S_cap, taco.decoder.stop_threshold, dec, post, align, stop, pad, wbuf)
+        with eng.lock:
+            if submit:
+                st, _, ticket = eng.taco_mbmelgan_submit(*args)
+                eng.taco_mbmelgan_finish(ticket, dev)
+            else:
+                st, _ = eng.taco_mbmelgan_infer(*args)
+        assert list(st) == steps_a
+        L = voc.hop * (max(steps_a) * r + 2 * pad)
+        assert torch.equal(wbuf[:B * L].view(B, 1, L), ref_a[4])
+        assert torch.equal(post[:, :max(steps_a) * r], ref_a[1])
+
+    # rows that stop at step 2 at r = 1: 2 frames, below the vocoder's reflection pad
+    taco.decoder.set_r(1)
+    thr = taco.decoder.stop_threshold
+    taco.decoder.stop_threshold = -1.0
+    try:
+        with torch.no_grad(), pytest.raises(RuntimeError, match="shorter than the vocoder"):
+            taco.inference_vocoded(x, voc, text_lengths=lens, max_decoder_steps=[10] * B)
+    finally:
+        taco.decoder.stop_threshold = thr
+        taco.decoder.set_r(2)
+    with torch.no_grad():
+        again = taco.inference_vocoded(x, voc, text_lengths=lens, max_decoder_steps=steps_a)
+    for u, v in zip(ref_a, again):
+        assert torch.equal(u, v)
+
+
 def test_bench_workload_full_size_r1_vs_oracle():
     """The bench line's r = 1 run at its full length (bench.py `r1`: the same 32 LJ-profile
     utterances, forced lengths of up to 857 decoder steps, one frame per step as the

@@ -6,6 +6,7 @@ missing, every entry point raises ``RuntimeError``.
 """
 
 import atexit
+import collections
 import ctypes
 import os
 import threading
@@ -41,6 +42,10 @@ SIGNATURES = [
     ("tts_taco_mbmelgan_infer", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
                                                _c_int_p, ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
                                                _vp, ctypes.c_int, _vp, _c_int_p, _c_int_p, _vp]),
+    ("tts_taco_mbmelgan_submit", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, ctypes.c_int,
+                                                _c_int_p, ctypes.c_int, ctypes.c_float, _vp, _vp, _vp, _vp, _vp,
+                                                _vp, ctypes.c_int, _vp, _c_int_p, _c_int_p, _c_i64_p, _vp]),
+    ("tts_taco_mbmelgan_finish", ctypes.c_int, [_vp, ctypes.c_int64, _vp]),
     ("tts_taco_speaker_dim", ctypes.c_int, [_vp, _c_i_p, _c_i_p]),
     ("tts_taco_set_options", ctypes.c_int, [_vp, ctypes.c_int, ctypes.c_int, ctypes.c_int]),
     ("tts_taco_encoder", ctypes.c_int, [_vp, _vp, _c_int_p, ctypes.c_int, ctypes.c_int, _vp, _vp]),
@@ -127,6 +132,7 @@ class Engine:
         # this device, and ctypes releases the GIL inside each call. (Each C entry point also locks
         # the context; this lock makes multi-call sequences such as Glow encode + decode atomic.)
         self.lock = threading.RLock()
+        self._live = collections.OrderedDict()  # ticket -> (post, wav) of unfinished fused submissions
         h = ctypes.c_void_p()
         _check(self.lib.tts_ctx_create(device_index, ctypes.byref(h)))
         self.h = h
@@ -201,6 +207,37 @@ class Engine:
                                                 _ptr(wav), steps.ctypes.data_as(_c_int_p),
                                                 status.ctypes.data_as(_c_int_p), _stream(ids.device)))
         return steps, status
+
+    def taco_mbmelgan_submit(self, ids, lens, r, max_steps, S_cap, stop_threshold, dec, post, align, stop, pad, wav,
+                             speaker_ids=None, speaker_embeddings=None):
+        """The first half of taco_mbmelgan_infer (tts_taco_mbmelgan_submit): returns (steps, status,
+        ticket) once the decode is done, the vocoder still running; ``post`` and ``wav`` must stay
+        untouched until ``taco_mbmelgan_finish(ticket)``."""
+        B, T = ids.shape
+        lens_a, lens_p = _i32(lens)
+        ms_a, ms_p = _i32(max_steps)
+        steps = np.zeros(B, np.int32)
+        status = np.zeros(B, np.int32)
+        ticket = ctypes.c_int64(0)
+        sid = None if speaker_ids is None else _ptr(speaker_ids)
+        semb = None if speaker_embeddings is None else _ptr(speaker_embeddings)
+        _check(self.lib.tts_taco_mbmelgan_submit(self.h, _ptr(ids), lens_p, B, T, r, ms_p, S_cap, float(stop_threshold),
+                                                 sid, semb, _ptr(dec), _ptr(post), _ptr(align), _ptr(stop), int(pad),
+                                                 _ptr(wav), steps.ctypes.data_as(_c_int_p),
+                                                 status.ctypes.data_as(_c_int_p), ctypes.byref(ticket),
+                                                 _stream(ids.device)))
+        # a fp32 re-run at finish reads post and writes wav: keep them allocated while the library
+        # may still do that (it finishes a ticket at the latest when the 5th submission after it
+        # reuses its slot)
+        self._live[ticket.value] = (post, wav)
+        while len(self._live) > 4:
+            self._live.popitem(last=False)
+        return steps, status, ticket.value
+
+    def taco_mbmelgan_finish(self, ticket, device):
+        """Completes a submission (tts_taco_mbmelgan_finish): its waveforms are final after this."""
+        _check(self.lib.tts_taco_mbmelgan_finish(self.h, int(ticket), _stream(device)))
+        self._live.pop(int(ticket), None)
 
     def taco_speaker_dim(self):
         d, n = ctypes.c_int(0), ctypes.c_int(0)

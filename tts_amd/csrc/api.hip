@@ -11,6 +11,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <functional>
 #include <map>
 #include <memory>
 #include <mutex>
@@ -334,7 +335,7 @@ constexpr int PMAX_LAUNCH = 4;  // persistent decoder launches per decode (MT = 
 constexpr int PBAR_CAND = 16;   // candidate barrier blocks timed for them
 constexpr int ENC_NDOM_MAX = 4;  // BiLSTM recurrences (barrier blocks) per launch
 constexpr int TS_ENC = 16, TS_DEC = TS_ENC + ENC_NDOM_MAX, TS_RES = TS_DEC + PMAX_LAUNCH, TS_FLAG = TS_RES + 3 * BMAX,
-              TS_END = TS_FLAG + 1, TS_N = TS_END + PMAX_LAUNCH;
+              TS_END = TS_FLAG + 1, TS_VERR = TS_END + PMAX_LAUNCH, TS_N = TS_VERR + 1;
 static_assert(TS_N <= 240, "status words fit the pinned block below check_encoder_barrier's words");
 
 struct TacoWS {
@@ -480,14 +481,31 @@ struct PwganWS {
   DevBuf lens, ca, cb, xa, xb, skip, zeros;
 };
 
+// one submitted fused call: what its fp32 re-run needs if the split-f16 vocoder raised the range
+// flag (the caller keeps d_post and d_wav untouched until the ticket is finished)
+constexpr int NVT = 4, TK_PIN = 248;
+struct VocTicket {
+  int64_t id = 0;
+  bool pending = false;       // not finished: the caller's stream is not yet ordered after the vocoder
+  bool x3 = false;            // vocoder launched on split-f16 kernels: its range flag is to be looked at
+  hipEvent_t ev = nullptr;    // recorded after the vocoder, the copy of its flag and the row packing
+  const float* d_post = nullptr;
+  int64_t st[3] = {0, 0, 0};
+  std::vector<int32_t> lens;  // decoded mel lengths, caller order
+  int B = 0, M = 0, pad = 0;
+  float* d_wav = nullptr;
+};
+
 struct tts_ctx {
   std::recursive_mutex mu;  // held by every entry point (guarded_ctx)
   int device = 0;
   hipStream_t s = nullptr;
   hipEvent_t ev_in = nullptr, ev_out = nullptr, ev_chunk[2] = {nullptr, nullptr};
   hipEvent_t ev_dec[PMAX_LAUNCH + 1] = {};  // around the persistent decoder launches
+  hipEvent_t ev_status = nullptr;  // a fused call's decode status words are on the host
   int* pinned = nullptr;  // [256]: [0:4) chunk polling, [12] range flag, [TS_*]: status words of the last
-                          // Tacotron2 call (one copy of TacoWS::stat)
+                          // Tacotron2 call (one copy of TacoWS::stat), [240:244) BiLSTM barrier
+                          // words, [TK_PIN + k]: range flag of the vocoder of ticket slot k
   bool flag_read = false; // the entry point already fetched the range flag into pinned[12]
   int dec_end[PMAX_LAUNCH] = {};  // step index after each persistent launch of the last decode
   int dec_path = 0;       // last decode: 0 = step graphs, 1 = persistent kernel
@@ -514,6 +532,9 @@ struct tts_ctx {
   GlowWS glws;
   // last decode configuration (for tts_time_decoder_kernel)
   int last_B = 0, last_T = 0, last_S = 0, last_r = 0;
+  // fused Tacotron2 + MB-MelGAN submissions whose vocoder may still run (tts_taco_mbmelgan_submit)
+  VocTicket vt[NVT];
+  int64_t next_ticket = 1;
 };
 
 // range flag for the split-f16 kernels of the current call, or null (fp32 kernels)
@@ -1306,9 +1327,23 @@ __global__ void taco_mlens_kernel(const int* ctl, int B, int r, int* mlens) {
 struct DecSlots {
   int v[PMAX_LAUNCH];
 };
+// A fused call (vlens set) also writes the vocoder's mel lengths in caller order, steps * r of
+// decode row inv[b], raised to Lmin where shorter (TS_VERR: the call fails)
 __global__ void taco_status_kernel(const unsigned* enc_bar, int nenc, const unsigned* dec_bar, DecSlots dslot, int ndec,
-                                   const int* ctl, const unsigned* flag, int* st) {
+                                   const int* ctl, const unsigned* flag, int* st, int B, const int* inv, int r,
+                                   int Lmin, int* vlens) {
   const int i = threadIdx.x;
+  int short_row = 0;
+  if (vlens && i < B) {
+    int L = ctl[4 + BMAX + inv[i]] * r;
+    if (L < Lmin) {
+      short_row = 1;
+      L = Lmin;
+    }
+    vlens[i] = L;
+  }
+  short_row = __syncthreads_or(short_row);
+  if (i == 0) st[TS_VERR] = short_row;
   if (i < 3 * BMAX) st[TS_RES + i] = ctl[4 + i];
   if (i < ENC_NDOM_MAX) st[TS_ENC + i] = enc_bar && i < nenc ? (int)enc_bar[i * BAR_WORDS + 16] : 0;
   if (i < PMAX_LAUNCH) {
@@ -1568,10 +1603,22 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   }
 }
 
+// the vocoder half of a fused Tacotron2 + MB-MelGAN call: the decode's status kernel writes the
+// vocoder's lengths into vlens (device, caller order), and enqueue() launches the vocoder on them
+// before the host waits for the status words, so the GPU runs both models back to back
+constexpr const char* VOC_SHORT_MSG =
+    "MB-MelGAN: a decoded mel is shorter than the vocoder's reflection pads allow (ReflectionPad1d(3): mel frames "
+    "+ 2*padding must be >= 4; a residual stack's dilation must be < the first stage's length)";
+struct FusedVoc {
+  int* vlens;
+  int Lmin;
+  std::function<void()> enqueue;
+};
+
 void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, int T_max, int r,
                 const int32_t* h_max_steps, int S_cap, float thr, float* d_dec, float* d_post, float* d_align,
                 float* d_stop, int32_t* h_steps, int32_t* h_status, void* stream,
-                const int64_t* d_spk_ids = nullptr, const float* d_spk_emb = nullptr) {
+                const int64_t* d_spk_ids = nullptr, const float* d_spk_emb = nullptr, const FusedVoc* fv = nullptr) {
   auto& M = c->taco;
   TTS_CHECK(M.ready, "tacotron2 weights not finalized");
   TTS_CHECK(B >= 1 && B <= BMAX, "B must be in [1, 64]");
@@ -1730,11 +1777,18 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     const unsigned* lc = reinterpret_cast<const unsigned*>(W.lc.p);
     taco_status_kernel<<<1, 256, 0, s>>>(W.enc_persist ? lc : nullptr, W.enc_ndom,
                                          persist ? reinterpret_cast<const unsigned*>(W.pbar.p) : nullptr,
-                                         DecSlots{{W.pslot[0], W.pslot[1], W.pslot[2], W.pslot[3]}}, c->dec_nlaunch, W.ctl.i(), c->gemm_x3 ? x3_flag(c) : nullptr, W.stat.i());
+                                         DecSlots{{W.pslot[0], W.pslot[1], W.pslot[2], W.pslot[3]}}, c->dec_nlaunch, W.ctl.i(), c->gemm_x3 ? x3_flag(c) : nullptr, W.stat.i(),
+                                         B, d_map + BMAX, r, fv ? fv->Lmin : 0, fv ? fv->vlens : nullptr);
     HIP_OK(hipGetLastError());
     int* pin = c->pinned;
     HIP_OK(hipMemcpyAsync(pin + TS_ENC, W.stat.i() + TS_ENC, (TS_N - TS_ENC) * 4, hipMemcpyDeviceToHost, s));
-    HIP_OK(hipStreamSynchronize(s));
+    if (fv) {  // the vocoder goes in behind the status words; the host waits for the words only
+      HIP_OK(hipEventRecord(c->ev_status, s));
+      fv->enqueue();
+      HIP_OK(hipEventSynchronize(c->ev_status));
+    } else {
+      HIP_OK(hipStreamSynchronize(s));
+    }
     TTS_CHECK(!W.enc_persist || (pin[TS_ENC] == 0 && pin[TS_ENC + 1] == 0 && pin[TS_ENC + 2] == 0 && pin[TS_ENC + 3] == 0),
               "persistent BiLSTM: grid barrier timed out (workgroups not co-resident) or preempted past "
               "TTS_BARRIER_TIMEOUT_MS; retrying the call is safe)");
@@ -1746,6 +1800,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
       c->flag_read = true;
     }
     for (int i = 0; i < PMAX_LAUNCH; ++i) c->dec_end[i] = persist && i < c->dec_nlaunch ? pin[TS_END + i] : 0;
+    TTS_CHECK(!fv || pin[TS_VERR] == 0, VOC_SHORT_MSG);
   }
   const int* res = c->pinned + TS_RES;
   for (int i = 0; i < B; ++i) {
@@ -1754,7 +1809,10 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     h_steps[b] = res[BMAX + i];
     h_status[b] = res[2 * BMAX + i];
   }
-  leave(c, stream);
+  if (fv)  // the caller's stream waits for the decode's outputs here, for the vocoder at finish
+    HIP_OK(hipStreamWaitEvent((hipStream_t)stream, c->ev_status, 0));
+  else
+    leave(c, stream);
   c->last_B = B;
   c->last_T = T_max;
   c->last_S = S_cap;
@@ -1938,13 +1996,15 @@ static bool ct_fuse_on() {
 }
 
 // returns total upsampling factor; writes bands (B, out_ch, up*(M_max+2pad)) into `out`
+// dev_lens: W.lens already holds the lengths on the device (a fused call's decode wrote them,
+// checked there against vocoder_min_len); h_lens are then per-row upper bounds, used for tile counts
 int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, int M_max, int pad, float* out,
-                  hipStream_t s, GenTail* tail = nullptr, const int64_t* mel_strides = nullptr) {
+                  hipStream_t s, GenTail* tail = nullptr, const int64_t* mel_strides = nullptr, bool dev_lens = false) {
   auto& G = c->mg;
   auto& W = c->mws;
   TTS_CHECK(G.ready, "melgan weights not finalized");
   TTS_CHECK(B >= 1, "B >= 1");
-  for (int b = 0; b < B; ++b) {
+  for (int b = 0; b < B && !dev_lens; ++b) {
     TTS_CHECK(h_lens[b] >= 1 && h_lens[b] <= M_max, "mel lens out of range");
     TTS_CHECK(h_lens[b] + 2 * pad >= 4, "ReflectionPad1d(3): mel frames + 2*padding must be >= 4");
     for (int k = 0; k < G.nres && !G.ups.empty(); ++k)  // ResidualStack ReflectionPad1d(dilation), stage 0
@@ -1967,7 +2027,8 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   W.xa.ensure((size_t)B * maxelems * 4);
   W.xb.ensure((size_t)B * maxelems * 4);
   std::vector<int> lens(h_lens, h_lens + B);
-  HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  if (!dev_lens) HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  else TTS_CHECK(W.lens.bytes >= (size_t)B * 4, "vocoder lengths buffer");
   ConvCall cc;
   cc.lens = W.lens.i();
   cc.B = B;
@@ -3124,6 +3185,8 @@ int tts_ctx_create(int device, tts_ctx** out) {
     HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[0], hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[1], hipEventDisableTiming));
     for (auto& e : c->ev_dec) HIP_OK(hipEventCreate(&e));
+    HIP_OK(hipEventCreateWithFlags(&c->ev_status, hipEventDisableTiming));
+    for (auto& t : c->vt) HIP_OK(hipEventCreateWithFlags(&t.ev, hipEventDisableTiming));
     HIP_OK(hipHostMalloc(reinterpret_cast<void**>(&c->pinned), 1024, hipHostMallocDefault));
     std::memset(c->pinned, 0, 1024);
     *out = c.release();
@@ -3149,6 +3212,8 @@ int tts_ctx_destroy(tts_ctx* c) {
       hipStream_t s = c->s;
       std::vector<hipEvent_t> e = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1]};
       for (auto ev : c->ev_dec) e.push_back(ev);
+      e.push_back(c->ev_status);
+      for (auto& t : c->vt) e.push_back(t.ev);
       int* pin = c->pinned;
       delete c;
       for (auto ev : e) (void)hipEventDestroy(ev);
@@ -3439,7 +3504,7 @@ int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, 
 // MultibandMelganGenerator.inference body on c->s: generator, output conv and PQMF synthesis into
 // d_wav (B, 1, hop * (M_max + 2 pad)), rows zero past their own length
 static void mbmelgan_body(tts_ctx* c, const float* d_mel, const int64_t* mel_strides, const int32_t* h_lens, int B,
-                          int M_max, int pad, float* d_wav) {
+                          int M_max, int pad, float* d_wav, bool dev_lens = false) {
   auto& G = c->mg;
   int up = 1;
   for (int u : G.ups) up *= u;
@@ -3448,14 +3513,14 @@ static void mbmelgan_body(tts_ctx* c, const float* d_mel, const int64_t* mel_str
   const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
   if (fused) {
     GenTail t;
-    run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t, mel_strides);
+    run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t, mel_strides, dev_lens);
     TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
     TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
                               G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
               "fused output/PQMF shape not covered");
   } else {
     c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
-    run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s, nullptr, mel_strides);
+    run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s, nullptr, mel_strides, dev_lens);
     launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
                           2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
   }
@@ -3475,37 +3540,166 @@ static int melgan_infer_impl(tts_ctx* c, const float* d_mel, const int64_t* mel_
   });
 }
 
+// the shortest mel (frames) the vocoder accepts at inference padding pad: run_generator's checks
+static int vocoder_min_len(const MelganModel& G, int pad) {
+  int L = std::max(1, 4 - 2 * pad);
+  for (int k = 0; k < G.nres && !G.ups.empty(); ++k)
+    while ((long)(L + 2 * pad) * G.ups[0] <= G.dconv[k].dil) ++L;
+  return L;
+}
+
+// completes a submitted fused call: if its split-f16 vocoder raised the range flag, the vocoder
+// runs again on the fp32 kernels from the postnet output (the two-call path's fallback); then the
+// caller's stream is ordered after it
+static void finish_ticket(tts_ctx* c, VocTicket& tk, void* stream) {
+  if (!tk.pending) return;
+  tk.pending = false;
+  if (tk.x3) {
+    HIP_OK(hipEventSynchronize(tk.ev));
+    if (c->pinned[TK_PIN + tk.id % NVT]) {
+      c->x3_fallbacks++;
+      c->gemm_x3 = false;
+      try {
+        mbmelgan_body(c, tk.d_post, tk.st, tk.lens.data(), tk.B, tk.M, tk.pad, tk.d_wav);
+      } catch (...) {
+        c->gemm_x3 = true;
+        throw;
+      }
+      c->gemm_x3 = true;
+      HIP_OK(hipEventRecord(tk.ev, c->s));
+    }
+  }
+  HIP_OK(hipStreamWaitEvent((hipStream_t)stream, tk.ev, 0));
+}
+
+// Tacotron2 decode + MB-MelGAN, submitted: the vocoder is launched on the device-side decoded
+// lengths before the host waits for the decode's status words, and the call returns with the
+// vocoder still running (ticket); finish_ticket completes it.
+static int64_t taco_mbmelgan_submit(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                                    const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
+                                    const float* d_spk_emb, float* d_dec, float* d_post, float* d_align,
+                                    float* d_stop, int pad, float* d_wav, int32_t* h_steps, int32_t* h_status,
+                                    void* stream) {
+  TTS_CHECK(d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && d_wav && h_steps && h_status,
+            "null argument");
+  TTS_CHECK(pad >= 0, "pad >= 0");
+  auto& G = c->mg;
+  TTS_CHECK(G.ready && G.pqmf, "melgan (with PQMF) not finalized");
+  TTS_CHECK(G.in_ch == 80, "vocoder input channels must be the decoder's 80 mel channels");
+  TTS_CHECK(B >= 1 && B <= BMAX && r >= 1, "bad sizes");
+  const int64_t id = c->next_ticket++;
+  VocTicket& tk = c->vt[id % NVT];
+  finish_ticket(c, tk, stream);  // the slot's previous submission completes first
+  tk.id = id;
+  // per-row upper bounds of the decoded lengths (tile counts of the vocoder's persistent kernels)
+  const int Lmin = vocoder_min_len(G, pad);
+  std::vector<int32_t> bound(B);
+  for (int b = 0; b < B; ++b) {
+    TTS_CHECK(h_max_steps[b] >= 1 && h_max_steps[b] <= S_cap, "max_steps out of range");
+    bound[b] = h_max_steps[b] * r;
+    TTS_CHECK(bound[b] >= Lmin, VOC_SHORT_MSG);
+  }
+  c->mws.lens.ensure(BMAX * 4);
+  const int64_t st[3] = {(int64_t)S_cap * r * 80, 1, 80};
+  bool voc_x3 = false;
+  int* slot = c->pinned + TK_PIN + id % NVT;
+  FusedVoc fv{c->mws.lens.i(), Lmin, [&] {
+                voc_x3 = c->gemm_x3;
+                // the vocoder's input is the postnet output read in place, frame-major; rows are
+                // hop (S_cap r + 2 pad) samples apart until the decoded lengths are on the host
+                mbmelgan_body(c, d_post, st, bound.data(), B, S_cap * r, pad, d_wav, /*dev_lens=*/true);
+                if (voc_x3) HIP_OK(hipMemcpyAsync(slot, x3_flag(c), 4, hipMemcpyDeviceToHost, c->s));
+              }};
+  if (c->gemm_x3) HIP_OK(hipMemsetAsync(x3_flag(c), 0, 4, c->s));  // behind earlier calls' flag copies on c->s
+  c->flag_read = false;
+  taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+             h_status, stream, d_spk_ids, d_spk_emb, &fv);
+  const bool taco_oflow = c->gemm_x3 && c->flag_read && c->pinned[12];
+  c->flag_read = false;
+  int S = 0;
+  for (int b = 0; b < B; ++b) S = std::max(S, (int)h_steps[b]);
+  std::vector<int32_t> mlens(B);
+  for (int b = 0; b < B; ++b) mlens[b] = h_steps[b] * r;
+  int up = 1;
+  for (int u : G.ups) up *= u;
+  const size_t row = (size_t)G.out_ch * up;  // hop: samples per mel frame
+  if (taco_oflow) {
+    // the decode left the f16 range: decode and vocoder again on the fp32 kernels (the split
+    // vocoder already queued is overwritten), as the two separate calls would each have done
+    c->x3_fallbacks++;
+    c->gemm_x3 = false;
+    try {
+      taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+                 h_status, stream, d_spk_ids, d_spk_emb);
+      S = 0;
+      for (int b = 0; b < B; ++b) {
+        S = std::max(S, (int)h_steps[b]);
+        mlens[b] = h_steps[b] * r;
+      }
+      mbmelgan_body(c, d_post, st, mlens.data(), B, S * r, pad, d_wav);
+    } catch (...) {
+      c->gemm_x3 = true;
+      throw;
+    }
+    c->gemm_x3 = true;
+    leave(c, stream);
+    return id;
+  }
+  if (S < S_cap) {  // pack the rows to hop (S r + 2 pad) samples apart, as the two calls return them
+    const size_t P = row * ((size_t)S * r + 2 * pad), Pc = row * ((size_t)S_cap * r + 2 * pad);
+    c->mws.bands.ensure((size_t)B * P * 4);
+    HIP_OK(hipMemcpy2DAsync(c->mws.bands.p, P * 4, d_wav, Pc * 4, P * 4, B, hipMemcpyDeviceToDevice, c->s));
+    HIP_OK(hipMemcpyAsync(d_wav, c->mws.bands.p, (size_t)B * P * 4, hipMemcpyDeviceToDevice, c->s));
+  }
+  HIP_OK(hipEventRecord(tk.ev, c->s));
+  tk.pending = true;
+  tk.x3 = voc_x3;
+  tk.d_post = d_post;
+  std::copy(st, st + 3, tk.st);
+  tk.lens = mlens;
+  tk.B = B;
+  tk.M = S * r;
+  tk.pad = pad;
+  tk.d_wav = d_wav;
+  return id;
+}
+
+int tts_taco_mbmelgan_submit(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
+                             const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
+                             const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
+                             int pad, float* d_wav, int32_t* h_steps, int32_t* h_status, int64_t* h_ticket,
+                             void* stream) {
+  return guarded_ctx(c, [&] {
+    TTS_CHECK(c && h_ticket, "null argument");
+    DeviceGuard g(c->device);
+    *h_ticket = taco_mbmelgan_submit(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_spk_ids, d_spk_emb,
+                                     d_dec, d_post, d_align, d_stop, pad, d_wav, h_steps, h_status, stream);
+  });
+}
+
+int tts_taco_mbmelgan_finish(tts_ctx* c, int64_t ticket, void* stream) {
+  return guarded_ctx(c, [&] {
+    TTS_CHECK(c, "null ctx");
+    TTS_CHECK(ticket >= 1 && ticket < c->next_ticket, "unknown ticket");
+    DeviceGuard g(c->device);
+    VocTicket& tk = c->vt[ticket % NVT];
+    if (tk.id == ticket) finish_ticket(c, tk, stream);  // else a later submission already finished it
+  });
+}
+
 int tts_taco_mbmelgan_infer(tts_ctx* c, const int64_t* d_ids, const int32_t* h_lens, int B, int T_max, int r,
                             const int32_t* h_max_steps, int S_cap, float thr, const int64_t* d_spk_ids,
                             const float* d_spk_emb, float* d_dec, float* d_post, float* d_align, float* d_stop,
                             int pad, float* d_wav, int32_t* h_steps, int32_t* h_status, void* stream) {
   return guarded_ctx(c, [&] {
-    TTS_CHECK(c && d_ids && h_lens && h_max_steps && d_dec && d_post && d_align && d_stop && d_wav && h_steps &&
-                  h_status,
-              "null argument");
-    TTS_CHECK(pad >= 0, "pad >= 0");
-    TTS_CHECK(c->mg.ready && c->mg.pqmf, "melgan (with PQMF) not finalized");
-    TTS_CHECK(c->mg.in_ch == 80, "vocoder input channels must be the decoder's 80 mel channels");
+    TTS_CHECK(c, "null ctx");
     DeviceGuard g(c->device);
-    std::vector<int32_t> mlens(B);
-    // one range-flag scope over both models: a split-f16 overflow anywhere re-runs the whole call
-    // in fp32 (decode included), as the two separate calls would each have done
-    with_x3_fallback(c, [&] {
-      taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
-                 h_status, stream, d_spk_ids, d_spk_emb);
-      if (c->gemm_x3 && c->flag_read && c->pinned[12]) return;  // the decode overflowed: re-run it all
-      c->flag_read = false;  // the vocoder raises the same flag: with_x3_fallback reads it after it
-      // the decoded lengths go from the decode's status words (already on the host) straight to
-      // the vocoder, whose input is the postnet output read in place, frame-major
-      int S = 0;
-      for (int b = 0; b < B; ++b) {
-        S = std::max(S, (int)h_steps[b]);
-        mlens[b] = h_steps[b] * r;
-      }
-      const int64_t st[3] = {(int64_t)S_cap * r * 80, 1, 80};
-      mbmelgan_body(c, d_post, st, mlens.data(), B, S * r, pad, d_wav);
-      leave(c, stream);
-    });
+    const int64_t id = taco_mbmelgan_submit(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_spk_ids,
+                                            d_spk_emb, d_dec, d_post, d_align, d_stop, pad, d_wav, h_steps, h_status,
+                                            stream);
+    VocTicket& tk = c->vt[id % NVT];
+    if (tk.id == id) finish_ticket(c, tk, stream);
+    HIP_OK(hipStreamSynchronize(c->s));  // returns with the call's work done, as before
   });
 }
 

@@ -213,7 +213,8 @@ struct ResArgs {
 void launch_resblock(const ResArgs& a, int C, hipStream_t s);
 bool resblock_x3_supported(int C);
 // persistent: one workgroup per CU loops over the (utterance, position) tiles; h_lens = the
-// host copy of lens (tile count)
+// host copy of lens, or per-row upper bounds of the device lens (grid size; the kernel counts
+// the tiles from the device lens)
 void launch_resblock_x3(const ResArgs& a, const int* h_lens, int C, hipStream_t s);
 void pack_resblock_x3(const std::vector<float>& wd, const std::vector<float>& wf, int C,
                       std::vector<uint16_t>& wd16, std::vector<uint16_t>& wf16);

@@ -122,6 +122,8 @@ __global__ __launch_bounds__(64 * WM * WN) void resblock_x3_kernel(ResArgs a, in
     if (lane == 63) tcum[64] = v;
   }
   lds_barrier();
+  // the host's count may be an upper bound (lengths decoded on the device): the tiles that exist
+  ntiles = min(ntiles, __builtin_amdgcn_readfirstlane(tcum[64]));
   auto tile_of = [&](int i) {
     const bool hit = lane < a.B && tcum[lane] <= i && i < tcum[lane + 1];
     const unsigned long long m = __ballot(hit);

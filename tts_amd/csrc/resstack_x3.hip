@@ -143,6 +143,8 @@ __global__ __launch_bounds__(64 * (C / 16) * WN) void resstack_x3_kernel(StackAr
     for (int i = tid; i < C * CTU; i += NTHR) bct[i] = a.ct_bias[i];
   }
   lds_barrier();
+  // the host's count may be an upper bound (lengths decoded on the device): the tiles that exist
+  ntiles = min(ntiles, __builtin_amdgcn_readfirstlane(tcum[64]));
   struct Tile {
     int b, q0, L;
   };

@@ -43,6 +43,24 @@ class Decoder(Container):
         self.r = int(new_r)
 
 
+class VocodedResult:
+    """A submitted ``Tacotron2.inference_vocoded_submit`` call. ``outputs`` holds the decode's
+    (decoder_outputs, postnet_outputs, alignments, stop_tokens), ready on return; the waveforms are
+    final once ``result()`` has returned (it completes the library ticket)."""
+
+    def __init__(self, outputs, wav, eng=None, ticket=None):
+        self.outputs = outputs
+        self._wav = wav
+        self._eng, self._ticket = eng, ticket
+
+    def result(self):
+        if self._ticket is not None:
+            with self._eng.lock:
+                self._eng.taco_mbmelgan_finish(self._ticket, self._wav.device)
+            self._ticket = None
+        return tuple(self.outputs) + (self._wav,)
+
+
 class Tacotron2(nn.Module):
     def __init__(self, num_chars, num_speakers=0, r=7, postnet_output_dim=80, decoder_output_dim=80,
                  attn_type="original", attn_win=False, attn_norm="softmax", prenet_type="original",
@@ -250,10 +268,25 @@ class Tacotron2(nn.Module):
         """``inference`` followed by ``vocoder.inference(postnet_outputs.transpose(1, 2),
         lengths=last_mel_lengths)`` -- the pair TTS/server/synthesizer.py:150-159 runs -- in one
         library call when ``vocoder`` is a MultibandMelganGenerator on the same device and the batch
-        fits one decode (tts_taco_mbmelgan_infer: the decoded lengths go from the decode's status
-        words straight to the vocoder, no Python between the models); otherwise the two calls.
-        Returns (decoder_outputs, postnet_outputs, alignments, stop_tokens, waveforms (B, 1, hop *
-        (M + 2 pad))), bit-identical to the two calls either way."""
+        fits one decode (tts_taco_mbmelgan_infer: the vocoder is launched on the decoded lengths the
+        decode leaves on the device, no host round trip between the models); otherwise the two
+        calls. Returns (decoder_outputs, postnet_outputs, alignments, stop_tokens, waveforms (B, 1,
+        hop * (M + 2 pad))), bit-identical to the two calls either way."""
+        return self._vocoded(text, vocoder, speaker_ids, speaker_embeddings, text_lengths, max_decoder_steps,
+                             submit=False).result()
+
+    @torch.no_grad()
+    def inference_vocoded_submit(self, text, vocoder, speaker_ids=None, speaker_embeddings=None,
+                                 text_lengths: Optional[Sequence[int]] = None, max_decoder_steps=None):
+        """``inference_vocoded`` in two halves (tts_taco_mbmelgan_submit / _finish): returns a
+        ``VocodedResult`` once the decode is done, with the vocoder still running on the device, so
+        that the caller can queue the next batch behind it; ``.result()`` waits for the vocoder
+        (re-running it in fp32 if its split-f16 operands left the f16 range) and returns what
+        ``inference_vocoded`` returns. The decode outputs (``.outputs[:4]``) are ready at once."""
+        return self._vocoded(text, vocoder, speaker_ids, speaker_embeddings, text_lengths, max_decoder_steps,
+                             submit=True)
+
+    def _vocoded(self, text, vocoder, speaker_ids, speaker_embeddings, text_lengths, max_decoder_steps, submit):
         from .vocoder import MultibandMelganGenerator
         dev, eng, text, lens, ms, r, spk_ids, spk_emb, limit = self._prepare(
             text, speaker_ids, speaker_embeddings, text_lengths, max_decoder_steps)
@@ -263,7 +296,7 @@ class Tacotron2(nn.Module):
             dec, post, align, stop = self.inference(text, speaker_ids=speaker_ids, speaker_embeddings=speaker_embeddings,
                                                     text_lengths=lens, max_decoder_steps=ms)
             wav = vocoder.inference(post.transpose(1, 2), lengths=self.last_mel_lengths)
-            return dec, post, align, stop, wav
+            return VocodedResult((dec, post, align, stop), wav)
         pad = int(vocoder.inference_padding)
         Tn = int(lens.max())
         sub = text[:, :Tn].contiguous()
@@ -274,12 +307,15 @@ class Tacotron2(nn.Module):
         with eng.lock:
             self._sync(eng)
             vocoder._sync(eng)
-            steps, status = eng.taco_mbmelgan_infer(sub, lens, r, ms, S_cap, self.decoder.stop_threshold, dec, post,
-                                                    align, stop, pad, wbuf, speaker_ids=spk_ids,
-                                                    speaker_embeddings=spk_emb)
+            args = (sub, lens, r, ms, S_cap, self.decoder.stop_threshold, dec, post, align, stop, pad, wbuf)
+            if submit:
+                steps, status, ticket = eng.taco_mbmelgan_submit(*args, speaker_ids=spk_ids, speaker_embeddings=spk_emb)
+            else:
+                steps, status = eng.taco_mbmelgan_infer(*args, speaker_ids=spk_ids, speaker_embeddings=spk_emb)
+                ticket = None
         res = self._assemble([(dec, post, align, stop, steps, status)], text.shape, lens, r, dev)
         L = hop * (int(steps.max()) * r + 2 * pad)
-        return res + (wbuf[:B * L].view(B, 1, L),)
+        return VocodedResult(res, wbuf[:B * L].view(B, 1, L), eng, ticket)
 
     @torch.no_grad()
     def decoder_state(self):
