@@ -557,8 +557,11 @@ struct DeviceGuard {
   }
 };
 
-// stream ordering with the caller's stream
+// stream ordering with the caller's stream (nothing to wait for when all of its work is complete:
+// a server loop's stream holds only waits on this context's own finished events)
 void enter(tts_ctx* c, void* stream) {
+  if (hipStreamQuery((hipStream_t)stream) == hipSuccess) return;
+  (void)hipGetLastError();  // hipErrorNotReady is not an error here; clear it for later launch checks
   HIP_OK(hipEventRecord(c->ev_in, (hipStream_t)stream));
   HIP_OK(hipStreamWaitEvent(c->s, c->ev_in, 0));
 }
@@ -1275,7 +1278,8 @@ struct TacoSetup {
   int B, MT;
   int perm[BMAX], inv[BMAX], lens[BMAX], max_steps[BMAX];
 };
-__global__ void taco_setup_kernel(TacoSetup a, int* map, int* lens, int* ctl) {
+__global__ void taco_setup_kernel(TacoSetup a, int* map, int* lens, int* ctl, unsigned* zero_flag) {
+  if (zero_flag && threadIdx.x == 0) *zero_flag = 0u;  // a fused call's range flag (no separate fill)
   for (int e = threadIdx.x; e < 4 + 4 * BMAX; e += blockDim.x) {
     const int ms = e - 4 - 3 * BMAX;
     ctl[e] = e == 2 ? a.MT : (ms >= 0 && ms < a.B ? a.max_steps[ms] : 0);
@@ -1657,7 +1661,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
       ta.lens[i] = h_lens[perm[i]];
       ta.max_steps[i] = h_max_steps[perm[i]];
     }
-    taco_setup_kernel<<<1, 256, 0, s>>>(ta, W.map.i(), W.lens.i(), W.ctl.i());
+    taco_setup_kernel<<<1, 256, 0, s>>>(ta, W.map.i(), W.lens.i(), W.ctl.i(), fv ? x3_flag(c) : nullptr);
     HIP_OK(hipGetLastError());
   }
   int* d_map = W.map.i();
@@ -3610,7 +3614,6 @@ static int64_t taco_mbmelgan_submit(tts_ctx* c, const int64_t* d_ids, const int3
                 mbmelgan_body(c, d_post, st, bound.data(), B, S_cap * r, pad, d_wav, /*dev_lens=*/true);
                 if (voc_x3) HIP_OK(hipMemcpyAsync(slot, x3_flag(c), 4, hipMemcpyDeviceToHost, c->s));
               }};
-  if (c->gemm_x3) HIP_OK(hipMemsetAsync(x3_flag(c), 0, 4, c->s));  // behind earlier calls' flag copies on c->s
   c->flag_read = false;
   taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
              h_status, stream, d_spk_ids, d_spk_emb, &fv);
