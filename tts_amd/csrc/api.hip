@@ -1565,7 +1565,6 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
   static const bool xdiag = std::getenv("TTS_DIAG_XCC") != nullptr;
   DevBuf& xdiag_buf = W.xdiag;
   if (xdiag) xdiag_buf.ensure((size_t)PMAX_LAUNCH * 256 * 4);
-  HIP_OK(hipEventRecord(c->ev_dec[0], s));
   c->dec_nlaunch = 0;
   c->dec_presplit = persist_presplit(a);
   for (int mt = W.MT; mt >= 1; --mt) {
@@ -1576,7 +1575,9 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
     a.trace = li == trace_li ? trace_p : nullptr;
     a.atrace = li == trace_li ? atrace_p : nullptr;
     a.diag = xdiag ? static_cast<unsigned*>(xdiag_buf.p) + 256 * li : nullptr;
-    launch_persist_decoder(a, mt, s, false);
+    // launch timing from the dispatches themselves: ev_dec[0] at the first launch's start, ev_dec[i + 1]
+    // at launch i's end (event-record packets between the launches cost ~5 us of idle each)
+    launch_persist_decoder(a, mt, s, false, li == 0 ? c->ev_dec[0] : nullptr, c->ev_dec[li + 1]);
     if (tr && li == trace_li) {  // one launch is traced
       HIP_OK(hipStreamSynchronize(s));
       std::vector<unsigned long long> h((size_t)8 * 24 * 256);
@@ -1589,8 +1590,7 @@ void run_persistent(tts_ctx* c, int r, float thr, hipStream_t s) {
       a.atrace = nullptr;
       tr = nullptr;
     }
-    const int i = c->dec_nlaunch++;
-    HIP_OK(hipEventRecord(c->ev_dec[i + 1], s));
+    c->dec_nlaunch++;
   }
   a.diag = nullptr;
   if (xdiag) {  // TTS_DIAG_XCC: print each launch's workgroup -> XCD map and the hand-off addresses

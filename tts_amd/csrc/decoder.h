@@ -192,7 +192,9 @@ bool persist_trace_built();          // phase stamps compiled in (-DTTS_PHASE_TR
 // `nwant` fastest in slot[] (TTS_BAR_CALIBRATE=0: slots 0 .. nwant-1); one decoder grid per block
 void pick_barrier_blocks(unsigned* pool, int ncand, int nwant, int* slot, hipStream_t s);
 // arm: zero the barrier block first (false: the caller armed it, e.g. in its state fill)
-void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm = true);
+// ev0 / ev1: optional timing events taken from the launch itself (before / after the kernel)
+void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm = true, hipEvent_t ev0 = nullptr,
+                            hipEvent_t ev1 = nullptr);
 // whether that launch publishes h_att / ctx / h_dec pre-split (decoder_persist.hip presplit_of)
 bool persist_presplit(const PArgs& a);
 

@@ -1779,7 +1779,7 @@ static int persist_var(const PArgs& a) {
 }
 bool persist_presplit(const PArgs& a) { return presplit_of(persist_var(a)); }
 
-void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
+void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm, hipEvent_t ev0, hipEvent_t ev1) {
   TTS_CHECK(MT >= 1 && MT <= 4, "persistent decoder: MT must be in [1, 4]");
   TTS_CHECK(PJ_WG0 + a.ntj * (MT > 2 ? 4 : 2) <= PW && a.ntj >= 17, "persistent decoder: projection job count");
   TTS_CHECK(a.D.B <= 64 && NATT * 4 * 4 == 1024, "persistent decoder: attention_rnn layout");
@@ -1803,5 +1803,5 @@ void launch_persist_decoder(const PArgs& a, int MT, hipStream_t s, bool arm) {
   if (arm) arm_barrier(a.bar, 1, s);
   PArgs copy = a;
   void* kargs[] = {&copy};
-  launch_resident(f, dim3(PW), dim3(PT), kargs, P_LDS, s);
+  launch_resident(f, dim3(PW), dim3(PT), kargs, P_LDS, s, ev0, ev1);
 }

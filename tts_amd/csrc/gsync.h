@@ -28,6 +28,7 @@
 // by another queue on the same GPU does not trip it.
 #pragma once
 #include "common.h"
+#include <hip/hip_ext.h>
 #include "split16.h"
 
 #include <cstdlib>
@@ -73,7 +74,10 @@ inline bool gsync_count_ok(unsigned n) { return n > 0 && n % (n >= 256 ? 16u : 8
 // hipLaunchCooperativeKernel also sets up HIP's cooperative queue, whose teardown at process exit
 // collides with the HSA runtime rocprofv3 preloads (SIGSEGV in exit() after the profile is
 // written), so the plain launch is the default. TTS_COOP_LAUNCH=1 restores it.
-inline void launch_resident(const void* f, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s) {
+// ev0 / ev1 (optional): timing events taken from the launch itself (hipExtLaunchKernel), so that no
+// event-record packet sits between the kernel and its neighbours on the stream
+inline void launch_resident(const void* f, dim3 grid, dim3 block, void** args, size_t lds, hipStream_t s,
+                            hipEvent_t ev0 = nullptr, hipEvent_t ev1 = nullptr) {
   static std::mutex mu;
   static std::map<std::pair<const void*, int>, int> fits;  // (kernel, device) -> workgroups it holds at once
   static const bool coop = [] {
@@ -96,8 +100,15 @@ inline void launch_resident(const void* f, dim3 grid, dim3 block, void** args, s
   TTS_CHECK((long)grid.x * grid.y * grid.z <= cap, "grid-barrier kernel: grid larger than the device holds at once");
   TTS_CHECK(grid.y == 1 && grid.z == 1 && gsync_count_ok(grid.x),
             "grid-barrier kernel: a 1-D grid that is a multiple of the barrier's counter fan-in");
-  if (coop) HIP_OK(hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)lds, s));
-  else HIP_OK(hipLaunchKernel(f, grid, block, args, lds, s));
+  if (coop) {
+    if (ev0) HIP_OK(hipEventRecord(ev0, s));
+    HIP_OK(hipLaunchCooperativeKernel(f, grid, block, args, (unsigned)lds, s));
+    if (ev1) HIP_OK(hipEventRecord(ev1, s));
+  } else if (ev0 || ev1) {
+    HIP_OK(hipExtLaunchKernel(f, grid, block, args, lds, s, ev0, ev1, 0));
+  } else {
+    HIP_OK(hipLaunchKernel(f, grid, block, args, lds, s));
+  }
 }
 
 // ------------------------------------------------------------------ coherent access helpers
