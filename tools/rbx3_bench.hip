@@ -248,6 +248,8 @@ int main(int argc, char** argv) {
       timeit("x3 TQ64 6x2 (MI2 NI2)", [&] { launch_rbx3<192, 64, 6, 2, 3>(a, kM, S); });
       timeit("x3 TQ48 12x1 CPB2", [&] { launch_rbx3<192, 48, 12, 1, 3, 2>(a, kM, S); });
       timeit("x3 TQ48 12x1 CPB3", [&] { launch_rbx3<192, 48, 12, 1, 3, 3>(a, kM, S); });
+      timeit("x3 TQ64 12x1 R6", [&] { launch_rbx3<192, 64, 12, 1, 6>(a, kM, S); });
+      timeit("x3 TQ64 6x1 (MI2 NI4)", [&] { launch_rbx3<192, 64, 6, 1, 3>(a, kM, S); });
     } else if (C == 96) {
       timeit("x3 TQ128 6x2", [&] { launch_rbx3<96, 128, 6, 2, 3>(a, kM, S); });
       timeit("x3 TQ96 6x2 (NI3)", [&] { launch_rbx3<96, 96, 6, 2, 3>(a, kM, S); });
@@ -256,6 +258,9 @@ int main(int argc, char** argv) {
       timeit("x3 TQ128 2x4 (MI3 NI2)", [&] { launch_rbx3<96, 128, 2, 4, 3>(a, kM, S); });
       timeit("x3 TQ64 6x2 CPB3 (NI2)", [&] { launch_rbx3<96, 64, 6, 2, 3, 3>(a, kM, S); });
       timeit("x3 TQ64 6x1 CPB3 (NI4)", [&] { launch_rbx3<96, 64, 6, 1, 3, 3>(a, kM, S); });
+      timeit("x3 TQ128 3x4 (MI2 NI2)", [&] { launch_rbx3<96, 128, 3, 4, 3>(a, kM, S); });
+      timeit("x3 TQ128 3x2 (MI2 NI4)", [&] { launch_rbx3<96, 128, 3, 2, 3>(a, kM, S); });
+      timeit("x3 TQ96 3x2 (MI2 NI3)", [&] { launch_rbx3<96, 96, 3, 2, 3>(a, kM, S); });
     } else {
       timeit("x3 TQ128 3x4", [&] { launch_rbx3<48, 128, 3, 4, 3>(a, kM, S); });
       timeit("x3 TQ192 3x4 (NI3)", [&] { launch_rbx3<48, 192, 3, 4, 3>(a, kM, S); });
