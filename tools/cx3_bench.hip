@@ -9,6 +9,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstdlib>
+#include <cstring>
 #include <functional>
 #include <random>
 #include <string>
@@ -251,6 +252,47 @@ int main(int argc, char** argv) {
       const float tm = time_it([&] { launch_conv_x3(r.am, S); });
       printf("%-24s                              x3 %8.1f us (%6.1f TF/s fp32-equiv)  phase-merged\n", sh.c.name.c_str(),
              tm, r.flop / (tm * 1e-6) / 1e12);
+    }
+  }
+  if (argc > 1 && std::string(argv[1]) == "sweep") {
+    // tile shapes beside the library's choice on the C2 shapes; every variant's output must equal
+    // the library tile's bit for bit (the same k-step order per output element)
+    struct V {
+      const char* name;
+      int tc;
+      std::function<void(const ConvArgs&)> run;
+    };
+    std::vector<V> vs = {
+        {"128x48 (2,3,4,1)", 128, [](const ConvArgs& a) { cx_taps<2, 3, 4, 1, 2>(a, S); }},
+        {"128x64 (2,4,4,1)", 128, [](const ConvArgs& a) { cx_taps<2, 4, 4, 1, 2>(a, S); }},
+        {"64x128 (2,4,2,2)", 64, [](const ConvArgs& a) { cx_taps<2, 4, 2, 2, 1>(a, S); }},
+        {"192x64 (3,4,4,1)", 192, [](const ConvArgs& a) { cx_taps<3, 4, 4, 1, 2>(a, S); }},
+        {"96x128 (3,4,2,2)", 96, [](const ConvArgs& a) { cx_taps<3, 4, 2, 2, 1>(a, S); }},
+        {"128x32 (2,2,4,1)", 128, [](const ConvArgs& a) { cx_taps<2, 2, 4, 1, 2>(a, S); }},
+        {"256x32 (2,2,8,1)", 256, [](const ConvArgs& a) { cx_taps<2, 2, 8, 1, 2>(a, S); }},
+        {"128x64 (1,4,8,1)", 128, [](const ConvArgs& a) { cx_taps<1, 4, 8, 1, 2>(a, S); }},
+    };
+    for (auto& sh : shapes) {
+      if (sh.c.Cout == 80 || sh.c.Cout == 48) continue;
+      Built r = build(sh.c, 99, 1.f);
+      const ConvArgs& a = sh.c.nph > 1 ? r.am : r.a;
+      launch_conv_x3(a, S);
+      HIP_OK(hipStreamSynchronize(S));
+      std::vector<float> ref(r.out_elems), got(r.out_elems);
+      HIP_OK(hipMemcpy(ref.data(), r.out, r.out_elems * 4, hipMemcpyDeviceToHost));
+      const float tl = time_it([&] { launch_conv_x3(a, S); });
+      printf("%-24s library %8.1f us\n", sh.c.name.c_str(), tl);
+      for (auto& v : vs) {
+        if (a.Cout % v.tc) continue;
+        HIP_OK(hipMemset(r.out, 0, r.out_elems * 4));
+        v.run(a);
+        HIP_OK(hipStreamSynchronize(S));
+        HIP_OK(hipMemcpy(got.data(), r.out, r.out_elems * 4, hipMemcpyDeviceToHost));
+        const bool same = std::memcmp(got.data(), ref.data(), r.out_elems * 4) == 0;
+        const float t = time_it([&] { v.run(a); });
+        printf("%-24s %-18s %8.1f us  %s\n", "", v.name, t, same ? "same bits" : "DIFFERENT");
+        fails += !same;
+      }
     }
   }
   printf(fails ? "FAILED\n" : "all checks passed\n");
