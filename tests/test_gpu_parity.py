@@ -1664,7 +1664,8 @@ def test_fused_submit_pipelined_and_short_decode():
     ahead, as bench.py times it: two batches with different ragged forced lengths submitted back to
     back, then both finished; each batch bit-identical to its two-call form. Then the vocoder
     launched on device-side lengths below the S_cap bound (S_cap = max steps + 7: the waveform rows
-    are packed back to hop (M + 2 pad) samples apart), blocking and submitted; and a decode whose
+    are packed back to hop (M + 2 pad) samples apart), blocking and submitted; one utterance at
+    padding 2 against its two calls, and an unknown ticket refused; and a decode whose
     rows stop at step 2 (stop threshold -1, r = 1: 2 mel frames, shorter than ReflectionPad1d(3)
     allows) fails the call with the vocoder's length message, the context usable afterwards."""
     import bench
@@ -1715,6 +1716,27 @@ def test_fused_submit_pipelined_and_short_decode():
         L = voc.hop * (max(steps_a) * r + 2 * pad)
         assert torch.equal(wbuf[:B * L].view(B, 1, L), ref_a[4])
         assert torch.equal(post[:, :max(steps_a) * r], ref_a[1])
+
+    # one utterance, inference padding 2, S_cap above its steps; a ticket never handed out is refused
+    voc.inference_padding = 2
+    try:
+        x1 = x[3:4, :lens[3]].contiguous()
+        with torch.no_grad():
+            a1 = taco.inference(x1, max_decoder_steps=[steps_a[3]])
+            w1 = voc.inference(a1[1].transpose(1, 2), lengths=taco.last_mel_lengths.copy())
+        S1 = steps_a[3] + 5
+        dec, post, align, stop = taco._out_tensors(1, S1, r, lens[3], dev)
+        wbuf = torch.full((voc.hop * (S1 * r + 4),), float("nan"), device=dev)
+        with eng.lock:
+            st, _, ticket = eng.taco_mbmelgan_submit(x1, [lens[3]], r, np.asarray([steps_a[3]]), S1,
+                                                     taco.decoder.stop_threshold, dec, post, align, stop, 2, wbuf)
+            eng.taco_mbmelgan_finish(ticket, dev)
+            with pytest.raises(RuntimeError, match="unknown ticket"):
+                eng.taco_mbmelgan_finish(ticket + 1000, dev)
+        L1 = voc.hop * (steps_a[3] * r + 4)
+        assert list(st) == [steps_a[3]] and torch.equal(wbuf[:L1].view(1, 1, L1), w1)
+    finally:
+        voc.inference_padding = 0
 
     # rows that stop at step 2 at r = 1: 2 frames, below the vocoder's reflection pad
     taco.decoder.set_r(1)
