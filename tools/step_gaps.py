@@ -1,11 +1,35 @@
-"""Timeline of the last headline step in a rocprofv3 kernel trace: per-kernel start, gap to the
-previous kernel's end and duration, then span vs busy time, and the idle time between the previous
-step's last kernel (out_pqmf) and this step's first (taco_setup).
-  python tools/step_gaps.py gpurun_out/prof/run_kernel_trace.csv [--all]"""
+"""Timeline of bench steps in a rocprofv3 kernel trace.
+
+  python tools/step_gaps.py gpurun_out/prof/run_kernel_trace.csv [--all]
+      the last headline step: per-kernel start, gap to the previous kernel's end and duration,
+      then span vs busy time, and the idle time between the previous step's last kernel
+      (out_pqmf) and this step's first (taco_setup)
+  python tools/step_gaps.py <trace.csv> --steps
+      one line per step (taco_setup to the next taco_setup): span, kernel-busy time and the idle
+      time inside it, for every step of the run (bench.py's passes in order: warmup, pipelined
+      warmup, the timed pipelined loop, the blocking and two-call loops, the stage split, ...)
+"""
 import csv
 import sys
 
 rows = sorted(csv.DictReader(open(sys.argv[1])), key=lambda r: int(r["Start_Timestamp"]))
+
+if "--steps" in sys.argv:
+    setups = [i for i, r in enumerate(rows) if "taco_setup_kernel" in r["Kernel_Name"]]
+    for n, (a, b) in enumerate(zip(setups, setups[1:] + [len(rows)])):
+        s0 = int(rows[a]["Start_Timestamp"])
+        end = s0
+        busy = 0
+        for r in rows[a:b]:  # union of the kernels' intervals
+            s, e = int(r["Start_Timestamp"]), int(r["End_Timestamp"])
+            if e > end:
+                busy += e - max(s, end)
+                end = e
+        nxt = int(rows[b]["Start_Timestamp"]) if b < len(rows) else end
+        print(f"step {n:2d}: span to the next step {(nxt - s0) / 1e3:9.1f} us, busy {busy / 1e3:9.1f} us, "
+              f"idle {(nxt - s0 - busy) / 1e3:7.1f} us")
+    sys.exit(0)
+
 idx = [i for i, r in enumerate(rows) if "persist_decoder_kernel<2, 8>" in r["Kernel_Name"]]
 i0 = idx[-1]
 j = i0
