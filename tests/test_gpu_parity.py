@@ -1754,6 +1754,31 @@ def test_fused_submit_pipelined_and_short_decode():
         assert torch.equal(u, v)
 
 
+def test_fused_submit_b64_equals_two_calls():
+    """The fused submission at the largest batch one decode takes (64 rows: the LJ profile twice,
+    MT = 4 batch tiles; the vocoder's persistent kernels count their tiles from 64 device-side
+    lengths): every output bit-identical to Tacotron2.inference + MultibandMelganGenerator.inference."""
+    import bench
+    from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids
+    dev = _dev()
+    taco, tsd, voc, vsd, tcfg, vcfg = bench.build_models(dev)
+    taco.decoder.set_r(2)
+    taco.decoder.verbose = False
+    T_prof, M_prof = lj_profile()
+    ids = synthetic_ids(T_prof) * 2
+    steps = [max(3, s_ // 6) for s_ in forced_steps(M_prof, 2)] * 2
+    steps = steps[32:] + steps[:32][::-1]
+    batch, lens = pad_batch(ids)
+    x = torch.from_numpy(batch).to(dev)
+    with torch.no_grad():
+        a = taco.inference(x, text_lengths=lens, max_decoder_steps=steps)
+        wa = voc.inference(a[1].transpose(1, 2), lengths=taco.last_mel_lengths.copy())
+        b = taco.inference_vocoded_submit(x, voc, text_lengths=lens, max_decoder_steps=steps).result()
+    assert len(b[0]) == 64
+    for u, v in zip(a + (wa,), b):
+        assert u.shape == v.shape and torch.equal(u, v)
+
+
 def test_bench_workload_full_size_r1_vs_oracle():
     """The bench line's r = 1 run at its full length (bench.py `r1`: the same 32 LJ-profile
     utterances, forced lengths of up to 857 decoder steps, one frame per step as the
