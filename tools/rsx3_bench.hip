@@ -65,7 +65,7 @@ int main(int argc, char** argv) {
   HIP_OK(hipStreamCreate(&S));
   const int nB = argc > 1 ? std::atoi(argv[1]) : 32;
   const int C = argc > 2 ? std::atoi(argv[2]) : 48;  // 48 (mul 64) or 96 (mul 32)
-  const int mul = C == 48 ? 64 : 32, pad = 2;
+  const int mul = C == 48 ? 64 : 32, pad = argc > 3 ? std::atoi(argv[3]) : 2;  // inference padding
   int Mmax = 0;
   std::vector<int> hl(kM, kM + nB);
   for (int b = 0; b < nB; ++b) Mmax = std::max(Mmax, kM[b]);
@@ -189,6 +189,7 @@ int main(int argc, char** argv) {
     StackArgs v = sa; v.ext[2] = 0; v.ext[1] = 9; v.ext[0] = 12; launch_rsx3<48, TQ, WN, NI>(v, hl.data(), S); }))
   if (C == 48) {
     VAR(208, 4, 4);
+    VAR(192, 4, 4);
     VAR(176, 4, 4);
   }
   // the fused kernel's blocks 0-1 keep phase 2 untransposed (their output goes to LDS), the
