@@ -261,8 +261,8 @@ def main(argv=None):
     argv = sys.argv[1:] if argv is None else list(argv)
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=5)
-    ap.add_argument("--warmup", type=int, default=2)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--r", type=int, default=2)
     ap.add_argument("--per-gpu-batch", type=int, default=32)
     ap.add_argument("--cpu-seconds", type=float, default=30.0)
