@@ -20,7 +20,7 @@
 #include <vector>
 
 void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int num_rows, int D,
-                         const int* lens, int B, float* out, hipStream_t s);
+                         const int* lens, int B, float* out, hipStream_t s, const int* rowmap = nullptr);
 int launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
                           int B, float* hbuf, unsigned* bar, float* out, hipStream_t s);
 void launch_glu_ln_res(const float* x, long xb, int C2, const float* gamma, const float* beta, const float* res,
@@ -346,7 +346,7 @@ struct TacoWS {
   DevBuf p1, pb, gatt, hatt, catt, hdec0, hdec1, cdec, ctx, y, pq, spart, alpha, acum, energy, ctl;
   DevBuf dec, align, stop, pa, pbb;
   DevBuf aps, apm, apu, acnt;  // attention chunk partials + per-utterance arrival counters
-  DevBuf ids, post, map;       // rows in decode order (longest first); map = [perm | inverse]
+  DevBuf post, map;            // rows in decode order (longest first); map = [perm | inverse]
   DevBuf stat;                 // status words for the host, laid out as tts_ctx::pinned (TS_*)
   DevBuf ypart, pbar;          // persistent decoder: projection halves, grid-barrier words
   // the decoder launches' barrier blocks: PBAR_CAND candidates in pbar, the PMAX_LAUNCH fastest
@@ -924,7 +924,6 @@ void taco_workspace(tts_ctx* c, int B, int T_max, int S_cap, int r) {
   grow<float>(W.stop, (size_t)B * S_cap, g);
   grow<float>(W.pa, (size_t)B * 512 * S_cap * r, g);
   grow<float>(W.pbb, (size_t)B * 512 * S_cap * r, g);
-  grow<int64_t>(W.ids, (size_t)B * T_max, g);
   grow<float>(W.post, (size_t)B * S_cap * r * 80, g);
   grow<int>(W.map, 2 * BMAX, g);
   grow<int>(W.stat, 256, g);
@@ -1160,11 +1159,13 @@ __global__ __launch_bounds__(256) void spk_bias_kernel(const float* __restrict__
   for (int m = MB; m < Bp; ++m) out[(long)m * N + n] = base;  // rows past the speaker rows (Bp > MB)
 }
 
-void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_out, hipStream_t s) {
+// rowmap (optional, device): encoder row b reads ids row rowmap[b] (the decode order)
+void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_out, hipStream_t s,
+                 const int* rowmap = nullptr) {
   auto& M = c->taco;
   auto& W = c->tws;
   const int* lens = W.lens.i();
-  launch_embed_gather(ids, T_max, M.emb.f(), M.num_chars, 512, lens, B, W.x0.f(), s);
+  launch_embed_gather(ids, T_max, M.emb.f(), M.num_chars, 512, lens, B, W.x0.f(), s, rowmap);
   ConvCall cc;
   cc.lens = lens;
   cc.B = B;
@@ -1191,16 +1192,19 @@ void run_encoder(tts_ctx* c, const int64_t* ids, int B, int T_max, float* enc_ou
   cc.ot = 2048;
   cc.epi = 0;
   run_conv(M.lstm_in, cc, s);
-  HIP_OK(hipMemsetAsync(enc_out, 0, (size_t)B * T_max * 512 * 4, s));
-  // one cooperative launch for the whole recurrence (W.lc then holds its grid-barrier words);
-  // per-step launches when cooperative launch is unavailable or TTS_ENCODER=steps
+  // one cooperative launch for the whole recurrence (W.lc then holds its grid-barrier words; its
+  // fill zeroes enc_out too); per-step launches when cooperative launch is unavailable or
+  // TTS_ENCODER=steps
   const char* e = std::getenv("TTS_ENCODER");
   W.enc_ndom = (e && std::string(e) == "steps")
                    ? 0
                    : launch_bilstm_persist(W.gin.f(), M.whhT.f(), c->gemm_x3 ? M.whhT16.h() : nullptr, lens, T_max, B,
                                            W.lh.f(), reinterpret_cast<unsigned*>(W.lc.p), enc_out, s);
   W.enc_persist = W.enc_ndom > 0;
-  if (!W.enc_persist) launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
+  if (!W.enc_persist) {
+    HIP_OK(hipMemsetAsync(enc_out, 0, (size_t)B * T_max * 512 * 4, s));
+    launch_bilstm(W.gin.f(), M.whhT.f(), lens, T_max, B, W.lh.f(), W.lc.f(), enc_out, s);
+  }
 }
 
 // a persistent BiLSTM whose grid barrier timed out set its error word. The words are read on the
@@ -1268,6 +1272,27 @@ void gather_rows(const T* src, T* dst, const int* d_map, long row, int B, hipStr
   if (row <= 0 || B <= 0) return;
   dim3 g((unsigned)std::min<long>((row + 255) / 256, 64), B);
   gather_rows_kernel<T><<<g, 256, 0, s>>>(src, dst, d_map, row);
+  HIP_OK(hipGetLastError());
+}
+
+// the decoder's four outputs scattered back to the caller's row order in one launch (entry z)
+struct Gather4 {
+  const float* src[4];
+  float* dst[4];
+  long row[4];
+};
+__global__ void gather4_rows_kernel(Gather4 g, const int* __restrict__ map) {
+  const int z = blockIdx.z;
+  const long row = g.row[z], i = blockIdx.y;
+  const float* __restrict__ sr = g.src[z] + (long)map[i] * row;
+  float* __restrict__ dr = g.dst[z] + i * row;
+  for (long e = (long)blockIdx.x * blockDim.x + threadIdx.x; e < row; e += (long)gridDim.x * blockDim.x) dr[e] = sr[e];
+}
+void gather4_rows(const Gather4& g, const int* d_map, int B, hipStream_t s) {
+  long mx = 0;
+  for (int z = 0; z < 4; ++z) mx = std::max(mx, g.row[z]);
+  if (mx <= 0 || B <= 0) return;
+  gather4_rows_kernel<<<dim3((unsigned)std::min<long>((mx + 255) / 256, 64), B, 4), 256, 0, s>>>(g, d_map);
   HIP_OK(hipGetLastError());
 }
 
@@ -1665,7 +1690,6 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     HIP_OK(hipGetLastError());
   }
   int* d_map = W.map.i();
-  gather_rows<int64_t>(ids, reinterpret_cast<int64_t*>(W.ids.p), d_map, T_max, B, s);
   W.thr = thr;
   // speaker vectors in decode order: external embeddings, or rows of the learned table
   TTS_CHECK(!M.variant() || use_persistent(c), "BN prenet / attention windowing / forward / Graves attention run on "
@@ -1685,7 +1709,7 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
     }
   }
   // encoder + processed inputs
-  run_encoder(c, reinterpret_cast<const int64_t*>(W.ids.p), B, T_max, W.enc.f(), s);
+  run_encoder(c, ids, B, T_max, W.enc.f(), s, d_map);
   {
     ConvCall cc;
     cc.lens = W.lens.i();
@@ -1772,10 +1796,9 @@ void taco_infer(tts_ctx* c, const int64_t* ids, const int32_t* h_lens, int B, in
   const long fb = (long)S_cap * r * 80;  // W.post was zeroed with the decoder state
   run_postnet(c, W.dec.f(), fb, W.mlens.i(), B, S_cap * r, S_cap * r, W.post.f(), fb, s);
   // scatter back to the caller's row order: output row b <- decode row inv[b]
-  gather_rows<float>(W.post.f(), d_post, d_map + BMAX, fb, B, s);
-  gather_rows<float>(W.dec.f(), d_dec, d_map + BMAX, fb, B, s);
-  gather_rows<float>(W.align.f(), d_align, d_map + BMAX, (long)S_cap * T_max, B, s);
-  gather_rows<float>(W.stop.f(), d_stop, d_map + BMAX, S_cap, B, s);
+  gather4_rows(Gather4{{W.post.f(), W.dec.f(), W.align.f(), W.stop.f()}, {d_post, d_dec, d_align, d_stop},
+                       {fb, fb, (long)S_cap * T_max, (long)S_cap}},
+               d_map + BMAX, B, s);
   // one host round trip per call: barrier error words, per-row results, range flag, launch steps
   {
     const unsigned* lc = reinterpret_cast<const unsigned*>(W.lc.p);
@@ -3513,9 +3536,8 @@ static void mbmelgan_body(tts_ctx* c, const float* d_mel, const int64_t* mel_str
   int up = 1;
   for (int u : G.ups) up *= u;
   const long Ls = (long)(M_max + 2 * pad) * up;
-  HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
   const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
-  if (fused) {
+  if (fused) {  // launch_out_pqmf writes the rows' zero padding itself
     GenTail t;
     run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t, mel_strides, dev_lens);
     TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
@@ -3523,6 +3545,7 @@ static void mbmelgan_body(tts_ctx* c, const float* d_mel, const int64_t* mel_str
                               G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
               "fused output/PQMF shape not covered");
   } else {
+    HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
     c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
     run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s, nullptr, mel_strides, dev_lens);
     launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),

@@ -252,7 +252,8 @@ bool resstack_x3_fits(const StackArgs& a, const int* h_lens);
 void launch_resstack_x3(const StackArgs& a, const int* h_lens, int C, hipStream_t s);
 
 // fused MB-MelGAN output conv (C -> 4, k7, LReLU + reflect pad 3 + tanh) and PQMF synthesis
-// (melgan_out.hip); returns false when the shape is not covered (N != 4, 63 taps, C not 32/48)
+// (melgan_out.hip); returns false when the shape is not covered (N != 4, 63 taps, C not 32/48).
+// launch_out_pqmf writes every row's band positions [0, maxL): zeros past its own length
 void launch_out_conv1(const float* x, long xb, long xc, int C, const float* W, const float* bo, const int* lens,
                       int len_add, int L_mul, int maxL, int B, float* y, long yb, hipStream_t s);
 bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, const float* bo, const float* G,

@@ -18,20 +18,22 @@ constexpr int LRS = 20;
 
 __global__ __launch_bounds__(256) void embed_gather_kernel(const int64_t* __restrict__ ids, int T_max,
                                                            const float* __restrict__ table, int num_rows,
-                                                           int D, const int* lens,
+                                                           int D, const int* lens, const int* rowmap,
                                                            float* __restrict__ out /* (B,T_max,D) */) {
   const int b = blockIdx.y, t = blockIdx.x;
   float* o = out + ((long)b * T_max + t) * D;
   const bool valid = t < lens[b];
-  long id = valid ? ids[(long)b * T_max + t] : 0;
+  const long ib = rowmap ? rowmap[b] : b;  // ids row of output row b (the decode order's map)
+  long id = valid ? ids[ib * T_max + t] : 0;
   if (id < 0 || id >= num_rows) id = 0;  // host validates ids; never read out of bounds
   for (int c = threadIdx.x; c < D; c += blockDim.x) o[c] = valid ? table[id * D + c] : 0.f;
 }
 
+// rowmap (optional, device): output row b takes ids row rowmap[b] (lens are in output order)
 void launch_embed_gather(const int64_t* ids, int T_max, const float* table, int num_rows, int D,
-                         const int* lens, int B, float* out, hipStream_t s) {
+                         const int* lens, int B, float* out, hipStream_t s, const int* rowmap) {
   if (B <= 0 || T_max <= 0) return;
-  embed_gather_kernel<<<dim3(T_max, B), 256, 0, s>>>(ids, T_max, table, num_rows, D, lens, out);
+  embed_gather_kernel<<<dim3(T_max, B), 256, 0, s>>>(ids, T_max, table, num_rows, D, lens, rowmap, out);
   HIP_OK(hipGetLastError());
 }
 
@@ -272,8 +274,9 @@ __global__ __launch_bounds__(64 * LSTM_NW) void lstm_persist_kernel(const float*
 std::atomic<int> g_test_stall_lstm{-1};
 
 template <int H, int NDIR>
+// zero_out: the launch's fill also zeroes out (B, T_max, NDIR H): the padding past each length
 static int launch_lstm_persist_t(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
-                                 int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
+                                 int B, float* hbuf, unsigned* bar, float* out, hipStream_t s, bool zero_out = false) {
   int dev = 0, coop = 0;
   HIP_OK(hipGetDevice(&dev));
   HIP_OK(hipDeviceGetAttribute(&coop, hipDeviceAttributeCooperativeLaunch, dev));
@@ -287,8 +290,13 @@ static int launch_lstm_persist_t(const float* Gin, const float* Whh, const uint1
   const int MT0 = (B + 15) / 16;
   const int RG = (rg_on && MT0 % 2 == 0 && 2 * NDIR * (H / 4) <= device_cu_count()) ? 2 : 1;
   const int MT = MT0 / RG, Bp = MT * 16;
-  HIP_OK(hipMemsetAsync(hbuf, 0, (size_t)2 * RG * NDIR * Bp * H * 4, s));
-  arm_barrier(bar, RG * NDIR, s);
+  {
+    FillList f;  // state, barrier blocks and (zero_out) the output in one launch
+    f.add(hbuf, (size_t)2 * RG * NDIR * Bp * H * 4);
+    if (zero_out) f.add(out, (size_t)B * T_max * NDIR * H * 4);
+    add_barrier_fills(f, bar, RG * NDIR);
+    launch_fills(f, s);
+  }
   int stall = g_test_stall_lstm.load();  // test hook (tts_test_stall_lstm), -1 in production
   void* args[] = {(void*)&Whh, (void*)&Whh16, (void*)&Gin, (void*)&lens, (void*)&T_max,
                   (void*)&B,   (void*)&hbuf,  (void*)&out, (void*)&bar, (void*)&stall};
@@ -301,11 +309,11 @@ static int launch_lstm_persist_t(const float* Gin, const float* Whh, const uint1
   return RG * NDIR;
 }
 
-// encoder BiLSTM (H = 256, both directions): the number of recurrences (barrier blocks in `bar`),
-// 0 = cooperative launch unavailable
+// encoder BiLSTM (H = 256, both directions; zeroes out first): the number of recurrences (barrier
+// blocks in `bar`), 0 = cooperative launch unavailable (nothing launched, out untouched)
 int launch_bilstm_persist(const float* Gin, const float* Whh, const uint16_t* Whh16, const int* lens, int T_max,
                           int B, float* hbuf, unsigned* bar, float* out, hipStream_t s) {
-  return launch_lstm_persist_t<256, 2>(Gin, Whh, Whh16, lens, T_max, B, hbuf, bar, out, s);
+  return launch_lstm_persist_t<256, 2>(Gin, Whh, Whh16, lens, T_max, B, hbuf, bar, out, s, true);
 }
 
 // GE2E speaker-encoder LSTM layer (H = 768, forward only); hbuf >= 2 x 64 x 768 floats, bar >= 512 words

@@ -29,7 +29,8 @@ template <int C>
 __global__ __launch_bounds__(256) void out_pqmf_kernel(const float* __restrict__ x, long xb, long xc,
                                                        const float* __restrict__ Wo, const float* __restrict__ bo,
                                                        const float* __restrict__ G, const int* __restrict__ lens,
-                                                       int len_add, int L_mul, float* __restrict__ y, long yb) {
+                                                       int len_add, int L_mul, int maxL, float* __restrict__ y,
+                                                       long yb) {
   static_assert(C % OP_CC == 0, "channel chunking");
   constexpr int NCH = C / OP_CC;
   // chunk buffer [OP_CC][OP_XW]; after the conv it holds the band tile [4][OP_NB]
@@ -39,8 +40,13 @@ __global__ __launch_bounds__(256) void out_pqmf_kernel(const float* __restrict__
   const int b = blockIdx.y;
   const int L = (lens[b] + len_add) * L_mul;  // band length of this utterance
   const int p0 = blockIdx.x * OP_TB;
-  if (p0 >= L) return;
   const int tid = threadIdx.x;
+  if (p0 >= L) {  // a tile past the utterance: its samples are the row's zero padding
+    float* yp = y + (long)b * yb;
+    for (int m = p0 + tid; m < min(p0 + OP_TB, maxL); m += 256)
+      *reinterpret_cast<f32x4*>(yp + 4L * m) = f32x4{0.f, 0.f, 0.f, 0.f};
+    return;
+  }
   const float* xp = x + (long)b * xb;
   for (int i = tid; i < OP_N * 64; i += 256) {
     const int k = i >> 6, jj = (i >> 2) & 15, r = i & 3;
@@ -141,7 +147,8 @@ __global__ __launch_bounds__(256) void out_pqmf_kernel(const float* __restrict__
   for (int i = 0; i < 4; ++i) {
     const int mm = tid + 256 * i;
     const int m = p0 + mm;
-    if (mm < OP_TB && m < L) *reinterpret_cast<f32x4*>(yp + 4L * m) = (float)OP_N * out[i];
+    if (mm < OP_TB && m < maxL)  // zeros past the utterance (the row is padded to maxL)
+      *reinterpret_cast<f32x4*>(yp + 4L * m) = m < L ? (float)OP_N * out[i] : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 }
 
@@ -154,8 +161,8 @@ bool launch_out_pqmf(const float* x, long xb, long xc, int C, const float* Wo, c
   if ((long)C * xc >= (1L << 31)) return false;                                  // 32-bit staging offsets
   dim3 grid((maxL + OP_TB - 1) / OP_TB, B);
   switch (C) {
-    case 48: out_pqmf_kernel<48><<<grid, 256, 0, s>>>(x, xb, xc, Wo, bo, G, lens, len_add, L_mul, y, yb); break;
-    case 32: out_pqmf_kernel<32><<<grid, 256, 0, s>>>(x, xb, xc, Wo, bo, G, lens, len_add, L_mul, y, yb); break;
+    case 48: out_pqmf_kernel<48><<<grid, 256, 0, s>>>(x, xb, xc, Wo, bo, G, lens, len_add, L_mul, maxL, y, yb); break;
+    case 32: out_pqmf_kernel<32><<<grid, 256, 0, s>>>(x, xb, xc, Wo, bo, G, lens, len_add, L_mul, maxL, y, yb); break;
     default: return false;
   }
   HIP_OK(hipGetLastError());
