@@ -90,6 +90,31 @@ def test_mbmelgan_batched_equals_single(melgan):
         assert not wav[i, 0, len(ref):].any()
 
 
+def test_mbmelgan_writes_zero_padding_itself(melgan):
+    """The fused output stage (melgan_out.hip out_pqmf_kernel) writes every row's samples up to the
+    padded length, zeros past the row's own length (whole tiles past it included), so the caller's
+    buffer needs no memset: a NaN-filled buffer comes back with the same samples as the batched
+    call and exact zeros in the padding."""
+    from tts_amd._lib import get_engine
+    fx, cfg, sd, v = melgan
+    v.inference_padding = 0
+    mels = [fx["M64_p0_mel"][0], fx["M7_p0_mel"][0]]
+    batch = np.zeros((2, 80, 64), np.float32)
+    for i, m in enumerate(mels):
+        batch[i, :, :m.shape[1]] = m
+    x = torch.from_numpy(batch).cuda()
+    ref = v.inference(x, lengths=[64, 7])
+    wav = torch.full_like(ref, float("nan"))
+    eng = get_engine(x.device)
+    with eng.lock:
+        v._sync(eng)
+        eng.melgan_infer(x, np.array([64, 7]), 0, wav)
+    torch.cuda.synchronize()
+    assert not torch.isnan(wav).any()
+    assert torch.equal(wav, ref)
+    assert not wav[1, 0, v.hop * 7:].any()  # 3 whole 1008-position tiles past row 1's 448
+
+
 def test_mbmelgan_random_vs_oracle(melgan):
     fx, cfg, sd, v = melgan
     orc = melgan_oracle(cfg, sd)
