@@ -1684,6 +1684,63 @@ def test_fused_taco_mbmelgan_equals_two_calls(pad):
     assert wa.shape[-1] == voc.hop * (max(ml) + 2 * pad)
 
 
+def test_mbmelgan_beside_concurrent_bilstm_bit_identical():
+    """MB-MelGAN.inference of one library context on its own stream while another context runs
+    persistent encoder BiLSTM launches: every waveform bit-identical to the same call run alone.
+    Before the PQMF synthesis loop's FMAs were kept out of v_pk_fma_f32 (melgan_out.hip,
+    fma_nopk), 13 of 80 such trials had runs of 16 wrong samples in output phases 0 / 2
+    (tools/race_probe.py, profiles/r06/v26_pqmf_opsel.txt); 24 trials would have caught it
+    with probability ~0.99."""
+    from concurrent.futures import ThreadPoolExecutor
+
+    import bench
+    from tts_amd._lib import Engine, get_engine
+    from tts_amd.workload import forced_steps, lj_profile, pad_batch, synthetic_ids
+    dev = _dev()
+    taco, tsd, voc, vsd, tcfg, vcfg = bench.build_models(dev)
+    taco.decoder.set_r(2)
+    taco.decoder.verbose = False
+    T_prof, M_prof = lj_profile()
+    batch, lens = pad_batch(synthetic_ids(T_prof))
+    x = torch.from_numpy(batch).to(dev)
+    with torch.no_grad():
+        _, post, _, _ = taco.inference(x, text_lengths=lens, max_decoder_steps=forced_steps(M_prof, 2))
+    ml = np.asarray(taco.last_mel_lengths, np.int64)
+    c = post.transpose(1, 2).contiguous()
+    B, _, M = c.shape
+    engB = Engine(0)
+    try:
+        voc._sync(engB)
+        ea = get_engine(dev)
+        sV = torch.cuda.Stream(dev)
+
+        def voc_call():
+            with torch.cuda.stream(sV):
+                w = torch.full((B, 1, voc.hop * M), float("nan"), device=dev)
+                engB.melgan_infer(c, ml, 0, w)
+                sV.synchronize()
+            return w
+
+        ref = voc_call().clone()
+        assert not torch.isnan(ref).any()
+        eo = torch.empty(x.shape[0], x.shape[1], 512, device=dev)
+        bad = []
+        with ThreadPoolExecutor(1) as ex:
+            for trial in range(24):
+                torch.cuda.synchronize()
+                fut = ex.submit(voc_call)
+                with ea.lock:
+                    for _ in range(6):
+                        ea.taco_encoder(x, lens, eo)
+                w = fut.result()
+                torch.cuda.synchronize()
+                if not torch.equal(w, ref):
+                    bad.append((trial, int((w != ref).sum())))
+        assert not bad, f"waveforms differ beside the BiLSTM (trial, samples): {bad}"
+    finally:
+        engB.close()
+
+
 def test_fused_submit_pipelined_and_short_decode():
     """The fused call's two halves (tts_taco_mbmelgan_submit / _finish) with the host one batch
     ahead, as bench.py times it: two batches with different ragged forced lengths submitted back to

@@ -23,6 +23,16 @@ constexpr int OP_CC = 8;                  // channels per staged chunk
 constexpr int OP_TAPS = 63;
 constexpr int OP_PER = (OP_CC * OP_XW + 255) / 256;  // staged floats per thread per chunk
 typedef float f32x2 __attribute__((ext_vector_type(2)));
+
+// fp32 FMA kept out of v_pk_fma_f32: packed, the synthesis loop broadcasts the band value from
+// the high dword of a ds_read2 register pair (op_sel:[0,1,0]), and those low-half results were
+// wrong (runs of 16 lanes, output phases 0 / 2) in 4 of 30 runs beside a persistent BiLSTM launch
+// of another context (tools/race_probe.py, profiles/r06/v26_pqmf_opsel.txt)
+__device__ __forceinline__ float fma_nopk(float a, float b, float c) {
+  float d;
+  asm("v_fma_f32 %0, %1, %2, %3" : "=v"(d) : "v"(a), "v"(b), "v"(c));
+  return d;
+}
 }  // namespace
 
 template <int C>
@@ -138,7 +148,8 @@ __global__ __launch_bounds__(256) void out_pqmf_kernel(const float* __restrict__
       for (int i = 0; i < 4; ++i) {
         const int mm = min(tid + 256 * i, OP_TB - 1);  // local band position of the output quad
         const float bv = Bs[k * OP_NB + mm + 1 + jj];
-        out[i] = g * bv + out[i];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) out[i][r] = fma_nopk(g[r], bv, out[i][r]);
       }
     }
   }
