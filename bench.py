@@ -4,8 +4,9 @@ One "step" = Tacotron2.inference on the rank's 32-utterance batch (encoder, pers
 autoregressive decoder, postnet) followed by MultibandMelganGenerator.inference on the
 resulting mels (generator + PQMF), as ONE library submission (Tacotron2.inference_vocoded_submit ->
 tts_taco_mbmelgan_submit / _finish; bit-identical to the two calls). The timed loop keeps the host
-one batch ahead: batch i + 1 is queued behind batch i's vocoder before batch i's waveforms are
-taken, and every batch is finished inside the timed region; the blocking one-call and two-call
+one batch ahead: batch i + 1 is submitted (its Tacotron2 runs beside batch i's vocoder, which the
+library keeps on a second stream) before batch i's waveforms are taken, and every batch is
+finished inside the timed region; the blocking one-call and two-call
 forms are timed beside it. Forced lengths: stop bias -1e4 and
 max_decoder_steps_i = ceil(M_i / r), so every run does exactly the same work.
 
@@ -350,7 +351,8 @@ def main(argv=None):
     def pipelined(steps, n):
         """n batches through both models with the host one batch ahead (Tacotron2.
         inference_vocoded_submit -> tts_taco_mbmelgan_submit / _finish): batch i + 1 is submitted,
-        its encoder and decode queued behind batch i's vocoder, before batch i's result is taken.
+        its encoder and decode running beside batch i's vocoder (the library's second stream), before
+        batch i's result is taken.
         Every batch's waveforms are final (range flag checked) inside the caller's timed region."""
         frames = 0
         prev = None
@@ -581,7 +583,7 @@ def main(argv=None):
         "sync_call_ms_per_step": round(m2["sync_ms"], 3),
         "two_call_ms_per_step": round(m2["two_call_ms"], 3),
         "entry": "Tacotron2.inference_vocoded_submit -> tts_taco_mbmelgan_submit / _finish, the host one batch "
-                 "ahead (batch i+1 queued behind batch i's vocoder); sync_call_ms_per_step: one blocking "
+                 "ahead (batch i+1's Tacotron2 beside batch i's vocoder on the library's second stream); sync_call_ms_per_step: one blocking "
                  "tts_taco_mbmelgan_infer per batch; two_call_ms_per_step: Tacotron2.inference + "
                  "MultibandMelganGenerator.inference",
         "tacotron2_mel_frames_per_s": round(my_frames / (taco_ms / 1000.0) * world, 1),

@@ -535,11 +535,32 @@ struct tts_ctx {
   // fused Tacotron2 + MB-MelGAN submissions whose vocoder may still run (tts_taco_mbmelgan_submit)
   VocTicket vt[NVT];
   int64_t next_ticket = 1;
+  // the fused submissions' vocoders run on sv (TTS_VOC_STREAM=0: sv is s), behind their decode's
+  // status event, so the next submission's Tacotron2 on s overlaps them. Each ticket slot has its own
+  // device lengths and range flag (vslot: [NVT][BMAX] lengths, then NVT flags). Every other entry
+  // joins sv first (enter); a fused submission's Tacotron2 does not (in_submit).
+  hipStream_t sv = nullptr;
+  hipEvent_t ev_sv = nullptr;  // after the last vocoder enqueued on sv
+  bool sv_live = false;        // sv may hold work that s has not joined
+  bool in_submit = false;
+  DevBuf vslot;
+  unsigned* flag_override = nullptr;  // range flag of the vocoder being enqueued (x3_flag)
+  int* vlens_override = nullptr;      // device lengths of the vocoder being enqueued (run_generator)
 };
+
+int* vslot_lens(tts_ctx* c, int k) {
+  c->vslot.ensure((size_t)NVT * (BMAX + 1) * 4);
+  return reinterpret_cast<int*>(c->vslot.p) + k * BMAX;
+}
+unsigned* vslot_flag(tts_ctx* c, int k) {
+  c->vslot.ensure((size_t)NVT * (BMAX + 1) * 4);
+  return reinterpret_cast<unsigned*>(c->vslot.p) + NVT * BMAX + k;
+}
 
 // range flag for the split-f16 kernels of the current call, or null (fp32 kernels)
 unsigned* x3_flag(tts_ctx* c) {
   if (!c->gemm_x3) return nullptr;
+  if (c->flag_override) return c->flag_override;
   c->x3flag.ensure(4);
   return reinterpret_cast<unsigned*>(c->x3flag.p);
 }
@@ -560,6 +581,10 @@ struct DeviceGuard {
 // stream ordering with the caller's stream (nothing to wait for when all of its work is complete:
 // a server loop's stream holds only waits on this context's own finished events)
 void enter(tts_ctx* c, void* stream) {
+  if (c->sv_live && !c->in_submit) {  // a fused submission's vocoder may still use the vocoder workspace
+    HIP_OK(hipStreamWaitEvent(c->s, c->ev_sv, 0));
+    c->sv_live = false;
+  }
   if (hipStreamQuery((hipStream_t)stream) == hipSuccess) return;
   (void)hipGetLastError();  // hipErrorNotReady is not an error here; clear it for later launch checks
   HIP_OK(hipEventRecord(c->ev_in, (hipStream_t)stream));
@@ -2050,14 +2075,19 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
       maxelems = std::max(maxelems, (size_t)Cc * Lb * mul);
     }
   }
-  W.lens.ensure(B * 4);
+  // device lengths: the ticket slot's (a fused submission's vocoder) or the workspace's
+  int* vld = c->vlens_override;
+  if (!vld) {
+    W.lens.ensure(B * 4);
+    vld = W.lens.i();
+  }
   W.xa.ensure((size_t)B * maxelems * 4);
   W.xb.ensure((size_t)B * maxelems * 4);
   std::vector<int> lens(h_lens, h_lens + B);
-  if (!dev_lens) HIP_OK(hipMemcpyAsync(W.lens.p, lens.data(), B * 4, hipMemcpyHostToDevice, s));
-  else TTS_CHECK(W.lens.bytes >= (size_t)B * 4, "vocoder lengths buffer");
+  if (!dev_lens) HIP_OK(hipMemcpyAsync(vld, lens.data(), B * 4, hipMemcpyHostToDevice, s));
+  else TTS_CHECK(c->vlens_override || W.lens.bytes >= (size_t)B * 4, "vocoder lengths buffer");
   ConvCall cc;
-  cc.lens = W.lens.i();
+  cc.lens = vld;
   cc.B = B;
   cc.oflow = x3_flag(c);
   cc.len_add = 2 * pad;
@@ -2101,7 +2131,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
     sa.y = ys;
     sa.sb = (long)Cs * Lss;
     sa.Ls = (int)Lss;
-    sa.lens = W.lens.i();
+    sa.lens = vld;
     sa.len_add = 2 * pad;
     sa.mul = muls;
     for (int k = 0; k < 3; ++k) {
@@ -2175,7 +2205,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
       ra.y = xo;
       ra.sb = (long)C * Ls;
       ra.Ls = (int)Ls;
-      ra.lens = W.lens.i();
+      ra.lens = vld;
       ra.len_add = 2 * pad;
       ra.mul = mul;
       ra.dil = dl.dil;
@@ -2206,7 +2236,7 @@ int run_generator(tts_ctx* c, const float* mel, const int32_t* h_lens, int B, in
   }
   if (G.out_ch == 1) {  // full-band output stage on the VALU (melgan_out.hip)
     HIP_OK(hipMemsetAsync(out, 0, (size_t)B * Ls * 4, s));
-    launch_out_conv1(x, (long)C * Ls, Ls, C, G.out_w.f(), G.out_b.f(), W.lens.i(), 2 * pad, mul, (int)(Lb * mul), B,
+    launch_out_conv1(x, (long)C * Ls, Ls, C, G.out_w.f(), G.out_b.f(), vld, 2 * pad, mul, (int)(Lb * mul), B,
                      out, Ls, s);
     return up;
   }
@@ -3207,6 +3237,10 @@ int tts_ctx_create(int device, tts_ctx** out) {
     if (const char* e = std::getenv("TTS_GEMM")) c->gemm_x3 = std::string(e) != "f32";
     DeviceGuard g(device);
     HIP_OK(hipStreamCreateWithFlags(&c->s, hipStreamNonBlocking));
+    const char* vs = std::getenv("TTS_VOC_STREAM");
+    if (vs && std::atoi(vs) == 0) c->sv = c->s;
+    else HIP_OK(hipStreamCreateWithFlags(&c->sv, hipStreamNonBlocking));
+    HIP_OK(hipEventCreateWithFlags(&c->ev_sv, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->ev_in, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->ev_out, hipEventDisableTiming));
     HIP_OK(hipEventCreateWithFlags(&c->ev_chunk[0], hipEventDisableTiming));
@@ -3226,6 +3260,7 @@ int tts_ctx_destroy(tts_ctx* c) {
     { std::lock_guard<std::recursive_mutex> lk(c->mu); }  // a call still inside the context ends first
     {
       DeviceGuard g(c->device);
+      (void)hipStreamSynchronize(c->sv);
       (void)hipStreamSynchronize(c->s);
       for (auto& ge : c->tws.graphs)
         if (ge) {
@@ -3236,14 +3271,15 @@ int tts_ctx_destroy(tts_ctx* c) {
     int dev = c->device;
     {
       DeviceGuard g(dev);
-      hipStream_t s = c->s;
-      std::vector<hipEvent_t> e = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1]};
+      hipStream_t s = c->s, sv = c->sv;
+      std::vector<hipEvent_t> e = {c->ev_in, c->ev_out, c->ev_chunk[0], c->ev_chunk[1], c->ev_sv};
       for (auto ev : c->ev_dec) e.push_back(ev);
       e.push_back(c->ev_status);
       for (auto& t : c->vt) e.push_back(t.ev);
       int* pin = c->pinned;
       delete c;
       for (auto ev : e) (void)hipEventDestroy(ev);
+      if (sv && sv != s) (void)hipStreamDestroy(sv);
       (void)hipStreamDestroy(s);
       (void)hipHostFree(pin);
     }
@@ -3511,6 +3547,8 @@ int tts_melgan_finalize(tts_ctx* c, int in_ch, int out_ch, int base, const int32
   return guarded_ctx(c, [&] {
     TTS_CHECK(c && ups && n_up >= 1 && n_up <= 6, "bad arguments");
     DeviceGuard g(c->device);
+    HIP_OK(hipStreamSynchronize(c->sv));  // no submitted vocoder still reads the weights replaced here
+    c->sv_live = false;
     HostMapConsumer consume{c->mg_host};
     melgan_finalize(c, in_ch, out_ch, base, ups, n_up, nres, use_pqmf);
   });
@@ -3528,10 +3566,11 @@ int tts_melgan_generator(tts_ctx* c, const float* d_mel, const int32_t* h_lens, 
   });
 }
 
-// MultibandMelganGenerator.inference body on c->s: generator, output conv and PQMF synthesis into
+// MultibandMelganGenerator.inference body on s (default c->s): generator, output conv and PQMF synthesis into
 // d_wav (B, 1, hop * (M_max + 2 pad)), rows zero past their own length
 static void mbmelgan_body(tts_ctx* c, const float* d_mel, const int64_t* mel_strides, const int32_t* h_lens, int B,
-                          int M_max, int pad, float* d_wav, bool dev_lens = false) {
+                          int M_max, int pad, float* d_wav, bool dev_lens = false, hipStream_t s = nullptr) {
+  if (!s) s = c->s;
   auto& G = c->mg;
   int up = 1;
   for (int u : G.ups) up *= u;
@@ -3539,17 +3578,19 @@ static void mbmelgan_body(tts_ctx* c, const float* d_mel, const int64_t* mel_str
   const bool fused = G.out_ch == 4 && G.taps == 62 && (G.C_last == 32 || G.C_last == 48);
   if (fused) {  // launch_out_pqmf writes the rows' zero padding itself
     GenTail t;
-    run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, c->s, &t, mel_strides, dev_lens);
+    run_generator(c, d_mel, h_lens, B, M_max, pad, nullptr, s, &t, mel_strides, dev_lens);
     TTS_CHECK(t.Ls == Ls, "generator length bookkeeping");
+    const int* dl = c->vlens_override ? c->vlens_override : c->mws.lens.i();
     TTS_CHECK(launch_out_pqmf(t.x, (long)t.C * t.Ls, t.Ls, t.C, G.out_w.f(), G.out_b.f(), G.G.f(), G.out_ch,
-                              G.taps, c->mws.lens.i(), 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s),
+                              G.taps, dl, 2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, s),
               "fused output/PQMF shape not covered");
   } else {
-    HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, c->s));
+    HIP_OK(hipMemsetAsync(d_wav, 0, (size_t)B * G.out_ch * Ls * 4, s));
     c->mws.bands.ensure((size_t)B * G.out_ch * Ls * 4);
-    run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), c->s, nullptr, mel_strides, dev_lens);
-    launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, c->mws.lens.i(),
-                          2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, c->s);
+    run_generator(c, d_mel, h_lens, B, M_max, pad, c->mws.bands.f(), s, nullptr, mel_strides, dev_lens);
+    const int* dl = c->vlens_override ? c->vlens_override : c->mws.lens.i();
+    launch_pqmf_synthesis(c->mws.bands.f(), (long)G.out_ch * Ls, Ls, G.G.f(), G.out_ch, G.taps, dl,
+                          2 * pad, up, (int)Ls, B, d_wav, (long)G.out_ch * Ls, s);
   }
 }
 
@@ -3578,22 +3619,48 @@ static int vocoder_min_len(const MelganModel& G, int pad) {
 // completes a submitted fused call: if its split-f16 vocoder raised the range flag, the vocoder
 // runs again on the fp32 kernels from the postnet output (the two-call path's fallback); then the
 // caller's stream is ordered after it
+// the vocoder being enqueued uses a ticket slot's device lengths and range flag
+struct VocSlot {
+  tts_ctx* c;
+  VocSlot(tts_ctx* c_, unsigned* flag, int* lens) : c(c_) {
+    c->flag_override = flag;
+    c->vlens_override = lens;
+  }
+  ~VocSlot() {
+    c->flag_override = nullptr;
+    c->vlens_override = nullptr;
+  }
+};
+// the vocoder work just enqueued on sv: later entries join it (enter)
+static void sv_mark(tts_ctx* c) {
+  HIP_OK(hipEventRecord(c->ev_sv, c->sv));
+  c->sv_live = c->sv != c->s;
+}
+static void sv_join(tts_ctx* c) {
+  if (!c->sv_live) return;
+  HIP_OK(hipStreamWaitEvent(c->s, c->ev_sv, 0));
+  c->sv_live = false;
+}
+
 static void finish_ticket(tts_ctx* c, VocTicket& tk, void* stream) {
   if (!tk.pending) return;
   tk.pending = false;
   if (tk.x3) {
     HIP_OK(hipEventSynchronize(tk.ev));
-    if (c->pinned[TK_PIN + tk.id % NVT]) {
+    const int k = (int)(tk.id % NVT);
+    if (c->pinned[TK_PIN + k]) {
       c->x3_fallbacks++;
       c->gemm_x3 = false;
-      try {
-        mbmelgan_body(c, tk.d_post, tk.st, tk.lens.data(), tk.B, tk.M, tk.pad, tk.d_wav);
+      try {  // on sv, behind any later submission's vocoder; the slot's lengths from the host
+        VocSlot vs(c, nullptr, vslot_lens(c, k));
+        mbmelgan_body(c, tk.d_post, tk.st, tk.lens.data(), tk.B, tk.M, tk.pad, tk.d_wav, false, c->sv);
       } catch (...) {
         c->gemm_x3 = true;
         throw;
       }
       c->gemm_x3 = true;
-      HIP_OK(hipEventRecord(tk.ev, c->s));
+      HIP_OK(hipEventRecord(tk.ev, c->sv));
+      sv_mark(c);
     }
   }
   HIP_OK(hipStreamWaitEvent((hipStream_t)stream, tk.ev, 0));
@@ -3617,6 +3684,7 @@ static int64_t taco_mbmelgan_submit(tts_ctx* c, const int64_t* d_ids, const int3
   const int64_t id = c->next_ticket++;
   VocTicket& tk = c->vt[id % NVT];
   finish_ticket(c, tk, stream);  // the slot's previous submission completes first
+  if (tk.id != 0) HIP_OK(hipStreamWaitEvent(c->s, tk.ev, 0));  // its vocoder is done with the slot
   tk.id = id;
   // per-row upper bounds of the decoded lengths (tile counts of the vocoder's persistent kernels)
   const int Lmin = vocoder_min_len(G, pad);
@@ -3626,20 +3694,38 @@ static int64_t taco_mbmelgan_submit(tts_ctx* c, const int64_t* d_ids, const int3
     bound[b] = h_max_steps[b] * r;
     TTS_CHECK(bound[b] >= Lmin, VOC_SHORT_MSG);
   }
-  c->mws.lens.ensure(BMAX * 4);
   const int64_t st[3] = {(int64_t)S_cap * r * 80, 1, 80};
   bool voc_x3 = false;
-  int* slot = c->pinned + TK_PIN + id % NVT;
-  FusedVoc fv{c->mws.lens.i(), Lmin, [&] {
+  const int k = (int)(id % NVT);
+  int* slot = c->pinned + TK_PIN + k;
+  int* vl = vslot_lens(c, k);
+  unsigned* vf = vslot_flag(c, k);
+  hipStream_t sv = c->sv;
+  FusedVoc fv{vl, Lmin, [&] {
                 voc_x3 = c->gemm_x3;
-                // the vocoder's input is the postnet output read in place, frame-major; rows are
-                // hop (S_cap r + 2 pad) samples apart until the decoded lengths are on the host
-                mbmelgan_body(c, d_post, st, bound.data(), B, S_cap * r, pad, d_wav, /*dev_lens=*/true);
-                if (voc_x3) HIP_OK(hipMemcpyAsync(slot, x3_flag(c), 4, hipMemcpyDeviceToHost, c->s));
+                // on sv behind the decode's status event (recorded just before), with the ticket
+                // slot's lengths (the status kernel wrote them) and range flag; the vocoder's input
+                // is the postnet output read in place, frame-major; rows are hop (S_cap r + 2 pad)
+                // samples apart until the decoded lengths are on the host
+                if (sv != c->s) HIP_OK(hipStreamWaitEvent(sv, c->ev_status, 0));
+                if (voc_x3) HIP_OK(hipMemsetAsync(vf, 0, 4, sv));
+                {
+                  VocSlot vs(c, vf, vl);
+                  mbmelgan_body(c, d_post, st, bound.data(), B, S_cap * r, pad, d_wav, /*dev_lens=*/true, sv);
+                }
+                if (voc_x3) HIP_OK(hipMemcpyAsync(slot, vf, 4, hipMemcpyDeviceToHost, sv));
+                sv_mark(c);
               }};
   c->flag_read = false;
-  taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
-             h_status, stream, d_spk_ids, d_spk_emb, &fv);
+  c->in_submit = true;  // this submission's Tacotron2 does not wait for earlier vocoders on sv
+  try {
+    taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
+               h_status, stream, d_spk_ids, d_spk_emb, &fv);
+  } catch (...) {
+    c->in_submit = false;
+    throw;
+  }
+  c->in_submit = false;
   const bool taco_oflow = c->gemm_x3 && c->flag_read && c->pinned[12];
   c->flag_read = false;
   int S = 0;
@@ -3654,6 +3740,7 @@ static int64_t taco_mbmelgan_submit(tts_ctx* c, const int64_t* d_ids, const int3
     // vocoder already queued is overwritten), as the two separate calls would each have done
     c->x3_fallbacks++;
     c->gemm_x3 = false;
+    sv_join(c);  // the split vocoder queued on sv writes d_wav before the fp32 one below
     try {
       taco_infer(c, d_ids, h_lens, B, T_max, r, h_max_steps, S_cap, thr, d_dec, d_post, d_align, d_stop, h_steps,
                  h_status, stream, d_spk_ids, d_spk_emb);
@@ -3674,10 +3761,11 @@ static int64_t taco_mbmelgan_submit(tts_ctx* c, const int64_t* d_ids, const int3
   if (S < S_cap) {  // pack the rows to hop (S r + 2 pad) samples apart, as the two calls return them
     const size_t P = row * ((size_t)S * r + 2 * pad), Pc = row * ((size_t)S_cap * r + 2 * pad);
     c->mws.bands.ensure((size_t)B * P * 4);
-    HIP_OK(hipMemcpy2DAsync(c->mws.bands.p, P * 4, d_wav, Pc * 4, P * 4, B, hipMemcpyDeviceToDevice, c->s));
-    HIP_OK(hipMemcpyAsync(d_wav, c->mws.bands.p, (size_t)B * P * 4, hipMemcpyDeviceToDevice, c->s));
+    HIP_OK(hipMemcpy2DAsync(c->mws.bands.p, P * 4, d_wav, Pc * 4, P * 4, B, hipMemcpyDeviceToDevice, sv));
+    HIP_OK(hipMemcpyAsync(d_wav, c->mws.bands.p, (size_t)B * P * 4, hipMemcpyDeviceToDevice, sv));
   }
-  HIP_OK(hipEventRecord(tk.ev, c->s));
+  HIP_OK(hipEventRecord(tk.ev, sv));
+  sv_mark(c);
   tk.pending = true;
   tk.x3 = voc_x3;
   tk.d_post = d_post;
@@ -3725,7 +3813,8 @@ int tts_taco_mbmelgan_infer(tts_ctx* c, const int64_t* d_ids, const int32_t* h_l
                                             stream);
     VocTicket& tk = c->vt[id % NVT];
     if (tk.id == id) finish_ticket(c, tk, stream);
-    HIP_OK(hipStreamSynchronize(c->s));  // returns with the call's work done, as before
+    HIP_OK(hipStreamSynchronize(c->sv));  // returns with the call's work done, as before
+    HIP_OK(hipStreamSynchronize(c->s));
   });
 }
 
